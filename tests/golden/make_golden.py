@@ -1,0 +1,292 @@
+"""Generate golden fixtures by running the REFERENCE's own torch modules.
+
+Run here (where /root/reference exists), never on the GPU box:
+
+    python tests/golden/make_golden.py
+
+The reference imports FEniCS/DOLFIN/PETSc/prettytable, none of which exist in
+this image; they are replaced by inert ``MagicMock`` modules.  Everything
+FEniCS would *compute* (M, W, F_ROM_BC, Y, Gamma, alpha) is supplied by the
+oracle's generic P1 restatement (oracle/fem.py).  ``torch.solve`` (removed in
+torch 2) is shimmed to ``torch.linalg.solve`` (ROM.py:59-62; same math).
+Random draws are injected by patching ``torch.randn_like`` / ``torch.randperm``
+with queues of pre-drawn tensors, which are saved with the fixtures.
+
+Outputs (small .npz, float32 unless noted) -- inputs, outputs and gradients:
+  codec_c32.npz / codec_c64.npz   CNNEncoder / CNNDecoder fwd + bwd
+  rom_c32.npz                     ROM solve + ReducedOrderModelOperator bwd
+  elbo_c32.npz                    GenerativeModel.elbo (armortized + freeX) + bwd
+  vo_c32.npz                      VirtualObservable.update / precision (fp64)
+  terms.npz                       DGLL / KL known values
+"""
+import os
+import sys
+import types
+from unittest import mock
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+REF = '/root/reference'
+sys.path.insert(0, ROOT)
+from oracle import fem  # noqa: E402
+
+for m in ['fenics', 'dolfin', 'petsc4py', 'petsc4py.PETSc', 'prettytable']:
+    sys.modules[m] = mock.MagicMock()
+sys.path.insert(0, REF)
+
+import bottleneck.utils as R_utils            # noqa: E402
+import bottleneck.ROM as R_ROM                # noqa: E402
+import bottleneck.components as R_comp        # noqa: E402
+import bottleneck.generative as R_gen         # noqa: E402
+import bottleneck.VirtualObservables as R_VO  # noqa: E402
+from bottleneck.Encoder import CNNEncoder     # noqa: E402
+from bottleneck.Decoder import CNNDecoder     # noqa: E402
+
+R_ROM.ROM._solve_eqs = lambda self, A, B: torch.linalg.solve(A, B)
+
+
+def sd(module, prefix=''):
+    return {prefix + k: v.detach().cpu().numpy().copy() for k, v in module.state_dict().items()}
+
+
+def grads(module, prefix='grad.'):
+    return {prefix + k: p.grad.detach().cpu().numpy().copy()
+            for k, p in module.named_parameters() if p.grad is not None}
+
+
+def randomize_bn(module, gen):
+    with torch.no_grad():
+        for m in module.modules():
+            if isinstance(m, torch.nn.BatchNorm2d):
+                m.weight.copy_(1.0 + 0.3 * torch.randn(m.weight.shape, generator=gen))
+                m.bias.copy_(0.2 * torch.randn(m.bias.shape, generator=gen))
+
+
+def random_fields(gen, n_img, n):
+    # smooth-ish log-conductivity images (separable SE correlation)
+    x = (np.arange(n) + 0.5) / n
+    C = np.exp(-0.5 * (x[:, None] - x[None, :]) ** 2 / 0.15 ** 2) + 1e-6 * np.eye(n)
+    L = np.linalg.cholesky(C)
+    G = gen.normal(size=(n_img, n, n))
+    return 0.4 + 0.8 * np.einsum('ij,bjk,lk->bil', L, G, L)
+
+
+# --------------------------------------------------------------------------
+def make_codec(tag, imsize, dz, latent, blocks, growth, f_enc, f_dec, B):
+    torch.manual_seed(0)
+    gen = torch.Generator().manual_seed(1)
+    enc = CNNEncoder(imsize, dz, blocks, growth, f_enc, drop_rate=0)
+    dec = CNNDecoder(imsize, dz, (latent, latent), 1, f_dec, blocks, False, growth, drop_rate=0.,
+                     upsample='nearest', force_single_output=False)
+    randomize_bn(enc, gen)
+    randomize_bn(dec, gen)
+    rng = np.random.default_rng(2)
+    X = torch.tensor(random_fields(rng, B, imsize), dtype=torch.float32, requires_grad=True)
+    mu, ls = enc(X)
+    wm = torch.randn(mu.shape, generator=gen)
+    ws = torch.randn(ls.shape, generator=gen)
+    (torch.sum(mu * wm) + torch.sum(ls * ws)).backward()
+    Z = torch.randn(B, dz, generator=gen).requires_grad_(True)
+    mx, lsx = dec(Z)
+    vm = torch.randn(mx.shape, generator=gen)
+    vs = torch.randn(lsx.shape, generator=gen)
+    (torch.sum(mx * vm) + torch.sum(lsx * vs)).backward()
+    out = dict(X=X.detach().numpy(), enc_mu=mu.detach().numpy(), enc_ls=ls.detach().numpy(),
+               enc_wm=wm.numpy(), enc_ws=ws.numpy(), grad_X=X.grad.numpy(),
+               Z=Z.detach().numpy(), dec_mu=mx.detach().numpy(), dec_ls=lsx.detach().numpy(),
+               dec_vm=vm.numpy(), dec_vs=vs.numpy(), grad_Z=Z.grad.numpy(),
+               cfg=np.array([imsize, dz, latent, growth, f_enc, f_dec] + list(blocks)))
+    out.update(sd(enc, 'enc.'))
+    out.update(grads(enc, 'enc.grad.'))
+    out.update(sd(dec, 'dec.'))
+    out.update(grads(dec, 'dec.grad.'))
+    np.savez_compressed(os.path.join(HERE, 'codec_%s.npz' % tag), **out)
+    print('codec', tag, 'enc params', sum(p.numel() for p in enc.parameters()),
+          'dec params', sum(p.numel() for p in dec.parameters()))
+
+
+# --------------------------------------------------------------------------
+def c32_physics():
+    nc, r = 4, 8
+    mc = fem.unit_square_mesh(nc)
+    mf = fem.unit_square_mesh(nc * r)
+    M = fem.rom_stiffness_tensor(mc)
+    W = fem.prolongation_free(mc, mf)
+    cdofs, fdofs = fem.dirichlet_split(mc)
+    return nc, r, mc, mf, M, W, cdofs, fdofs
+
+
+class _Phys(object):
+    def __init__(self, c, f):
+        self.constrained_dofs = c
+        self.free_dofs = f
+
+
+def make_rom():
+    nc, r, mc, mf, M, W, cdofs, fdofs = c32_physics()
+    rng = np.random.default_rng(3)
+    N = 6
+    rom = R_ROM.ROM(_Phys(cdofs, fdofs), torch.tensor(M, dtype=torch.float32), torch.float32, 'cpu')
+    g = R_comp.ReducedOrderModelOperator(rom, torch.tensor(W, dtype=torch.float32),
+                                         dtype=torch.float32, device='cpu')
+    with torch.no_grad():
+        g.logsigmas_y.copy_(torch.tensor(rng.normal(0.5, 0.3, W.shape[0]), dtype=torch.float32))
+    U = rng.uniform(-0.5, 0.5, (N, 4))
+    F = torch.tensor(np.stack([fem.f_rom_bc(mc, u) for u in U]), dtype=torch.float32)
+    effprop = torch.tensor(rng.normal(0, 0.7, (N, M.shape[2])), dtype=torch.float32, requires_grad=True)
+    mu, ls = g(effprop, F)
+    Y = torch.tensor(rng.normal(0, 0.3, mu.shape), dtype=torch.float32)
+    L = R_utils.DiagonalGaussianLogLikelihood(Y, mu, 2 * ls)
+    (-L).backward()
+    np.savez_compressed(os.path.join(HERE, 'rom_c32.npz'), M=M.astype(np.float32), W=W.astype(np.float32),
+                        bc_dofs=cdofs, U=U, F=F.numpy(), effprop=effprop.detach().numpy(),
+                        logsigmas_y=g.logsigmas_y.detach().numpy(), mu_y=mu.detach().numpy(),
+                        Y=Y.numpy(), logL=L.detach().numpy(), grad_effprop=effprop.grad.numpy(),
+                        grad_logsigmas_y=g.logsigmas_y.grad.numpy())
+    print('rom ok', float(L))
+
+
+# --------------------------------------------------------------------------
+class _DS(object):
+    """Minimal stand-in for utils.data.DataSet (utils/data.py:419-445)."""
+
+    def __init__(self, **t):
+        self.t = t
+        self.N = next(iter(t.values())).shape[0]
+
+    def get(self, key, random_subset=None):
+        if random_subset is None:
+            return self.t[key]
+        perm = torch.randperm(self.N, dtype=torch.long)
+        return self.t[key][perm[0:random_subset], ]
+
+
+def make_elbo():
+    nc, r, mc, mf, M, W, cdofs, fdofs = c32_physics()
+    n = nc * r
+    rng = np.random.default_rng(4)
+    Nu, bs, Ns = 16, 8, 4
+    dz = 16
+    torch.manual_seed(0)
+    gen = torch.Generator().manual_seed(5)
+    enc = CNNEncoder(n, dz, [1, 1], 4, 4, drop_rate=0)
+    dec = CNNDecoder(n, dz, (8, 8), 1, 4, [1, 1], False, 4, drop_rate=0., upsample='nearest',
+                     force_single_output=False, homoscedastic=False)
+    randomize_bn(enc, gen)
+    randomize_bn(dec, gen)
+    rom = R_ROM.ROM(_Phys(cdofs, fdofs), torch.tensor(M, dtype=torch.float32), torch.float32, 'cpu')
+    g = R_comp.ReducedOrderModelOperator(rom, torch.tensor(W, dtype=torch.float32),
+                                         dtype=torch.float32, device='cpu')
+    gp = R_comp.EffectivePropertyMap(dz, M.shape[2], num_hidden_layers=0, independent_X=True,
+                                     dtype=torch.float32, device='cpu')
+    model = R_gen.GenerativeModel(f=dec, g=g, gp=gp, dtype=torch.float32, device='cpu')
+    model.encoder = enc
+
+    Xu = torch.tensor(random_fields(rng, Nu, n), dtype=torch.float32)
+    Xs_img = random_fields(rng, Ns, n)
+    Xs = torch.tensor(Xs_img, dtype=torch.float32)
+    U = rng.uniform(-0.5, 0.5, (Ns, 4))
+    Y = np.stack([fem.solve_fom(mf, np.exp(fem.image_to_cells(x)), u) for x, u in zip(Xs_img, U)])
+    F = np.stack([fem.f_rom_bc(mc, u) for u in U])
+    ds_sup = _DS(X=Xs, Y=torch.tensor(Y, dtype=torch.float32), F_ROM_BC=torch.tensor(F, dtype=torch.float32))
+    ds_uns = _DS(X=Xu)
+    model.register_datasets({'supervised': ds_sup, 'unsupervised': ds_uns}, None,
+                            create_unsupervised_variational_approximation=False)
+    with torch.no_grad():
+        for q in (model.q_z['supervised'], model.q_X['supervised']):
+            q._mean.copy_(torch.tensor(rng.normal(0, 0.5, q._mean.shape)))
+            q._logsigma.copy_(torch.tensor(rng.normal(-1.0, 0.3, q._logsigma.shape)))
+        g.logsigmas_y.copy_(torch.tensor(rng.normal(-2.0, 0.2, g.logsigmas_y.shape)))
+
+    perm = torch.tensor(rng.permutation(Nu), dtype=torch.long)
+    eps = [torch.tensor(rng.normal(size=s), dtype=torch.float32)
+           for s in [(bs, dz), (Ns, dz), (Ns, M.shape[2])]]
+    queue = list(eps)
+    real_randn_like = torch.randn_like
+
+    def fake_randn_like(t, *a, **k):
+        e = queue.pop(0)
+        assert e.shape == t.shape, (e.shape, t.shape)
+        return e.to(dtype=t.dtype)
+
+    state0 = {k: v.detach().cpu().numpy().copy() for k, v in model.state_dict().items()}
+    with mock.patch('torch.randperm', lambda N, **k: perm.clone()), \
+            mock.patch('torch.randn_like', fake_randn_like):
+        elbo = model.elbo(step=0, armortized_bs=bs)
+    assert not queue
+    (-elbo).backward()
+    out = {'state.' + k: v for k, v in state0.items()}
+    out.update({'grad.' + k: p.grad.detach().numpy() for k, p in model.named_parameters() if p.grad is not None})
+    out.update(Xu=Xu.numpy(), Xs=Xs.numpy(), Y=Y.astype(np.float32), F=F.astype(np.float32), U=U,
+               perm=perm.numpy(), eps_enc=eps[0].numpy(), eps_qz=eps[1].numpy(), eps_qX=eps[2].numpy(),
+               elbo=np.float64(elbo.item()), M=M.astype(np.float32), W=W.astype(np.float32), bc_dofs=cdofs,
+               cfg=np.array([n, nc, dz, Nu, bs, Ns]))
+    np.savez_compressed(os.path.join(HERE, 'elbo_c32.npz'), **out)
+    print('elbo ok', elbo.item(), 'n params', sum(p.numel() for p in model.parameters()))
+    del real_randn_like
+
+
+# --------------------------------------------------------------------------
+def make_vo():
+    nc, r, mc, mf, M, W, cdofs, fdofs = c32_physics()
+    n = nc * r
+    rng = np.random.default_rng(6)
+    Nvo = 3
+    imgs = random_fields(rng, Nvo, n)
+    U = rng.uniform(-0.5, 0.5, (Nvo, 4))
+    Gam, alp, G, P = [], [], [], []
+    for img, u in zip(imgs, U):
+        Gm, a = fem.cgr_query(mf, W, np.exp(fem.image_to_cells(img)), u)
+        Gam.append(Gm)
+        alp.append(a)
+        y = fem.solve_fom(mf, np.exp(fem.image_to_cells(img)), u)
+        G.append(y + rng.normal(0, 0.05, y.shape))
+        P.append(1.0 / rng.uniform(0.01, 0.05, y.shape) ** 2)
+
+    class _Q(object):
+        pass
+
+    means, vars_ = [], []
+    vo_var = torch.tensor(rng.uniform(1e-6, 1e-4, Gam[0].shape[0]), dtype=torch.double)
+    for Gm, a, g_, p_ in zip(Gam, alp, G, P):
+        q = mock.MagicMock()
+        q.Gamma = torch.tensor(Gm)
+        q.GammaTransposed = torch.tensor(Gm).t()
+        q.alpha = torch.tensor(a)
+        vo = R_VO.VirtualObservable.__new__(R_VO.VirtualObservable)
+        vo._querry = q
+        vo._device = torch.device('cpu')
+        vo._vo_variances = vo_var
+        with mock.patch('torch.cholesky', torch.linalg.cholesky):
+            vo.update(torch.tensor(g_), torch.tensor(p_), 0, ForceUpdate=True)
+        means.append(vo.mean.numpy())
+        vars_.append(vo.vars.numpy())
+    beta = 0
+    for Gm, a, mu, v in zip(Gam, alp, means, vars_):
+        beta = beta + (Gm @ mu - a) ** 2 + (Gm ** 2) @ v
+    np.savez_compressed(os.path.join(HERE, 'vo_c32.npz'), imgs=imgs, U=U, Gamma=np.stack(Gam),
+                        alpha=np.stack(alp), g=np.stack(G), prec=np.stack(P), vo_var=vo_var.numpy(),
+                        mean=np.stack(means), vars=np.stack(vars_), prec_beta=0.5 * beta + 1e-6)
+    print('vo ok')
+
+
+def make_terms():
+    rng = np.random.default_rng(7)
+    t = torch.tensor(rng.normal(size=(5, 7)))
+    m = torch.tensor(rng.normal(size=(5, 7)))
+    lv = torch.tensor(rng.normal(size=(5, 7)))
+    np.savez_compressed(os.path.join(HERE, 'terms.npz'), t=t.numpy(), m=m.numpy(), lv=lv.numpy(),
+                        dgll=R_utils.DiagonalGaussianLogLikelihood(t, m, lv).numpy(),
+                        kl=R_utils.UnitGaussianKullbackLeiblerDivergence(m, lv).numpy())
+
+
+if __name__ == '__main__':
+    make_terms()
+    make_codec('c32', 32, 16, 8, [1, 1], 4, 4, 4, B=8)
+    make_codec('c64', 64, 64, 8, [1, 2, 1], 4, 6, 6, B=4)
+    make_rom()
+    make_elbo()
+    make_vo()

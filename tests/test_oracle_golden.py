@@ -1,0 +1,121 @@
+"""Pin the CPU oracle against golden fixtures produced by the reference's own
+modules (tests/golden/make_golden.py).  CPU only."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import codec as ocodec
+from oracle import elbo as oelbo
+
+GOLD = os.path.join(os.path.dirname(__file__), 'golden')
+
+
+def load(name):
+    return dict(np.load(os.path.join(GOLD, name), allow_pickle=False))
+
+
+def params(d, prefix, dtype=torch.float64, grad=False):
+    out = {}
+    for k, v in d.items():
+        if k.startswith(prefix) and '.grad.' not in k and not k.startswith(prefix + 'grad.'):
+            name = k[len(prefix):]
+            if name.endswith('running_mean') or name.endswith('running_var') or name.endswith('num_batches_tracked'):
+                continue
+            out[name] = torch.tensor(v, dtype=dtype, requires_grad=grad)
+    return out
+
+
+def test_terms():
+    d = load('terms.npz')
+    t, m, lv = (torch.tensor(d[k]) for k in ('t', 'm', 'lv'))
+    np.testing.assert_allclose(oelbo.dgll(t, m, lv).item(), d['dgll'], rtol=1e-12)
+    np.testing.assert_allclose(oelbo.kl_unit(m, lv).item(), d['kl'], rtol=1e-12)
+
+
+@pytest.mark.parametrize('tag', ['c32', 'c64'])
+def test_codec(tag):
+    d = load('codec_%s.npz' % tag)
+    imsize, dz, latent, growth, f_enc, f_dec = [int(v) for v in d['cfg'][:6]]
+    blocks = [int(v) for v in d['cfg'][6:]]
+    pe = params(d, 'enc.', grad=True)
+    X = torch.tensor(d['X'], dtype=torch.float64, requires_grad=True)
+    mu, ls = ocodec.encoder_forward(pe, X, imsize, blocks, growth, f_enc)
+    np.testing.assert_allclose(mu.detach().numpy(), d['enc_mu'], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(ls.detach().numpy(), d['enc_ls'], rtol=1e-4, atol=1e-5)
+    (torch.sum(mu * torch.tensor(d['enc_wm'])) + torch.sum(ls * torch.tensor(d['enc_ws']))).backward()
+    np.testing.assert_allclose(X.grad.numpy(), d['grad_X'], rtol=1e-3, atol=1e-4)
+    for k, p in pe.items():
+        np.testing.assert_allclose(p.grad.numpy(), d['enc.grad.' + k], rtol=1e-3, atol=2e-4, err_msg=k)
+
+    pd = params(d, 'dec.', grad=True)
+    Z = torch.tensor(d['Z'], dtype=torch.float64, requires_grad=True)
+    mx, lsx = ocodec.decoder_forward(pd, Z, latent, blocks, growth, f_dec)
+    np.testing.assert_allclose(mx.detach().numpy(), d['dec_mu'], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(lsx.detach().numpy(), d['dec_ls'], rtol=1e-4, atol=1e-5)
+    (torch.sum(mx * torch.tensor(d['dec_vm'])) + torch.sum(lsx * torch.tensor(d['dec_vs']))).backward()
+    np.testing.assert_allclose(Z.grad.numpy(), d['grad_Z'], rtol=1e-3, atol=1e-4)
+    for k, p in pd.items():
+        np.testing.assert_allclose(p.grad.numpy(), d['dec.grad.' + k], rtol=1e-3, atol=2e-3, err_msg=k)
+
+
+def test_rom():
+    d = load('rom_c32.npz')
+    M = torch.tensor(d['M'], dtype=torch.float64)
+    W = torch.tensor(d['W'], dtype=torch.float64)
+    e = torch.tensor(d['effprop'], dtype=torch.float64, requires_grad=True)
+    ls = torch.tensor(d['logsigmas_y'], dtype=torch.float64, requires_grad=True)
+    mu, lsr = oelbo.rom_operator(W, M, torch.tensor(d['bc_dofs']), e, torch.tensor(d['F'], dtype=torch.float64), ls)
+    np.testing.assert_allclose(mu.detach().numpy(), d['mu_y'], rtol=1e-4, atol=1e-5)
+    L = oelbo.dgll(torch.tensor(d['Y'], dtype=torch.float64), mu, 2 * lsr)
+    np.testing.assert_allclose(L.item(), d['logL'], rtol=1e-5)
+    (-L).backward()
+    np.testing.assert_allclose(e.grad.numpy(), d['grad_effprop'], rtol=2e-3, atol=1e-3)
+    np.testing.assert_allclose(ls.grad.numpy(), d['grad_logsigmas_y'], rtol=1e-3, atol=1e-4)
+
+
+def test_elbo_step():
+    d = load('elbo_c32.npz')
+    n, nc, dz, Nu, bs, Ns = [int(v) for v in d['cfg']]
+    st = {k[len('state.'):]: torch.tensor(v, dtype=torch.float64, requires_grad=True)
+          for k, v in d.items() if k.startswith('state.') and not k.endswith(('running_mean', 'running_var', 'num_batches_tracked'))}
+    enc_p = {k[len('encoder.'):]: v for k, v in st.items() if k.startswith('encoder.')}
+    dec_p = {k[len('f.'):]: v for k, v in st.items() if k.startswith('f.')}
+    M = torch.tensor(d['M'], dtype=torch.float64)
+    W = torch.tensor(d['W'], dtype=torch.float64)
+    bc = torch.tensor(d['bc_dofs'])
+    enc = lambda x: ocodec.encoder_forward(enc_p, x, n, [1, 1], 4, 4)
+    dec = lambda z: ocodec.decoder_forward(dec_p, z, 8, [1, 1], 4, 4)
+    Xu = torch.tensor(d['Xu'], dtype=torch.float64)[torch.tensor(d['perm'][:bs])]
+    e1, _ = oelbo.elbo_unsupervised_armortized(enc, dec, Xu, torch.tensor(d['eps_enc'], dtype=torch.float64))
+    gp = lambda z: torch.nn.functional.linear(z, st['gp.fc.weight'], st['gp.fc.bias'])
+    rom = lambda x, F: oelbo.rom_operator(W, M, bc, x, F, st['g.logsigmas_y'])
+    e2, _ = oelbo.elbo_supervised_freeX(
+        dec, gp, st['gp.logsigmas_X'], rom,
+        (st['q_z.supervised._mean'], st['q_z.supervised._logsigma']),
+        (st['q_X.supervised._mean'], st['q_X.supervised._logsigma']),
+        torch.tensor(d['Xs'], dtype=torch.float64), torch.tensor(d['Y'], dtype=torch.float64),
+        torch.tensor(d['F'], dtype=torch.float64),
+        torch.tensor(d['eps_qz'], dtype=torch.float64), torch.tensor(d['eps_qX'], dtype=torch.float64))
+    elbo = e1 + e2
+    np.testing.assert_allclose(elbo.item(), float(d['elbo']), rtol=2e-5)
+    (-elbo).backward()
+    for k, p in st.items():
+        ref = d.get('grad.' + k)
+        assert ref is not None, k
+        scale = max(np.abs(ref).max(), 1.0)
+        np.testing.assert_allclose(p.grad.numpy() / scale, ref / scale, atol=2e-4, err_msg=k)
+
+
+def test_vo_update():
+    d = load('vo_c32.npz')
+    for i in range(d['Gamma'].shape[0]):
+        mean, var = oelbo.vo_condition(torch.tensor(d['Gamma'][i]), torch.tensor(d['alpha'][i]),
+                                       torch.tensor(d['g'][i]), torch.tensor(d['prec'][i]),
+                                       torch.tensor(d['vo_var']))
+        np.testing.assert_allclose(mean.numpy(), d['mean'][i], rtol=1e-9, atol=1e-10)
+        np.testing.assert_allclose(var.numpy(), d['vars'][i], rtol=1e-7, atol=1e-12)
+    beta = oelbo.vo_precision_beta([torch.tensor(g) for g in d['Gamma']], [torch.tensor(a) for a in d['alpha']],
+                                   [torch.tensor(m) for m in d['mean']], [torch.tensor(v) for v in d['vars']])
+    np.testing.assert_allclose(beta.numpy(), d['prec_beta'], rtol=1e-9)
