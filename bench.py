@@ -1,0 +1,268 @@
+"""ELBO training-step throughput of the native MI355X path.
+
+metric : ELBO-step samples/sec on 64x64 grids (BASELINE.json), whole job.
+step   : random armortized subset + reparametrisation noise + ELBO forward
+         (encoder, dense head, decoder with fused Gaussian log-lik, ROM solve
+         with fused log-lik) + backward + [RCCL SUM all-reduce of the shared
+         gradients] + Adam over every parameter  (training.py:405-417 without
+         the PredictionEnsemble / monitoring extras).
+work   : per GPU B_u = 256 unlabeled + N_s = 32 labeled 64x64 samples
+         (highres codec, ROM 8x8, drop_rate 0), weak scaling over GPUs.
+
+Usage: python bench.py [--gpus N --steps K --warmup W]; for N > 1 launch one
+process per GPU with torch.distributed.run (RCCL backend).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, 'generative-physics-informed-pde_amd')
+for _p in (ROOT, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+
+CONFIGS = {
+    # name: (factory, B_u, N_s, pool, field params (mean, std, corrlength))
+    'c64': ('highres', 256, 32, 1024, (0.4, 0.8, 0.04)),
+    'c32': ('highres32', 64, 16, 256, (0.4, 0.8, 0.15)),
+    'c128': ('highres128', 256, 32, 512, (0.4, 0.8, 0.04)),
+}
+
+
+def make_data(fac, n, pool, N_s, field, seed, device):
+    from physics.RandomField import NormalRandomFieldSampler
+    from physics.grid import pixel_to_cells
+    rng = np.random.default_rng(seed)
+    rfs = NormalRandomFieldSampler.FromImage(n, n, *field)
+    Xu = rfs.sample(batch_size=pool, rng=rng)
+    Xs = rfs.sample(batch_size=N_s, rng=rng)
+    U = rng.uniform(-0.5, 0.5, (N_s, 4))
+    physics = fac._physics()
+    fom, rom = physics['fom'].grid, physics['rom'].grid
+    Y = np.stack([fom.solve(np.exp(pixel_to_cells(x)), u) for x, u in zip(Xs, U)])
+    F = np.stack([rom.full_force(u) for u in U])
+    t = lambda a: torch.tensor(a, dtype=torch.float32, device=device).contiguous()
+    return t(Xu), t(Xs), t(Y), t(F), U
+
+
+def build(cfg_name, device, seed):
+    from factories.model import ModelFactory
+    from utils.data import DataSet, DataLoader
+    fname, B_u, N_s, pool, field = CONFIGS[cfg_name]
+    fac = ModelFactory.FromIdentifier(fname)
+    fac.set('device', 'cuda')
+    torch.manual_seed(0)                       # identical shared parameters on every rank
+    physics, model, _, encoder, dtype, _ = fac.setup()
+    model = model.to(device)
+    encoder = encoder.to(device)
+    n = physics['fom'].grid.n
+    Xu, Xs, Y, F, U = make_data(fac, n, pool, N_s, field, seed, device)
+
+    class _T(object):       # device-resident dataset views
+        def __init__(self, **t):
+            self.t = t
+            self.N = next(iter(t.values())).shape[0]
+
+        def __bool__(self):
+            return True
+
+        def get(self, k, random_subset=None):
+            return self.t[k]
+
+    model.encoder = encoder
+    model.register_datasets({'supervised': _T(X=Xs, Y=Y, F_ROM_BC=F), 'unsupervised': _T(X=Xu)}, None,
+                            create_unsupervised_variational_approximation=False)
+    return model, (Xu, Xs, Y, F), (B_u, N_s), physics
+
+
+def conv_bytes(d, B, fwd):
+    """Algorithmic HBM bytes of one conv launch (each tensor read / written once)."""
+    hwi, hwo = d.h_in * d.w_in, d.h_out * d.w_out
+    if fwd:
+        b = B * (d.cin * hwi + d.cout * hwo)
+        if d.epilogue == 2:
+            b += B * (hwo + 2 * hwo)             # target read + gradient write
+    else:
+        b = B * (d.cin * hwi + (2 if d.gout_mode == 0 else 1) * d.cout * hwo)
+        if d.gin_off >= 0:
+            b += B * d.cin * hwi * (2 if d.gin_accumulate else 1)
+    return 4.0 * b
+
+
+def profile_kernels(step, reps=20):
+    """Per-launch device time of every codec operator, measured with HIP events on
+    the stream the kernels run on; returns [(name, ms, bytes)]."""
+    import ctypes as C
+    from gpi import _lib as L
+    e = step.engine
+    lib = L.lib()
+    st = L.stream_handle()
+    out = []
+    progs = []
+    if e.ep is not None:
+        progs.append((e.ep, e.enc_descs, e.ectx, e.B_u))
+    progs.append((e.dp, e.dec_descs, e.dctx, e.B))
+    for prog, descs, ctx, B in progs:
+        for i, op in enumerate(prog.ops):
+            for fwd in (True, False):
+                fn = lib.gpi_conv_forward if fwd else lib.gpi_conv_backward
+                d = descs[i]
+                for _ in range(3):
+                    fn(C.byref(d), C.byref(ctx), st)
+                t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                t0.record()
+                for _ in range(reps):
+                    fn(C.byref(d), C.byref(ctx), st)
+                t1.record()
+                torch.cuda.synchronize()
+                out.append(('%s.%s' % (op.name, 'fwd' if fwd else 'bwd'), t0.elapsed_time(t1) / reps,
+                            conv_bytes(d, B, fwd)))
+    return out
+
+
+def cpu_baseline(model, data, B_u, N_s, physics, budget_s=12.0, max_steps=20):
+    """The oracle (CPU port of the reference step, torch fp32) timed on the host cores."""
+    from oracle import codec as ocodec
+    from oracle import elbo as oelbo
+    from oracle import fem
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    Xu, Xs, Y, F = [t.detach().cpu() for t in data]
+    enc, dec = model.encoder, model.f
+    ec, dc = enc.native_config(), dec.native_config()
+    params = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in model.named_parameters()}
+    nc = physics['rom'].grid.n
+    n = physics['fom'].grid.n
+    M = torch.tensor(fem.rom_stiffness_tensor(fem.unit_square_mesh(nc)), dtype=torch.float32)
+    W = torch.tensor(physics['W'], dtype=torch.float32)
+    bc = torch.tensor(physics['rom'].grid.constrained_dofs)
+    pe = {k[8:]: v for k, v in params.items() if k.startswith('encoder.')}
+    pd = {k[2:]: v for k, v in params.items() if k.startswith('f.')}
+    opt = torch.optim.Adam(params.values(), lr=1e-2)
+
+    def one_step():
+        opt.zero_grad()
+        idx = torch.randperm(Xu.shape[0])[:B_u]
+        X = Xu[idx]
+        encf = lambda x: ocodec.encoder_forward(pe, x, ec['imsize'], ec['blocks'], ec['growth'], ec['init_features'])
+        decf = lambda z: ocodec.decoder_forward(pd, z, dc['latent_img_size'], dc['blocks'], dc['growth'],
+                                                dc['init_features'])
+        e1, _ = oelbo.elbo_unsupervised_armortized(encf, decf, X, torch.randn(B_u, dec.dim_latent))
+        gp = lambda z: torch.nn.functional.linear(z, params['gp.fc.weight'], params['gp.fc.bias'])
+        rom = lambda x, Fm: oelbo.rom_operator(W, M, bc, x, Fm, params['g.logsigmas_y'])
+        qz = (params['q_z.supervised._mean'], params['q_z.supervised._logsigma'])
+        qx = (params['q_X.supervised._mean'], params['q_X.supervised._logsigma'])
+        e2, _ = oelbo.elbo_supervised_freeX(decf, gp, params['gp.logsigmas_X'], rom, qz, qx, Xs, Y, F,
+                                            torch.randn(N_s, dec.dim_latent), torch.randn(N_s, qx[0].shape[1]))
+        (-(e1 + e2)).backward()
+        opt.step()
+
+    one_step()                      # warm-up
+    t0 = time.perf_counter()
+    k = 0
+    while k < max_steps and (time.perf_counter() - t0) < budget_s:
+        one_step()
+        k += 1
+    dt = time.perf_counter() - t0
+    return dict(value=(B_u + N_s) * k / dt, unit='samples/s', cores=threads, kind='port',
+                sample='%d steps of the same C64 step (B_u=%d, N_s=%d) on CPU torch fp32 (oracle port)' % (
+                    k, B_u, N_s))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=50)
+    ap.add_argument('--warmup', type=int, default=10)
+    ap.add_argument('--config', default='c64', choices=sorted(CONFIGS))
+    ap.add_argument('--no-graph', action='store_true')
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-roofline', action='store_true')
+    args = ap.parse_args()
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    distributed = world > 1
+    if distributed:
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    device = torch.device('cuda', local)
+    torch.cuda.set_device(device)
+
+    from gpi.train import FusedElboStep
+    model, data, (B_u, N_s), physics = build(args.config, device, seed=1000 + rank)
+    Xu, Xs, Y, F = data
+    step = FusedElboStep(model, Xu, B_u, Xs, Y, F, lr=1e-2, seed=4321 + rank, distributed=distributed)
+    if not args.no_graph:
+        step.capture()
+    for _ in range(args.warmup):
+        step.step()
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step.step()
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    t1 = time.perf_counter()
+    dt = torch.tensor([t1 - t0], dtype=torch.float64, device=device)
+    if distributed:
+        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    dt = float(dt.item())
+    elbo = float(step.elbo().item())
+    if not math.isfinite(elbo):
+        raise RuntimeError('non-finite ELBO %r' % elbo)
+    step.engine.check_flag()
+
+    roof = None
+    cpu = None
+    if rank == 0 and not args.no_roofline:
+        prof = profile_kernels(step)
+        name, ms, byts = max(prof, key=lambda t: t[1])
+        ach = byts / (ms * 1e-3) / 1e9
+        roof = dict(bound='hbm', achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit='GB/s',
+                    frac=round(ach / HBM_PEAK_GBS, 4), traffic=None, kernel=name,
+                    kernel_ms=round(ms, 5), bytes_per_launch=byts,
+                    codec_ms_sum=round(sum(t[1] for t in prof), 4))
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(model, data, B_u, N_s, physics)
+
+    if rank == 0:
+        per_step = B_u + N_s
+        value = world * per_step * args.steps / dt
+        line = {
+            'metric': 'ELBO training-step samples/sec (64x64 grids)' if args.config == 'c64' else
+            'ELBO training-step samples/sec (%s)' % args.config,
+            'value': round(value, 1), 'unit': 'samples/s', 'n_gpus': world, 'steps': args.steps,
+            'warmup': args.warmup, 'ms_per_step': round(1e3 * dt / args.steps, 4), 'higher_is_better': True,
+            'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32', 'data': 'synthetic',
+            'config': {'workload': 'BASELINE config 2/3: %s grid, B_u=%d unlabeled + N_s=%d labeled per GPU, '
+                                   'ROM %dx%d, fused native step' % (args.config, B_u, N_s,
+                                                                     physics['rom'].grid.n, physics['rom'].grid.n),
+                       'global_batch': world * per_step, 'grid': physics['fom'].grid.n,
+                       'parallelism': 'dp%d' % world, 'graph': not args.no_graph},
+            'elbo_last': elbo,
+            'roofline': roof,
+            'cpu_baseline': cpu,
+        }
+        print(json.dumps(line))
+    if distributed:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

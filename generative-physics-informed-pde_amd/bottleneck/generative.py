@@ -1,0 +1,312 @@
+"""GenerativeModel (reference bottleneck/generative.py:10-644) on the native ELBO engine.
+
+Same constructor, registration API, ``elbo(...)`` signature and return value
+(a 0-d autograd tensor whose ``backward()`` fills every parameter's ``.grad``)
+as the reference, so training.py's loop (zero_grad -> elbo -> backward ->
+Adam.step) runs unchanged.  The armortized-unsupervised and supervised
+(independent_X) terms run as ONE fused native step (gpi/engine.py); the
+per-term methods are kept for callers that use them individually.
+"""
+import copy
+
+import numpy as np
+import torch
+
+import lamp.modules
+from bottleneck.components import VariationalApproximation
+from bottleneck.utils import DiagonalGaussianLogLikelihood
+from gpi.engine import ElboEngine
+from gpi.flat import FlatParameters
+from gpi.native import anchor, set_flat, engine_for
+from gpi import _lib as L
+
+SHARED_PREFIXES = ('f.', 'g.', 'gp.', 'encoder.')
+
+
+class _ElboFunction(torch.autograd.Function):
+
+    @staticmethod
+    def forward(ctx, a, engine):
+        ctx.engine = engine
+        return engine.forward()
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        e = ctx.engine
+        e.backward()
+        tmp = torch.empty_like(e.flat.G)
+        e.finalize(tmp)
+        tmp.mul_(-grad_out)                 # engine gradients are d(-elbo)/dtheta
+        e.flat.deliver(tmp)
+        return None, None
+
+
+class GenerativeModel(lamp.modules.BaseModule):
+
+    def __init__(self, f, g, gp, writer=None, *, dtype, device):
+        super().__init__()
+        self.writer = writer
+        self.f = f
+        self.g = g
+        self.gp = gp
+        self.encoder = None
+        self.q_z = torch.nn.ModuleDict()
+        self.q_X = torch.nn.ModuleDict()
+        self._dtype = dtype
+        self._device = device
+        self._datasets = dict()
+        self.VO = None
+        self.disable_elbo_vo = False
+        self.disable_elbo_supervised = False
+        self.disable_elbo_unsupervised = False
+        self.manual_logging = False
+        self.manual_log = {'elbo_supervised': [], 'elbo_unsupervised': [], 'elbo_vo': []}
+        self._independent_X = gp.independent_X
+        self.config = {'reconstruct_log_eff_property': True}
+        self._tensorboard_logging_interval = 1
+        self.preprocess_y_fct = None
+        self._flat = None
+
+    # ------------------------------------------------------------ plumbing
+    def set(self, ckey, value):
+        if ckey not in self.config:
+            raise KeyError('{} is not a valid property for the generative model'.format(ckey))
+        self.config[ckey] = value
+
+    @property
+    def tensorboard_logging_interval(self):
+        return self._tensorboard_logging_interval
+
+    @tensorboard_logging_interval.setter
+    def tensorboard_logging_interval(self, value):
+        assert isinstance(value, int) and value > 0
+        self._tensorboard_logging_interval = value
+
+    def _add_scalar(self, tag, value, global_step):
+        if self.writer is not None and np.mod(global_step, self._tensorboard_logging_interval) == 0:
+            self.writer.add_scalar(tag, value, global_step=global_step)
+
+    @property
+    def datasets(self):
+        return self._datasets
+
+    @property
+    def dtype(self):
+        return self._dtype
+
+    @property
+    def device(self):
+        return self._device
+
+    @property
+    def dim_effective_property(self):
+        return self.g.dim_effective_property
+
+    @property
+    def dim_y(self):
+        return self.g.dim_out
+
+    @property
+    def dim_latent(self):
+        return self.f.dim_latent
+
+    def register_encoder(self, encoder):
+        self.encoder = encoder
+
+    def init_by_encoder(self, encoder):
+        for qz in self.q_z.values():
+            qz.init_by_encoder(encoder)
+
+    def get_encoder_decoder_states(self):
+        if self.encoder is None:
+            raise RuntimeError('Encoder is not set - cannot return encoder state')
+        return self.encoder.state(), self.f.state()
+
+    def set_encoder_decoder_states(self, results):
+        if self.encoder is None:
+            raise Exception('The encoder is not set')
+        self.encoder.load(results.encoder_state)
+        self.f.load(results.decoder_state)
+
+    # ------------------------------------------------------------ datasets
+    def register_supervised_data(self, dataset):
+        X = dataset.get('X')
+        self.q_z['supervised'] = VariationalApproximation(self.dim_latent, X.shape[0], X=X)
+        if self._independent_X:
+            self.q_X['supervised'] = VariationalApproximation(self.dim_effective_property, X.shape[0], X=X)
+        self._datasets['supervised'] = dataset
+        self._flat = None
+
+    def register_unsupervised_data(self, dataset, create_variational_approximation=True):
+        if create_variational_approximation:
+            X = dataset.get('X')
+            self.q_z['unsupervised'] = VariationalApproximation(self.dim_latent, X.shape[0], X=X)
+        self._datasets['unsupervised'] = dataset
+        self._flat = None
+
+    def register_virtual_observables(self, dataset, VO):
+        X = dataset.get('X')
+        self.q_z['vo'] = VariationalApproximation(self.dim_latent, X.shape[0], X=X)
+        if self._independent_X:
+            self.q_X['vo'] = VariationalApproximation(self.dim_effective_property, X.shape[0], X=X)
+        self.VO = VO
+        self._datasets['vo'] = dataset
+        self._flat = None
+
+    def register_datasets(self, datasets, VO=None, create_unsupervised_variational_approximation=True):
+        if datasets.get('supervised'):
+            self.register_supervised_data(datasets['supervised'])
+        if datasets.get('unsupervised'):
+            self.register_unsupervised_data(datasets['unsupervised'],
+                                            create_variational_approximation=create_unsupervised_variational_approximation)
+        if datasets.get('vo'):
+            if VO is None:
+                raise ValueError('If datasets contains vo, need to pass virtual ensemble')
+            self.register_virtual_observables(datasets['vo'], VO)
+
+    # ------------------------------------------------------------ native
+    def native_flat(self):
+        """Flatten every parameter into one device buffer (shared first, per-sample q last)."""
+        params = list(self.named_parameters())
+        if self._flat is None or not all(self._flat.owns(p) for _, p in params) or \
+                len(params) != len(self._flat.params):
+            dev = params[0][1].device
+            self._flat = FlatParameters(params, dev, shared_prefixes=SHARED_PREFIXES)
+            set_flat(self, self._flat)
+        return self._flat
+
+    def _elbo_engine(self, B_u, N_s, normalize):
+        flat = self.native_flat()
+        return engine_for(self, ('elbo', B_u, N_s, bool(normalize), id(flat)),
+                          lambda: ElboEngine(self, B_u, N_s, normalize=normalize))
+
+    def _run_engine(self, engine, X_u=None, X_s=None, Y=None, F=None, eps=None):
+        if eps is None:
+            engine.eps_z().normal_()
+            if engine.N_s > 0:
+                engine.eps_x().normal_()
+        else:
+            engine.eps_z().copy_(eps[0])
+            if engine.N_s > 0:
+                engine.eps_x().copy_(eps[1])
+        engine.bind(X_u=X_u, X_s=X_s, Y=Y, F=F)
+        return _ElboFunction.apply(anchor(self, engine.flat.P.device), engine)
+
+    def _log_terms(self, engine, step, prefix_map=None):
+        if self.writer is None or np.mod(step, self._tensorboard_logging_interval) != 0:
+            return
+        for k, v in engine.terms().items():
+            self.writer.add_scalar('objective/' + k, v, global_step=step)
+
+    # ------------------------------------------------------------ ELBO
+    def elbo(self, step, vo_holdoff=False, disable_vo=False, armortized_bs=None, normalize=False, l1_penalty=None,
+             l2_penalty=None, eps=None):
+        """Reference generative.py:247-287.  ``eps`` optionally injects the
+        reparametrisation noise as (eps_z [B_u + N_s, d_z], eps_X [N_s, n_T])."""
+        assert not (armortized_bs is not None and self.encoder is None)
+        if l1_penalty is not None:
+            raise NotImplementedError
+        if self._datasets.get('vo') and not disable_vo and not self.disable_elbo_vo:
+            raise NotImplementedError('the virtual-observable ELBO term is not yet on the native path')
+        X_u = None
+        B_u = 0
+        if self._datasets.get('unsupervised') and not self.disable_elbo_unsupervised:
+            if self.encoder is None:
+                raise NotImplementedError('non-armortized unsupervised q_z is not on the native path')
+            if armortized_bs is None:
+                raise ValueError('If armortized learning is used, we need to provide a batch size')
+            X_u = self._datasets['unsupervised'].get('X', random_subset=armortized_bs).detach().contiguous()
+            B_u = X_u.shape[0]
+        N_s = 0
+        X_s = Y = F = None
+        if self._datasets.get('supervised') and not self.disable_elbo_supervised:
+            if not self._independent_X:
+                raise NotImplementedError('the lockX supervised variant is not on the native path')
+            ds = self._datasets['supervised']
+            X_s, Y, F = ds.get('X').detach(), ds.get('Y').detach(), ds.get('F_ROM_BC').detach()
+            if self.preprocess_y_fct is not None:
+                raise NotImplementedError('preprocess_y_fct is not supported on the native path')
+            N_s = X_s.shape[0]
+        if B_u == 0 and N_s == 0:
+            return 0
+        engine = self._elbo_engine(B_u, N_s, normalize)
+        elbo = self._run_engine(engine, X_u, X_s, Y, F, eps)
+        if l2_penalty is not None:
+            pen = sum(torch.norm(p) for p in self.f.parameters())
+            if self.encoder is not None:
+                pen = pen + sum(torch.norm(p) for p in self.encoder.parameters())
+            elbo = elbo - l2_penalty * pen
+            self._add_scalar('elbo_l2_penalty', pen, step)
+        if self.writer is not None:
+            self._log_terms(engine, step)
+            self._add_scalar('elbo', elbo, step)
+        return elbo
+
+    def elbo_unsupervised_armortized(self, X, step, encoder=None, return_reconstruction=False, normalize=False):
+        if self.disable_elbo_unsupervised:
+            return 0
+        if self.encoder is None:
+            raise RuntimeError('Cannot use armortized inference, if encoder has not been registered')
+        if 'unsupervised' in self.q_z:
+            raise RuntimeError("Cannot use armortized inference, if q_z['unsupervised'] has been registered")
+        if return_reconstruction:
+            raise NotImplementedError
+        engine = self._elbo_engine(X.shape[0], 0, normalize)
+        return self._run_engine(engine, X_u=X.detach().contiguous().float())
+
+    def elbo_supervised(self, X, Y, step, normalize=False):
+        if self.disable_elbo_supervised:
+            return 0
+        if not self._independent_X:
+            raise NotImplementedError('the lockX supervised variant is not on the native path')
+        F = self._datasets['supervised'].get('F_ROM_BC').detach()
+        engine = self._elbo_engine(0, X.shape[0], normalize)
+        return self._run_engine(engine, X_s=X.detach(), Y=Y.detach(), F=F)
+
+    def random_field_likelihood(self, predict, target):
+        if not isinstance(predict, tuple):
+            raise NotImplementedError('binary fields are not on the ELBO path')
+        if self.config['reconstruct_log_eff_property']:
+            return DiagonalGaussianLogLikelihood(target, predict[0], 2 * predict[1])
+        return DiagonalGaussianLogLikelihood(torch.exp(target), torch.exp(predict[0]), 2 * predict[1])
+
+    @torch.no_grad()
+    def record(self, step):
+        if self.writer is None:
+            return
+        if self._independent_X and 'supervised' in self.q_X:
+            self.writer.add_scalar('Monitoring/logEffProp_sup_mean', torch.mean(self.q_X['supervised'].mean), step)
+            self.writer.add_scalar('Monitoring/logEffProp_sup_sigma', torch.mean(self.q_X['supervised'].logsigma),
+                                   step)
+        self.writer.add_scalar('Monitoring/S_avg_precisions', torch.mean(torch.exp(-2 * self.g.logsigmas_y)), step)
+
+    def extract_discriminative_model(self, *, FromLatentEncoding, duplicate, encoder=None):
+        if not duplicate:
+            raise RuntimeError('We are only able to return duplicates')
+        enc = None if FromLatentEncoding else copy.deepcopy(encoder if encoder is not None else self.encoder)
+        return DiscriminativeModel(encoder=enc, gp=copy.deepcopy(self.gp.extract_deterministic_map(duplicate=True)),
+                                   g=copy.deepcopy(self.g), dim_latent=self.dim_latent)
+
+    def forward(self, X, Y):
+        raise NotImplementedError
+
+
+class DiscriminativeModel(lamp.modules.BaseModule):
+    """x -> (encoder) -> gp mean -> ROM (generative.py:605-644)."""
+
+    def __init__(self, encoder, gp, g, dim_latent):
+        super().__init__()
+        if gp is None or g is None:
+            raise ValueError
+        self._encoder = encoder
+        self._gp = gp
+        self._g = g
+        self._dim_latent = dim_latent
+
+    def curtail(self):
+        self._encoder = None
+
+    def forward(self, x, F):
+        if self._encoder is not None:
+            x = self._encoder(x)[0]
+        return self._g(self._gp(x), F=F)

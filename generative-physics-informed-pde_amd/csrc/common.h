@@ -1,0 +1,92 @@
+// Shared device helpers for libgpi_hip.so (gfx950, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+#include "gpi.h"
+
+#define GPI_LOG2PI 1.8378770664093453f
+
+#define GPI_CHECK_LAUNCH()                                   \
+    do {                                                     \
+        if (hipGetLastError() != hipSuccess) return GPI_ERR_LAUNCH; \
+    } while (0)
+
+namespace gpi {
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Block-wide sum of NV per-thread values into red[0..NV) (caller syncs after).
+// scratch: >= NV * (blockDim/64) floats.
+template <int NV>
+__device__ __forceinline__ void block_sum(float (&v)[NV], float* scratch, float* red) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        float s = wave_sum(v[i]);
+        if (lane == 0) scratch[i * nw + wid] = s;
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < NV) {
+        float s = 0.f;
+        for (int w = 0; w < nw; ++w) s += scratch[threadIdx.x * nw + w];
+        red[threadIdx.x] = s;
+    }
+}
+
+__device__ __forceinline__ int floordiv2(int x) { return x >> 1; }   // arithmetic shift = floor
+__device__ __forceinline__ int ceildiv2(int x) { return -((-x) >> 1); }
+
+__device__ __forceinline__ int group_of(const gpi_groups& g, int s) {
+    int k = 0;
+    while (k + 1 < g.n_groups && s >= g.start[k + 1]) ++k;
+    return k;
+}
+
+// train-mode BN coefficients from fp64 sums (biased variance, torch semantics)
+__device__ __forceinline__ void bn_mean_invstd(const gpi_stat& st, double n, float eps, float& mean,
+                                               float& invstd) {
+    double m = st.sum / n;
+    double var = st.sumsq / n - m * m;
+    if (var < 0.0) var = 0.0;
+    mean = (float)m;
+    invstd = (float)(1.0 / sqrt(var + (double)eps));
+}
+
+// ---------------------------------------------------------------- Philox4x32-10
+struct uint4_ { uint32_t x, y, z, w; };
+
+__device__ __forceinline__ uint4_ philox(uint64_t ctr_lo, uint64_t ctr_hi, uint64_t key) {
+    uint32_t c0 = (uint32_t)ctr_lo, c1 = (uint32_t)(ctr_lo >> 32);
+    uint32_t c2 = (uint32_t)ctr_hi, c3 = (uint32_t)(ctr_hi >> 32);
+    uint32_t k0 = (uint32_t)key, k1 = (uint32_t)(key >> 32);
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+        uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+        uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+        uint32_t n1 = (uint32_t)p1;
+        uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        uint32_t n3 = (uint32_t)p0;
+        c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return {c0, c1, c2, c3};
+}
+
+__device__ __forceinline__ float u01(uint32_t x) {   // (0, 1]
+    return ((float)(x >> 8) + 1.0f) * (1.0f / 16777216.0f);
+}
+
+}  // namespace gpi

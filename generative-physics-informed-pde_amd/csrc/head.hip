@@ -1,0 +1,336 @@
+// Dense (per-sample) part of the ELBO and its backward.
+//
+// One workgroup per sample runs the whole per-sample chain in LDS:
+//   encoder FC -> ReLU -> (mu, logsigma) heads      (Encoder.py:175-182, codec.py:495-504)
+//   z = mu + exp(logsigma) eps, KL                  (bottleneck/utils.py:216-219,246-248)
+//   or z from q_z, KL                               (components.py:167-172,192-193)
+//   decoder latent map                              (Decoder.py:213,293)
+//   gp(z), X~ = q_X sample, log-lik, entropy        (generative.py:464-478, components.py:195-197,224-229)
+// The backward writes per-sample deltas; the shared-weight gradients
+// (sum over samples of delta (x) input) are formed by gpi_outer_gemm, the
+// per-sample variational parameters' gradients are written directly.
+#include "common.h"
+
+using namespace gpi;
+
+namespace {
+
+constexpr int HT = 128;     // threads per sample
+constexpr int VMAX = 512;   // max vector length
+
+__device__ __forceinline__ float block_sum128(float v, float* scratch) {
+    v = wave_sum(v);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane == 0) scratch[wid] = v;
+    __syncthreads();
+    return scratch[0] + scratch[1];
+}
+
+// y[j] = b[j] + sum_k W[j*K + k] x[k]
+__device__ __forceinline__ void matvec(const float* __restrict__ W, const float* __restrict__ b, const float* x,
+                                       int J, int K, float* y) {
+    for (int j = threadIdx.x; j < J; j += HT) {
+        float a = b ? b[j] : 0.f;
+        const float* w = W + (int64_t)j * K;
+        for (int k = 0; k < K; ++k) a = fmaf(w[k], x[k], a);
+        y[j] = a;
+    }
+}
+
+// y[k] (+)= sum_j W[j*K + k] d[j]
+__device__ __forceinline__ void matvec_t(const float* __restrict__ W, const float* d, int J, int K, float* y,
+                                         bool accumulate) {
+    for (int k = threadIdx.x; k < K; k += HT) {
+        float a = accumulate ? y[k] : 0.f;
+        for (int j = 0; j < J; ++j) a = fmaf(W[(int64_t)j * K + k], d[j], a);
+        y[k] = a;
+    }
+}
+
+__global__ __launch_bounds__(HT) void head_fwd_kernel(gpi_head_desc d, const float* __restrict__ P, float* ws) {
+    __shared__ float v0[VMAX], v1[VMAX], v2[VMAX], v3[VMAX];
+    __shared__ float scratch[4];
+    const int s = blockIdx.x;
+    const int tid = threadIdx.x;
+    const bool enc = s < d.n_enc;
+    const int q = s - d.n_enc;
+    const int dz = d.d_z;
+    float* z = v2;
+
+    if (enc) {
+        if (d.flags & GPI_HEAD_ENC) {
+            const float* f = ws + d.feat + (int64_t)s * d.d_feat;
+            for (int k = tid; k < d.d_feat; k += HT) v0[k] = f[k];
+            __syncthreads();
+            matvec(P + d.fc_w, P + d.fc_b, v0, d.d_feat, d.d_feat, v1);
+            __syncthreads();
+            for (int k = tid; k < d.d_feat; k += HT) {
+                ws[d.hpre + (int64_t)s * d.d_feat + k] = v1[k];
+                v1[k] = fmaxf(v1[k], 0.f);
+            }
+            __syncthreads();
+            matvec(P + d.mu_w, P + d.mu_b, v1, dz, d.d_feat, v0);              // mu
+            matvec(P + d.ls_w, P + d.ls_b, v1, dz, d.d_feat, v3);              // logsigma
+            __syncthreads();
+            for (int k = tid; k < dz; k += HT) {
+                ws[d.zmu + (int64_t)s * dz + k] = v0[k];
+                ws[d.zls + (int64_t)s * dz + k] = v3[k];
+            }
+        } else {
+            for (int k = tid; k < dz; k += HT) {
+                v0[k] = ws[d.zmu + (int64_t)s * dz + k];
+                v3[k] = ws[d.zls + (int64_t)s * dz + k];
+            }
+        }
+        __syncthreads();
+        if (d.flags & GPI_HEAD_REPARAM) {
+            float kl = 0.f;
+            for (int k = tid; k < dz; k += HT) {
+                const float mu = v0[k], ls = v3[k];
+                const float e = expf(ls);
+                const float zz = fmaf(e, ws[d.eps_z + (int64_t)s * dz + k], mu);
+                z[k] = zz;
+                ws[d.z + (int64_t)s * dz + k] = zz;
+                kl += 1.f + 2.f * ls - mu * mu - e * e;
+            }
+            kl = block_sum128(kl, scratch);
+            if (tid == 0) atomicAdd(d.terms + 0, -0.5 * (double)kl);
+        } else {
+            for (int k = tid; k < dz; k += HT) z[k] = ws[d.z + (int64_t)s * dz + k];
+        }
+    } else {
+        if (d.flags & GPI_HEAD_QZ) {
+            float kl = 0.f;
+            for (int k = tid; k < dz; k += HT) {
+                const float mu = P[d.qz_mu + (int64_t)q * dz + k], ls = P[d.qz_ls + (int64_t)q * dz + k];
+                const float e = expf(ls);
+                const float zz = fmaf(e, ws[d.eps_z + (int64_t)s * dz + k], mu);
+                z[k] = zz;
+                ws[d.z + (int64_t)s * dz + k] = zz;
+                kl += 1.f + 2.f * ls - mu * mu - e * e;
+            }
+            kl = block_sum128(kl, scratch);
+            if (tid == 0) atomicAdd(d.terms + 1, -0.5 * (double)kl);
+        } else {
+            for (int k = tid; k < dz; k += HT) z[k] = ws[d.z + (int64_t)s * dz + k];
+        }
+    }
+    __syncthreads();
+    if (d.flags & GPI_HEAD_LATENT) {
+        float* lat = ws + d.lat + (int64_t)s * d.d_lat;
+        for (int j = tid; j < d.d_lat; j += HT) {
+            float a = P[d.lat_b + j];
+            const float* w = P + d.lat_w + (int64_t)j * dz;
+            for (int k = 0; k < dz; ++k) a = fmaf(w[k], z[k], a);
+            lat[j] = a;
+        }
+    }
+    if (!enc && (d.flags & GPI_HEAD_GP)) {
+        float lx = 0.f, ent = 0.f;
+        for (int t = tid; t < d.d_x; t += HT) {
+            float a = P[d.gp_b + t];
+            const float* w = P + d.gp_w + (int64_t)t * dz;
+            for (int k = 0; k < dz; ++k) a = fmaf(w[k], z[k], a);
+            const int64_t qi = (int64_t)q * d.d_x + t;
+            const float lsq = P[d.qx_ls + qi];
+            const float xs = fmaf(expf(lsq), ws[d.eps_x + qi], P[d.qx_mu + qi]);
+            ws[d.mux + qi] = a;
+            ws[d.xs + qi] = xs;
+            const float gls = P[d.gp_ls + t];
+            const float r = xs - a;
+            lx += -0.5f * (2.f * gls + r * r * expf(-2.f * gls) + GPI_LOG2PI);
+            ent += lsq;
+        }
+        lx = block_sum128(lx, scratch);
+        ent = block_sum128(ent, scratch);
+        if (tid == 0) {
+            atomicAdd(d.terms + 2, (double)lx);
+            atomicAdd(d.terms + 3, (double)ent);
+        }
+    }
+}
+
+__global__ __launch_bounds__(HT) void head_bwd_kernel(gpi_head_desc d, const float* __restrict__ P, float* ws,
+                                                      double* gacc) {
+    __shared__ float v0[VMAX], v1[VMAX], v2[VMAX], v3[VMAX];
+    const int s = blockIdx.x;
+    const int tid = threadIdx.x;
+    const bool enc = s < d.n_enc;
+    const int q = s - d.n_enc;
+    const int dz = d.d_z;
+    float* dz_ = v0;   // dJ/dz
+
+    // latent map: dz = lat_w^T glat
+    if (d.flags & GPI_HEAD_LATENT) {
+        const float* gl = ws + d.glat + (int64_t)s * d.d_lat;
+        for (int j = tid; j < d.d_lat; j += HT) v1[j] = gl[j];
+        __syncthreads();
+        matvec_t(P + d.lat_w, v1, d.d_lat, dz, dz_, false);
+    } else {
+        for (int k = tid; k < dz; k += HT) dz_[k] = ws[d.gz + (int64_t)s * dz + k];
+    }
+    __syncthreads();
+
+    if (!enc && (d.flags & GPI_HEAD_GP)) {
+        for (int t = tid; t < d.d_x; t += HT) {
+            const int64_t qi = (int64_t)q * d.d_x + t;
+            const float gls = P[d.gp_ls + t];
+            const float e2 = expf(-2.f * gls);
+            const float xs = ws[d.xs + qi], mux = ws[d.mux + qi];
+            const float r = xs - mux;
+            const float gm = -d.lx_scale * r * e2;            // dJ/dmu_X
+            v2[t] = gm;
+            ws[d.gmux + qi] = gm;
+            atomicAdd(gacc + d.gp_ls + t, (double)(d.lx_scale * (1.f - r * r * e2)));
+            const float dxs = ws[d.gxs + qi] + d.lx_scale * r * e2;   // dJ/dX~
+            const float lsq = P[d.qx_ls + qi];
+            gacc[d.qx_mu + qi] += (double)dxs;
+            gacc[d.qx_ls + qi] += (double)(dxs * expf(lsq) * ws[d.eps_x + qi] - d.lx_scale);
+        }
+        __syncthreads();
+        matvec_t(P + d.gp_w, v2, d.d_x, dz, dz_, true);
+        __syncthreads();
+    }
+
+    if (!enc) {
+        if (d.flags & GPI_HEAD_QZ) {
+            for (int k = tid; k < dz; k += HT) {
+                const int64_t qi = (int64_t)q * dz + k;
+                const float mu = P[d.qz_mu + qi], ls = P[d.qz_ls + qi];
+                const float e = expf(ls);
+                gacc[d.qz_mu + qi] += (double)(dz_[k] + d.kl_scale_q * mu);
+                gacc[d.qz_ls + qi] += (double)(dz_[k] * e * ws[d.eps_z + (int64_t)s * dz + k] +
+                                               d.kl_scale_q * (e * e - 1.f));
+            }
+        }
+        return;
+    }
+
+    // encoder samples: reparametrisation + KL
+    for (int k = tid; k < dz; k += HT) {
+        float dmu = dz_[k], dls = 0.f;
+        const float mu = ws[d.zmu + (int64_t)s * dz + k], ls = ws[d.zls + (int64_t)s * dz + k];
+        if (d.flags & GPI_HEAD_REPARAM) {
+            const float e = expf(ls);
+            dls = dz_[k] * e * ws[d.eps_z + (int64_t)s * dz + k] + d.kl_scale_enc * (e * e - 1.f);
+            dmu += d.kl_scale_enc * mu;
+        } else {
+            dls = ws[d.dzls + (int64_t)s * dz + k];   // caller-provided d/dlogsigma
+        }
+        v1[k] = dmu;
+        v2[k] = dls;
+        ws[d.dzmu + (int64_t)s * dz + k] = dmu;
+        ws[d.dzls + (int64_t)s * dz + k] = dls;
+    }
+    __syncthreads();
+    if (!(d.flags & GPI_HEAD_ENC)) return;
+    // heads: dh = mu_w^T dmu + ls_w^T dls ; ReLU ; FC
+    matvec_t(P + d.mu_w, v1, dz, d.d_feat, v3, false);
+    __syncthreads();
+    matvec_t(P + d.ls_w, v2, dz, d.d_feat, v3, true);
+    __syncthreads();
+    for (int k = tid; k < d.d_feat; k += HT) {
+        const float hp = ws[d.hpre + (int64_t)s * d.d_feat + k];
+        const float g = hp > 0.f ? v3[k] : 0.f;
+        v3[k] = g;
+        ws[d.dhpre + (int64_t)s * d.d_feat + k] = g;
+    }
+    __syncthreads();
+    matvec_t(P + d.fc_w, v3, d.d_feat, d.d_feat, v0, false);
+    __syncthreads();
+    for (int k = tid; k < d.d_feat; k += HT) ws[d.gfeat + (int64_t)s * d.d_feat + k] = v0[k];
+}
+
+struct GemmArgs {
+    gpi_gemm_item it[GPI_MAX_GEMM_ITEMS];
+    int32_t first_block[GPI_MAX_GEMM_ITEMS + 1];
+    int32_t tiles_n[GPI_MAX_GEMM_ITEMS];
+    int32_t n;
+};
+
+// C (M x (N+1)) tile 16 x 16 per workgroup; column N is the bias (B = 1).
+// item.flags bit 0: apply ReLU to B (h = relu(hpre)).
+__global__ __launch_bounds__(256) void outer_gemm_kernel(GemmArgs a, const float* __restrict__ ws, double* gacc) {
+    __shared__ float As[32][17], Bs[32][17];
+    int k = 0;
+    while (k + 1 < a.n && (int)blockIdx.x >= a.first_block[k + 1]) ++k;
+    const gpi_gemm_item it = a.it[k];
+    const int local = blockIdx.x - a.first_block[k];
+    const int tm = local / a.tiles_n[k], tn = local - tm * a.tiles_n[k];
+    const int m0 = tm * 16, n0 = tn * 16;
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+    const bool relu_b = it.flags & 1;
+    float acc = 0.f;
+    for (int sb = 0; sb < it.S; sb += 32) {
+        for (int e = threadIdx.x; e < 32 * 16; e += 256) {
+            const int r = e >> 4, cc = e & 15;
+            const int s = sb + r;
+            float av = 0.f, bv = 0.f;
+            if (s < it.S) {
+                if (m0 + cc < it.M) av = ws[it.a_off + (int64_t)s * it.lda + m0 + cc];
+                const int n = n0 + cc;
+                if (n < it.N) {
+                    bv = ws[it.b_off + (int64_t)s * it.ldb + n];
+                    if (relu_b) bv = fmaxf(bv, 0.f);
+                } else if (n == it.N) {
+                    bv = 1.f;
+                }
+            }
+            As[r][cc] = av;
+            Bs[r][cc] = bv;
+        }
+        __syncthreads();
+#pragma unroll 8
+        for (int r = 0; r < 32; ++r) acc = fmaf(As[r][ty], Bs[r][tx], acc);
+        __syncthreads();
+    }
+    const int m = m0 + ty, n = n0 + tx;
+    if (m < it.M) {
+        if (n < it.N) gacc[it.c_off + (int64_t)m * it.N + n] += (double)acc;
+        else if (n == it.N && it.bias_off >= 0) gacc[it.bias_off + m] += (double)acc;
+    }
+}
+
+bool head_ok(const gpi_head_desc* d) {
+    return d && d->d_z > 0 && d->d_z <= VMAX && d->d_feat <= VMAX && d->d_lat <= VMAX && d->d_x <= VMAX &&
+           d->n_enc >= 0 && d->n_q >= 0 && (d->n_enc + d->n_q) > 0 && d->terms;
+}
+
+}  // namespace
+
+extern "C" int gpi_head_forward(const gpi_head_desc* d, const float* params, float* ws, void* stream) {
+    if (!head_ok(d) || !params || !ws) return GPI_ERR_ARG;
+    hipLaunchKernelGGL(head_fwd_kernel, dim3(d->n_enc + d->n_q), dim3(HT), 0, (hipStream_t)stream, *d, params, ws);
+    GPI_CHECK_LAUNCH();
+    return GPI_OK;
+}
+
+extern "C" int gpi_head_backward(const gpi_head_desc* d, const float* params, float* ws, double* gacc,
+                                 void* stream) {
+    if (!head_ok(d) || !params || !ws || !gacc) return GPI_ERR_ARG;
+    hipLaunchKernelGGL(head_bwd_kernel, dim3(d->n_enc + d->n_q), dim3(HT), 0, (hipStream_t)stream, *d, params, ws,
+                       gacc);
+    GPI_CHECK_LAUNCH();
+    return GPI_OK;
+}
+
+extern "C" int gpi_outer_gemm(const gpi_gemm_item* items, int n_items, const float* ws, double* gacc,
+                              void* stream) {
+    if (!items || n_items < 0 || n_items > GPI_MAX_GEMM_ITEMS || !ws || !gacc) return GPI_ERR_ARG;
+    if (n_items == 0) return GPI_OK;
+    GemmArgs a;
+    a.n = n_items;
+    int nb = 0;
+    for (int k = 0; k < n_items; ++k) {
+        a.it[k] = items[k];
+        a.first_block[k] = nb;
+        const int tm = (items[k].M + 15) / 16, tn = (items[k].N + 1 + 15) / 16;
+        a.tiles_n[k] = tn;
+        nb += tm * tn;
+    }
+    a.first_block[n_items] = nb;
+    hipLaunchKernelGGL(outer_gemm_kernel, dim3(nb), dim3(256), 0, (hipStream_t)stream, a, ws, gacc);
+    GPI_CHECK_LAUNCH();
+    return GPI_OK;
+}

@@ -1,0 +1,165 @@
+// Step plumbing kernels: gradient finalisation, flat Adam, device RNG.
+#include "common.h"
+
+using namespace gpi;
+
+namespace {
+
+__global__ __launch_bounds__(256) void grad_finalize_kernel(const double* __restrict__ gacc, float* grad, int64_t n,
+                                                            int accumulate, int64_t* step) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (step && i == 0) *step += 1;
+    if (i >= n) return;
+    const float g = (float)gacc[i];
+    grad[i] = accumulate ? grad[i] + g : g;
+}
+
+// torch.optim.Adam single-tensor math (torch/optim/adam.py, defaults:
+// no weight decay, no amsgrad, maximize=False).
+__global__ __launch_bounds__(256) void adam_kernel(gpi_adam_desc d) {
+    const int64_t t = *d.step;
+    const float lr = *d.lr;
+    const double bc1 = 1.0 - pow((double)d.beta1, (double)t);
+    const double bc2 = 1.0 - pow((double)d.beta2, (double)t);
+    const float step_size = (float)((double)lr / bc1);
+    const float bc2_sqrt = (float)sqrt(bc2);
+    const float w = 1.f - d.beta1;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < d.n; i += (int64_t)gridDim.x * 256) {
+        const float g = d.g[i];
+        float m = d.m[i];
+        m = m + w * (g - m);                                   // lerp_(grad, 1 - beta1)
+        float v = d.v[i] * d.beta2 + (1.f - d.beta2) * g * g;  // mul_(beta2).addcmul_(g, g, 1 - beta2)
+        d.m[i] = m;
+        d.v[i] = v;
+        const float denom = sqrtf(v) / bc2_sqrt + d.eps;
+        d.p[i] = d.p[i] - step_size * (m / denom);
+    }
+}
+
+__global__ __launch_bounds__(256) void randn_kernel(float* out, int64_t n, uint64_t seed, const uint64_t* offset,
+                                                    uint64_t sub) {
+    const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;   // one Philox block -> 4 normals
+    if (q * 4 >= n) return;
+    const uint64_t base = offset ? *offset : 0;
+    const uint4_ r = philox(base + (uint64_t)q, sub, seed);
+    const float u0 = u01(r.x), u1 = u01(r.y), u2 = u01(r.z), u3 = u01(r.w);
+    const float r0 = sqrtf(-2.f * logf(u0)), r1 = sqrtf(-2.f * logf(u2));
+    const float t0 = 6.2831853071795864f * u1, t1 = 6.2831853071795864f * u3;
+    float v[4] = {r0 * cosf(t0), r0 * sinf(t0), r1 * cosf(t1), r1 * sinf(t1)};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (q * 4 + k < n) out[q * 4 + k] = v[k];
+}
+
+__global__ void rng_advance_kernel(uint64_t* offset, uint64_t by) { *offset += by; }
+
+// random subset: sort (random key, index) pairs with a bitonic network in LDS
+__global__ __launch_bounds__(1024) void subset_kernel(int32_t* out, int32_t n, int32_t k, uint64_t seed,
+                                                      const uint64_t* offset, uint64_t sub, int32_t npow2) {
+    extern __shared__ __attribute__((aligned(16))) unsigned long long keys[];
+    const uint64_t base = offset ? *offset : 0;
+    for (int i = threadIdx.x; i < npow2; i += 1024) {
+        unsigned long long key;
+        if (i < n) {
+            const uint4_ r = philox(base + (uint64_t)i, sub, seed);
+            key = ((unsigned long long)r.x << 32) | (unsigned)i;
+        } else {
+            key = ~0ull;
+        }
+        keys[i] = key;
+    }
+    __syncthreads();
+    for (int size = 2; size <= npow2; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int i = threadIdx.x; i < npow2; i += 1024) {
+                const int j = i ^ stride;
+                if (j > i) {
+                    const bool up = (i & size) == 0;
+                    const unsigned long long a = keys[i], b = keys[j];
+                    if ((a > b) == up) { keys[i] = b; keys[j] = a; }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (int i = threadIdx.x; i < k; i += 1024) out[i] = (int32_t)(keys[i] & 0xffffffffu);
+}
+
+}  // namespace
+
+extern "C" int gpi_version(void) { return 1; }
+
+extern "C" int gpi_struct_sizes(int64_t* out, int n) {
+    const int64_t s[] = {(int64_t)sizeof(gpi_stat), (int64_t)sizeof(gpi_groups), (int64_t)sizeof(gpi_conv_desc),
+                         (int64_t)sizeof(gpi_codec_ctx), (int64_t)sizeof(gpi_reduce_item), (int64_t)sizeof(gpi_head_desc),
+                         (int64_t)sizeof(gpi_gemm_item), (int64_t)sizeof(gpi_rom_desc), (int64_t)sizeof(gpi_residual_desc),
+                         (int64_t)sizeof(gpi_adam_desc)};
+    const int k = (int)(sizeof(s) / sizeof(s[0]));
+    if (!out || n < k) return GPI_ERR_ARG;
+    for (int i = 0; i < k; ++i) out[i] = s[i];
+    return k;
+}
+
+extern "C" const char* gpi_error_string(int code) {
+    switch (code) {
+        case GPI_OK: return "ok";
+        case GPI_ERR_ARG: return "invalid argument";
+        case GPI_ERR_LAUNCH: return "kernel launch failed";
+        case GPI_ERR_UNSUPPORTED: return "unsupported configuration";
+        default: return "unknown error";
+    }
+}
+
+extern "C" int gpi_grad_finalize(const double* gacc, float* grad, int64_t n, int accumulate, int64_t* step,
+                                 void* stream) {
+    if (!gacc || !grad || n < 0) return GPI_ERR_ARG;
+    const int64_t nb = n > 0 ? (n + 255) / 256 : 1;
+    hipLaunchKernelGGL(grad_finalize_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, gacc, grad, n,
+                       accumulate, step);
+    GPI_CHECK_LAUNCH();
+    return GPI_OK;
+}
+
+extern "C" int gpi_adam(const gpi_adam_desc* d, void* stream) {
+    if (!d || !d->p || !d->g || !d->m || !d->v || !d->lr || !d->step || d->n < 0) return GPI_ERR_ARG;
+    if (d->n == 0) return GPI_OK;
+    int64_t nb = (d->n + 255) / 256;
+    if (nb > 2048) nb = 2048;
+    hipLaunchKernelGGL(adam_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, *d);
+    GPI_CHECK_LAUNCH();
+    return GPI_OK;
+}
+
+extern "C" int gpi_randn(float* out, int64_t n, uint64_t seed, const uint64_t* offset, uint64_t sub, void* stream) {
+    if (!out || n < 0) return GPI_ERR_ARG;
+    if (n == 0) return GPI_OK;
+    const int64_t nq = (n + 3) / 4;
+    hipLaunchKernelGGL(randn_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, (hipStream_t)stream, out, n,
+                       seed, offset, sub);
+    GPI_CHECK_LAUNCH();
+    return GPI_OK;
+}
+
+extern "C" int gpi_rng_advance(uint64_t* offset, uint64_t by, void* stream) {
+    if (!offset) return GPI_ERR_ARG;
+    hipLaunchKernelGGL(rng_advance_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, offset, by);
+    GPI_CHECK_LAUNCH();
+    return GPI_OK;
+}
+
+extern "C" int gpi_random_subset(int32_t* out, int32_t n, int32_t k, uint64_t seed, const uint64_t* offset,
+                                 uint64_t sub, void* stream) {
+    if (!out || n <= 0 || k < 0 || k > n || n > 16384) return GPI_ERR_ARG;
+    int32_t np2 = 1;
+    while (np2 < n) np2 <<= 1;
+    const size_t lds = sizeof(unsigned long long) * np2;
+    if (lds > 64 * 1024) {
+        if (hipFuncSetAttribute((const void*)subset_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+            hipSuccess)
+            return GPI_ERR_LAUNCH;
+    }
+    hipLaunchKernelGGL(subset_kernel, dim3(1), dim3(1024), lds, (hipStream_t)stream, out, n, k, seed, offset, sub,
+                       np2);
+    GPI_CHECK_LAUNCH();
+    return GPI_OK;
+}

@@ -1,0 +1,161 @@
+"""ctypes binding of libgpi_hip.so (include/gpi.h).
+
+The library is loaded after ``torch`` so that both share torch's HIP runtime
+(libamdhip64.so.7 is matched by soname).  There is no fallback: if the
+library is missing, or a kernel is requested without a GPU, the call raises.
+"""
+import ctypes as C
+import os
+
+import torch  # noqa: F401  (must be imported before the HIP library is loaded)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, 'libgpi_hip.so')
+
+GPI_MAX_GROUPS = 4
+GPI_MAX_CIN = 32
+GPI_MAX_COUT = 8
+GPI_MAX_REDUCE_ITEMS = 48
+GPI_MAX_GEMM_ITEMS = 12
+
+EPI_STORE, EPI_STORE_STATS, EPI_GAUSS_LOSS = 0, 1, 2
+HEAD_ENC, HEAD_REPARAM, HEAD_QZ, HEAD_LATENT, HEAD_GP = 0x01, 0x02, 0x04, 0x08, 0x10
+ROM_FORWARD, ROM_LOGLIK, ROM_BACKWARD = 0, 1, 2
+
+i32, i64, f32, u64 = C.c_int32, C.c_int64, C.c_float, C.c_uint64
+vp = C.c_void_p
+
+
+class Stat(C.Structure):
+    _fields_ = [('sum', C.c_double), ('sumsq', C.c_double), ('ssum', C.c_double), ('sxsum', C.c_double)]
+
+
+class Groups(C.Structure):
+    _fields_ = [('n_groups', i32), ('start', i32 * (GPI_MAX_GROUPS + 1))]
+
+
+class ConvDesc(C.Structure):
+    _fields_ = [('cin', i32), ('cout', i32), ('k', i32), ('stride', i32), ('pad', i32), ('upsample', i32),
+                ('h_in', i32), ('w_in', i32), ('h_out', i32), ('w_out', i32),
+                ('in_off', i64), ('in_ctot', i32), ('in_c0', i32), ('in_bn', i32), ('gin_accumulate', i32),
+                ('gamma_off', i64), ('beta_off', i64), ('in_stat', i64), ('w_off', i64),
+                ('out_off', i64), ('out_ctot', i32), ('out_c0', i32), ('out_stat', i64),
+                ('epilogue', i32), ('gout_mode', i32), ('gout_off', i64), ('gin_off', i64), ('wpart_off', i64)]
+
+
+class CodecCtx(C.Structure):
+    _fields_ = [('params', vp), ('ws', vp), ('stats', vp), ('gacc', vp), ('wpart', vp),
+                ('ext_in', vp), ('ext_idx', vp), ('ext_stride', i64),
+                ('tgt', vp * GPI_MAX_GROUPS), ('tgt_idx', vp * GPI_MAX_GROUPS),
+                ('loss_scale', f32 * GPI_MAX_GROUPS), ('loss_acc', vp), ('bn_eps', f32),
+                ('groups', Groups)]
+
+
+class ReduceItem(C.Structure):
+    _fields_ = [('part_off', i64), ('w_off', i64), ('blocks', i32), ('numel', i32)]
+
+
+class HeadDesc(C.Structure):
+    _fields_ = [('flags', i32), ('n_enc', i32), ('n_q', i32), ('d_feat', i32), ('d_z', i32), ('d_lat', i32),
+                ('d_x', i32), ('_pad', i32)] + \
+               [(n, i64) for n in ('fc_w', 'fc_b', 'mu_w', 'mu_b', 'ls_w', 'ls_b', 'lat_w', 'lat_b', 'gp_w', 'gp_b',
+                                   'gp_ls', 'qz_mu', 'qz_ls', 'qx_mu', 'qx_ls', 'feat', 'gfeat', 'hpre', 'zmu',
+                                   'zls', 'eps_z', 'z', 'gz', 'lat', 'glat', 'eps_x', 'xs', 'mux', 'gxs', 'gmux',
+                                   'dzmu', 'dzls', 'dhpre')] + \
+               [('kl_scale_enc', f32), ('kl_scale_q', f32), ('lx_scale', f32), ('_fpad', f32), ('terms', vp)]
+
+
+class GemmItem(C.Structure):
+    _fields_ = [('a_off', i64), ('b_off', i64), ('c_off', i64), ('bias_off', i64),
+                ('S', i32), ('M', i32), ('N', i32), ('lda', i32), ('ldb', i32), ('flags', i32)]
+
+
+class RomDesc(C.Structure):
+    _fields_ = [('nc', i32), ('refine', i32), ('n', i32), ('mode', i32), ('input_kappa', i32), ('_pad', i32),
+                ('x', vp), ('x_stride', i64), ('F', vp), ('mu_y', vp), ('Y', vp), ('logsig_y', vp),
+                ('loss_scale', f32), ('gx_accumulate', i32), ('dmu', vp), ('duc', vp), ('gx', vp), ('gx_stride', i64),
+                ('gacc_logsig', vp), ('loss_acc', vp), ('flag', vp), ('uc', vp)]
+
+
+class ResidualDesc(C.Structure):
+    _fields_ = [('n_fine', i32), ('nc', i32), ('n', i32), ('_pad', i32),
+                ('logkappa', vp), ('y', vp), ('bc', vp), ('r', vp), ('r_flux', vp)]
+
+
+class AdamDesc(C.Structure):
+    _fields_ = [('p', vp), ('g', vp), ('m', vp), ('v', vp), ('n', i64), ('lr', vp), ('step', vp),
+                ('beta1', f32), ('beta2', f32), ('eps', f32), ('_pad', f32)]
+
+
+STRUCTS = [Stat, Groups, ConvDesc, CodecCtx, ReduceItem, HeadDesc, GemmItem, RomDesc, ResidualDesc, AdamDesc]
+
+# name -> (restype, argtypes)
+SIGNATURES = {
+    'gpi_version': (C.c_int, []),
+    'gpi_struct_sizes': (C.c_int, [C.POINTER(i64), C.c_int]),
+    'gpi_error_string': (C.c_char_p, [C.c_int]),
+    'gpi_conv_blocks': (C.c_int, [C.POINTER(ConvDesc), C.POINTER(Groups), C.POINTER(i32)]),
+    'gpi_conv_forward': (C.c_int, [C.POINTER(ConvDesc), C.POINTER(CodecCtx), vp]),
+    'gpi_conv_backward': (C.c_int, [C.POINTER(ConvDesc), C.POINTER(CodecCtx), vp]),
+    'gpi_codec_forward': (C.c_int, [C.POINTER(ConvDesc), C.c_int, C.POINTER(CodecCtx), vp]),
+    'gpi_codec_backward': (C.c_int, [C.POINTER(ConvDesc), C.c_int, C.POINTER(CodecCtx), vp]),
+    'gpi_wgrad_reduce': (C.c_int, [C.POINTER(ReduceItem), C.c_int, vp, vp, vp]),
+    'gpi_head_forward': (C.c_int, [C.POINTER(HeadDesc), vp, vp, vp]),
+    'gpi_head_backward': (C.c_int, [C.POINTER(HeadDesc), vp, vp, vp, vp]),
+    'gpi_outer_gemm': (C.c_int, [C.POINTER(GemmItem), C.c_int, vp, vp, vp]),
+    'gpi_rom': (C.c_int, [C.POINTER(RomDesc), vp]),
+    'gpi_cgr_residual': (C.c_int, [C.POINTER(ResidualDesc), vp]),
+    'gpi_grad_finalize': (C.c_int, [vp, vp, i64, C.c_int, vp, vp]),
+    'gpi_adam': (C.c_int, [C.POINTER(AdamDesc), vp]),
+    'gpi_randn': (C.c_int, [vp, i64, u64, vp, u64, vp]),
+    'gpi_rng_advance': (C.c_int, [vp, u64, vp]),
+    'gpi_random_subset': (C.c_int, [vp, i32, i32, u64, vp, u64, vp]),
+}
+
+_LIB = None
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load (once) and return the native library.  Raises if it is missing."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise NativeError('libgpi_hip.so not built (%s); run __graft_entry__.build() / make -C csrc' % LIB_PATH)
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        sizes = (i64 * 16)()
+        k = L.gpi_struct_sizes(sizes, 16)
+        if k != len(STRUCTS):
+            raise NativeError('ABI mismatch: %d structs in the library, %d in the binding' % (k, len(STRUCTS)))
+        for s, cls in zip(sizes[:k], STRUCTS):
+            if s != C.sizeof(cls):
+                raise NativeError('ABI mismatch for %s: C %d bytes, ctypes %d' % (cls.__name__, s, C.sizeof(cls)))
+        _LIB = L
+    return _LIB
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = lib().gpi_error_string(rc).decode()
+        raise NativeError('%s failed: %s (%d)' % (what, msg, rc))
+
+
+def require_device(t):
+    if not isinstance(t, torch.Tensor) or t.device.type != 'cuda':
+        raise NativeError('the HIP path needs tensors on a ROCm GPU (got %s); there is no CPU fallback'
+                          % (t.device if isinstance(t, torch.Tensor) else type(t)))
+
+
+def ptr(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else C.c_void_p(0)
+
+
+def stream_handle(device=None):
+    return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)

@@ -1,0 +1,512 @@
+"""Execution engines: the ELBO training step and the standalone codec / ROM
+operators, each a fixed sequence of libgpi_hip.so launches over
+pre-planned workspaces.  No host synchronisation anywhere on the path.
+
+ElboEngine = GenerativeModel.elbo (generative.py:247-287) for the armortized
+unsupervised term (generative.py:546-585) + the supervised freeX term
+(generative.py:461-500), and its backward:
+
+  forward   encoder program (B_u)            conv.hip  (11 launches at C64)
+            dense head (all samples)          head.hip  (1)
+            decoder program (B_u + N_s, two BN groups, fused Gaussian loss)  (12)
+            ROM solve + log-lik + adjoint     rom.hip   (1)
+  backward  decoder program (reverse), dense head, encoder program (reverse),
+            weight-gradient slab reduction, outer-product GEMMs, finalize.
+"""
+import ctypes as C
+import math
+
+import torch
+
+from . import _lib as L
+from .plan import Arena, encoder_program, decoder_program
+
+ENT_CONST = 0.5 * (math.log(2 * math.pi) + 1)
+N_TERMS = 16
+# term slots in the fp64 scratch
+T_LX0 = 0          # decoder Gaussian log-lik per group (0..3)
+T_KL_ENC, T_KL_Q, T_LOGL_X, T_ENT, T_LOGL_Y = 4, 5, 6, 7, 8
+
+
+def groups_struct(sizes):
+    g = L.Groups()
+    g.n_groups = len(sizes)
+    s = 0
+    g.start[0] = 0
+    for i, n in enumerate(sizes):
+        s += n
+        g.start[i + 1] = s
+    for i in range(len(sizes) + 1, L.GPI_MAX_GROUPS + 1):
+        g.start[i] = s
+    return g
+
+
+class Workspace(object):
+    def __init__(self):
+        self.ws = Arena()
+        self.stats = Arena(align=1)
+        self.parts = Arena()
+        self.t_ws = None
+
+    def alloc(self, n):
+        return self.ws.alloc(n)
+
+    def materialize(self, device):
+        self.t_ws = torch.zeros(max(self.ws.size, 64), dtype=torch.float32, device=device)
+        self.t_scr = torch.zeros(N_TERMS + self.stats.size * L.GPI_MAX_GROUPS * 4 + 4, dtype=torch.float64,
+                                 device=device)
+        self.t_parts = torch.zeros(max(self.parts.size, 64), dtype=torch.float32, device=device)
+        self.t_flag = torch.zeros(4, dtype=torch.int32, device=device)
+
+    def view(self, off, *shape):
+        n = 1
+        for s in shape:
+            n *= s
+        return self.t_ws[off:off + n].view(*shape)
+
+    def fptr(self, off):
+        return C.c_void_p(self.t_ws.data_ptr() + 4 * off)
+
+    @property
+    def terms(self):
+        return self.t_scr[:N_TERMS]
+
+    def term_ptr(self, k):
+        return C.c_void_p(self.t_scr.data_ptr() + 8 * k)
+
+    @property
+    def stats_ptr(self):
+        return C.c_void_p(self.t_scr.data_ptr() + 8 * N_TERMS)
+
+    def zero_scratch(self):
+        self.t_scr.zero_()
+
+
+def make_ctx(ws, flat, group_sizes):
+    c = L.CodecCtx()
+    c.params = flat.P.data_ptr()
+    c.ws = ws.t_ws.data_ptr()
+    c.stats = ws.stats_ptr.value
+    c.gacc = flat.gacc.data_ptr()
+    c.wpart = ws.t_parts.data_ptr()
+    c.ext_in = None
+    c.ext_idx = None
+    c.ext_stride = 0
+    c.loss_acc = ws.term_ptr(T_LX0).value
+    c.bn_eps = 1e-5
+    c.groups = groups_struct(group_sizes)
+    for g in range(L.GPI_MAX_GROUPS):
+        c.loss_scale[g] = 1.0
+    return c
+
+
+def _lib():
+    return L.lib()
+
+
+def _run(fn, *args, what=None):
+    L.check(fn(*args), what or fn.__name__)
+
+
+class ElboEngine(object):
+    """Fused armortized-unsupervised + supervised-freeX ELBO of a GenerativeModel."""
+
+    def __init__(self, model, B_u, N_s, normalize=False):
+        self.model = model
+        flat = model._flat
+        self.flat = flat
+        dev = flat.P.device
+        self.B_u, self.N_s = int(B_u), int(N_s)
+        self.B = self.B_u + self.N_s
+        self.normalize = bool(normalize)
+        enc, dec, gp, g = model.encoder, model.f, model.gp, model.g
+        self.enc, self.dec = enc, dec
+        ws = Workspace()
+        self.ws = ws
+        offE = (lambda n: flat.offset(enc.get_parameter(n))) if enc is not None else None
+        offD = lambda n: flat.offset(dec.get_parameter(n))
+        dz = dec.dim_latent
+        self.dz = dz
+        # ---- encoder program
+        if self.B_u > 0:
+            ec = enc.native_config()
+            self.ep = encoder_program(**ec)
+            self.enc_descs = self.ep.layout(self.B_u, ws.ws, ws.stats, ws.parts, groups_struct([self.B_u]), offE)
+            d_feat = self.ep.d_feat
+        else:
+            self.ep = None
+            d_feat = 1
+        # ---- decoder program (groups: unsup, sup)
+        dc = dec.native_config()
+        self.dp = decoder_program(final_epilogue=L.EPI_GAUSS_LOSS, **dc)
+        self.dec_sizes = [n for n in (self.B_u, self.N_s) if n > 0]
+        self.dec_descs = self.dp.layout(self.B, ws.ws, ws.stats, ws.parts, groups_struct(self.dec_sizes), offD)
+        # ---- dense head buffers
+        d_lat = self.dp.input.per_sample
+        d_x = g.dim_effective_property if self.N_s > 0 else 1
+        self.d_x = d_x
+        hb = {}
+        for name, n in (('hpre', self.B_u * d_feat), ('dhpre', self.B_u * d_feat),
+                        ('zmu', self.B * dz), ('zls', self.B * dz), ('eps_z', self.B * dz), ('z', self.B * dz),
+                        ('gz', self.B * dz), ('dzmu', self.B * dz), ('dzls', self.B * dz),
+                        ('eps_x', self.N_s * d_x), ('xs', self.N_s * d_x), ('mux', self.N_s * d_x),
+                        ('gxs', self.N_s * d_x), ('gmux', self.N_s * d_x)):
+            hb[name] = ws.alloc(max(n, 1))
+        self.hb = hb
+        ws.materialize(dev)
+        P = lambda mod, n: flat.offset(mod.get_parameter(n))
+        h = L.HeadDesc()
+        h.flags = L.HEAD_LATENT
+        if self.B_u > 0:
+            h.flags |= L.HEAD_ENC | L.HEAD_REPARAM
+        if self.N_s > 0:
+            h.flags |= L.HEAD_QZ | L.HEAD_GP
+        h.n_enc, h.n_q = self.B_u, self.N_s
+        h.d_feat, h.d_z, h.d_lat, h.d_x = d_feat, dz, d_lat, d_x
+        if self.B_u > 0:
+            h.fc_w, h.fc_b = P(enc, 'features.FC.weight'), P(enc, 'features.FC.bias')
+            h.mu_w, h.mu_b = P(enc, 'features.SplitDense.fc_mean.weight'), P(enc, 'features.SplitDense.fc_mean.bias')
+            h.ls_w, h.ls_b = P(enc, 'features.SplitDense.fc_logvar.weight'), P(enc, 'features.SplitDense.fc_logvar.bias')
+            h.feat, h.gfeat = self.ep.output.off, self.ep.output.s_off
+        else:
+            h.fc_w = h.fc_b = h.mu_w = h.mu_b = h.ls_w = h.ls_b = -1
+            h.feat = h.gfeat = 0
+        h.lat_w, h.lat_b = P(dec, 'latent_map.weight'), P(dec, 'latent_map.bias')
+        if self.N_s > 0:
+            qz, qx = model.q_z['supervised'], model.q_X['supervised']
+            h.gp_w, h.gp_b, h.gp_ls = P(gp, 'fc.weight'), P(gp, 'fc.bias'), P(gp, 'logsigmas_X')
+            h.qz_mu, h.qz_ls = flat.offset(qz._mean), flat.offset(qz._logsigma)
+            h.qx_mu, h.qx_ls = flat.offset(qx._mean), flat.offset(qx._logsigma)
+        else:
+            h.gp_w = h.gp_b = h.gp_ls = h.qz_mu = h.qz_ls = h.qx_mu = h.qx_ls = -1
+        for k, v in hb.items():
+            setattr(h, k, v)
+        h.lat, h.glat = self.dp.input.off, self.dp.input.s_off
+        su = 1.0 / self.B_u if (self.normalize and self.B_u) else 1.0
+        ss = 1.0 / self.N_s if (self.normalize and self.N_s) else 1.0
+        self.su, self.ss = su, ss
+        h.kl_scale_enc, h.kl_scale_q, h.lx_scale = su, ss, ss
+        h.terms = ws.term_ptr(T_KL_ENC).value
+        self.head = h
+        # ---- contexts
+        if self.ep is not None:
+            self.ectx = make_ctx(ws, flat, [self.B_u])
+            self.ectx.ext_stride = self.ep.input.per_sample
+        self.dctx = make_ctx(ws, flat, self.dec_sizes)
+        for gi, scale in enumerate([su] * (self.B_u > 0) + [ss] * (self.N_s > 0)):
+            self.dctx.loss_scale[gi] = scale
+        # ---- gradient reductions
+        items = []
+        if self.ep is not None:
+            items += self.ep.reduce_items(offE)
+        items += self.dp.reduce_items(offD)
+        self.reduce_items = (L.ReduceItem * len(items))(*items)
+        gi = []
+        B = self.B
+
+        def gemm(a, b, S, M, N, lda, ldb, c, bias, flags=0):
+            it = L.GemmItem()
+            it.a_off, it.b_off, it.c_off, it.bias_off = a, b, c, bias
+            it.S, it.M, it.N, it.lda, it.ldb, it.flags = S, M, N, lda, ldb, flags
+            gi.append(it)
+
+        gemm(self.dp.input.s_off, hb['z'], B, d_lat, dz, d_lat, dz, h.lat_w, h.lat_b)
+        if self.N_s > 0:
+            gemm(hb['gmux'], hb['z'] + self.B_u * dz, self.N_s, d_x, dz, d_x, dz, h.gp_w, h.gp_b)
+        if self.B_u > 0:
+            gemm(hb['dzmu'], hb['hpre'], self.B_u, dz, d_feat, dz, d_feat, h.mu_w, h.mu_b, 1)
+            gemm(hb['dzls'], hb['hpre'], self.B_u, dz, d_feat, dz, d_feat, h.ls_w, h.ls_b, 1)
+            gemm(hb['dhpre'], h.feat, self.B_u, d_feat, d_feat, d_feat, d_feat, h.fc_w, h.fc_b)
+        self.gemm_items = (L.GemmItem * len(gi))(*gi)
+        # ---- ROM
+        if self.N_s > 0:
+            r = L.RomDesc()
+            rom = g.rom
+            r.nc, r.refine, r.n, r.mode = rom.nc, rom.refine, self.N_s, L.ROM_LOGLIK
+            r.x = ws.fptr(hb['xs']).value
+            r.x_stride = d_x
+            r.logsig_y = flat.P.data_ptr() + 4 * flat.offset(g.logsigmas_y)
+            r.loss_scale = ss
+            r.gx_accumulate = 0
+            r.gx = ws.fptr(hb['gxs']).value
+            r.gx_stride = d_x
+            r.gacc_logsig = flat.gacc.data_ptr() + 8 * flat.offset(g.logsigmas_y)
+            r.loss_acc = ws.term_ptr(T_LOGL_Y).value
+            r.flag = ws.t_flag.data_ptr()
+            r.mu_y = None
+            r.uc = None
+            r.dmu = None
+            self.rom = r
+        self._fixed = (self.B_u, self.N_s)
+
+    # ------------------------------------------------------------------
+    def eps_z(self):
+        return self.ws.view(self.hb['eps_z'], self.B, self.dz)
+
+    def eps_x(self):
+        return self.ws.view(self.hb['eps_x'], self.N_s, self.d_x)
+
+    def bind(self, X_u=None, u_index=None, X_s=None, Y=None, F=None):
+        """Point the launch descriptors at this step's data tensors."""
+        if self.B_u > 0:
+            L.require_device(X_u)
+            assert X_u.dtype == torch.float32 and X_u.is_contiguous()
+            self.ectx.ext_in = X_u.data_ptr()
+            self.ectx.ext_idx = u_index.data_ptr() if u_index is not None else None
+            self.dctx.tgt[0] = X_u.data_ptr()
+            self.dctx.tgt_idx[0] = u_index.data_ptr() if u_index is not None else None
+        if self.N_s > 0:
+            gs = 1 if self.B_u > 0 else 0
+            for t in (X_s, Y, F):
+                L.require_device(t)
+                assert t.dtype == torch.float32 and t.is_contiguous()
+            self.dctx.tgt[gs] = X_s.data_ptr()
+            self.dctx.tgt_idx[gs] = None
+            self.rom.Y = Y.data_ptr()
+            self.rom.F = F.data_ptr()
+
+    def forward(self, stream=None, compute_value=True):
+        """Launch the forward; returns the 0-d ELBO tensor (no host sync)."""
+        lib = _lib()
+        st = stream if stream is not None else L.stream_handle()
+        self.ws.zero_scratch()
+        self.flat.gacc.zero_()
+        if self.ep is not None:
+            _run(lib.gpi_codec_forward, self.enc_descs, len(self.enc_descs), C.byref(self.ectx), st,
+                 what='encoder forward')
+        _run(lib.gpi_head_forward, C.byref(self.head), C.c_void_p(self.flat.P.data_ptr()),
+             C.c_void_p(self.ws.t_ws.data_ptr()), st, what='head forward')
+        _run(lib.gpi_codec_forward, self.dec_descs, len(self.dec_descs), C.byref(self.dctx), st,
+             what='decoder forward')
+        if self.N_s > 0:
+            _run(lib.gpi_rom, C.byref(self.rom), st, what='rom')
+        return self.elbo_value() if compute_value else None
+
+    def elbo_value(self):
+        t = self.ws.terms
+        su, ss = self.su, self.ss
+        val = t.new_zeros(())
+        gi = 0
+        if self.B_u > 0:
+            val = val + su * (t[T_LX0 + gi] - t[T_KL_ENC])
+            gi += 1
+        if self.N_s > 0:
+            val = val + ss * (t[T_LX0 + gi] + t[T_LOGL_Y] + t[T_LOGL_X] + t[T_ENT] + self.N_s * ENT_CONST
+                              - t[T_KL_Q])
+        return val.to(torch.float32)
+
+    def terms(self):
+        """Dictionary of the individual ELBO terms (host sync)."""
+        t = self.ws.terms.cpu()
+        out = {}
+        gi = 0
+        if self.B_u > 0:
+            out['ARM_unsupervised_logL_x'] = float(t[T_LX0])
+            out['ARM_unsupervised_DKL_z'] = float(t[T_KL_ENC])
+            gi = 1
+        if self.N_s > 0:
+            out['supervised_logL_x'] = float(t[T_LX0 + gi])
+            out['supervised_logL_X'] = float(t[T_LOGL_X])
+            out['supervised_logL_y'] = float(t[T_LOGL_Y])
+            out['supervised_DKL_z'] = float(t[T_KL_Q])
+            out['supervised_entropy_X'] = float(t[T_ENT]) + self.N_s * ENT_CONST
+        return out
+
+    def backward(self, stream=None):
+        """Gradients of -ELBO into flat.gacc (fp64)."""
+        lib = _lib()
+        st = stream if stream is not None else L.stream_handle()
+        _run(lib.gpi_codec_backward, self.dec_descs, len(self.dec_descs), C.byref(self.dctx), st,
+             what='decoder backward')
+        _run(lib.gpi_head_backward, C.byref(self.head), C.c_void_p(self.flat.P.data_ptr()),
+             C.c_void_p(self.ws.t_ws.data_ptr()), C.c_void_p(self.flat.gacc.data_ptr()), st, what='head backward')
+        if self.ep is not None:
+            _run(lib.gpi_codec_backward, self.enc_descs, len(self.enc_descs), C.byref(self.ectx), st,
+                 what='encoder backward')
+        _run(lib.gpi_wgrad_reduce, self.reduce_items, len(self.reduce_items),
+             C.c_void_p(self.ws.t_parts.data_ptr()), C.c_void_p(self.flat.gacc.data_ptr()), st,
+             what='wgrad reduce')
+        _run(lib.gpi_outer_gemm, self.gemm_items, len(self.gemm_items), C.c_void_p(self.ws.t_ws.data_ptr()),
+             C.c_void_p(self.flat.gacc.data_ptr()), st, what='outer gemm')
+
+    def finalize(self, out, accumulate=False, step=None, stream=None):
+        st = stream if stream is not None else L.stream_handle()
+        _run(_lib().gpi_grad_finalize, C.c_void_p(self.flat.gacc.data_ptr()), C.c_void_p(out.data_ptr()),
+             self.flat.numel, 1 if accumulate else 0, C.c_void_p(step.data_ptr()) if step is not None else None, st,
+             what='grad finalize')
+
+    def check_flag(self):
+        """Lazy replacement of ROM.py:75's per-step host sync."""
+        if int(self.ws.t_flag[0].item()) != 0:
+            raise ValueError('At least one of the conductivity values supplied to the ROM was smaller than 1e-12')
+
+
+# ==========================================================================
+# standalone operators (CNNEncoder.forward, CNNDecoder.forward, ROM, CGR)
+# ==========================================================================
+class EncoderEngine(object):
+    """CNNEncoder.forward (Encoder.py:191-196): x -> (mean, logsigma) and its backward."""
+
+    def __init__(self, enc, flat, B):
+        self.flat, self.B = flat, int(B)
+        ws = Workspace()
+        self.ws = ws
+        off = lambda n: flat.offset(enc.get_parameter(n))
+        self.p = encoder_program(**enc.native_config())
+        self.descs = self.p.layout(self.B, ws.ws, ws.stats, ws.parts, groups_struct([self.B]), off)
+        d_feat, dz = self.p.d_feat, enc.latent_dim
+        self.dz = dz
+        hb = {k: ws.alloc(self.B * n) for k, n in (('hpre', d_feat), ('dhpre', d_feat), ('zmu', dz), ('zls', dz),
+                                                    ('eps_z', dz), ('z', dz), ('gz', dz), ('dzmu', dz),
+                                                    ('dzls', dz))}
+        hb.update({k: 0 for k in ('eps_x', 'xs', 'mux', 'gxs', 'gmux')})
+        ws.materialize(flat.P.device)
+        h = L.HeadDesc()
+        h.flags = L.HEAD_ENC
+        h.n_enc, h.n_q, h.d_feat, h.d_z, h.d_lat, h.d_x = self.B, 0, d_feat, dz, 1, 1
+        h.fc_w, h.fc_b = off('features.FC.weight'), off('features.FC.bias')
+        h.mu_w, h.mu_b = off('features.SplitDense.fc_mean.weight'), off('features.SplitDense.fc_mean.bias')
+        h.ls_w, h.ls_b = off('features.SplitDense.fc_logvar.weight'), off('features.SplitDense.fc_logvar.bias')
+        h.lat_w = h.lat_b = h.gp_w = h.gp_b = h.gp_ls = h.qz_mu = h.qz_ls = h.qx_mu = h.qx_ls = -1
+        for k, v in hb.items():
+            setattr(h, k, v)
+        h.feat, h.gfeat = self.p.output.off, self.p.output.s_off
+        h.lat = h.glat = 0
+        h.kl_scale_enc = h.kl_scale_q = h.lx_scale = 1.0
+        h.terms = ws.term_ptr(T_KL_ENC).value
+        self.head, self.hb = h, hb
+        self.ctx = make_ctx(ws, flat, [self.B])
+        self.ctx.ext_stride = self.p.input.per_sample
+        items = self.p.reduce_items(off)
+        self.reduce_items = (L.ReduceItem * len(items))(*items)
+        gi = []
+        for a, c, b in ((hb['dzmu'], h.mu_w, h.mu_b), (hb['dzls'], h.ls_w, h.ls_b)):
+            it = L.GemmItem(a_off=a, b_off=hb['hpre'], c_off=c, bias_off=b, S=self.B, M=dz, N=d_feat, lda=dz,
+                            ldb=d_feat, flags=1)
+            gi.append(it)
+        gi.append(L.GemmItem(a_off=hb['dhpre'], b_off=h.feat, c_off=h.fc_w, bias_off=h.fc_b, S=self.B, M=d_feat,
+                             N=d_feat, lda=d_feat, ldb=d_feat, flags=0))
+        self.gemm_items = (L.GemmItem * len(gi))(*gi)
+
+    def forward(self, x):
+        L.require_device(x)
+        x = x.contiguous().float()
+        self._x = x
+        self.ctx.ext_in = x.data_ptr()
+        self.ctx.ext_idx = None
+        lib, st = _lib(), L.stream_handle()
+        self.ws.zero_scratch()
+        _run(lib.gpi_codec_forward, self.descs, len(self.descs), C.byref(self.ctx), st, what='encoder forward')
+        _run(lib.gpi_head_forward, C.byref(self.head), C.c_void_p(self.flat.P.data_ptr()),
+             C.c_void_p(self.ws.t_ws.data_ptr()), st, what='head forward')
+        return (self.ws.view(self.hb['zmu'], self.B, self.dz).clone(),
+                self.ws.view(self.hb['zls'], self.B, self.dz).clone())
+
+    def backward(self, dmu, dls):
+        lib, st = _lib(), L.stream_handle()
+        self.ws.view(self.hb['gz'], self.B, self.dz).copy_(dmu)
+        self.ws.view(self.hb['dzls'], self.B, self.dz).copy_(dls)
+        self.flat.gacc.zero_()
+        _run(lib.gpi_head_backward, C.byref(self.head), C.c_void_p(self.flat.P.data_ptr()),
+             C.c_void_p(self.ws.t_ws.data_ptr()), C.c_void_p(self.flat.gacc.data_ptr()), st, what='head backward')
+        _run(lib.gpi_codec_backward, self.descs, len(self.descs), C.byref(self.ctx), st, what='encoder backward')
+        _run(lib.gpi_wgrad_reduce, self.reduce_items, len(self.reduce_items), C.c_void_p(self.ws.t_parts.data_ptr()),
+             C.c_void_p(self.flat.gacc.data_ptr()), st, what='wgrad reduce')
+        _run(lib.gpi_outer_gemm, self.gemm_items, len(self.gemm_items), C.c_void_p(self.ws.t_ws.data_ptr()),
+             C.c_void_p(self.flat.gacc.data_ptr()), st, what='outer gemm')
+
+
+class DecoderEngine(object):
+    """CNNDecoder.forward (Decoder.py:288-305): z -> (mean, logsigma) [B, H, W] and its backward."""
+
+    def __init__(self, dec, flat, B):
+        self.flat, self.B = flat, int(B)
+        ws = Workspace()
+        self.ws = ws
+        off = lambda n: flat.offset(dec.get_parameter(n))
+        self.p = decoder_program(final_epilogue=None, **dec.native_config())
+        self.descs = self.p.layout(self.B, ws.ws, ws.stats, ws.parts, groups_struct([self.B]), off)
+        dz = dec.dim_latent
+        self.dz = dz
+        d_lat = self.p.input.per_sample
+        hb = {k: ws.alloc(self.B * dz) for k in ('zmu', 'zls', 'eps_z', 'z', 'gz', 'dzmu', 'dzls')}
+        hb.update({k: 0 for k in ('hpre', 'dhpre', 'eps_x', 'xs', 'mux', 'gxs', 'gmux')})
+        ws.materialize(flat.P.device)
+        h = L.HeadDesc()
+        h.flags = L.HEAD_LATENT
+        h.n_enc, h.n_q, h.d_feat, h.d_z, h.d_lat, h.d_x = self.B, 0, 1, dz, d_lat, 1
+        h.fc_w = h.fc_b = h.mu_w = h.mu_b = h.ls_w = h.ls_b = -1
+        h.gp_w = h.gp_b = h.gp_ls = h.qz_mu = h.qz_ls = h.qx_mu = h.qx_ls = -1
+        h.lat_w, h.lat_b = off('latent_map.weight'), off('latent_map.bias')
+        for k, v in hb.items():
+            setattr(h, k, v)
+        h.feat = h.gfeat = 0
+        h.lat, h.glat = self.p.input.off, self.p.input.s_off
+        h.kl_scale_enc = h.kl_scale_q = h.lx_scale = 1.0
+        h.terms = ws.term_ptr(T_KL_ENC).value
+        self.head, self.hb = h, hb
+        self.ctx = make_ctx(ws, flat, [self.B])
+        items = self.p.reduce_items(off)
+        self.reduce_items = (L.ReduceItem * len(items))(*items)
+        self.gemm_items = (L.GemmItem * 1)(L.GemmItem(a_off=h.glat, b_off=hb['z'], c_off=h.lat_w, bias_off=h.lat_b,
+                                                      S=self.B, M=d_lat, N=dz, lda=d_lat, ldb=dz, flags=0))
+        o = self.p.output
+        self.out_shape = (self.B, o.C, o.H, o.W)
+
+    def forward(self, z):
+        L.require_device(z)
+        lib, st = _lib(), L.stream_handle()
+        self.ws.view(self.hb['z'], self.B, self.dz).copy_(z)
+        self.ws.zero_scratch()
+        _run(lib.gpi_head_forward, C.byref(self.head), C.c_void_p(self.flat.P.data_ptr()),
+             C.c_void_p(self.ws.t_ws.data_ptr()), st, what='latent map')
+        _run(lib.gpi_codec_forward, self.descs, len(self.descs), C.byref(self.ctx), st, what='decoder forward')
+        return self.ws.view(self.p.output.off, *self.out_shape).clone()
+
+    def backward(self, dout):
+        lib, st = _lib(), L.stream_handle()
+        self.ws.view(self.p.output.s_off, *self.out_shape).copy_(dout)
+        self.flat.gacc.zero_()
+        _run(lib.gpi_codec_backward, self.descs, len(self.descs), C.byref(self.ctx), st, what='decoder backward')
+        _run(lib.gpi_head_backward, C.byref(self.head), C.c_void_p(self.flat.P.data_ptr()),
+             C.c_void_p(self.ws.t_ws.data_ptr()), C.c_void_p(self.flat.gacc.data_ptr()), st, what='latent map bwd')
+        _run(lib.gpi_wgrad_reduce, self.reduce_items, len(self.reduce_items), C.c_void_p(self.ws.t_parts.data_ptr()),
+             C.c_void_p(self.flat.gacc.data_ptr()), st, what='wgrad reduce')
+        _run(lib.gpi_outer_gemm, self.gemm_items, len(self.gemm_items), C.c_void_p(self.ws.t_ws.data_ptr()),
+             C.c_void_p(self.flat.gacc.data_ptr()), st, what='outer gemm')
+        return self.ws.view(self.hb['dzmu'], self.B, self.dz).clone()
+
+
+def ROM_NN(nc):
+    """Number of coarse nodes of the nc x nc ROM mesh."""
+    return (nc + 1) ** 2
+
+
+def rom_call(nc, refine, x, F, input_kappa, mode, mu_y=None, uc=None, dmu=None, duc=None, gx=None, Y=None,
+             logsig_y=None, gacc_logsig=None, loss_acc=None, flag=None, loss_scale=1.0, gx_accumulate=False):
+    """Thin launcher of gpi_rom for the standalone ROM / ReducedOrderModelOperator."""
+    for t in (x, F):
+        L.require_device(t)
+    r = L.RomDesc()
+    r.nc, r.refine, r.n, r.mode, r.input_kappa = nc, refine, x.shape[0], mode, 1 if input_kappa else 0
+    r.x, r.x_stride, r.F = x.data_ptr(), x.stride(0), F.data_ptr()
+    p = lambda t: t.data_ptr() if t is not None else None
+    r.mu_y, r.uc, r.dmu, r.duc, r.gx, r.Y, r.logsig_y = p(mu_y), p(uc), p(dmu), p(duc), p(gx), p(Y), p(logsig_y)
+    r.gx_stride = gx.stride(0) if gx is not None else 0
+    r.gacc_logsig, r.loss_acc, r.flag = p(gacc_logsig), p(loss_acc), p(flag)
+    r.loss_scale, r.gx_accumulate = loss_scale, 1 if gx_accumulate else 0
+    _run(_lib().gpi_rom, C.byref(r), L.stream_handle(), what='rom')
+
+
+def cgr_residual(logkappa_img, y, bc, nc):
+    """W^T [K(kappa) yhat]_free for a batch of fields -> [N, (nc+1)^2]."""
+    for t in (logkappa_img, y, bc):
+        L.require_device(t)
+    N, n = logkappa_img.shape[0], logkappa_img.shape[-1]
+    r = torch.empty(N, (nc + 1) ** 2, dtype=torch.float32, device=y.device)
+    d = L.ResidualDesc()
+    lk, yy, bb = logkappa_img.contiguous().float(), y.contiguous().float(), bc.contiguous().float()
+    d.n_fine, d.nc, d.n = n, nc, N
+    d.logkappa, d.y, d.bc, d.r, d.r_flux = lk.data_ptr(), yy.data_ptr(), bb.data_ptr(), r.data_ptr(), None
+    _run(_lib().gpi_cgr_residual, C.byref(d), L.stream_handle(), what='cgr residual')
+    return r

@@ -1,0 +1,68 @@
+"""Flat parameter / gradient storage.
+
+All parameters of a model live in ONE fp32 device buffer (each nn.Parameter's
+``.data`` becomes a view of it), gradients land in ONE fp32 buffer (each
+``.grad`` a view), and kernels accumulate gradients in a parallel fp64
+buffer.  One flat buffer gives: single-offset parameter addressing in the
+kernels, one all-reduce for data parallelism, one Adam launch.
+The Parameter objects themselves are unchanged, so optimizers built on
+``model.parameters()`` and ``state_dict()`` / ``load_state_dict()`` keep working.
+"""
+import torch
+
+
+class FlatParameters(object):
+
+    def __init__(self, named_params, device, shared_prefixes=None):
+        named = [(n, p) for n, p in named_params]
+        # shared parameters first, rank-local ones (per-sample variational params) last
+        if shared_prefixes is not None:
+            named.sort(key=lambda np_: 0 if any(np_[0].startswith(s) for s in shared_prefixes) else 1)
+        self.names = [n for n, _ in named]
+        self.params = [p for _, p in named]
+        self.offsets = {}
+        self.name_offsets = {}
+        total = 0
+        for n, p in named:
+            self.offsets[id(p)] = total
+            self.name_offsets[n] = total
+            total += p.numel()
+        self.numel = total
+        self.P = torch.empty(total, dtype=torch.float32, device=device)
+        self.G = torch.zeros(total, dtype=torch.float32, device=device)
+        self.gacc = torch.zeros(total, dtype=torch.float64, device=device)
+        for n, p in named:
+            o = self.offsets[id(p)]
+            self.P[o:o + p.numel()].copy_(p.detach().reshape(-1))
+            p.data = self.P[o:o + p.numel()].view(p.shape)
+        self.n_shared = total
+        if shared_prefixes is not None:
+            local = [n for n in self.names if not any(n.startswith(s) for s in shared_prefixes)]
+            self.n_shared = self.name_offsets[local[0]] if local else total
+
+    def offset(self, p):
+        return self.offsets[id(p)]
+
+    def owns(self, p):
+        return id(p) in self.offsets and p.data.data_ptr() == self.P.data_ptr() + 4 * self.offsets[id(p)]
+
+    def grad_view(self, p):
+        o = self.offsets[id(p)]
+        return self.G[o:o + p.numel()].view(p.shape)
+
+    def deliver(self, tmp):
+        """Hand the flat gradient ``tmp`` to the parameters with torch
+        accumulation semantics (None -> assign a view, existing -> add)."""
+        grads = [p.grad for p in self.params]
+        if all(g is None for g in grads):
+            self.G.copy_(tmp)
+            for p in self.params:
+                p.grad = self.grad_view(p)
+        elif all(g is not None and g.data_ptr() == self.G.data_ptr() + 4 * self.offsets[id(p)]
+                 for g, p in zip(grads, self.params)):
+            self.G.add_(tmp)
+        else:
+            for p in self.params:
+                o = self.offsets[id(p)]
+                v = tmp[o:o + p.numel()].view(p.shape)
+                p.grad = v.clone() if p.grad is None else p.grad + v

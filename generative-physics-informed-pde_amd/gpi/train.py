@@ -1,0 +1,120 @@
+"""Fused native training step: Trainer.run's loop body (training.py:403-417)
+without Python/autograd glue, for production runs and the benchmark.
+
+One step = random armortized subset (utils/data.py:444) + reparametrisation
+noise (device Philox) + ELBO forward/backward (ElboEngine) + gradient
+finalisation + [one SUM all-reduce of the shared-parameter gradients over
+RCCL] + flat Adam (training.py:254,417).  Per-sample variational parameters
+(q_z / q_X rows of this rank's labeled samples) are rank-local and never
+communicated.  Every launch is stream-ordered with no host synchronisation,
+so the whole step can be captured once into a HIP graph and replayed.
+"""
+import ctypes as C
+
+import torch
+import torch.distributed as dist
+
+from . import _lib as L
+from .engine import ElboEngine
+
+
+class FusedElboStep(object):
+
+    def __init__(self, model, X_pool, B_u, X_s=None, Y=None, F=None, lr=1e-2, betas=(0.9, 0.999), eps=1e-8,
+                 seed=0, normalize=False, process_group=None, distributed=False):
+        self.model = model
+        self.flat = model.native_flat()
+        self.N_s = 0 if X_s is None else int(X_s.shape[0])
+        self.B_u = int(B_u)
+        self.engine = ElboEngine(model, self.B_u, self.N_s, normalize=normalize)
+        dev = self.flat.P.device
+        self.X_pool = X_pool.contiguous().float() if X_pool is not None else None
+        self.X_s, self.Y, self.F = X_s, Y, F
+        self.idx = torch.zeros(max(self.B_u, 1), dtype=torch.int32, device=dev)
+        self.rng_off = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.step_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.lr = torch.tensor([lr], dtype=torch.float32, device=dev)
+        self.m = torch.zeros_like(self.flat.P)
+        self.v = torch.zeros_like(self.flat.P)
+        self.seed = int(seed)
+        self.distributed = distributed
+        self.pg = process_group
+        self.adam = L.AdamDesc(p=self.flat.P.data_ptr(), g=self.flat.G.data_ptr(), m=self.m.data_ptr(),
+                               v=self.v.data_ptr(), n=self.flat.numel, lr=self.lr.data_ptr(),
+                               step=self.step_ctr.data_ptr(), beta1=betas[0], beta2=betas[1], eps=eps)
+        self.engine.bind(X_u=self.X_pool, u_index=self.idx if self.B_u else None, X_s=X_s, Y=Y, F=F)
+        n_pool = self.X_pool.shape[0] if self.X_pool is not None else 0
+        self.n_pool = n_pool
+        self.rng_span = max(n_pool, (self.engine.B * self.engine.dz + 3) // 4 + 1,
+                            (self.N_s * self.engine.d_x + 3) // 4 + 1)
+        self.graph = None
+
+    # ------------------------------------------------------------------
+    def _launch_noise(self, st):
+        lib = L.lib()
+        if self.B_u:
+            L.check(lib.gpi_random_subset(L.ptr(self.idx), self.n_pool, self.B_u, self.seed, L.ptr(self.rng_off), 1,
+                                          st), 'random subset')
+        ez = self.engine.eps_z()
+        L.check(lib.gpi_randn(L.ptr(ez), ez.numel(), self.seed, L.ptr(self.rng_off), 2, st), 'randn z')
+        if self.N_s:
+            ex = self.engine.eps_x()
+            L.check(lib.gpi_randn(L.ptr(ex), ex.numel(), self.seed, L.ptr(self.rng_off), 3, st), 'randn x')
+
+    def forward_backward(self, stream=None):
+        st = stream if stream is not None else L.stream_handle()
+        self._launch_noise(st)
+        self.engine.forward(st, compute_value=False)
+        self.engine.backward(st)
+        self.engine.finalize(self.flat.G, step=self.step_ctr, stream=st)
+
+    def allreduce(self):
+        if self.distributed:
+            n = self.flat.n_shared
+            dist.all_reduce(self.flat.G[:n], op=dist.ReduceOp.SUM, group=self.pg)
+
+    def update(self, stream=None):
+        st = stream if stream is not None else L.stream_handle()
+        L.check(L.lib().gpi_adam(C.byref(self.adam), st), 'adam')
+        L.check(L.lib().gpi_rng_advance(L.ptr(self.rng_off), self.rng_span, st), 'rng advance')
+
+    def step_eager(self):
+        self.forward_backward()
+        self.allreduce()
+        self.update()
+
+    # ------------------------------------------------------------------
+    def capture(self):
+        """Capture the step into HIP graph(s); the all-reduce stays outside the graph."""
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):          # warm up allocator / kernels on the side stream
+                self.step_eager()
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        self.g_fb = torch.cuda.CUDAGraph()
+        self.g_up = None
+        if self.distributed:
+            with torch.cuda.graph(self.g_fb):
+                self.forward_backward()
+            self.g_up = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.g_up):
+                self.update()
+        else:
+            with torch.cuda.graph(self.g_fb):
+                self.forward_backward()
+                self.update()
+        self.graph = True
+
+    def step(self):
+        if self.graph is None:
+            return self.step_eager()
+        self.g_fb.replay()
+        if self.distributed:
+            self.allreduce()
+            self.g_up.replay()
+
+    def elbo(self):
+        """Current ELBO value of the last forward (0-d tensor)."""
+        return self.engine.elbo_value()

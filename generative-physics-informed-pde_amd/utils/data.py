@@ -1,0 +1,103 @@
+"""Datasets (reference utils/data.py:8-459): images, labels, BCs, restrictions.
+
+``DataLoader`` holds N log-conductivity images with their boundary
+conditions and (after ``assemble``) the FOM labels Y on the fine free nodes
+and the coarse F_ROM_BC vectors (utils/data.py:72-103; setup-side, host
+float64, structured-grid solves instead of FEniCS).  ``DataSet`` is a view
+on a subset of indices with device-cached tensors and the reference's
+``get(key, random_subset)`` semantics (utils/data.py:419-445).
+"""
+import numpy as np
+import torch
+
+from physics.BoundaryConditions import BoundaryConditionEnsemble
+from physics.grid import pixel_to_cells
+
+
+class DataLoader(object):
+
+    def __init__(self, X, bce=None):
+        self.X = np.asarray(X, dtype=np.float64)        # [N, py, px] log-conductivity images
+        self.BCE = bce if bce is not None else BoundaryConditionEnsemble.FromFactory(self.X.shape[0])
+        self.X_DG = None
+        self.Y = None
+        self.F_ROM_BC = None
+
+    @classmethod
+    def FromSampler(cls, sampler, N, rng=None):
+        rng = rng or np.random
+        X = sampler.sample(batch_size=N, rng=rng)
+        return cls(X, BoundaryConditionEnsemble.FromFactory(N, rng))
+
+    @property
+    def N(self):
+        return self.X.shape[0]
+
+    def assemble(self, physics, indices=None, solve=True):
+        """X_DG, FOM labels Y (free dofs) and F_ROM_BC for ``indices`` (default: all)."""
+        fom, rom = physics['fom'], physics['rom']
+        self.BCE.register_function_space('fom', fom)
+        self.BCE.register_function_space('rom', rom)
+        self.X_DG = pixel_to_cells(self.X)
+        self.F_ROM_BC = self.BCE.FULL_F_WITH_APPLIED_BC('rom')
+        if solve:
+            idx = range(self.N) if indices is None else indices
+            Y = np.full((self.N, fom.dim_out), np.nan)
+            for n in idx:
+                Y[n] = fom.grid.solve(np.exp(self.X_DG[n]), self.BCE[n].u)
+            self.Y = Y
+        return self
+
+    def save(self, path):
+        torch.save({'X': torch.tensor(self.X), 'U': torch.tensor(self.BCE.U)}, path)
+
+    @classmethod
+    def FromFile(cls, path):
+        d = torch.load(path, weights_only=True)
+        return cls(d['X'].numpy(), BoundaryConditionEnsemble.FromEncoding(d['U'].numpy()))
+
+
+class DataSet(object):
+
+    VALID = ('X', 'X_DG', 'Y', 'F_ROM_BC', 'BCE')
+
+    def __init__(self, dataloader, indices, dtype=torch.float32, device=None, label=''):
+        self._dl = dataloader
+        self.indices = np.asarray(indices, dtype=np.int64)
+        self._dtype = dtype
+        self._device = device
+        self._cache = {}
+        self.label = label
+
+    @property
+    def N(self):
+        return self.indices.size
+
+    def __len__(self):
+        return self.N
+
+    def __bool__(self):
+        return self.N > 0
+
+    def restrict(self, N):
+        self.indices = self.indices[:N]
+        self._cache = {}
+
+    def get(self, key, random_subset=None):
+        if key not in self.VALID:
+            raise ValueError(key)
+        if key not in self._cache:
+            if key == 'BCE':
+                q = self._dl.BCE[list(self.indices)]
+            else:
+                q = torch.tensor(getattr(self._dl, key)[self.indices])
+                if key in ('X', 'Y', 'F_ROM_BC'):
+                    q = q.to(dtype=self._dtype, device=self._device).contiguous()
+            self._cache[key] = q
+        if random_subset is None:
+            return self._cache[key]
+        perm = torch.randperm(self.N, dtype=torch.long, device=self._device)
+        return self._cache[key][perm[0:random_subset]]
+
+    def __repr__(self):
+        return 'Virtual dataset with {} datapoints | {}'.format(self.N, self.label)

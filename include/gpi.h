@@ -1,0 +1,258 @@
+/*
+ * gpi.h -- C ABI of libgpi_hip.so, the MI355X (gfx950) kernels behind the
+ * physics-informed ELBO training step of pkmtum/generative-physics-informed-pde.
+ *
+ * The reference has no native layer of its own: its hot path is PyTorch
+ * (cuDNN/cuBLAS/torch.solve) plus FEniCS assembly at setup.  These entry
+ * points replace exactly the third-party kernels on that path
+ * (SURVEY.md section 2.2); each one cites the reference code it stands in for.
+ *
+ * Conventions
+ *   - The caller owns every buffer.  Device pointers / element offsets in,
+ *     results out; the library never allocates and never synchronises the
+ *     host, so every call is safe inside hipStreamBeginCapture.
+ *   - Calls are stream-ordered on the hipStream_t passed as `stream`
+ *     (NULL = the legacy default stream).
+ *   - Every entry point returns int: GPI_OK (0) or a negative error code;
+ *     nothing throws across the ABI.  gpi_error_string() names the code.
+ *   - fp32 storage and arithmetic; statistics, loss sums and parameter
+ *     gradients are accumulated in fp64.
+ *   - Offsets in the descriptors are element offsets into the buffers named
+ *     by the context (params / workspace / gradient accumulator).
+ */
+#ifndef GPI_H
+#define GPI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GPI_OK 0
+#define GPI_ERR_ARG (-1)
+#define GPI_ERR_LAUNCH (-2)
+#define GPI_ERR_UNSUPPORTED (-3)
+
+#define GPI_MAX_GROUPS 4
+#define GPI_MAX_CIN 32
+#define GPI_MAX_COUT 8
+#define GPI_MAX_REDUCE_ITEMS 48
+#define GPI_MAX_GEMM_ITEMS 12
+
+/* Conv epilogues */
+#define GPI_EPI_STORE 0        /* store raw output */
+#define GPI_EPI_STORE_STATS 1  /* store raw output + per-channel fp64 sum / sum^2 (train-mode BN) */
+#define GPI_EPI_GAUSS_LOSS 2   /* cout == 2: (mean, logsigma) -> Gaussian log-lik vs target, writes d(-elbo)/d(out) */
+
+/* Per-channel BatchNorm statistics record, one per (channel, group). */
+typedef struct gpi_stat {
+    double sum;     /* sum x           (forward)  */
+    double sumsq;   /* sum x^2         (forward)  */
+    double ssum;    /* sum S           (backward: S = sum_c gamma_c dL/d(bn_c)) */
+    double sxsum;   /* sum S * xhat    (backward) */
+} gpi_stat;
+
+/* Samples of one codec call are split into BN-statistics groups: the
+ * reference calls the decoder once per batch (unsupervised, supervised, ...)
+ * and train-mode BatchNorm normalises each call with its own batch
+ * statistics (bottleneck/codec.py:164-294; nothing calls .eval()).  One
+ * launch here serves all groups. */
+typedef struct gpi_groups {
+    int32_t n_groups;
+    int32_t start[GPI_MAX_GROUPS + 1];   /* group g = samples [start[g], start[g+1]) */
+} gpi_groups;
+
+/* One convolution of the DenseNet codec with its fused neighbours:
+ *   out = conv(act(in)),  act = relu(batchnorm_train(.)) or identity,
+ * nearest x2 upsampling folded into the addressing, dense-block concat
+ * never materialised (channel offsets into a shared block buffer).
+ * Replaces nn.Conv2d / nn.BatchNorm2d / ReLU / UpsamplingNearest2d /
+ * torch.cat of bottleneck/codec.py:150-298, Encoder.py:151, Decoder.py:217. */
+typedef struct gpi_conv_desc {
+    int32_t cin, cout, k, stride, pad, upsample;
+    int32_t h_in, w_in, h_out, w_out;
+    /* input: raw (pre-BN) features; in_off < 0 selects ctx->ext_in */
+    int64_t in_off;
+    int32_t in_ctot, in_c0;
+    int32_t in_bn;                 /* 1: relu(BN) applied on the fly */
+    int32_t gin_accumulate;        /* backward: 0 overwrite gin, 1 add */
+    int64_t gamma_off, beta_off;   /* param offsets of the input BN affine */
+    int64_t in_stat;               /* stat index of input channel in_c0 */
+    int64_t w_off;                 /* param offset, weight [cout][cin][k][k] */
+    /* output */
+    int64_t out_off;
+    int32_t out_ctot, out_c0;
+    int64_t out_stat;              /* stat index of output channel out_c0, or -1 */
+    int32_t epilogue;              /* GPI_EPI_* */
+    int32_t gout_mode;             /* backward: 0 = BN-backward of the S buffer, 1 = direct gradient */
+    int64_t gout_off;              /* S buffer (mode 0) / gradient buffer (mode 1), output layout */
+    int64_t gin_off;               /* S buffer / gradient of the input (input layout), or -1 */
+    int64_t wpart_off;             /* weight-gradient partial slab (one row per block) */
+} gpi_conv_desc;
+
+/* Per-call pointers shared by all codec operators. */
+typedef struct gpi_codec_ctx {
+    const float* params;           /* flat fp32 parameters */
+    float* ws;                     /* workspace (activations, S / gradient buffers) */
+    gpi_stat* stats;               /* BN statistics records [stat][group] */
+    double* gacc;                  /* fp64 gradient accumulator, parallel to params */
+    float* wpart;                  /* weight-gradient partial slabs */
+    const float* ext_in;           /* external input (e.g. the unlabeled image pool) */
+    const int32_t* ext_idx;        /* row of ext_in for each sample (NULL: identity) */
+    int64_t ext_stride;            /* floats per ext_in row */
+    const float* tgt[GPI_MAX_GROUPS];      /* Gaussian-loss targets per group */
+    const int32_t* tgt_idx[GPI_MAX_GROUPS];/* target row per sample of the group (NULL: identity) */
+    float loss_scale[GPI_MAX_GROUPS];      /* d(-elbo)/d(logL): 1, or 1/batch when normalize */
+    double* loss_acc;              /* [n_groups] sum of Gaussian log-likelihood per group */
+    float bn_eps;                  /* 1e-5 (torch default) */
+    gpi_groups groups;
+} gpi_codec_ctx;
+
+/* Weight-gradient reduction item: gacc[w_off + i] += sum_b wpart[part_off + b*numel + i]. */
+typedef struct gpi_reduce_item {
+    int64_t part_off, w_off;
+    int32_t blocks, numel;
+} gpi_reduce_item;
+
+/* Dense (per-sample) part of the ELBO: encoder FC / ReLU / split heads
+ * (Encoder.py:175-182, codec.py:495-504), reparametrisation
+ * (bottleneck/utils.py:216-219, components.py:167-172), KL
+ * (bottleneck/utils.py:246-248), the decoder latent map (Decoder.py:213),
+ * and the effective-property map with its Gaussian log-likelihood
+ * (components.py:201-256, generative.py:469-470).
+ * Samples [0, n_enc) take the amortised-encoder path, samples
+ * [n_enc, n_enc + n_q) the per-sample variational path. */
+#define GPI_HEAD_ENC      0x01  /* feat -> FC -> relu -> (mu, logsigma) for encoder samples */
+#define GPI_HEAD_REPARAM  0x02  /* z = mu + exp(logsigma) eps, KL (encoder samples) */
+#define GPI_HEAD_QZ       0x04  /* z from q_z params, KL (q samples) */
+#define GPI_HEAD_LATENT   0x08  /* lat = latent_map(z) for all samples */
+#define GPI_HEAD_GP       0x10  /* gp(z), X-sample from q_X, log-lik + entropy (q samples) */
+
+typedef struct gpi_head_desc {
+    int32_t flags;
+    int32_t n_enc, n_q;
+    int32_t d_feat, d_z, d_lat, d_x;
+    int32_t _pad;
+    /* parameter offsets (-1 if absent) */
+    int64_t fc_w, fc_b, mu_w, mu_b, ls_w, ls_b;
+    int64_t lat_w, lat_b;
+    int64_t gp_w, gp_b, gp_ls;
+    int64_t qz_mu, qz_ls, qx_mu, qx_ls;
+    /* workspace offsets */
+    int64_t feat, gfeat, hpre;       /* [n_enc, d_feat] */
+    int64_t zmu, zls, eps_z, z, gz;  /* [n_enc + n_q, d_z] */
+    int64_t lat, glat;               /* [n_enc + n_q, d_lat] */
+    int64_t eps_x, xs, mux, gxs, gmux; /* [n_q, d_x] */
+    int64_t dzmu, dzls;              /* [n_enc + n_q, d_z] backward deltas */
+    int64_t dhpre;                   /* [n_enc, d_feat] backward delta */
+    float kl_scale_enc, kl_scale_q, lx_scale, _fpad;
+    /* fp64 term accumulators (terms[0..]): KL_enc, KL_q, logL_X, entropy */
+    double* terms;
+} gpi_head_desc;
+
+/* Batched outer-product GEMM for shared dense-layer gradients:
+ *   gacc[c_off + m*N + n] += sum_s A[s*lda + m] * B[s*ldb + n]
+ *   gacc[bias_off + m]    += sum_s A[s*lda + m]       (bias_off >= 0)   */
+typedef struct gpi_gemm_item {
+    int64_t a_off, b_off, c_off, bias_off;
+    int32_t S, M, N, lda, ldb, flags;   /* flags bit 0: ReLU applied to B */
+} gpi_gemm_item;
+
+/* Coarse-grained model (ROM) on the nc x nc "/" mesh: K(kappa) from the
+ * closed-form 5-point stencil, Dirichlet nodes eliminated (the SPD interior
+ * system equals ROM.py's row-replaced system), banded Cholesky per sample,
+ * P1 prolongation to the fine free nodes, optional fused Gaussian
+ * log-likelihood and its adjoint.
+ * Replaces ROM.__call__/GetStiffness/_solve_eqs (bottleneck/ROM.py:59-100),
+ * ReducedOrderModelOperator.forward (components.py:296-302) and
+ * DiagonalGaussianLogLikelihood(Y, mu_y, 2 logsigma_y) (generative.py:473). */
+#define GPI_ROM_FORWARD 0   /* mu_y = W solve(K(exp(x)+1e-8), F) */
+#define GPI_ROM_LOGLIK  1   /* forward + log-lik + backward to x and logsigma_y */
+#define GPI_ROM_BACKWARD 2  /* given d(mu_y): backward to x */
+
+typedef struct gpi_rom_desc {
+    int32_t nc, refine, n, mode;
+    int32_t input_kappa;       /* 1: x holds kappa itself (ROM.__call__), 0: log effective property */
+    int32_t _pad;
+    const float* x;            /* [n, 2 nc^2] log effective property */
+    int64_t x_stride;
+    const float* F;            /* [n, (nc+1)^2] F_ROM_BC */
+    float* mu_y;               /* [n, d_y] out (optional) */
+    const float* Y;            /* [n, d_y] targets (LOGLIK) */
+    const float* logsig_y;     /* [d_y] (LOGLIK) */
+    float loss_scale;          /* d(-elbo)/d(logL_y) */
+    int32_t gx_accumulate;
+    const float* dmu;          /* [n, d_y] upstream gradient (BACKWARD), or NULL */
+    const float* duc;          /* [n, (nc+1)^2] upstream gradient w.r.t. the coarse solution (BACKWARD), or NULL */
+    float* gx;                 /* [n, 2 nc^2] d/dx out */
+    int64_t gx_stride;
+    double* gacc_logsig;       /* fp64 accumulator for d/d logsigma_y (LOGLIK) */
+    double* loss_acc;          /* sum log-lik (LOGLIK) */
+    int32_t* flag;             /* set to 1 if any kappa <= 1e-12 (ROM.py:74-76), checked lazily */
+    float* uc;                 /* optional [n, (nc+1)^2] coarse solution */
+} gpi_rom_desc;
+
+/* Coarse-grained residual on the fine grid (VirtualObservables CGR query,
+ * VirtualObservables.py:57-69,297-321 + physics/LinearElliptic.py:137-159):
+ *   r = W^T [K_f(kappa) yhat]_free  (= Gamma y - alpha),
+ * kappa = exp(logkappa image) per pixel, yhat = y on free nodes and the NDP
+ * Dirichlet data u0..u3 on x=0 / x=1.  Matrix-free 5-point stencil. */
+typedef struct gpi_residual_desc {
+    int32_t n_fine, nc, n, _pad;
+    const float* logkappa;     /* [n, n_fine, n_fine] image (row 0 = top) */
+    const float* y;            /* [n, d_y] fine free values */
+    const float* bc;           /* [n, 4] u0..u3 */
+    float* r;                  /* [n, (nc+1)^2] CGR residual */
+    float* r_flux;             /* [n, 2 nc^2] flux residual (or NULL), bottleneck/flux.py */
+} gpi_residual_desc;
+
+/* Flat Adam (torch.optim.Adam semantics, no weight decay / amsgrad),
+ * training.py:254,417.  step and lr are read from device memory so the
+ * update can be replayed from a captured graph. */
+typedef struct gpi_adam_desc {
+    float* p; const float* g; float* m; float* v;
+    int64_t n;
+    const float* lr;           /* device scalar */
+    const int64_t* step;       /* device scalar: step number after increment */
+    float beta1, beta2, eps, _pad;
+} gpi_adam_desc;
+
+/* ---------------------------------------------------------------- API */
+int gpi_version(void);
+/* sizeof of every struct above, in declaration order (ABI self-check); returns the count. */
+int gpi_struct_sizes(int64_t* out, int n);
+const char* gpi_error_string(int code);
+
+/* Number of workgroups (= partial-slab rows) a conv launch uses. */
+int gpi_conv_blocks(const gpi_conv_desc* op, const gpi_groups* groups, int32_t* blocks);
+int gpi_conv_forward(const gpi_conv_desc* op, const gpi_codec_ctx* ctx, void* stream);
+int gpi_conv_backward(const gpi_conv_desc* op, const gpi_codec_ctx* ctx, void* stream);
+/* Run a codec program: ops in order (forward) / reverse order (backward). */
+int gpi_codec_forward(const gpi_conv_desc* ops, int n_ops, const gpi_codec_ctx* ctx, void* stream);
+int gpi_codec_backward(const gpi_conv_desc* ops, int n_ops, const gpi_codec_ctx* ctx, void* stream);
+int gpi_wgrad_reduce(const gpi_reduce_item* items, int n_items, const float* wpart, double* gacc, void* stream);
+
+int gpi_head_forward(const gpi_head_desc* d, const float* params, float* ws, void* stream);
+int gpi_head_backward(const gpi_head_desc* d, const float* params, float* ws, double* gacc, void* stream);
+int gpi_outer_gemm(const gpi_gemm_item* items, int n_items, const float* ws, double* gacc, void* stream);
+
+int gpi_rom(const gpi_rom_desc* d, void* stream);
+int gpi_cgr_residual(const gpi_residual_desc* d, void* stream);
+
+/* Gradient finalisation: grad[i] = (accumulate ? grad[i] : 0) + (float) gacc[i];
+ * also increments the device step counter (if non-NULL) for gpi_adam. */
+int gpi_grad_finalize(const double* gacc, float* grad, int64_t n, int accumulate, int64_t* step, void* stream);
+int gpi_adam(const gpi_adam_desc* d, void* stream);
+
+/* Device Philox4x32-10 normals: out[i] = N(0,1) for counter (*offset + i);
+ * offset is a device uint64 advanced by gpi_rng_advance (graph-replay safe). */
+int gpi_randn(float* out, int64_t n, uint64_t seed, const uint64_t* offset, uint64_t sub, void* stream);
+int gpi_rng_advance(uint64_t* offset, uint64_t by, void* stream);
+/* Uniform random subset (randperm(n)[:k] semantics, utils/data.py:444). */
+int gpi_random_subset(int32_t* out, int32_t n, int32_t k, uint64_t seed, const uint64_t* offset, uint64_t sub, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GPI_H */

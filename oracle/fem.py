@@ -204,15 +204,25 @@ def f_rom_bc(mesh_c, u_bc):
 # --------------------------------------------------------------------------
 # prolongation W (components.py:38-60, fawkes/utils.py:115-192)
 # --------------------------------------------------------------------------
+def _bary_tables(mesh):
+    if getattr(mesh, '_bary', None) is None:
+        P = mesh.coords[mesh.cells]                               # [nc, 3, 2]
+        G = np.stack([barycentric_gradients(p)[1] for p in P])    # [nc, 3, 2]
+        mesh._bary = (P, G)
+    return mesh._bary
+
+
 def locate(mesh, pt, tol=1e-12):
-    for t, cell in enumerate(mesh.cells):
-        p = mesh.coords[cell]
-        area, g = barycentric_gradients(p)
-        lam = np.array([1.0 - g[1] @ (pt - p[0]) - g[2] @ (pt - p[0]),
-                        g[1] @ (pt - p[0]), g[2] @ (pt - p[0])])
-        if np.all(lam >= -tol):
-            return t, lam
-    raise ValueError('point outside mesh')
+    """First cell containing pt (bounding-box-tree first collision semantics) and its barycentrics."""
+    P, G = _bary_tables(mesh)
+    d = pt[None, :] - P[:, 0, :]
+    l1 = np.einsum('ck,ck->c', G[:, 1], d)
+    l2 = np.einsum('ck,ck->c', G[:, 2], d)
+    lam = np.stack([1.0 - l1 - l2, l1, l2], 1)
+    hit = np.where(np.all(lam >= -tol, 1))[0]
+    if hit.size == 0:
+        raise ValueError('point outside mesh')
+    return int(hit[0]), lam[hit[0]]
 
 
 def prolongation(mesh_c, points):

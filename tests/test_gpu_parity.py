@@ -1,0 +1,264 @@
+"""GPU parity: the HIP kernels (through the C ABI and the drop-in modules)
+against golden fixtures produced by the reference's own modules and against
+the oracle.  Tolerances: fp32 kernels vs fp32/fp64 references, stated per test."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import fem
+from oracle import elbo as oelbo
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), 'golden')
+
+
+def load(name):
+    return dict(np.load(os.path.join(GOLD, name), allow_pickle=False))
+
+
+def cuda(a, dtype=torch.float32):
+    return torch.tensor(np.asarray(a), dtype=dtype, device='cuda')
+
+
+def rel(a, b):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    return np.abs(a - b).max() / max(np.abs(b).max(), 1e-30)
+
+
+# ---------------------------------------------------------------- ROM
+def test_rom_operator_forward_backward(device):
+    from gpi.native import RomOperatorFunction
+    d = load('rom_c32.npz')
+    x = cuda(d['effprop']).requires_grad_(True)
+    F = cuda(d['F'])
+    mu, uc = RomOperatorFunction.apply(x, F, 4, 8, False)
+    assert rel(mu.detach().cpu(), d['mu_y']) < 2e-5
+    ls = cuda(d['logsigmas_y']).requires_grad_(True)
+    Y = cuda(d['Y'])
+    L = torch.sum(-0.5 * (2 * ls + (Y - mu) ** 2 * torch.exp(-2 * ls) + 1.8378770664093453))
+    (-L).backward()
+    assert abs(L.item() - float(d['logL'])) / abs(float(d['logL'])) < 1e-5
+    assert rel(x.grad.cpu(), d['grad_effprop']) < 1e-3
+    assert rel(ls.grad.cpu(), d['grad_logsigmas_y']) < 1e-4
+
+
+def test_rom_fused_loglik(device):
+    from gpi.engine import rom_call
+    from gpi import _lib as L
+    d = load('rom_c32.npz')
+    x, F, Y, ls = cuda(d['effprop']), cuda(d['F']), cuda(d['Y']), cuda(d['logsigmas_y'])
+    gx = torch.zeros_like(x)
+    gls = torch.zeros(ls.shape[0], dtype=torch.float64, device='cuda')
+    acc = torch.zeros(1, dtype=torch.float64, device='cuda')
+    flag = torch.zeros(1, dtype=torch.int32, device='cuda')
+    rom_call(4, 8, x, F, False, L.ROM_LOGLIK, Y=Y, logsig_y=ls, gx=gx, gacc_logsig=gls, loss_acc=acc, flag=flag)
+    assert abs(acc.item() - float(d['logL'])) / abs(float(d['logL'])) < 1e-5
+    assert rel(gx.cpu(), d['grad_effprop']) < 1e-3
+    assert rel(gls.cpu(), d['grad_logsigmas_y']) < 1e-4
+    assert flag.item() == 0
+
+
+def test_rom_call_matches_reference_semantics(device):
+    """ROM.__call__(kappa, F): Dirichlet-row dense solve of the reference (ROM.py:65-100)."""
+    from bottleneck.ROM import ROM
+    from physics.grid import StructuredGrid
+    d = load('rom_c32.npz')
+    kap = torch.exp(torch.tensor(d['effprop'], dtype=torch.float64)) + 1e-8
+    ref = oelbo.rom_solve(torch.tensor(d['M'], dtype=torch.float64), kap, torch.tensor(d['F'], dtype=torch.float64),
+                          torch.tensor(d['bc_dofs']))
+    rom = ROM(StructuredGrid(4), 8)
+    u = rom(kap.float().cuda(), cuda(d['F']))
+    assert rel(u.cpu(), ref) < 2e-5
+
+
+# ---------------------------------------------------------------- CGR residual
+def test_cgr_residual_fp32_match(device):
+    """North-star residual check: fp32 kernel vs fp64 Gamma y - alpha, error normalised by
+    ||Gamma||_F ||y|| + ||alpha||, tolerance 1e-5."""
+    from gpi.engine import cgr_residual
+    d = load('vo_c32.npz')
+    imgs, U, G, A, y = d['imgs'], d['U'], d['Gamma'], d['alpha'], d['g']
+    r = cgr_residual(cuda(imgs), cuda(y), cuda(U), nc=4).cpu().numpy()
+    for i in range(imgs.shape[0]):
+        ref = G[i] @ y[i] - A[i]
+        scale = np.linalg.norm(G[i]) * np.linalg.norm(y[i]) + np.linalg.norm(A[i])
+        assert np.abs(r[i] - ref).max() / scale < 1e-5
+
+
+@pytest.mark.parametrize('nc,r,N', [(8, 8, 3), (4, 4, 5), (2, 16, 2)])
+def test_cgr_residual_random_fields(device, nc, r, N):
+    from gpi.engine import cgr_residual
+    rng = np.random.default_rng(nc * r)
+    n = nc * r
+    mc, mf = fem.unit_square_mesh(nc), fem.unit_square_mesh(n)
+    W = fem.prolongation_free(mc, mf)
+    imgs = rng.normal(0.4, 0.8, (N, n, n))
+    U = rng.uniform(-0.5, 0.5, (N, 4))
+    y = rng.normal(0, 0.3, (N, W.shape[0]))
+    out = cgr_residual(cuda(imgs), cuda(y), cuda(U), nc=nc).cpu().numpy()
+    for i in range(N):
+        Gm, a = fem.cgr_query(mf, W, np.exp(fem.image_to_cells(imgs[i])), U[i])
+        ref = Gm @ y[i] - a
+        scale = np.linalg.norm(Gm) * np.linalg.norm(y[i]) + np.linalg.norm(a)
+        assert np.abs(out[i] - ref).max() / scale < 1e-5
+
+
+def test_cgr_residual_vanishes_at_fom_solution(device):
+    from gpi.engine import cgr_residual
+    rng = np.random.default_rng(0)
+    nc, n = 8, 64
+    mf = fem.unit_square_mesh(n)
+    img = rng.normal(0.4, 0.8, (1, n, n))
+    u = rng.uniform(-0.5, 0.5, (1, 4))
+    y = fem.solve_fom(mf, np.exp(fem.image_to_cells(img[0])), u[0])[None]
+    r = cgr_residual(cuda(img), cuda(y), cuda(u), nc=nc).cpu().numpy()
+    assert np.abs(r).max() < 1e-4
+
+
+# ---------------------------------------------------------------- codec
+def _codec(tag):
+    from bottleneck.Encoder import CNNEncoder
+    from bottleneck.Decoder import CNNDecoder
+    d = load('codec_%s.npz' % tag)
+    imsize, dz, latent, growth, f_enc, f_dec = [int(v) for v in d['cfg'][:6]]
+    blocks = [int(v) for v in d['cfg'][6:]]
+    enc = CNNEncoder(imsize, dz, blocks, growth, f_enc, drop_rate=0)
+    dec = CNNDecoder(imsize, dz, (latent, latent), 1, f_dec, blocks, False, growth, drop_rate=0.)
+    enc.load_state_dict({k[4:]: torch.tensor(v) for k, v in d.items() if k.startswith('enc.') and
+                         not k.startswith('enc.grad.')})
+    dec.load_state_dict({k[4:]: torch.tensor(v) for k, v in d.items() if k.startswith('dec.') and
+                         not k.startswith('dec.grad.')})
+    return d, enc.cuda(), dec.cuda()
+
+
+@pytest.mark.parametrize('tag', ['c32', 'c64'])
+def test_encoder_forward_backward(device, tag):
+    d, enc, _ = _codec(tag)
+    mu, ls = enc(cuda(d['X']))
+    assert rel(mu.detach().cpu(), d['enc_mu']) < 1e-4
+    assert rel(ls.detach().cpu(), d['enc_ls']) < 1e-4
+    (torch.sum(mu * cuda(d['enc_wm'])) + torch.sum(ls * cuda(d['enc_ws']))).backward()
+    for k, p in enc.named_parameters():
+        assert rel(p.grad.cpu(), d['enc.grad.' + k]) < 2e-3, k
+
+
+@pytest.mark.parametrize('tag', ['c32', 'c64'])
+def test_decoder_forward_backward(device, tag):
+    d, _, dec = _codec(tag)
+    Z = cuda(d['Z']).requires_grad_(True)
+    mx, lsx = dec(Z)
+    assert rel(mx.detach().cpu(), d['dec_mu']) < 1e-4
+    assert rel(lsx.detach().cpu(), d['dec_ls']) < 1e-4
+    (torch.sum(mx * cuda(d['dec_vm'])) + torch.sum(lsx * cuda(d['dec_vs']))).backward()
+    assert rel(Z.grad.cpu(), d['grad_Z']) < 2e-3
+    for k, p in dec.named_parameters():
+        assert rel(p.grad.cpu(), d['dec.grad.' + k]) < 2e-3, k
+
+
+# ---------------------------------------------------------------- full ELBO step
+class _DS(object):
+    def __init__(self, perm=None, **t):
+        self.t = t
+        self.perm = perm
+        self.N = next(iter(t.values())).shape[0]
+
+    def __bool__(self):
+        return True
+
+    def get(self, key, random_subset=None):
+        if random_subset is None:
+            return self.t[key]
+        return self.t[key][self.perm[:random_subset]]
+
+
+def build_golden_model(d):
+    from bottleneck.Encoder import CNNEncoder
+    from bottleneck.Decoder import CNNDecoder
+    from bottleneck.components import EffectivePropertyMap, ReducedOrderModelOperator
+    from bottleneck.ROM import ROM
+    from bottleneck.generative import GenerativeModel
+    from physics.grid import StructuredGrid
+    n, nc, dz, Nu, bs, Ns = [int(v) for v in d['cfg']]
+    enc = CNNEncoder(n, dz, [1, 1], 4, 4, drop_rate=0)
+    dec = CNNDecoder(n, dz, (8, 8), 1, 4, [1, 1], False, 4, drop_rate=0.)
+    rom = ROM(StructuredGrid(nc), n // nc)
+    g = ReducedOrderModelOperator(rom, torch.tensor(d['W']), dtype=torch.float32, device='cuda')
+    gp = EffectivePropertyMap(dz, 2 * nc * nc, dtype=torch.float32, device='cuda')
+    model = GenerativeModel(f=dec.cuda(), g=g, gp=gp, dtype=torch.float32, device=torch.device('cuda'))
+    model.encoder = enc.cuda()
+    perm = torch.tensor(d['perm'], device='cuda')
+    ds_s = _DS(X=cuda(d['Xs']), Y=cuda(d['Y']), F_ROM_BC=cuda(d['F']))
+    ds_u = _DS(perm=perm, X=cuda(d['Xu']))
+    model.register_datasets({'supervised': ds_s, 'unsupervised': ds_u}, None,
+                            create_unsupervised_variational_approximation=False)
+    state = {k[6:]: torch.tensor(v) for k, v in d.items() if k.startswith('state.')}
+    model.load_state_dict(state)
+    model.cuda()
+    return model, bs
+
+
+def test_elbo_step_matches_reference(device):
+    """GenerativeModel.elbo + backward vs the reference's (generative.py:247-287), injected eps."""
+    d = load('elbo_c32.npz')
+    model, bs = build_golden_model(d)
+    eps = (torch.cat([cuda(d['eps_enc']), cuda(d['eps_qz'])]), cuda(d['eps_qX']))
+    elbo = model.elbo(step=0, armortized_bs=bs, eps=eps)
+    assert abs(elbo.item() - float(d['elbo'])) / abs(float(d['elbo'])) < 2e-5
+    (-elbo).backward()
+    for k, p in model.named_parameters():
+        ref = d['grad.' + k]
+        scale = max(np.abs(ref).max(), 1.0)
+        err = np.abs(p.grad.cpu().numpy() - ref).max() / scale
+        assert err < 2e-3, (k, err)
+
+
+def test_elbo_grad_accumulation_semantics(device):
+    """zero_grad(set_to_none=False) + two backward passes accumulate like torch.
+    Atomic accumulation order is not fixed, so the two passes agree to fp32 rounding only."""
+    d = load('elbo_c32.npz')
+    model, bs = build_golden_model(d)
+    eps = (torch.cat([cuda(d['eps_enc']), cuda(d['eps_qz'])]), cuda(d['eps_qX']))
+    (-model.elbo(step=0, armortized_bs=bs, eps=eps)).backward()
+    g1 = {k: p.grad.clone() for k, p in model.named_parameters()}
+    (-model.elbo(step=0, armortized_bs=bs, eps=eps)).backward()
+    for k, p in model.named_parameters():
+        torch.testing.assert_close(p.grad, 2 * g1[k], rtol=1e-3, atol=1e-4 * max(1.0, g1[k].abs().max().item()))
+
+
+# ---------------------------------------------------------------- plumbing kernels
+def test_flat_adam_matches_torch(device):
+    from gpi import _lib as L
+    import ctypes as C
+    torch.manual_seed(0)
+    p0 = torch.randn(1000, device='cuda')
+    p_ref = p0.clone().requires_grad_(True)
+    opt = torch.optim.Adam([p_ref], lr=1e-2)
+    p = p0.clone()
+    m, v = torch.zeros_like(p), torch.zeros_like(p)
+    lr = torch.tensor([1e-2], device='cuda')
+    step = torch.zeros(1, dtype=torch.int64, device='cuda')
+    for it in range(5):
+        g = torch.randn(1000, device='cuda')
+        p_ref.grad = g.clone()
+        opt.step()
+        step += 1
+        dsc = L.AdamDesc(p=p.data_ptr(), g=g.data_ptr(), m=m.data_ptr(), v=v.data_ptr(), n=1000, lr=lr.data_ptr(),
+                         step=step.data_ptr(), beta1=0.9, beta2=0.999, eps=1e-8)
+        L.check(L.lib().gpi_adam(C.byref(dsc), L.stream_handle()), 'adam')
+    torch.testing.assert_close(p, p_ref.detach(), rtol=1e-5, atol=1e-6)
+
+
+def test_device_rng(device):
+    from gpi import _lib as L
+    import ctypes as C
+    x = torch.empty(1 << 20, device='cuda')
+    off = torch.zeros(1, dtype=torch.int64, device='cuda')
+    L.check(L.lib().gpi_randn(L.ptr(x), x.numel(), 1234, L.ptr(off), 7, L.stream_handle()), 'randn')
+    assert abs(x.mean().item()) < 5e-3 and abs(x.std().item() - 1) < 5e-3
+    idx = torch.empty(256, dtype=torch.int32, device='cuda')
+    L.check(L.lib().gpi_random_subset(L.ptr(idx), 2048, 256, 99, L.ptr(off), 3, L.stream_handle()), 'subset')
+    v = idx.cpu().numpy()
+    assert len(set(v.tolist())) == 256 and v.min() >= 0 and v.max() < 2048
