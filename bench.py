@@ -188,6 +188,7 @@ def main():
     ap.add_argument('--no-graph', action='store_true')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-roofline', action='store_true')
+    ap.add_argument('--kprof', default=None, help='write the per-operator HIP-event profile (JSON) here')
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -232,6 +233,9 @@ def main():
     cpu = None
     if rank == 0 and not args.no_roofline:
         prof = profile_kernels(step)
+        if args.kprof:
+            with open(args.kprof, 'w') as fh:
+                json.dump([dict(op=n, ms=m, bytes=b, gbs=b / (m * 1e-3) / 1e9) for n, m, b in prof], fh, indent=1)
         name, ms, byts = max(prof, key=lambda t: t[1])
         ach = byts / (ms * 1e-3) / 1e9
         roof = dict(bound='hbm', achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit='GB/s',

@@ -113,14 +113,43 @@ bool conv_geom(const gpi_conv_desc& d, const gpi_groups& g, ConvGeom& G) {
     return true;
 }
 
-constexpr int HDR = 2 * GPI_MAX_CIN + 96;   // scale/shift + reduction scratch (2*CP*4 + 2*CP <= 80)
+// Sum the GPI_REPLICAS copies of the stat records [stat0, stat0 + nch) of group grp into
+// dst[4 * nch] (LDS, fp64: sum, sumsq, ssum, sxsum).  Caller syncs before and after.
+__device__ __forceinline__ void gather_stats(const gpi_codec_ctx& c, int64_t stat0, int nch, int grp, double* dst) {
+    const int n = nch * GPI_REPLICAS;
+    for (int e = threadIdx.x; e < n; e += blockDim.x) {
+        const int ch = e / GPI_REPLICAS, r = e - ch * GPI_REPLICAS;
+        const gpi_stat st = c.stats[((int64_t)r * c.n_stats + stat0 + ch) * GPI_MAX_GROUPS + grp];
+        atomicAdd(&dst[4 * ch + 0], st.sum);
+        atomicAdd(&dst[4 * ch + 1], st.sumsq);
+        atomicAdd(&dst[4 * ch + 2], st.ssum);
+        atomicAdd(&dst[4 * ch + 3], st.sxsum);
+    }
+}
+
+__device__ __forceinline__ gpi_stat* stat_slot(const gpi_codec_ctx& c, int64_t stat, int grp) {
+    const int r = blockIdx.x % GPI_REPLICAS;
+    return c.stats + ((int64_t)r * c.n_stats + stat) * GPI_MAX_GROUPS + grp;
+}
+
+__device__ __forceinline__ void mean_invstd(const double* s4, double n, float eps, float& mean, float& invstd) {
+    const double m = s4[0] / n;
+    double var = s4[1] / n - m * m;
+    if (var < 0.0) var = 0.0;
+    mean = (float)m;
+    invstd = (float)(1.0 / sqrt(var + (double)eps));
+}
+
+constexpr int HDR_D = 4 * (GPI_MAX_CIN + GPI_MAX_COUT);   // fp64 gathered stats
+constexpr int HDR = 2 * HDR_D + 2 * GPI_MAX_CIN + 96;      // floats: stats, scale/shift, reduction scratch
 
 template <int K, int S, int UP, int CP>
 __global__ __launch_bounds__(256) void conv_fwd_kernel(gpi_conv_desc d, gpi_codec_ctx c, ConvGeom G) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    float* sc = smem;
-    float* sh = smem + GPI_MAX_CIN;
-    float* scratch = smem + 2 * GPI_MAX_CIN;   // 2*CP*4 floats
+    double* gst = (double*)smem;
+    float* sc = smem + 2 * HDR_D;
+    float* sh = sc + GPI_MAX_CIN;
+    float* scratch = sh + GPI_MAX_CIN;         // 2*CP*4 floats
     float* red = scratch + 2 * CP * 4;         // 2*CP floats
     float* tile = smem + HDR;
 
@@ -134,9 +163,13 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(gpi_conv_desc d, gpi_code
     const int HWi = d.h_in * d.w_in, HWo = d.h_out * d.w_out;
 
     if (d.in_bn) {
+        for (int e = tid; e < 4 * d.cin; e += 256) gst[e] = 0.0;
+        __syncthreads();
+        gather_stats(c, d.in_stat, d.cin, grp, gst);
+        __syncthreads();
         if (tid < d.cin) {
             float mean, inv;
-            bn_mean_invstd(c.stats[(d.in_stat + tid) * GPI_MAX_GROUPS + grp], (double)gsz * HWi, c.bn_eps, mean, inv);
+            mean_invstd(gst + 4 * tid, (double)gsz * HWi, c.bn_eps, mean, inv);
             const float gam = c.params[d.gamma_off + tid], bet = c.params[d.beta_off + tid];
             sc[tid] = gam * inv;
             sh[tid] = bet - mean * gam * inv;
@@ -224,7 +257,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(gpi_conv_desc d, gpi_code
         float v[1] = {L};
         block_sum<1>(v, scratch, red);
         __syncthreads();
-        if (tid == 0) atomicAdd(c.loss_acc + grp, (double)red[0]);
+        if (tid == 0) atomicAdd(c.loss_acc + grp * GPI_REPLICAS + blockIdx.x % GPI_REPLICAS, (double)red[0]);
         return;
     }
 
@@ -245,7 +278,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(gpi_conv_desc d, gpi_code
         block_sum<2 * CP>(v, scratch, red);
         __syncthreads();
         if (tid < 2 * d.cout) {
-            gpi_stat* st = c.stats + (d.out_stat + (tid >> 1)) * GPI_MAX_GROUPS + grp;
+            gpi_stat* st = stat_slot(c, d.out_stat + (tid >> 1), grp);
             atomicAdd((tid & 1) ? &st->sumsq : &st->sum, (double)red[tid]);
         }
     }
@@ -256,7 +289,8 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(gpi_conv_desc d, gpi_code
     extern __shared__ __attribute__((aligned(16))) float smem[];
     // header
     double* csum = (double*)smem;                // [MAX_CIN][2] fp64 per-channel BN-backward sums
-    float* i_mean = smem + 4 * GPI_MAX_CIN;      // [MAX_CIN]
+    double* gst = csum + 2 * GPI_MAX_CIN;        // [MAX_CIN + MAX_COUT][4] gathered stats
+    float* i_mean = smem + 4 * GPI_MAX_CIN + 2 * HDR_D;   // [MAX_CIN]
     float* i_inv = i_mean + GPI_MAX_CIN;
     float* i_gam = i_inv + GPI_MAX_CIN;
     float* i_bet = i_gam + GPI_MAX_CIN;
@@ -279,27 +313,29 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(gpi_conv_desc d, gpi_code
     const int gsz = c.groups.start[grp + 1] - c.groups.start[grp];
     const int HWi = d.h_in * d.w_in, HWo = d.h_out * d.w_out;
 
-    if (tid < d.cin) {
-        if (d.in_bn) {
-            float mean, inv;
-            bn_mean_invstd(c.stats[(d.in_stat + tid) * GPI_MAX_GROUPS + grp], (double)gsz * HWi, c.bn_eps, mean, inv);
-            i_mean[tid] = mean;
-            i_inv[tid] = inv;
-            i_gam[tid] = c.params[d.gamma_off + tid];
-            i_bet[tid] = c.params[d.beta_off + tid];
-        }
-        csum[2 * tid] = 0.0;
-        csum[2 * tid + 1] = 0.0;
+    for (int e = tid; e < HDR_D; e += 256) gst[e] = 0.0;
+    if (tid < 2 * GPI_MAX_CIN) csum[tid] = 0.0;
+    __syncthreads();
+    if (d.in_bn) gather_stats(c, d.in_stat, d.cin, grp, gst);
+    if (d.gout_mode == 0) gather_stats(c, d.out_stat, d.cout, grp, gst + 4 * GPI_MAX_CIN);
+    __syncthreads();
+    if (tid < d.cin && d.in_bn) {
+        float mean, inv;
+        mean_invstd(gst + 4 * tid, (double)gsz * HWi, c.bn_eps, mean, inv);
+        i_mean[tid] = mean;
+        i_inv[tid] = inv;
+        i_gam[tid] = c.params[d.gamma_off + tid];
+        i_bet[tid] = c.params[d.beta_off + tid];
     }
     if (d.gout_mode == 0 && tid < d.cout) {
-        const gpi_stat st = c.stats[(d.out_stat + tid) * GPI_MAX_GROUPS + grp];
+        const double* st = gst + 4 * (GPI_MAX_CIN + tid);
         const double n = (double)gsz * HWo;
         float mean, inv;
-        bn_mean_invstd(st, n, c.bn_eps, mean, inv);
+        mean_invstd(st, n, c.bn_eps, mean, inv);
         o_coef[4 * tid] = mean;
         o_coef[4 * tid + 1] = inv;
-        o_coef[4 * tid + 2] = (float)(st.ssum / n);
-        o_coef[4 * tid + 3] = (float)(st.sxsum / n);
+        o_coef[4 * tid + 2] = (float)(st[2] / n);
+        o_coef[4 * tid + 3] = (float)(st[3] / n);
     }
     for (int e = tid; e < nw; e += 256) wl[e] = c.params[d.w_off + e];
     __syncthreads();
@@ -409,7 +445,7 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(gpi_conv_desc d, gpi_code
                 __syncthreads();
             }
             if (part == 0 && j < J) {
-                float* wp = c.wpart + d.wpart_off + (int64_t)blockIdx.x * d.cout * J;
+                float* wp = c.wpart + d.wpart_off + (int64_t)blockIdx.x * (d.cout * J + (d.in_bn ? 2 * d.cin : 0));
 #pragma unroll
                 for (int co = 0; co < CP; ++co)
                     if (co < d.cout) wp[co * J + j] = acc[co];
@@ -488,17 +524,23 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(gpi_conv_desc d, gpi_code
                 *gp = prev + da;
             }
         }
-        if (d.in_bn) {
-            if (cur_ci >= 0) {
-                atomicAdd(&csum[2 * cur_ci], (double)sd);
-                atomicAdd(&csum[2 * cur_ci + 1], (double)sdx);
-            }
-            __syncthreads();
-            if (tid < d.cin) {
-                const double s_d = csum[2 * tid], s_dx = csum[2 * tid + 1];
-                atomicAdd(c.gacc + d.beta_off + tid, s_d);
-                atomicAdd(c.gacc + d.gamma_off + tid, s_dx);
-                gpi_stat* st = c.stats + (d.in_stat + tid) * GPI_MAX_GROUPS + grp;
+        if (d.in_bn && cur_ci >= 0) {
+            atomicAdd(&csum[2 * cur_ci], (double)sd);
+            atomicAdd(&csum[2 * cur_ci + 1], (double)sdx);
+        }
+    }
+    if (d.in_bn) {
+        // dbeta / dgamma partials go to this workgroup's slab row (reduced by gpi_wgrad_reduce);
+        // the S statistics of the input channels to a replica slot (summed by the producer's backward)
+        __syncthreads();
+        if (tid < d.cin) {
+            const double s_d = csum[2 * tid], s_dx = csum[2 * tid + 1];
+            const int J = d.cin * K * K;
+            float* row = c.wpart + d.wpart_off + (int64_t)blockIdx.x * (d.cout * J + 2 * d.cin) + d.cout * J;
+            row[tid] = (float)s_dx;            // dgamma
+            row[d.cin + tid] = (float)s_d;     // dbeta
+            if (d.gin_off >= 0) {
+                gpi_stat* st = stat_slot(c, d.in_stat + tid, grp);
                 const double gam = i_gam[tid];
                 atomicAdd(&st->ssum, gam * s_d);
                 atomicAdd(&st->sxsum, gam * s_dx);
@@ -513,7 +555,7 @@ size_t fwd_lds(const gpi_conv_desc& d, const ConvGeom& G) {
 
 size_t bwd_lds(const gpi_conv_desc& d, const ConvGeom& G, int cp) {
     const int nw = d.cout * d.cin * d.k * d.k;
-    size_t f = 8 * GPI_MAX_CIN + 4 * GPI_MAX_COUT + ((nw + 3) & ~3) + (size_t)G.spb * d.cout * G.gh * G.gw +
+    size_t f = 8 * GPI_MAX_CIN + 2 * HDR_D + 4 * GPI_MAX_COUT + ((nw + 3) & ~3) + (size_t)G.spb * d.cout * G.gh * G.gw +
                (size_t)G.spb * d.cin * G.rh * G.rw + (size_t)cp * 256;
     return f * sizeof(float);
 }
@@ -565,22 +607,45 @@ int launch(const gpi_conv_desc& d, const gpi_codec_ctx& c, hipStream_t st, bool 
     return GPI_OK;
 }
 
+// Slab reduction: workgroup (item, weight chunk of <= 256, row chunk of RROWS).
+// Thread (w, p) sums rows p, p + P, ... of its row chunk for weight w
+// (coalesced: consecutive w read consecutive floats of a slab row), the P
+// partials meet in LDS, one fp64 atomic per weight per workgroup.
+constexpr int RROWS = 64;
+
 struct ReduceArgs {
     gpi_reduce_item it[GPI_MAX_REDUCE_ITEMS];
     int32_t first_block[GPI_MAX_REDUCE_ITEMS + 1];
+    int32_t wchunks[GPI_MAX_REDUCE_ITEMS];
     int32_t n;
 };
 
 __global__ __launch_bounds__(256) void wgrad_reduce(ReduceArgs a, const float* __restrict__ wpart, double* gacc) {
+    __shared__ float red[256];
     int k = 0;
     while (k + 1 < a.n && (int)blockIdx.x >= a.first_block[k + 1]) ++k;
     const gpi_reduce_item it = a.it[k];
-    const int i = (blockIdx.x - a.first_block[k]) * 256 + threadIdx.x;
-    if (i >= it.numel) return;
-    double s = 0.0;
-    const float* p = wpart + it.part_off + i;
-    for (int b = 0; b < it.blocks; ++b) s += (double)p[(int64_t)b * it.numel];
-    gacc[it.w_off + i] += s;
+    const int local = blockIdx.x - a.first_block[k];
+    const int wc = local % a.wchunks[k], rc = local / a.wchunks[k];
+    const int w0 = wc * 256;
+    const int nw = min(256, it.numel - w0);
+    const int P = 256 / nw;
+    const int tid = threadIdx.x;
+    const int w = tid % nw, p = tid / nw;
+    const int r0 = rc * RROWS, r1 = min(it.blocks, r0 + RROWS);
+    float s = 0.f;
+    if (p < P) {
+        const float* base = wpart + it.part_off + w0 + w;
+#pragma unroll 4
+        for (int r = r0 + p; r < r1; r += P) s += base[(int64_t)r * it.row_stride];
+    }
+    red[tid] = s;
+    __syncthreads();
+    if (tid < nw) {
+        double t = 0.0;
+        for (int q = 0; q < P; ++q) t += (double)red[q * nw + tid];
+        atomicAdd(gacc + it.w_off + w0 + tid, t);
+    }
 }
 
 }  // namespace
@@ -624,6 +689,8 @@ extern "C" int gpi_codec_backward(const gpi_conv_desc* ops, int n_ops, const gpi
 extern "C" int gpi_wgrad_reduce(const gpi_reduce_item* items, int n_items, const float* wpart, double* gacc,
                                 void* stream) {
     if (!items || n_items < 0 || n_items > GPI_MAX_REDUCE_ITEMS || !wpart || !gacc) return GPI_ERR_ARG;
+    for (int k = 0; k < n_items; ++k)
+        if (items[k].row_stride < items[k].numel || items[k].numel <= 0) return GPI_ERR_ARG;
     if (n_items == 0) return GPI_OK;
     ReduceArgs a;
     a.n = n_items;
@@ -631,7 +698,8 @@ extern "C" int gpi_wgrad_reduce(const gpi_reduce_item* items, int n_items, const
     for (int k = 0; k < n_items; ++k) {
         a.it[k] = items[k];
         a.first_block[k] = nb;
-        nb += (items[k].numel + 255) / 256;
+        a.wchunks[k] = (items[k].numel + 255) / 256;
+        nb += a.wchunks[k] * ((items[k].blocks + RROWS - 1) / RROWS);
     }
     a.first_block[n_items] = nb;
     hipLaunchKernelGGL(wgrad_reduce, dim3(nb), dim3(256), 0, (hipStream_t)stream, a, wpart, gacc);

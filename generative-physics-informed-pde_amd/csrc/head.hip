@@ -95,7 +95,7 @@ __global__ __launch_bounds__(HT) void head_fwd_kernel(gpi_head_desc d, const flo
                 kl += 1.f + 2.f * ls - mu * mu - e * e;
             }
             kl = block_sum128(kl, scratch);
-            if (tid == 0) atomicAdd(d.terms + 0, -0.5 * (double)kl);
+            if (tid == 0) atomicAdd(d.terms + 0 * GPI_REPLICAS + blockIdx.x % GPI_REPLICAS, -0.5 * (double)kl);
         } else {
             for (int k = tid; k < dz; k += HT) z[k] = ws[d.z + (int64_t)s * dz + k];
         }
@@ -111,7 +111,7 @@ __global__ __launch_bounds__(HT) void head_fwd_kernel(gpi_head_desc d, const flo
                 kl += 1.f + 2.f * ls - mu * mu - e * e;
             }
             kl = block_sum128(kl, scratch);
-            if (tid == 0) atomicAdd(d.terms + 1, -0.5 * (double)kl);
+            if (tid == 0) atomicAdd(d.terms + 1 * GPI_REPLICAS + blockIdx.x % GPI_REPLICAS, -0.5 * (double)kl);
         } else {
             for (int k = tid; k < dz; k += HT) z[k] = ws[d.z + (int64_t)s * dz + k];
         }
@@ -145,8 +145,8 @@ __global__ __launch_bounds__(HT) void head_fwd_kernel(gpi_head_desc d, const flo
         lx = block_sum128(lx, scratch);
         ent = block_sum128(ent, scratch);
         if (tid == 0) {
-            atomicAdd(d.terms + 2, (double)lx);
-            atomicAdd(d.terms + 3, (double)ent);
+            atomicAdd(d.terms + 2 * GPI_REPLICAS + blockIdx.x % GPI_REPLICAS, (double)lx);
+            atomicAdd(d.terms + 3 * GPI_REPLICAS + blockIdx.x % GPI_REPLICAS, (double)ent);
         }
     }
 }

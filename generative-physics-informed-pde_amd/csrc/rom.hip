@@ -185,7 +185,7 @@ __global__ __launch_bounds__(64) void rom_kernel(gpi_rom_desc d, RomDims D) {
     }
     if (d.mode == GPI_ROM_LOGLIK) {
         Lsum = wave_sum(Lsum);
-        if (lane == 0 && d.loss_acc) atomicAdd(d.loss_acc, (double)Lsum);
+        if (lane == 0 && d.loss_acc) atomicAdd(d.loss_acc + blockIdx.x % GPI_REPLICAS, (double)Lsum);
     }
     if (d.mode == GPI_ROM_FORWARD) return;
     __syncthreads();

@@ -17,6 +17,7 @@ GPI_MAX_CIN = 32
 GPI_MAX_COUT = 8
 GPI_MAX_REDUCE_ITEMS = 48
 GPI_MAX_GEMM_ITEMS = 12
+GPI_REPLICAS = 32
 
 EPI_STORE, EPI_STORE_STATS, EPI_GAUSS_LOSS = 0, 1, 2
 HEAD_ENC, HEAD_REPARAM, HEAD_QZ, HEAD_LATENT, HEAD_GP = 0x01, 0x02, 0x04, 0x08, 0x10
@@ -47,12 +48,13 @@ class CodecCtx(C.Structure):
     _fields_ = [('params', vp), ('ws', vp), ('stats', vp), ('gacc', vp), ('wpart', vp),
                 ('ext_in', vp), ('ext_idx', vp), ('ext_stride', i64),
                 ('tgt', vp * GPI_MAX_GROUPS), ('tgt_idx', vp * GPI_MAX_GROUPS),
-                ('loss_scale', f32 * GPI_MAX_GROUPS), ('loss_acc', vp), ('bn_eps', f32),
+                ('loss_scale', f32 * GPI_MAX_GROUPS), ('loss_acc', vp), ('n_stats', i64), ('bn_eps', f32),
                 ('groups', Groups)]
 
 
 class ReduceItem(C.Structure):
-    _fields_ = [('part_off', i64), ('w_off', i64), ('blocks', i32), ('numel', i32)]
+    _fields_ = [('part_off', i64), ('w_off', i64), ('blocks', i32), ('numel', i32), ('row_stride', i32),
+                ('_pad', i32)]
 
 
 class HeadDesc(C.Structure):

@@ -23,6 +23,7 @@ from .plan import Arena, encoder_program, decoder_program
 
 ENT_CONST = 0.5 * (math.log(2 * math.pi) + 1)
 N_TERMS = 16
+R = L.GPI_REPLICAS
 # term slots in the fp64 scratch
 T_LX0 = 0          # decoder Gaussian log-lik per group (0..3)
 T_KL_ENC, T_KL_Q, T_LOGL_X, T_ENT, T_LOGL_Y = 4, 5, 6, 7, 8
@@ -53,7 +54,8 @@ class Workspace(object):
 
     def materialize(self, device):
         self.t_ws = torch.zeros(max(self.ws.size, 64), dtype=torch.float32, device=device)
-        self.t_scr = torch.zeros(N_TERMS + self.stats.size * L.GPI_MAX_GROUPS * 4 + 4, dtype=torch.float64,
+        self.n_stats = max(self.stats.size, 1)
+        self.t_scr = torch.zeros(N_TERMS * R + R * self.n_stats * L.GPI_MAX_GROUPS * 4 + 4, dtype=torch.float64,
                                  device=device)
         self.t_parts = torch.zeros(max(self.parts.size, 64), dtype=torch.float32, device=device)
         self.t_flag = torch.zeros(4, dtype=torch.int32, device=device)
@@ -69,14 +71,16 @@ class Workspace(object):
 
     @property
     def terms(self):
-        return self.t_scr[:N_TERMS]
+        """[N_TERMS] term sums (replica copies folded)."""
+        return self.t_scr[:N_TERMS * R].view(N_TERMS, R).sum(1)
 
     def term_ptr(self, k):
-        return C.c_void_p(self.t_scr.data_ptr() + 8 * k)
+        """Term slot k: GPI_REPLICAS consecutive fp64 accumulators."""
+        return C.c_void_p(self.t_scr.data_ptr() + 8 * k * R)
 
     @property
     def stats_ptr(self):
-        return C.c_void_p(self.t_scr.data_ptr() + 8 * N_TERMS)
+        return C.c_void_p(self.t_scr.data_ptr() + 8 * N_TERMS * R)
 
     def zero_scratch(self):
         self.t_scr.zero_()
@@ -93,6 +97,7 @@ def make_ctx(ws, flat, group_sizes):
     c.ext_idx = None
     c.ext_stride = 0
     c.loss_acc = ws.term_ptr(T_LX0).value
+    c.n_stats = ws.n_stats
     c.bn_eps = 1e-5
     c.groups = groups_struct(group_sizes)
     for g in range(L.GPI_MAX_GROUPS):
@@ -102,6 +107,15 @@ def make_ctx(ws, flat, group_sizes):
 
 def _lib():
     return L.lib()
+
+
+def run_reduce(items, ws, flat, st):
+    """gpi_wgrad_reduce over a Python list of ReduceItem, in launches of <= GPI_MAX_REDUCE_ITEMS."""
+    for k in range(0, len(items), L.GPI_MAX_REDUCE_ITEMS):
+        part = items[k:k + L.GPI_MAX_REDUCE_ITEMS]
+        arr = (L.ReduceItem * len(part))(*part)
+        _run(_lib().gpi_wgrad_reduce, arr, len(part), C.c_void_p(ws.t_parts.data_ptr()),
+             C.c_void_p(flat.gacc.data_ptr()), st, what='wgrad reduce')
 
 
 def _run(fn, *args, what=None):
@@ -200,7 +214,7 @@ class ElboEngine(object):
         if self.ep is not None:
             items += self.ep.reduce_items(offE)
         items += self.dp.reduce_items(offD)
-        self.reduce_items = (L.ReduceItem * len(items))(*items)
+        self.reduce_items = items
         gi = []
         B = self.B
 
@@ -238,6 +252,8 @@ class ElboEngine(object):
             r.dmu = None
             self.rom = r
         self._fixed = (self.B_u, self.N_s)
+        self._side = None
+        self._pending_join = False
 
     # ------------------------------------------------------------------
     def eps_z(self):
@@ -276,11 +292,29 @@ class ElboEngine(object):
                  what='encoder forward')
         _run(lib.gpi_head_forward, C.byref(self.head), C.c_void_p(self.flat.P.data_ptr()),
              C.c_void_p(self.ws.t_ws.data_ptr()), st, what='head forward')
+        if self.N_s > 0:
+            # the ROM solve only feeds the head backward: run it on a side stream,
+            # concurrently with the decoder (fork here, join in backward / value)
+            main = torch.cuda.current_stream()
+            if self._side is None:
+                self._side = torch.cuda.Stream(device=main.device)
+                self._ev_fork, self._ev_join = torch.cuda.Event(), torch.cuda.Event()
+            self._ev_fork.record(main)
+            self._side.wait_event(self._ev_fork)
+            _run(lib.gpi_rom, C.byref(self.rom), C.c_void_p(self._side.cuda_stream), what='rom')
+            self._ev_join.record(self._side)
+            self._pending_join = True
         _run(lib.gpi_codec_forward, self.dec_descs, len(self.dec_descs), C.byref(self.dctx), st,
              what='decoder forward')
-        if self.N_s > 0:
-            _run(lib.gpi_rom, C.byref(self.rom), st, what='rom')
-        return self.elbo_value() if compute_value else None
+        if compute_value:
+            self._join()
+            return self.elbo_value()
+        return None
+
+    def _join(self):
+        if self._pending_join:
+            torch.cuda.current_stream().wait_event(self._ev_join)
+            self._pending_join = False
 
     def elbo_value(self):
         t = self.ws.terms
@@ -318,14 +352,13 @@ class ElboEngine(object):
         st = stream if stream is not None else L.stream_handle()
         _run(lib.gpi_codec_backward, self.dec_descs, len(self.dec_descs), C.byref(self.dctx), st,
              what='decoder backward')
+        self._join()
         _run(lib.gpi_head_backward, C.byref(self.head), C.c_void_p(self.flat.P.data_ptr()),
              C.c_void_p(self.ws.t_ws.data_ptr()), C.c_void_p(self.flat.gacc.data_ptr()), st, what='head backward')
         if self.ep is not None:
             _run(lib.gpi_codec_backward, self.enc_descs, len(self.enc_descs), C.byref(self.ectx), st,
                  what='encoder backward')
-        _run(lib.gpi_wgrad_reduce, self.reduce_items, len(self.reduce_items),
-             C.c_void_p(self.ws.t_parts.data_ptr()), C.c_void_p(self.flat.gacc.data_ptr()), st,
-             what='wgrad reduce')
+        run_reduce(self.reduce_items, self.ws, self.flat, st)
         _run(lib.gpi_outer_gemm, self.gemm_items, len(self.gemm_items), C.c_void_p(self.ws.t_ws.data_ptr()),
              C.c_void_p(self.flat.gacc.data_ptr()), st, what='outer gemm')
 
@@ -378,7 +411,7 @@ class EncoderEngine(object):
         self.ctx = make_ctx(ws, flat, [self.B])
         self.ctx.ext_stride = self.p.input.per_sample
         items = self.p.reduce_items(off)
-        self.reduce_items = (L.ReduceItem * len(items))(*items)
+        self.reduce_items = items
         gi = []
         for a, c, b in ((hb['dzmu'], h.mu_w, h.mu_b), (hb['dzls'], h.ls_w, h.ls_b)):
             it = L.GemmItem(a_off=a, b_off=hb['hpre'], c_off=c, bias_off=b, S=self.B, M=dz, N=d_feat, lda=dz,
@@ -410,8 +443,7 @@ class EncoderEngine(object):
         _run(lib.gpi_head_backward, C.byref(self.head), C.c_void_p(self.flat.P.data_ptr()),
              C.c_void_p(self.ws.t_ws.data_ptr()), C.c_void_p(self.flat.gacc.data_ptr()), st, what='head backward')
         _run(lib.gpi_codec_backward, self.descs, len(self.descs), C.byref(self.ctx), st, what='encoder backward')
-        _run(lib.gpi_wgrad_reduce, self.reduce_items, len(self.reduce_items), C.c_void_p(self.ws.t_parts.data_ptr()),
-             C.c_void_p(self.flat.gacc.data_ptr()), st, what='wgrad reduce')
+        run_reduce(self.reduce_items, self.ws, self.flat, st)
         _run(lib.gpi_outer_gemm, self.gemm_items, len(self.gemm_items), C.c_void_p(self.ws.t_ws.data_ptr()),
              C.c_void_p(self.flat.gacc.data_ptr()), st, what='outer gemm')
 
@@ -447,7 +479,7 @@ class DecoderEngine(object):
         self.head, self.hb = h, hb
         self.ctx = make_ctx(ws, flat, [self.B])
         items = self.p.reduce_items(off)
-        self.reduce_items = (L.ReduceItem * len(items))(*items)
+        self.reduce_items = items
         self.gemm_items = (L.GemmItem * 1)(L.GemmItem(a_off=h.glat, b_off=hb['z'], c_off=h.lat_w, bias_off=h.lat_b,
                                                       S=self.B, M=d_lat, N=dz, lda=d_lat, ldb=dz, flags=0))
         o = self.p.output
@@ -470,8 +502,7 @@ class DecoderEngine(object):
         _run(lib.gpi_codec_backward, self.descs, len(self.descs), C.byref(self.ctx), st, what='decoder backward')
         _run(lib.gpi_head_backward, C.byref(self.head), C.c_void_p(self.flat.P.data_ptr()),
              C.c_void_p(self.ws.t_ws.data_ptr()), C.c_void_p(self.flat.gacc.data_ptr()), st, what='latent map bwd')
-        _run(lib.gpi_wgrad_reduce, self.reduce_items, len(self.reduce_items), C.c_void_p(self.ws.t_parts.data_ptr()),
-             C.c_void_p(self.flat.gacc.data_ptr()), st, what='wgrad reduce')
+        run_reduce(self.reduce_items, self.ws, self.flat, st)
         _run(lib.gpi_outer_gemm, self.gemm_items, len(self.gemm_items), C.c_void_p(self.ws.t_ws.data_ptr()),
              C.c_void_p(self.flat.gacc.data_ptr()), st, what='outer gemm')
         return self.ws.view(self.hb['dzmu'], self.B, self.dz).clone()

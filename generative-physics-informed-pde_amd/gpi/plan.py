@@ -145,21 +145,33 @@ class CodecProgram(object):
             L.check(L.lib().gpi_conv_blocks(C.byref(d), C.byref(groups), C.byref(nb)), 'gpi_conv_blocks(%s)' % op.name)
             op.blocks = nb.value
             op.numel = op.cout * op.cin * op.k * op.k
-            d.wpart_off = parts.alloc(op.blocks * op.numel) if grad else -1
+            op.rowlen = op.numel + (2 * op.cin if op.bn is not None else 0)
+            d.wpart_off = parts.alloc(op.blocks * op.rowlen) if grad else -1
             op.desc = d
             descs.append(d)
         arr = (L.ConvDesc * len(descs))(*descs)
         return arr
 
     def reduce_items(self, param_offset):
+        """Slab reductions: the conv weight, then the input BN's (dgamma, dbeta) that
+        follow it in every slab row (one item when gamma/beta are adjacent parameters)."""
         items = []
-        for op in self.ops:
+
+        def item(part, dst, numel, stride, blocks):
             it = L.ReduceItem()
-            it.part_off = op.desc.wpart_off
-            it.w_off = param_offset(op.w)
-            it.blocks = op.blocks
-            it.numel = op.numel
+            it.part_off, it.w_off, it.numel, it.row_stride, it.blocks = part, dst, numel, stride, blocks
             items.append(it)
+
+        for op in self.ops:
+            base = op.desc.wpart_off
+            item(base, param_offset(op.w), op.numel, op.rowlen, op.blocks)
+            if op.bn is not None:
+                g, b = param_offset(op.bn + '.weight'), param_offset(op.bn + '.bias')
+                if b == g + op.cin:
+                    item(base + op.numel, g, 2 * op.cin, op.rowlen, op.blocks)
+                else:
+                    item(base + op.numel, g, op.cin, op.rowlen, op.blocks)
+                    item(base + op.numel + op.cin, b, op.cin, op.rowlen, op.blocks)
         return items
 
 

@@ -39,6 +39,11 @@ extern "C" {
 #define GPI_MAX_COUT 8
 #define GPI_MAX_REDUCE_ITEMS 48
 #define GPI_MAX_GEMM_ITEMS 12
+/* Cross-workgroup scalar sums (BN statistics, loss / ELBO terms) are spread
+ * over GPI_REPLICAS copies indexed by workgroup % GPI_REPLICAS so that
+ * thousands of workgroups never serialise on one fp64 atomic address; the
+ * reader sums the replicas. */
+#define GPI_REPLICAS 32
 
 /* Conv epilogues */
 #define GPI_EPI_STORE 0        /* store raw output */
@@ -88,14 +93,15 @@ typedef struct gpi_conv_desc {
     int32_t gout_mode;             /* backward: 0 = BN-backward of the S buffer, 1 = direct gradient */
     int64_t gout_off;              /* S buffer (mode 0) / gradient buffer (mode 1), output layout */
     int64_t gin_off;               /* S buffer / gradient of the input (input layout), or -1 */
-    int64_t wpart_off;             /* weight-gradient partial slab (one row per block) */
+    int64_t wpart_off;             /* partial slab, one row per workgroup:
+                                      [cout*cin*k*k dW][cin dgamma][cin dbeta] (BN part only if in_bn) */
 } gpi_conv_desc;
 
 /* Per-call pointers shared by all codec operators. */
 typedef struct gpi_codec_ctx {
     const float* params;           /* flat fp32 parameters */
     float* ws;                     /* workspace (activations, S / gradient buffers) */
-    gpi_stat* stats;               /* BN statistics records [stat][group] */
+    gpi_stat* stats;               /* BN statistics records [GPI_REPLICAS][stat][GPI_MAX_GROUPS] */
     double* gacc;                  /* fp64 gradient accumulator, parallel to params */
     float* wpart;                  /* weight-gradient partial slabs */
     const float* ext_in;           /* external input (e.g. the unlabeled image pool) */
@@ -104,15 +110,17 @@ typedef struct gpi_codec_ctx {
     const float* tgt[GPI_MAX_GROUPS];      /* Gaussian-loss targets per group */
     const int32_t* tgt_idx[GPI_MAX_GROUPS];/* target row per sample of the group (NULL: identity) */
     float loss_scale[GPI_MAX_GROUPS];      /* d(-elbo)/d(logL): 1, or 1/batch when normalize */
-    double* loss_acc;              /* [n_groups] sum of Gaussian log-likelihood per group */
+    double* loss_acc;              /* [GPI_MAX_GROUPS][GPI_REPLICAS] Gaussian log-likelihood sums */
+    int64_t n_stats;               /* stat records per replica */
     float bn_eps;                  /* 1e-5 (torch default) */
     gpi_groups groups;
 } gpi_codec_ctx;
 
-/* Weight-gradient reduction item: gacc[w_off + i] += sum_b wpart[part_off + b*numel + i]. */
+/* Slab reduction item: gacc[w_off + i] += sum_b wpart[part_off + b*row_stride + i], i < numel. */
 typedef struct gpi_reduce_item {
     int64_t part_off, w_off;
     int32_t blocks, numel;
+    int32_t row_stride, _pad;      /* floats between consecutive slab rows */
 } gpi_reduce_item;
 
 /* Dense (per-sample) part of the ELBO: encoder FC / ReLU / split heads
@@ -148,7 +156,7 @@ typedef struct gpi_head_desc {
     int64_t dhpre;                   /* [n_enc, d_feat] backward delta */
     float kl_scale_enc, kl_scale_q, lx_scale, _fpad;
     /* fp64 term accumulators (terms[0..]): KL_enc, KL_q, logL_X, entropy */
-    double* terms;
+    double* terms;                   /* [4][GPI_REPLICAS] */
 } gpi_head_desc;
 
 /* Batched outer-product GEMM for shared dense-layer gradients:
@@ -188,7 +196,7 @@ typedef struct gpi_rom_desc {
     float* gx;                 /* [n, 2 nc^2] d/dx out */
     int64_t gx_stride;
     double* gacc_logsig;       /* fp64 accumulator for d/d logsigma_y (LOGLIK) */
-    double* loss_acc;          /* sum log-lik (LOGLIK) */
+    double* loss_acc;          /* [GPI_REPLICAS] sum log-lik (LOGLIK) */
     int32_t* flag;             /* set to 1 if any kappa <= 1e-12 (ROM.py:74-76), checked lazily */
     float* uc;                 /* optional [n, (nc+1)^2] coarse solution */
 } gpi_rom_desc;
