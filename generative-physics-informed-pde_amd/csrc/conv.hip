@@ -1,57 +1,101 @@
 // DenseNet codec convolutions for gfx950 (wave64, 256-thread workgroups).
 //
-// Forward (one launch per conv of bottleneck/codec.py):
-//   out = conv(act(in)),  act = relu(BN_train(.)) | identity
-//   - the input tile + halo of every input channel is staged in LDS already
-//     activated (BN scale/shift from the replicated fp64 batch sums written by
-//     the producer's epilogue, ReLU, zero padding applied AFTER the
-//     activation), nearest x2 upsampling folded into the addressing;
-//   - global loads are issued in batches of 8 per thread before any use, so a
-//     workgroup pays a few memory round trips, not one per element;
-//   - weights are staged transposed ([ci][tap][co]) so one LDS vector read
-//     broadcasts the taps of all output channels;
-//   - epilogue: raw store + per-channel sum / sum^2 (block reduction, fp64
-//     atomics into one of GPI_REPLICAS slots) for the consumer's train-mode BN,
-//     or the fused Gaussian log-likelihood of the decoder output.
-// Backward (one launch per conv, reverse order):
-//   - g_out = BN-backward of the accumulated S buffer of the output
-//     (S = sum over BN consumers c of gamma_c dL/d(bn_c); the per-channel means
-//     of S and S * xhat come from the consumers' replicated sums) or a direct
-//     gradient;
-//   - weight-gradient partial per workgroup (slab row, reduced by
-//     gpi_wgrad_reduce together with the dgamma/dbeta partials);
-//   - input gradient by gather: one thread per owned input pixel computes all
-//     input channels at once (weights staged [co][tap][ci]), then the ReLU mask,
-//     S_in (+)= gamma * dbn with all its global loads in flight together.
+// Every launch is one conv of bottleneck/codec.py.  A workgroup owns one tile:
+// `th` whole output rows of ONE sample, so every (channel, tile) operand is a
+// single contiguous run of global memory whose cache lines are used whole.
+// Operands live in LDS as row images with a zero halo of HALO columns on each
+// side (pitch = width + 2 HALO), filled by 16-byte LDS-DMA (global_load_lds);
+// halo chunks and rows outside the plane read a zero page.  A workgroup runs
+// in four phases so that it pays ONE global round trip before it computes:
+//   1. issue every global read at once: the LDS images (input, output
+//      gradient, BN-backward operand), the weights, the 32 replicas of the BN
+//      batch sums and the input-gradient operands (registers);
+//   2. BN coefficients from the fp64 sums (train mode, biased variance);
+//   3. activation transforms in LDS, in place (BN + ReLU of the input image,
+//      padding untouched so it stays zero AFTER the activation; BN-backward of
+//      the output gradient);
+//   4. compute, epilogue.
+// Forward (VALU, one output pixel per thread): out = conv(act(in)); epilogue
+// stores + per-channel sum / sum^2 into one of GPI_REPLICAS fp64 slots (the
+// consumer's train-mode BN) or the fused Gaussian log-likelihood of the decoder
+// output.  Backward (MFMA): weight-gradient partial per workgroup (slab row,
+// reduced by gpi_wgrad_reduce with the dgamma/dbeta partials) and the input
+// gradient with the ReLU mask and S_in (+)= gamma * dbn.
 #include "common.h"
 
 using namespace gpi;
 
 namespace {
 
-struct ConvGeom {
-    int spb, th, tw, tiles_y, tiles_x, nblocks;
-    int rh, rw;   // activated input region per (sample, channel)
-    int gh, gw;   // output-gradient region per (sample, channel)
+constexpr int HALO = 4;   // zero halo columns on each side of an LDS row image
+
+// 256 zero bytes in device memory: the source of LDS-DMA padding lanes and of
+// the stat loads of unused lanes.
+__device__ __attribute__((aligned(256))) float g_zero_page[64];
+
+// q = e / d without a division: e * d < 2^32 (checked on the host).
+struct Div {
+    uint32_t m, one;
 };
+
+Div mkdiv(int d) {
+    Div v;
+    v.one = d == 1;
+    v.m = d == 1 ? 0u : (uint32_t)(((1ull << 32) + (uint64_t)d - 1) / (uint64_t)d);
+    return v;
+}
+
+__device__ __forceinline__ int dq(int e, Div v) { return v.one ? e : (int)__umulhi((uint32_t)e, v.m); }
+
+// Phase stamps of the timing build (make timing): thread 0 of workgroup b writes the
+// shader clock at phase boundary i to g_phase[b % 4096][i], the 100 MHz real-time
+// clock at entry / exit to g_rt[b % 4096][0 / 1].  Compiled out of the product.
+#ifdef GPI_PHASE_TIMING
+__device__ unsigned long long g_phase[4096 * 16];
+__device__ unsigned long long g_rt[4096 * 2];
+#define PHASE(i)                                                                                     \
+    do {                                                                                             \
+        if (threadIdx.x == 0) g_phase[(blockIdx.x & 4095) * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#define RTSTAMP(i)                                                                                 \
+    do {                                                                                           \
+        if (threadIdx.x == 0) g_rt[(blockIdx.x & 4095) * 2 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define PHASE(i) \
+    do {         \
+    } while (0)
+#define RTSTAMP(i) \
+    do {           \
+    } while (0)
+#endif
 
 __host__ __device__ inline int fdiv2(int x) { return x >= 0 ? x / 2 : -((-x + 1) / 2); }
 __host__ __device__ inline int cdiv2(int x) { return -fdiv2(-x); }
+__host__ __device__ inline int pad256(int n) { return (n + 255) & ~255; }
 
-// input region needed by output positions [o0, o0 + t)
-__host__ __device__ inline void in_region(int k, int s, int up, int pad, int o0, int t, int& i0, int& len) {
+// Tile geometry: tile t of sample b covers output rows [t*th, (t+1)*th), all columns.
+struct ConvGeom {
+    int th, tiles, nblocks;
+    int rh, P;      // input image: rows [iy0, iy0 + rh), pitch P = w_in + 2H
+    int gh, PG;     // output-gradient image: rows [gy0, gy0 + gh), pitch PG = w_out + 2H
+    int ph;         // owned input rows (backward)
+    Div d_in4, d_P4, d_g4, d_PG4, d_cin, d_cout, d_win, d_tp, d_wout;
+};
+
+// first input row and row count of the input image of output rows [o0, o0 + t)
+__host__ __device__ inline void in_rows(int k, int s, int up, int pad, int o0, int t, int& i0, int& len) {
     if (up) {
-        int a = o0 - pad, b = o0 + t - 1 - pad + k - 1;
-        i0 = fdiv2(a);
-        len = fdiv2(b) - i0 + 1;
+        i0 = fdiv2(o0 - pad);
+        len = fdiv2(o0 + t - 1 - pad + k - 1) - i0 + 1;
     } else {
         i0 = o0 * s - pad;
         len = (t - 1) * s + k;
     }
 }
 
-// output-gradient region needed by the input pixels owned by the tile
-__host__ __device__ inline void g_region(int k, int s, int pad, int o0, int t, int& g0, int& len) {
+// output-gradient rows needed by the input rows owned by the tile (and by its own rows)
+__host__ __device__ inline void g_rows(int k, int s, int pad, int o0, int t, int& g0, int& len) {
     if (s == 2) {
         g0 = cdiv2(2 * o0 + pad - k + 1);
         len = fdiv2(2 * o0 + 2 * t - 1 + pad) - g0 + 1;
@@ -61,75 +105,150 @@ __host__ __device__ inline void g_region(int k, int s, int pad, int o0, int t, i
     }
 }
 
-// input pixels whose gradient this output tile owns (a partition of the input)
-__host__ __device__ inline void owned(int s, int up, int o0, int t, int& p0, int& len) {
+// input rows whose gradient the tile owns (a partition of the input rows)
+__host__ __device__ inline void owned_rows(int s, int up, int o0, int t, int& p0, int& len) {
     if (up) { p0 = o0 / 2; len = t / 2; }
     else if (s == 2) { p0 = 2 * o0; len = 2 * t; }
     else { p0 = o0; len = t; }
-}
-
-int gcd_i(int a, int b) {
-    while (b) { int t = a % b; a = b; b = t; }
-    return a;
 }
 
 bool conv_geom(const gpi_conv_desc& d, const gpi_groups& g, ConvGeom& G) {
     if (g.n_groups < 1 || g.n_groups > GPI_MAX_GROUPS) return false;
     if (d.cin < 1 || d.cin > GPI_MAX_CIN || d.cout < 1 || d.cout > GPI_MAX_COUT) return false;
     if (d.k != 1 && d.k != 3 && d.k != 5 && d.k != 7) return false;
+    if (d.pad > HALO || (d.w_in & 3) || (d.w_out & 3) || d.w_out > 256) return false;
     if (d.upsample) {
         if (d.stride != 1 || d.h_out != 2 * d.h_in || d.w_out != 2 * d.w_in || d.pad != d.k / 2) return false;
     } else if (d.stride == 2) {
-        if (d.h_in != 2 * d.h_out || d.w_in != 2 * d.w_out) return false;
+        if (d.h_in != 2 * d.h_out || d.w_in != 2 * d.w_out || d.pad != d.k / 2) return false;
     } else if (d.stride == 1) {
         if (d.h_in != d.h_out || d.w_in != d.w_out || d.pad != d.k / 2) return false;
     } else {
         return false;
     }
-    const int plane = d.h_out * d.w_out;
-    int B = g.start[g.n_groups] - g.start[0];
+    const int B = g.start[g.n_groups] - g.start[0];
     if (g.start[0] != 0 || B <= 0) return false;
-    if (plane >= 256) {
-        G.tw = d.w_out >= 16 ? 16 : d.w_out;
-        G.th = 256 / G.tw;
-        if (G.th > d.h_out) G.th = d.h_out;
-        G.spb = 1;
-    } else {
-        G.th = d.h_out;
-        G.tw = d.w_out;
-        int spb = 256 / plane;
-        int gg = 0;
-        for (int k = 0; k < g.n_groups; ++k) gg = gcd_i(gg, g.start[k + 1] - g.start[k]);
-        while (spb > 1 && (gg % spb)) --spb;
-        G.spb = spb;
-    }
-    if (d.upsample && ((G.th & 1) || (G.tw & 1))) return false;
-    G.tiles_y = (d.h_out + G.th - 1) / G.th;
-    G.tiles_x = (d.w_out + G.tw - 1) / G.tw;
-    if (d.h_out % G.th || d.w_out % G.tw) return false;
-    G.nblocks = (B / G.spb) * G.tiles_y * G.tiles_x;
+    const int target = d.stride == 2 ? 128 : 256;   // output pixels per tile
+    G.th = target / d.w_out;
+    if (G.th < 1) G.th = 1;
+    if (G.th > d.h_out) G.th = d.h_out;
+    while (d.h_out % G.th) --G.th;
+    if (d.upsample && (G.th & 1)) return false;
+    G.tiles = d.h_out / G.th;
+    G.nblocks = B * G.tiles;
     int i0;
-    in_region(d.k, d.stride, d.upsample, d.pad, 0, G.th, i0, G.rh);
-    in_region(d.k, d.stride, d.upsample, d.pad, 0, G.tw, i0, G.rw);
-    if (d.upsample) { G.rh += 1; G.rw += 1; }   // parity-independent bound
-    int g0;
-    g_region(d.k, d.stride, d.pad, 0, G.th, g0, G.gh);
-    g_region(d.k, d.stride, d.pad, 0, G.tw, g0, G.gw);
+    in_rows(d.k, d.stride, d.upsample, d.pad, 0, G.th, i0, G.rh);
+    if (d.upsample) G.rh += 1;   // parity-independent bound
+    G.P = d.w_in + 2 * HALO;
+    g_rows(d.k, d.stride, d.pad, 0, G.th, i0, G.gh);
+    G.PG = d.w_out + 2 * HALO;
+    owned_rows(d.stride, d.upsample, 0, G.th, i0, G.ph);
+    // exactness of the magic divisions: largest dividend * divisor < 2^32
+    const uint64_t lim = 1ull << 32;
+    const uint64_t in4 = (uint64_t)G.rh * G.P / 4, g4 = (uint64_t)G.gh * G.PG / 4;
+    const uint64_t ein = in4 * d.cin, eg = g4 * d.cout, eo = (uint64_t)G.ph * d.w_in;
+    if (ein * in4 >= lim || in4 * (G.P / 4) >= lim || eg * g4 >= lim || g4 * (G.PG / 4) >= lim ||
+        eo * d.w_in >= lim || 256ull * G.th * d.w_out >= lim)
+        return false;
+    G.d_in4 = mkdiv((int)in4);
+    G.d_P4 = mkdiv(G.P / 4);
+    G.d_g4 = mkdiv((int)g4);
+    G.d_PG4 = mkdiv(G.PG / 4);
+    G.d_cin = mkdiv(d.cin);
+    G.d_cout = mkdiv(d.cout);
+    G.d_win = mkdiv(d.w_in);
+    G.d_tp = mkdiv(G.th * d.w_out);
+    G.d_wout = mkdiv(d.w_out);
     return true;
 }
 
-// Sum the GPI_REPLICAS copies of the stat records [stat0, stat0 + nch) of group grp into
-// dst[4 * nch] (LDS, fp64: sum, sumsq, ssum, sxsum).  Caller zeroes dst and syncs around.
-__device__ __forceinline__ void gather_stats(const gpi_codec_ctx& c, int64_t stat0, int nch, int grp, double* dst) {
-    const int n = nch * GPI_REPLICAS;
-    for (int e = threadIdx.x; e < n; e += blockDim.x) {
-        const int ch = e / GPI_REPLICAS, r = e - ch * GPI_REPLICAS;
-        const gpi_stat st = c.stats[((int64_t)r * c.n_stats + stat0 + ch) * GPI_MAX_GROUPS + grp];
-        atomicAdd(&dst[4 * ch + 0], st.sum);
-        atomicAdd(&dst[4 * ch + 1], st.sumsq);
-        atomicAdd(&dst[4 * ch + 2], st.ssum);
-        atomicAdd(&dst[4 * ch + 3], st.sxsum);
+__device__ __forceinline__ void glds4(const float* g, float* lds_wave_base) {
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                     (__attribute__((address_space(3))) void*)lds_wave_base, 4, 0, 0);
+}
+
+__device__ __forceinline__ void glds16(const float* g, float* lds_wave_base) {
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                     (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+// dst[e] = *src(e) for e in [0, total) by 4-byte LDS-DMA; src(e) == nullptr reads the
+// zero page.  dst is padded to a multiple of 256 floats (whole waves write).
+template <typename Src>
+__device__ __forceinline__ void stage(float* dst, int total, Src src) {
+    const int wb = threadIdx.x & ~63;
+    for (int e0 = 0; e0 < total; e0 += 256) {
+        if (e0 + wb < total) {
+            const int e = e0 + (int)threadIdx.x;
+            const float* p = e < total ? src(e) : nullptr;
+            glds4(p ? p : g_zero_page, dst + e0 + wb);
+        }
     }
+}
+
+// Row image of nq planes (plane q at plane(q), an h x w plane): rows [r0, r0 + nr),
+// LDS pitch w + 2H, chunk e (16 B) of plane q = e / (nr * P / 4).  16-byte LDS-DMA;
+// halo chunks and rows outside [0, h) read the zero page.  dst padded to 256 floats.
+template <typename Plane>
+__device__ __forceinline__ void stage_img(float* dst, int nq, int nr, int P, Div d_q4, Div d_p4, int r0, int h,
+                                          int w, Plane plane) {
+    const int P4 = P >> 2, plane4 = nr * P4, total = nq * plane4;
+    const int wb = threadIdx.x & ~63;
+    for (int e0 = 0; e0 < total; e0 += 256) {
+        if (e0 + wb < total) {
+            const int e = e0 + (int)threadIdx.x;
+            const float* p = nullptr;
+            if (e < total) {
+                const int q = dq(e, d_q4), rem = e - q * plane4;
+                const int r = dq(rem, d_p4), col = 4 * (rem - r * P4) - HALO;
+                const int row = r0 + r;
+                if (row >= 0 && row < h && col >= 0 && col < w) p = plane(q) + row * w + col;
+            }
+            glds16(p ? p : g_zero_page, dst + 4 * (e0 + wb));
+        }
+    }
+}
+
+// Sums of the GPI_REPLICAS copies of the stat records of channels [0, na) of stat
+// a and [0, nb) of stat b (group grp) into LDS: threads 8 * ch + 4 * h + k own field
+// k of channel ch, replicas [16 h, 16 h + 16), all loads in flight at once; the two
+// halves meet by a lane exchange.  na + nb <= 32.
+constexpr int STAT_HALF = GPI_REPLICAS / 2;
+struct StatLoad {
+    double v[STAT_HALF];
+    double* out;
+};
+
+__device__ __forceinline__ void stat_issue(const gpi_codec_ctx& c, int grp, int64_t sa, int na, double* da,
+                                           int64_t sb, int nb, double* db, StatLoad& L) {
+    const int t = threadIdx.x, k = t & 3, h = (t >> 2) & 1, ch = t >> 3;
+    const double* p = (const double*)g_zero_page;
+    int64_t step = 0;
+    L.out = nullptr;
+    const int64_t rstride = c.n_stats * GPI_MAX_GROUPS * 4;   // doubles per replica
+    if (ch < na) {
+        p = &c.stats[(sa + ch) * GPI_MAX_GROUPS + grp].sum + k + h * STAT_HALF * rstride;
+        step = rstride;
+        L.out = da + 4 * ch + k;
+    } else if (ch - na < nb) {
+        p = &c.stats[(sb + ch - na) * GPI_MAX_GROUPS + grp].sum + k + h * STAT_HALF * rstride;
+        step = rstride;
+        L.out = db + 4 * (ch - na) + k;
+    }
+#pragma unroll
+    for (int r = 0; r < STAT_HALF; ++r) L.v[r] = p[r * step];
+}
+
+__device__ __forceinline__ void stat_finish(StatLoad& L) {
+    double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+    for (int r = 0; r < STAT_HALF; r += 2) {
+        s0 += L.v[r];
+        s1 += L.v[r + 1];
+    }
+    double s = s0 + s1;
+    s += __shfl_xor(s, 4, 64);
+    if (L.out && !(threadIdx.x & 4)) *L.out = s;
 }
 
 __device__ __forceinline__ gpi_stat* stat_slot(const gpi_codec_ctx& c, int64_t stat, int grp) {
@@ -143,32 +262,6 @@ __device__ __forceinline__ void mean_invstd(const double* s4, double n, float ep
     if (var < 0.0) var = 0.0;
     mean = (float)m;
     invstd = (float)(1.0 / sqrt(var + (double)eps));
-}
-
-// Fill dst[0, total) (LDS) with f(q, ry, rx), q = e / plane, (ry, rx) the position in the
-// rh x rw plane.  Eight elements per thread are loaded before any is stored, so their
-// global loads are in flight together.
-constexpr int FILL_U = 8;
-template <typename F>
-__device__ __forceinline__ void fill(float* dst, int total, int plane, int rw, F f) {
-    for (int e0 = threadIdx.x; e0 < total; e0 += FILL_U * 256) {
-        float v[FILL_U];
-#pragma unroll
-        for (int u = 0; u < FILL_U; ++u) {
-            const int e = e0 + u * 256;
-            v[u] = 0.f;
-            if (e < total) {
-                const int q = e / plane, pos = e - q * plane;
-                const int ry = pos / rw;
-                v[u] = f(q, ry, pos - ry * rw);
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < FILL_U; ++u) {
-            const int e = e0 + u * 256;
-            if (e < total) dst[e] = v[u];
-        }
-    }
 }
 
 template <int CP>
@@ -193,24 +286,64 @@ __device__ __forceinline__ void fma_vec(float (&acc)[CP], const float* w, float 
 }
 
 struct TileIdx {
-    int sb, oy0, ox0, s0, grp, gsz;
+    int b, oy0, grp, gsz;
 };
 
 __device__ __forceinline__ TileIdx tile_of(const ConvGeom& G, const gpi_groups& g) {
     TileIdx t;
-    const int tiles = G.tiles_y * G.tiles_x;
-    t.sb = blockIdx.x / tiles;
-    const int tt = blockIdx.x - t.sb * tiles;
-    t.oy0 = (tt / G.tiles_x) * G.th;
-    t.ox0 = (tt % G.tiles_x) * G.tw;
-    t.s0 = t.sb * G.spb;
-    t.grp = group_of(g, t.s0);
+    t.b = blockIdx.x / G.tiles;
+    t.oy0 = (blockIdx.x - t.b * G.tiles) * G.th;
+    t.grp = group_of(g, t.b);
     t.gsz = g.start[t.grp + 1] - g.start[t.grp];
     return t;
 }
 
+// Base of input channel in_c0 of the tile's sample (global).  ext input: one
+// dependent index load (the encoder's first conv only).
+__device__ __forceinline__ const float* input_base(const gpi_conv_desc& d, const gpi_codec_ctx& c, int b) {
+    const int HWi = d.h_in * d.w_in;
+    if (d.in_off >= 0) return c.ws + d.in_off + ((int64_t)b * d.in_ctot + d.in_c0) * HWi;
+    return c.ext_in + (int64_t)(c.ext_idx ? c.ext_idx[b] : b) * c.ext_stride + (int64_t)d.in_c0 * HWi;
+}
+
+// In-place BN + ReLU of an input row image (16-byte chunks); halo chunks and rows
+// outside the plane keep their zeros.
+__device__ __forceinline__ void activate_img(float* img, const ConvGeom& G, const gpi_conv_desc& d, int iy0,
+                                             const float* sc, const float* sh) {
+    const int P4 = G.P >> 2, plane4 = G.rh * P4, total = d.cin * plane4;
+    float4* im4 = reinterpret_cast<float4*>(img);
+    for (int e0 = threadIdx.x; e0 < total; e0 += 1024) {
+        float4 v[4];
+        bool ok[4];
+        int ci[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int e = e0 + 256 * u;
+            const int q = dq(e, G.d_in4), rem = e - q * plane4;
+            const int r = dq(rem, G.d_P4), col = 4 * (rem - r * P4) - HALO;
+            const int row = iy0 + r;
+            ok[u] = e < total && row >= 0 && row < d.h_in && col >= 0 && col < d.w_in;
+            ci[u] = q;
+            if (ok[u]) v[u] = im4[e];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (ok[u]) {
+                const float a = sc[ci[u]], b = sh[ci[u]];
+                float4 o;
+                o.x = fmaxf(fmaf(v[u].x, a, b), 0.f);
+                o.y = fmaxf(fmaf(v[u].y, a, b), 0.f);
+                o.z = fmaxf(fmaf(v[u].z, a, b), 0.f);
+                o.w = fmaxf(fmaf(v[u].w, a, b), 0.f);
+                im4[e0 + 256 * u] = o;
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------------- forward
-constexpr int FWD_HDR = 8 * GPI_MAX_CIN + 2 * GPI_MAX_CIN + 64 + 16;   // gst (fp64) | sc | sh | scratch | red
+// header floats: gst fp64 [4*MAX_CIN] | sc | sh [MAX_CIN] | scratch [64] | red [16]
+constexpr int FWD_HDR = 8 * GPI_MAX_CIN + 2 * GPI_MAX_CIN + 64 + 16;
 
 template <int K, int S, int UP, int CP>
 __global__ __launch_bounds__(256) void conv_fwd_kernel(gpi_conv_desc d, gpi_codec_ctx c, ConvGeom G) {
@@ -221,108 +354,115 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(gpi_conv_desc d, gpi_code
     float* sh = sc + GPI_MAX_CIN;
     float* scratch = sh + GPI_MAX_CIN;   // 2*CP*4 <= 64
     float* red = scratch + 64;           // 2*CP <= 16
-    float* wT = smem + FWD_HDR;          // [cin][KK][CP]
-    float* tile = wT + ((d.cin * KK * CP + 3) & ~3);
+    float* wT = smem + pad256(FWD_HDR);  // [cin][KK][CP]
+    const int nw = d.cin * KK * CP;
+    float* img = wT + pad256(nw);        // [cin][rh][P]
 
     const int tid = threadIdx.x;
+    RTSTAMP(0);
+    PHASE(0);
     const TileIdx T = tile_of(G, c.groups);
     const int HWi = d.h_in * d.w_in, HWo = d.h_out * d.w_out;
+    const float* ib = input_base(d, c, T.b);
+    PHASE(1);
 
-    if (d.in_bn) {
-        for (int e = tid; e < 4 * d.cin; e += 256) gst[e] = 0.0;
-        __syncthreads();
-        gather_stats(c, d.in_stat, d.cin, T.grp, gst);
-    }
-    for (int e = tid; e < d.cin * KK * CP; e += 256) {
+    // ---- phase 1: every global read of the tile in flight together
+    stage(wT, nw, [&](int e) -> const float* {
         const int co = e % CP, r = e / CP;
-        wT[e] = co < d.cout ? c.params[d.w_off + (int64_t)co * d.cin * KK + r] : 0.f;
-    }
-    __syncthreads();
-    if (d.in_bn && tid < d.cin) {
-        float mean, inv;
-        mean_invstd(gst + 4 * tid, (double)T.gsz * HWi, c.bn_eps, mean, inv);
-        const float gam = c.params[d.gamma_off + tid], bet = c.params[d.beta_off + tid];
-        sc[tid] = gam * inv;
-        sh[tid] = bet - mean * gam * inv;
-    }
-    __syncthreads();
-
-    int iy0, rh_, ix0, rw_;
-    in_region(K, S, UP, d.pad, T.oy0, G.th, iy0, rh_);
-    in_region(K, S, UP, d.pad, T.ox0, G.tw, ix0, rw_);
-    const int rw = G.rw;
-    const int plane_r = G.rh * rw;
-    const int per_s = d.cin * plane_r;
-    const float* inb = d.in_off >= 0 ? c.ws + d.in_off : nullptr;
-    fill(tile, G.spb * per_s, plane_r, rw, [&](int q, int ry, int rx) -> float {
-        const int s = q / d.cin, ci = q - s * d.cin;
-        const int iy = iy0 + ry, ix = ix0 + rx;
-        if (ry >= rh_ || rx >= rw_ || iy < 0 || iy >= d.h_in || ix < 0 || ix >= d.w_in) return 0.f;
-        const int gs = T.s0 + s;
-        const float* src = inb ? inb + (int64_t)gs * d.in_ctot * HWi
-                               : c.ext_in + (int64_t)(c.ext_idx ? c.ext_idx[gs] : gs) * c.ext_stride;
-        const float x = src[(int64_t)(d.in_c0 + ci) * HWi + iy * d.w_in + ix];
-        return d.in_bn ? fmaxf(fmaf(x, sc[ci], sh[ci]), 0.f) : x;
+        return co < d.cout ? c.params + d.w_off + (int64_t)co * d.cin * KK + r : nullptr;
     });
+    int iy0, rh_;
+    in_rows(K, S, UP, d.pad, T.oy0, G.th, iy0, rh_);
+    stage_img(img, d.cin, G.rh, G.P, G.d_in4, G.d_P4, iy0, d.h_in, d.w_in,
+              [&](int q) -> const float* { return ib + (int64_t)q * HWi; });
+    if (d.in_bn) {
+        float gam = 0.f, bet = 0.f;
+        if (tid < d.cin) {
+            gam = c.params[d.gamma_off + tid];
+            bet = c.params[d.beta_off + tid];
+        }
+        StatLoad L;
+        stat_issue(c, T.grp, d.in_stat, d.cin, gst, 0, 0, nullptr, L);
+        stat_finish(L);
+        __syncthreads();
+        PHASE(2);
+        // ---- phase 2: BN coefficients
+        if (tid < d.cin) {
+            float mean, inv;
+            mean_invstd(gst + 4 * tid, (double)T.gsz * HWi, c.bn_eps, mean, inv);
+            sc[tid] = gam * inv;
+            sh[tid] = bet - mean * gam * inv;
+        }
+        __syncthreads();
+        // ---- phase 3: BN + ReLU in LDS
+        activate_img(img, G, d, iy0, sc, sh);
+    }
     __syncthreads();
+    PHASE(4);
 
-    const int tp = G.th * G.tw;
-    const int s = tid / tp;
-    const int pr = tid - s * tp;
-    const int ty = pr / G.tw, tx = pr - ty * G.tw;
-    const int oy = T.oy0 + ty, ox = T.ox0 + tx;
-    const bool active = (s < G.spb) && oy < d.h_out && ox < d.w_out;
+    // ---- phase 4: compute (the loss target load is in flight meanwhile)
+    const int tp = G.th * d.w_out;
+    const int ty = dq(tid, G.d_wout), tx = tid - ty * d.w_out;
+    const int oy = T.oy0 + ty, ox = tx;
+    const bool active = tid < tp;
+    float tgt = 0.f;
+    if (d.epilogue == GPI_EPI_GAUSS_LOSS && active) {
+        int row = T.b - c.groups.start[T.grp];
+        if (c.tgt_idx[T.grp]) row = c.tgt_idx[T.grp][row];
+        tgt = c.tgt[T.grp][(int64_t)row * HWo + oy * d.w_out + ox];
+    }
+    PHASE(5);
     float acc[CP];
 #pragma unroll
     for (int co = 0; co < CP; ++co) acc[co] = 0.f;
     if (active) {
-        const float* tb = tile + s * per_s;
+        const int plane = G.rh * G.P;
         for (int ci = 0; ci < d.cin; ++ci) {
-            const float* tci = tb + ci * plane_r;
+            const float* tci = img + ci * plane;
             const float* wci = wT + ci * KK * CP;
 #pragma unroll
             for (int ky = 0; ky < K; ++ky) {
                 const int ry = UP ? (fdiv2(oy - d.pad + ky) - iy0) : (ty * S + ky);
+                const float* trow = tci + ry * G.P;
 #pragma unroll
                 for (int kx = 0; kx < K; ++kx) {
-                    const int rx = UP ? (fdiv2(ox - d.pad + kx) - ix0) : (tx * S + kx);
-                    fma_vec<CP>(acc, wci + (ky * K + kx) * CP, tci[ry * rw + rx]);
+                    const int col = UP ? fdiv2(ox - d.pad + kx) + HALO : ox * S - d.pad + kx + HALO;
+                    fma_vec<CP>(acc, wci + (ky * K + kx) * CP, trow[col]);
                 }
             }
         }
     }
+    PHASE(6);
 
-    const int gs = T.s0 + s;
     if (d.epilogue == GPI_EPI_GAUSS_LOSS) {
-        float L = 0.f;
+        float Lv = 0.f;
         if (active) {
             const float mu = acc[0], ls = acc[1];
-            int row = gs - c.groups.start[T.grp];
-            if (c.tgt_idx[T.grp]) row = c.tgt_idx[T.grp][row];
-            const float t = c.tgt[T.grp][(int64_t)row * HWo + oy * d.w_out + ox];
             const float e = expf(-2.f * ls);
-            const float r = t - mu;
-            L = -0.5f * (2.f * ls + r * r * e + GPI_LOG2PI);
+            const float r = tgt - mu;
+            Lv = -0.5f * (2.f * ls + r * r * e + GPI_LOG2PI);
             const float scl = c.loss_scale[T.grp];
-            float* go = c.ws + d.gout_off + (int64_t)gs * 2 * HWo + oy * d.w_out + ox;
+            float* go = c.ws + d.gout_off + (int64_t)T.b * 2 * HWo + oy * d.w_out + ox;
             go[0] = -scl * r * e;
             go[HWo] = scl * (1.f - r * r * e);
             if (d.out_off >= 0) {
-                float* o = c.ws + d.out_off + (int64_t)gs * d.out_ctot * HWo + (int64_t)d.out_c0 * HWo +
+                float* o = c.ws + d.out_off + (int64_t)T.b * d.out_ctot * HWo + (int64_t)d.out_c0 * HWo +
                            oy * d.w_out + ox;
                 o[0] = mu;
                 o[HWo] = ls;
             }
         }
-        float v[1] = {L};
+        float v[1] = {Lv};
         block_sum<1>(v, scratch, red);
         __syncthreads();
         if (tid == 0) atomicAdd(c.loss_acc + T.grp * GPI_REPLICAS + blockIdx.x % GPI_REPLICAS, (double)red[0]);
+        PHASE(7);
+        RTSTAMP(1);
         return;
     }
 
     if (active) {
-        float* o = c.ws + d.out_off + (int64_t)gs * d.out_ctot * HWo + (int64_t)d.out_c0 * HWo + oy * d.w_out + ox;
+        float* o = c.ws + d.out_off + ((int64_t)T.b * d.out_ctot + d.out_c0) * HWo + oy * d.w_out + ox;
 #pragma unroll
         for (int co = 0; co < CP; ++co)
             if (co < d.cout) o[(int64_t)co * HWo] = acc[co];
@@ -342,316 +482,425 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(gpi_conv_desc d, gpi_code
             atomicAdd((tid & 1) ? &st->sumsq : &st->sum, (double)red[tid]);
         }
     }
+    PHASE(7);
+    RTSTAMP(1);
 }
 
 // ---------------------------------------------------------------------------------- backward
-// header floats: csum fp64 [2*MAX_CIN] | gst fp64 [4*(MAX_CIN+MAX_COUT)] | i_sc i_sh i_mean i_inv i_gam [MAX_CIN] | o_coef [4*MAX_COUT]
-constexpr int BWD_HDR = 4 * GPI_MAX_CIN + 8 * (GPI_MAX_CIN + GPI_MAX_COUT) + 5 * GPI_MAX_CIN + 4 * GPI_MAX_COUT;
+// MFMA (v_mfma_f32_16x16x4_f32, exact f32 fmaf chains) for both contractions:
+//  * weight gradient by the column-shift form
+//      dW[(co,kx)][(ci,ky)] = sum_{ty,x} g[co][ty][ox(x, kx)] * a[ci][row(ty,ky)][col(x)]
+//    (x runs over the virtual input columns of an output row: rows M = cout*K,
+//    columns N = cin*K), the reduction split over the four waves by output row
+//    and summed in LDS in a fixed order;
+//  * input gradient as [owned pixels] x [cin] with reduction over (co, ky, kx):
+//    A = the output-gradient window of the pixel (LDS), B = W (LDS, [co*KK+tap][16]).
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-template <int K, int S, int UP, int CP, int CINP>
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// header floats: gst fp64 [4*(MAX_CIN+MAX_COUT)] | i_sc i_sh i_mean i_inv i_gam [MAX_CIN] | o_coef [4*MAX_COUT]
+constexpr int BWD_HDR = 8 * (GPI_MAX_CIN + GPI_MAX_COUT) + 5 * GPI_MAX_CIN + 4 * GPI_MAX_COUT;
+constexpr int BWD_RED = 2048;   // [4 waves][2 column blocks][4][64] partial dW / per-wave channel sums
+
+template <int K, int S, int UP>
 __global__ __launch_bounds__(256) void conv_bwd_kernel(gpi_conv_desc d, gpi_codec_ctx c, ConvGeom G) {
     constexpr int KK = K * K;
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    double* csum = (double*)smem;
-    double* gst = csum + 2 * GPI_MAX_CIN;
-    float* i_sc = smem + 4 * GPI_MAX_CIN + 8 * (GPI_MAX_CIN + GPI_MAX_COUT);
+    double* gst = (double*)smem;
+    float* i_sc = smem + 8 * (GPI_MAX_CIN + GPI_MAX_COUT);
     float* i_sh = i_sc + GPI_MAX_CIN;
     float* i_mean = i_sh + GPI_MAX_CIN;
     float* i_inv = i_mean + GPI_MAX_CIN;
     float* i_gam = i_inv + GPI_MAX_CIN;
     float* o_coef = i_gam + GPI_MAX_CIN;              // [MAX_COUT][4]: mean, inv, mS, mSx
-    float* wD = smem + BWD_HDR;                       // [cout][KK][CINP]
-    float* gl = wD + d.cout * KK * CINP;
-    const int gplane = G.gh * G.gw;
-    float* al = gl + ((G.spb * d.cout * gplane + 3) & ~3);
-    const int plane_r = G.rh * G.rw;
-    const int per_s = d.cin * plane_r;
-    float* wred = al + ((G.spb * per_s + 3) & ~3);    // [parts][CP][nthr_j]
+    const bool has_gin = d.gin_off >= 0;
+    const bool obn = d.gout_mode == 0;
+    float* wD = smem + pad256(BWD_HDR);               // [cout*KK][16]: W[co][ci][tap] at (co*KK + tap)*16 + ci
+    const int nwd = has_gin ? d.cout * KK * 16 : 0;
+    float* gl = wD + pad256(nwd);                     // [cout][gh][PG]
+    const int gplane = G.gh * G.PG;
+    const int ngl = d.cout * gplane;
+    float* gz = gl + pad256(ngl);                     // raw z of the output (BN-backward only)
+    float* al = gz + (obn ? pad256(ngl) : 0);         // [cin][rh][P]
+    const int aplane = G.rh * G.P;
+    float* red = al + pad256(d.cin * aplane);
 
     const int tid = threadIdx.x;
+    const int lane = tid & 63, wv = tid >> 6, kq = lane >> 4, l16 = lane & 15;
+    RTSTAMP(0);
+    PHASE(0);
     const TileIdx T = tile_of(G, c.groups);
     const int HWi = d.h_in * d.w_in, HWo = d.h_out * d.w_out;
+    const float* ib = input_base(d, c, T.b);
+    PHASE(1);
 
-    for (int e = tid; e < 2 * GPI_MAX_CIN + 4 * (GPI_MAX_CIN + GPI_MAX_COUT); e += 256) csum[e] = 0.0;
-    __syncthreads();
-    if (d.in_bn) gather_stats(c, d.in_stat, d.cin, T.grp, gst);
-    if (d.gout_mode == 0) gather_stats(c, d.out_stat, d.cout, T.grp, gst + 4 * GPI_MAX_CIN);
-    for (int e = tid; e < d.cout * KK * CINP; e += 256) {
-        const int ci = e % CINP, r = e / CINP;
-        const int co = r / KK, t = r - co * KK;
-        wD[e] = ci < d.cin ? c.params[d.w_off + ((int64_t)co * d.cin + ci) * KK + t] : 0.f;
+    // ---- phase 1: every global read in flight together
+    if (has_gin)
+        stage(wD, nwd, [&](int e) -> const float* {
+            const int ci = e & 15, k = e >> 4;
+            const int co = k / KK, t = k - co * KK;
+            return ci < d.cin ? c.params + d.w_off + ((int64_t)co * d.cin + ci) * KK + t : nullptr;
+        });
+    int gy0, gh_;
+    g_rows(K, S, d.pad, T.oy0, G.th, gy0, gh_);
+    const int64_t gbase = ((int64_t)T.b * d.out_ctot + d.out_c0) * HWo;
+    stage_img(gl, d.cout, G.gh, G.PG, G.d_g4, G.d_PG4, gy0, d.h_out, d.w_out,
+              [&](int q) -> const float* { return c.ws + d.gout_off + gbase + (int64_t)q * HWo; });
+    if (obn)
+        stage_img(gz, d.cout, G.gh, G.PG, G.d_g4, G.d_PG4, gy0, d.h_out, d.w_out,
+                  [&](int q) -> const float* { return c.ws + d.out_off + gbase + (int64_t)q * HWo; });
+    int iy0, rh_;
+    in_rows(K, S, UP, d.pad, T.oy0, G.th, iy0, rh_);
+    stage_img(al, d.cin, G.rh, G.P, G.d_in4, G.d_P4, iy0, d.h_in, d.w_in,
+              [&](int q) -> const float* { return ib + (int64_t)q * HWi; });
+    PHASE(8);
+    // input-gradient epilogue operands (x, previous S_in) of this wave's first four pixel
+    // blocks: lane (kq, l16) owns channel l16 at the 4 consecutive pixels 16 m + 4 kq + [0, 4)
+    int py0, ph_;
+    owned_rows(S, UP, T.oy0, G.th, py0, ph_);
+    const int nmblk = has_gin ? (G.ph * d.w_in) >> 4 : 0;
+    const int ci_l = min(l16, d.cin - 1);
+    const int64_t ibase = ((int64_t)T.b * d.in_ctot + d.in_c0 + ci_l) * HWi + (int64_t)py0 * d.w_in;
+    float4 xv4[4], pv4[4];
+    auto own_load = [&](int round) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int m = wv + 4 * (4 * round + u);
+            const bool ok = m < nmblk;
+            const int64_t o = ibase + 16 * m + 4 * kq;
+            if (d.in_bn) xv4[u] = *(const float4*)(ok ? c.ws + d.in_off + o : g_zero_page);
+            if (d.gin_accumulate) pv4[u] = *(const float4*)(ok ? c.ws + d.gin_off + o : g_zero_page);
+            else pv4[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    if (nmblk > 0) own_load(0);
+    PHASE(9);
+    float gam = 0.f, bet = 0.f;
+    if (d.in_bn && tid < d.cin) {
+        gam = c.params[d.gamma_off + tid];
+        bet = c.params[d.beta_off + tid];
+    }
+    {
+        StatLoad L;
+        stat_issue(c, T.grp, d.in_stat, d.in_bn ? d.cin : 0, gst, d.out_stat, obn ? d.cout : 0,
+                   gst + 4 * GPI_MAX_CIN, L);
+        PHASE(10);
+        stat_finish(L);
+        PHASE(11);
     }
     __syncthreads();
+    PHASE(2);
+
+    // ---- phase 2: coefficients
     if (tid < d.cin && d.in_bn) {
         float mean, inv;
         mean_invstd(gst + 4 * tid, (double)T.gsz * HWi, c.bn_eps, mean, inv);
-        const float gam = c.params[d.gamma_off + tid], bet = c.params[d.beta_off + tid];
         i_mean[tid] = mean;
         i_inv[tid] = inv;
         i_gam[tid] = gam;
         i_sc[tid] = gam * inv;
         i_sh[tid] = bet - mean * gam * inv;
     }
-    if (d.gout_mode == 0 && tid < d.cout) {
-        const double* st = gst + 4 * (GPI_MAX_CIN + tid);
+    if (obn && tid >= 64 && tid < 64 + d.cout) {
+        const int co = tid - 64;
+        const double* st = gst + 4 * (GPI_MAX_CIN + co);
         const double n = (double)T.gsz * HWo;
         float mean, inv;
         mean_invstd(st, n, c.bn_eps, mean, inv);
-        o_coef[4 * tid] = mean;
-        o_coef[4 * tid + 1] = inv;
-        o_coef[4 * tid + 2] = (float)(st[2] / n);
-        o_coef[4 * tid + 3] = (float)(st[3] / n);
+        o_coef[4 * co] = mean;
+        o_coef[4 * co + 1] = inv;
+        o_coef[4 * co + 2] = (float)(st[2] / n);
+        o_coef[4 * co + 3] = (float)(st[3] / n);
     }
     __syncthreads();
+    PHASE(3);
 
-    // ---- output-gradient region
-    int gy0, gh_, gx0, gw_;
-    g_region(K, S, d.pad, T.oy0, G.th, gy0, gh_);
-    g_region(K, S, d.pad, T.ox0, G.tw, gx0, gw_);
-    fill(gl, G.spb * d.cout * gplane, gplane, G.gw, [&](int q, int ry, int rx) -> float {
-        const int s = q / d.cout, co = q - s * d.cout;
-        const int oy = gy0 + ry, ox = gx0 + rx;
-        if (oy < 0 || oy >= d.h_out || ox < 0 || ox >= d.w_out) return 0.f;
-        const int64_t idx = ((int64_t)(T.s0 + s) * d.out_ctot + d.out_c0 + co) * HWo + oy * d.w_out + ox;
-        const float sv = c.ws[d.gout_off + idx];
-        if (d.gout_mode != 0) return sv;
-        const float z = c.ws[d.out_off + idx];
-        const float inv = o_coef[4 * co + 1];
-        const float xh = (z - o_coef[4 * co]) * inv;
-        return (sv - o_coef[4 * co + 2] - xh * o_coef[4 * co + 3]) * inv;
-    });
-    // ---- activated input region (same activation as the forward)
-    int iy0, rh_, ix0, rw_;
-    in_region(K, S, UP, d.pad, T.oy0, G.th, iy0, rh_);
-    in_region(K, S, UP, d.pad, T.ox0, G.tw, ix0, rw_);
-    const float* inb = d.in_off >= 0 ? c.ws + d.in_off : nullptr;
-    fill(al, G.spb * per_s, plane_r, G.rw, [&](int q, int ry, int rx) -> float {
-        const int s = q / d.cin, ci = q - s * d.cin;
-        const int iy = iy0 + ry, ix = ix0 + rx;
-        if (ry >= rh_ || rx >= rw_ || iy < 0 || iy >= d.h_in || ix < 0 || ix >= d.w_in) return 0.f;
-        const int gs = T.s0 + s;
-        const float* src = inb ? inb + (int64_t)gs * d.in_ctot * HWi
-                               : c.ext_in + (int64_t)(c.ext_idx ? c.ext_idx[gs] : gs) * c.ext_stride;
-        const float x = src[(int64_t)(d.in_c0 + ci) * HWi + iy * d.w_in + ix];
-        return d.in_bn ? fmaxf(fmaf(x, i_sc[ci], i_sh[ci]), 0.f) : x;
-    });
+    // ---- phase 3: activations in LDS
+    if (d.in_bn) activate_img(al, G, d, iy0, i_sc, i_sh);
+    if (obn) {
+        const int P4 = G.PG >> 2, plane4 = G.gh * P4, total = d.cout * plane4;
+        float4* g4 = reinterpret_cast<float4*>(gl);
+        const float4* z4 = reinterpret_cast<const float4*>(gz);
+        for (int e0 = tid; e0 < total; e0 += 512) {
+            float4 sv[2], zv[2];
+            bool ok[2];
+            int co[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int e = e0 + 256 * u;
+                const int q = dq(e, G.d_g4), rem = e - q * plane4;
+                const int r = dq(rem, G.d_PG4), col = 4 * (rem - r * P4) - HALO;
+                const int row = gy0 + r;
+                ok[u] = e < total && row >= 0 && row < d.h_out && col >= 0 && col < d.w_out;
+                co[u] = q;
+                if (ok[u]) {
+                    sv[u] = g4[e];
+                    zv[u] = z4[e];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                if (ok[u]) {
+                    const float* oc = o_coef + 4 * co[u];
+                    const float m = oc[0], inv = oc[1], mS = oc[2], mSx = oc[3];
+                    float4 o;
+                    o.x = (sv[u].x - mS - ((zv[u].x - m) * inv) * mSx) * inv;
+                    o.y = (sv[u].y - mS - ((zv[u].y - m) * inv) * mSx) * inv;
+                    o.z = (sv[u].z - mS - ((zv[u].z - m) * inv) * mSx) * inv;
+                    o.w = (sv[u].w - mS - ((zv[u].w - m) * inv) * mSx) * inv;
+                    g4[e0 + 256 * u] = o;
+                }
+            }
+        }
+    }
     __syncthreads();
+    PHASE(4);
 
-    // ---- weight gradient partial: dW[co][j] = sum_pixels g[co][o] * a[j-window of o]
+    // ---- phase 4a: weight gradient (MFMA, column-shift form) -> slab row
     const int J = d.cin * KK;
     const int rowlen = d.cout * J + (d.in_bn ? 2 * d.cin : 0);
+    float* slab = c.wpart + d.wpart_off + (int64_t)blockIdx.x * rowlen;
     {
-        const int nthr_j = J < 256 ? J : 256;
-        const int parts = 256 / nthr_j;
-        const int part = tid / nthr_j, jl = tid - part * nthr_j;
-        const int R = G.spb * G.th;          // (sample, row) pairs
-        for (int jb = 0; jb < J; jb += nthr_j) {
-            const int j = jb + jl;
-            float acc[CP];
+        const int MI = d.cout * K, NJ = d.cin * K;
+        const int nmb = (MI + 15) >> 4, nnb = (NJ + 15) >> 4;
+        const int XW = UP ? d.w_out + K - 1 : S * (d.w_out - 1) + K;   // virtual input columns
+        const int nxs = (XW + 3) >> 2;
+        for (int mb = 0; mb < nmb; ++mb) {
+            const int i = 16 * mb + l16;
+            const bool iok = i < MI;
+            const int co = min(i / K, d.cout - 1), kx = i - (i / K) * K;
+            for (int nb0 = 0; nb0 < nnb; nb0 += 2) {
+                const bool two = nb0 + 1 < nnb;
+                int ci[2], ky[2];
+                bool jok[2];
 #pragma unroll
-            for (int co = 0; co < CP; ++co) acc[co] = 0.f;
-            if (part < parts && j < J) {
-                const int ci = j / KK;
-                const int kk = j - ci * KK;
-                const int ky = kk / K, kx = kk - ky * K;
-                const int rb = part * R / parts, re = (part + 1) * R / parts;
-                for (int rr = rb; rr < re; ++rr) {
-                    const int s = rr / G.th;
-                    const int ty = rr - s * G.th;
-                    const int oy = T.oy0 + ty;
-                    const int ry = UP ? (fdiv2(oy - d.pad + ky) - iy0) : (ty * S + ky);
-                    const float* arow = al + s * per_s + ci * plane_r + ry * G.rw;
-                    const float* grow = gl + s * d.cout * gplane + (oy - gy0) * G.gw + (T.ox0 - gx0);
-                    for (int tx = 0; tx < G.tw; ++tx) {
-                        const int rx = UP ? (fdiv2(T.ox0 + tx - d.pad + kx) - ix0) : (tx * S + kx);
-                        const float a = arow[rx];
+                for (int u = 0; u < 2; ++u) {
+                    const int j = 16 * (nb0 + u) + l16;
+                    jok[u] = j < NJ;
+                    ci[u] = min(j / K, d.cin - 1);
+                    ky[u] = j - (j / K) * K;
+                }
+                f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+                for (int ty = wv; ty < G.th; ty += 4) {
+                    const float* grow = gl + (co * G.gh + (T.oy0 + ty - gy0)) * G.PG + HALO;
+                    const float* brow[2];
 #pragma unroll
-                        for (int co = 0; co < CP; ++co)
-                            if (co < d.cout) acc[co] = fmaf(grow[co * gplane + tx], a, acc[co]);
+                    for (int u = 0; u < 2; ++u) {
+                        const int ry = UP ? fdiv2(T.oy0 + ty - d.pad + ky[u]) - iy0 : ty * S + ky[u];
+                        brow[u] = al + (ci[u] * G.rh + ry) * G.P + HALO;
+                    }
+                    for (int xs = 0; xs < nxs; ++xs) {
+                        const int xv = 4 * xs + kq;          // virtual column index in [0, XW)
+                        const int t2 = xv - kx;
+                        bool aok = iok && t2 >= 0;
+                        int ox = t2;
+                        if (S == 2) {
+                            aok = aok && !(t2 & 1);
+                            ox = t2 >> 1;
+                        }
+                        aok = aok && ox < d.w_out;
+                        const float a = aok ? grow[aok ? ox : 0] : 0.f;
+                        const bool xok = xv < XW;
+                        const int ix = UP ? fdiv2(xv - d.pad) : xv - d.pad;   // input column (halo >= -pad)
+                        const int ixc = xok ? ix : 0;
+                        const float b0 = (jok[0] && xok) ? brow[0][ixc] : 0.f;
+                        acc[0] = mfma4(a, b0, acc[0]);
+                        if (two) {
+                            const float b1 = (jok[1] && xok) ? brow[1][ixc] : 0.f;
+                            acc[1] = mfma4(a, b1, acc[1]);
+                        }
                     }
                 }
-            }
-            if (parts > 1) {
-                if (part < parts) {
+                // fixed-order sum of the four waves' partial tiles
 #pragma unroll
-                    for (int co = 0; co < CP; ++co) wred[(part * CP + co) * nthr_j + jl] = acc[co];
+                for (int u = 0; u < 2; ++u)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) red[((wv * 2 + u) * 4 + r) * 64 + lane] = acc[u][r];
+                __syncthreads();
+                {
+                    const int r = tid >> 6, ln = tid & 63;
+                    const int i2 = 16 * mb + (ln >> 4) * 4 + r;
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+                        const int j2 = 16 * (nb0 + u) + (ln & 15);
+                        if ((u == 0 || two) && i2 < MI && j2 < NJ) {
+                            const float v = red[((0 * 2 + u) * 4 + r) * 64 + ln] + red[((1 * 2 + u) * 4 + r) * 64 + ln] +
+                                            red[((2 * 2 + u) * 4 + r) * 64 + ln] + red[((3 * 2 + u) * 4 + r) * 64 + ln];
+                            const int co2 = i2 / K, kx2 = i2 - co2 * K, ci2 = j2 / K, ky2 = j2 - ci2 * K;
+                            slab[co2 * J + ci2 * KK + ky2 * K + kx2] = v;
+                        }
+                    }
                 }
                 __syncthreads();
-                if (part == 0) {
-                    for (int p = 1; p < parts; ++p)
-#pragma unroll
-                        for (int co = 0; co < CP; ++co) acc[co] += wred[(p * CP + co) * nthr_j + jl];
-                }
-                __syncthreads();
-            }
-            if (part == 0 && j < J) {
-                float* wp = c.wpart + d.wpart_off + (int64_t)blockIdx.x * rowlen;
-#pragma unroll
-                for (int co = 0; co < CP; ++co)
-                    if (co < d.cout) wp[co * J + j] = acc[co];
             }
         }
     }
+    PHASE(5);
 
-    // ---- input gradient: one thread per owned input pixel, all input channels at once
-    float sd[CINP], sdx[CINP];
+    // ---- phase 4b: input gradient (MFMA) + BN backward of the input + S_in (+)= gamma * dbn
+    float sd = 0.f, sdx = 0.f;   // this lane's channel l16
+    if (nmblk > 0) {
+        float l_sc = 0.f, l_sh = 0.f, l_mean = 0.f, l_inv = 0.f, l_gam = 0.f;
+        if (d.in_bn) {
+            l_sc = i_sc[ci_l];
+            l_sh = i_sh[ci_l];
+            l_mean = i_mean[ci_l];
+            l_inv = i_inv[ci_l];
+            l_gam = i_gam[ci_l];
+        }
+        const int KD = d.cout * KK;
+        const int nkd = (KD + 3) >> 2;
+        const bool cok = l16 < d.cin;
+        for (int round = 0; wv + 16 * round < nmblk; ++round) {
+            if (round > 0) own_load(round);
 #pragma unroll
-    for (int ci = 0; ci < CINP; ++ci) { sd[ci] = 0.f; sdx[ci] = 0.f; }
-    if (d.gin_off >= 0) {
-        int py0, ph, px0, pw;
-        owned(S, UP, T.oy0, G.th, py0, ph);
-        owned(S, UP, T.ox0, G.tw, px0, pw);
-        const int pp = ph * pw;
-        const int total = G.spb * pp;
-        for (int e = tid; e < total; e += 256) {
-            const int s = e / pp;
-            const int r = e - s * pp;
-            const int qy = r / pw, qx = r - qy * pw;
-            const int py = py0 + qy, px = px0 + qx;
-            float da[CINP];
-#pragma unroll
-            for (int ci = 0; ci < CINP; ++ci) da[ci] = 0.f;
-            for (int co = 0; co < d.cout; ++co) {
-                const float* gc = gl + (s * d.cout + co) * gplane;
-                const float* wco = wD + co * KK * CINP;
-#pragma unroll
-                for (int ky = 0; ky < K; ++ky) {
-#pragma unroll
-                    for (int kx = 0; kx < K; ++kx) {
-                        float g;
+            for (int u = 0; u < 4; ++u) {
+                const int m = wv + 4 * (4 * round + u);
+                if (m < nmblk) {
+                    const int i = 16 * m + l16;                   // owned pixel of this lane's A row
+                    const int qy = dq(i, G.d_win), px = i - qy * d.w_in;
+                    const int py = py0 + qy;
+                    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+                    for (int ks = 0; ks < nkd; ++ks) {
+                        const int k = 4 * ks + kq;
+                        const bool kok = k < KD;
+                        const int kc = kok ? k : 0;
+                        const int co = kc / KK, tap = kc - co * KK;
+                        const int ky = tap / K, kx = tap - ky * K;
+                        const float* gc = gl + co * gplane + HALO;
+                        float a;
                         if (UP) {
-                            const int oy = 2 * py + d.pad - ky - gy0, ox = 2 * px + d.pad - kx - gx0;
-                            g = gc[oy * G.gw + ox] + gc[oy * G.gw + ox + 1] + gc[(oy + 1) * G.gw + ox] +
-                                gc[(oy + 1) * G.gw + ox + 1];
+                            const int o = (2 * py + d.pad - ky - gy0) * G.PG + (2 * px + d.pad - kx);
+                            a = (gc[o] + gc[o + 1]) + (gc[o + G.PG] + gc[o + G.PG + 1]);
                         } else if (S == 2) {
                             const int oy2 = py + d.pad - ky, ox2 = px + d.pad - kx;
-                            if ((oy2 & 1) || (ox2 & 1)) continue;
-                            g = gc[((oy2 >> 1) - gy0) * G.gw + ((ox2 >> 1) - gx0)];
+                            const bool ok2 = !((oy2 | ox2) & 1);
+                            const int o = ok2 ? ((oy2 >> 1) - gy0) * G.PG + (ox2 >> 1) : 0;
+                            a = ok2 ? gc[o] : 0.f;
                         } else {
-                            g = gc[(py + d.pad - ky - gy0) * G.gw + (px + d.pad - kx - gx0)];
+                            a = gc[(py + d.pad - ky - gy0) * G.PG + (px + d.pad - kx)];
                         }
-                        fma_vec<CINP>(da, wco + (ky * K + kx) * CINP, g);
+                        a = kok ? a : 0.f;
+                        const float b = kok ? wD[kc * 16 + l16] : 0.f;
+                        acc = mfma4(a, b, acc);
+                    }
+                    if (cok) {
+                        float* gp = c.ws + d.gin_off + ibase + 16 * m + 4 * kq;
+                        const float xa[4] = {xv4[u].x, xv4[u].y, xv4[u].z, xv4[u].w};
+                        const float pa[4] = {pv4[u].x, pv4[u].y, pv4[u].z, pv4[u].w};
+                        float o[4];
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            if (d.in_bn) {
+                                const float bnv = fmaf(xa[q], l_sc, l_sh);
+                                const float dbn = bnv > 0.f ? acc[q] : 0.f;
+                                o[q] = pa[q] + l_gam * dbn;
+                                sd += dbn;
+                                sdx += dbn * ((xa[q] - l_mean) * l_inv);
+                            } else {
+                                o[q] = pa[q] + acc[q];
+                            }
+                        }
+                        *(float4*)gp = make_float4(o[0], o[1], o[2], o[3]);
                     }
                 }
-            }
-            const int gs = T.s0 + s;
-            const int64_t idx0 = ((int64_t)gs * d.in_ctot + d.in_c0) * HWi + py * d.w_in + px;
-            float* gp = c.ws + d.gin_off + idx0;
-            if (d.in_bn) {
-                const float* xp = c.ws + d.in_off + idx0;
-                float xv[CINP], pv[CINP];
-#pragma unroll
-                for (int ci = 0; ci < CINP; ++ci) {
-                    xv[ci] = 0.f;
-                    pv[ci] = 0.f;
-                    if (ci < d.cin) {
-                        xv[ci] = xp[(int64_t)ci * HWi];
-                        if (d.gin_accumulate) pv[ci] = gp[(int64_t)ci * HWi];
-                    }
-                }
-#pragma unroll
-                for (int ci = 0; ci < CINP; ++ci) {
-                    if (ci < d.cin) {
-                        const float bnv = fmaf(xv[ci], i_sc[ci], i_sh[ci]);
-                        const float xh = (xv[ci] - i_mean[ci]) * i_inv[ci];
-                        const float dbn = bnv > 0.f ? da[ci] : 0.f;
-                        gp[(int64_t)ci * HWi] = pv[ci] + i_gam[ci] * dbn;
-                        sd[ci] += dbn;
-                        sdx[ci] += dbn * xh;
-                    }
-                }
-            } else {
-                float pv[CINP];
-#pragma unroll
-                for (int ci = 0; ci < CINP; ++ci)
-                    pv[ci] = (ci < d.cin && d.gin_accumulate) ? gp[(int64_t)ci * HWi] : 0.f;
-#pragma unroll
-                for (int ci = 0; ci < CINP; ++ci)
-                    if (ci < d.cin) gp[(int64_t)ci * HWi] = pv[ci] + da[ci];
             }
         }
     }
+    PHASE(6);
     if (d.in_bn) {
-        // per-channel sums -> csum (fp64 LDS), then slab row (dgamma, dbeta) and the S statistics
-        const int lane = tid & 63;
-#pragma unroll
-        for (int ci = 0; ci < CINP; ++ci) {
-            if (ci < d.cin) {
-                const float a = wave_sum(sd[ci]), b = wave_sum(sdx[ci]);
-                if (lane == 0) {
-                    atomicAdd(&csum[2 * ci], (double)a);
-                    atomicAdd(&csum[2 * ci + 1], (double)b);
-                }
-            }
+        // lanes 16 apart share a channel: fold them, then the four waves in a fixed order
+        sd += __shfl_xor(sd, 16, 64);
+        sdx += __shfl_xor(sdx, 16, 64);
+        sd += __shfl_xor(sd, 32, 64);
+        sdx += __shfl_xor(sdx, 32, 64);
+        if (kq == 0) {
+            red[wv * 32 + l16] = sd;
+            red[128 + wv * 32 + l16] = sdx;
         }
         __syncthreads();
         if (tid < d.cin) {
-            const double s_d = csum[2 * tid], s_dx = csum[2 * tid + 1];
-            float* row = c.wpart + d.wpart_off + (int64_t)blockIdx.x * rowlen + d.cout * J;
-            row[tid] = (float)s_dx;            // dgamma
-            row[d.cin + tid] = (float)s_d;     // dbeta
-            if (d.gin_off >= 0) {
-                gpi_stat* st = stat_slot(c, d.in_stat + tid, T.grp);
-                const double gam = i_gam[tid];
-                atomicAdd(&st->ssum, gam * s_d);
-                atomicAdd(&st->sxsum, gam * s_dx);
+            double s_d = 0.0, s_dx = 0.0;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                s_d += (double)red[w * 32 + tid];
+                s_dx += (double)red[128 + w * 32 + tid];
             }
+            slab[d.cout * J + tid] = (float)s_dx;            // dgamma
+            slab[d.cout * J + d.cin + tid] = (float)s_d;     // dbeta
+            gpi_stat* st = stat_slot(c, d.in_stat + tid, T.grp);
+            const double gm = i_gam[tid];
+            atomicAdd(&st->ssum, gm * s_d);
+            atomicAdd(&st->sxsum, gm * s_dx);
         }
     }
+    PHASE(7);
+    RTSTAMP(1);
 }
 
 size_t fwd_lds(const gpi_conv_desc& d, const ConvGeom& G, int cp) {
-    return sizeof(float) * ((size_t)FWD_HDR + ((d.cin * d.k * d.k * cp + 3) & ~3) +
-                            (size_t)G.spb * d.cin * G.rh * G.rw);
+    return sizeof(float) *
+           ((size_t)pad256(FWD_HDR) + pad256(d.cin * d.k * d.k * cp) + pad256(d.cin * G.rh * G.P));
 }
 
-size_t bwd_lds(const gpi_conv_desc& d, const ConvGeom& G, int cp, int cinp) {
-    size_t f = BWD_HDR + (size_t)d.cout * d.k * d.k * cinp + (((size_t)G.spb * d.cout * G.gh * G.gw + 3) & ~3) +
-               (((size_t)G.spb * d.cin * G.rh * G.rw + 3) & ~3) + (size_t)cp * 256;
+size_t bwd_lds(const gpi_conv_desc& d, const ConvGeom& G) {
+    const int ngl = pad256(d.cout * G.gh * G.PG);
+    size_t f = (size_t)pad256(BWD_HDR) + (d.gin_off >= 0 ? pad256(d.cout * d.k * d.k * 16) : 0) + ngl +
+               (d.gout_mode == 0 ? ngl : 0) + pad256(d.cin * G.rh * G.P) + BWD_RED;
     return f * sizeof(float);
 }
 
 typedef void (*conv_kernel_t)(gpi_conv_desc, gpi_codec_ctx, ConvGeom);
 
-template <int K, int S, int UP, int CP>
-conv_kernel_t pick_cinp(int cinp, bool fwd) {
-    if (fwd) return conv_fwd_kernel<K, S, UP, CP>;
-    return cinp == 8 ? conv_bwd_kernel<K, S, UP, CP, 8> : conv_bwd_kernel<K, S, UP, CP, 16>;
-}
-
 template <int K, int S, int UP>
-conv_kernel_t pick(int cp, int cinp, bool fwd) {
-    if (cp == 2) return pick_cinp<K, S, UP, 2>(cinp, fwd);
-    if (cp == 4) return pick_cinp<K, S, UP, 4>(cinp, fwd);
-    return pick_cinp<K, S, UP, 8>(cinp, fwd);
+conv_kernel_t pick(int cp, bool fwd) {
+    if (!fwd) return conv_bwd_kernel<K, S, UP>;
+    if (cp == 2) return conv_fwd_kernel<K, S, UP, 2>;
+    if (cp == 4) return conv_fwd_kernel<K, S, UP, 4>;
+    return conv_fwd_kernel<K, S, UP, 8>;
 }
 
-conv_kernel_t select_kernel(const gpi_conv_desc& d, int cp, int cinp, bool fwd) {
+conv_kernel_t select_kernel(const gpi_conv_desc& d, int cp, bool fwd) {
     const int key = d.k * 100 + d.stride * 10 + d.upsample;
     switch (key) {
-        case 110: return pick<1, 1, 0>(cp, cinp, fwd);
-        case 310: return pick<3, 1, 0>(cp, cinp, fwd);
-        case 311: return pick<3, 1, 1>(cp, cinp, fwd);
-        case 320: return pick<3, 2, 0>(cp, cinp, fwd);
-        case 510: return pick<5, 1, 0>(cp, cinp, fwd);
-        case 720: return pick<7, 2, 0>(cp, cinp, fwd);
+        case 110: return pick<1, 1, 0>(cp, fwd);
+        case 310: return pick<3, 1, 0>(cp, fwd);
+        case 311: return pick<3, 1, 1>(cp, fwd);
+        case 320: return pick<3, 2, 0>(cp, fwd);
+        case 510: return pick<5, 1, 0>(cp, fwd);
+        case 720: return pick<7, 2, 0>(cp, fwd);
         default: return nullptr;
     }
 }
 
 int cp_of(int cout) { return cout <= 2 ? 2 : (cout <= 4 ? 4 : 8); }
 
+// Alignment preconditions of the 16-byte operand paths (row images, float4 epilogue).
+bool aligned_ok(const gpi_conv_desc& d, const gpi_codec_ctx& c, bool fwd) {
+    if (((uintptr_t)c.ws & 15) || (d.in_off >= 0 && (d.in_off & 3))) return false;
+    if (d.in_off < 0 && (((uintptr_t)c.ext_in & 15) || (c.ext_stride & 3))) return false;
+    if (fwd) return true;
+    if (d.cin > 16) return false;
+    if (d.in_bn && (d.in_off < 0 || d.gin_off < 0)) return false;
+    if ((d.gout_off & 3) || (d.gout_mode == 0 && (d.out_off & 3))) return false;
+    if (d.gin_off >= 0 && (d.gin_off & 3)) return false;
+    return true;
+}
+
 int launch(const gpi_conv_desc& d, const gpi_codec_ctx& c, hipStream_t st, bool fwd) {
     ConvGeom G;
     if (!conv_geom(d, c.groups, G)) return GPI_ERR_UNSUPPORTED;
     if (d.epilogue == GPI_EPI_GAUSS_LOSS && d.cout != 2) return GPI_ERR_ARG;
-    if (!fwd && d.in_bn && d.in_off < 0) return GPI_ERR_ARG;
-    if (!fwd && d.cin > 16) return GPI_ERR_UNSUPPORTED;
+    if (d.in_off < 0 && !c.ext_in) return GPI_ERR_ARG;
+    if (!aligned_ok(d, c, fwd)) return GPI_ERR_UNSUPPORTED;
+    if (!fwd && d.gin_off >= 0 && ((G.ph * d.w_in) & 15)) return GPI_ERR_UNSUPPORTED;
     const int cp = cp_of(d.cout);
-    const int cinp = d.cin <= 8 ? 8 : 16;
-    conv_kernel_t k = select_kernel(d, cp, cinp, fwd);
+    conv_kernel_t k = select_kernel(d, cp, fwd);
     if (!k) return GPI_ERR_UNSUPPORTED;
-    const size_t lds = fwd ? fwd_lds(d, G, cp) : bwd_lds(d, G, cp, cinp);
+    const size_t lds = fwd ? fwd_lds(d, G, cp) : bwd_lds(d, G);
     if (lds > 160 * 1024) return GPI_ERR_UNSUPPORTED;
     if (lds > 64 * 1024) {
         if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
@@ -704,6 +953,20 @@ __global__ __launch_bounds__(256) void wgrad_reduce(ReduceArgs a, const float* _
 }
 
 }  // namespace
+
+#ifdef GPI_PHASE_TIMING
+// timing build only (not declared in gpi.h): copy the phase / real-time stamps out and clear them.
+extern "C" int gpi_debug_phase_stamps(unsigned long long* phase, unsigned long long* rt) {
+    static unsigned long long zeros[4096 * 16];
+    if (hipMemcpyFromSymbol(phase, HIP_SYMBOL(g_phase), sizeof(zeros)) != hipSuccess) return GPI_ERR_LAUNCH;
+    if (hipMemcpyFromSymbol(rt, HIP_SYMBOL(g_rt), sizeof(unsigned long long) * 4096 * 2) != hipSuccess)
+        return GPI_ERR_LAUNCH;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_phase), zeros, sizeof(zeros)) != hipSuccess) return GPI_ERR_LAUNCH;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_rt), zeros, sizeof(unsigned long long) * 4096 * 2) != hipSuccess)
+        return GPI_ERR_LAUNCH;
+    return GPI_OK;
+}
+#endif
 
 extern "C" int gpi_conv_blocks(const gpi_conv_desc* op, const gpi_groups* groups, int32_t* blocks) {
     if (!op || !groups || !blocks) return GPI_ERR_ARG;

@@ -11,6 +11,8 @@ import torch  # noqa: F401  (must be imported before the HIP library is loaded)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, 'libgpi_hip.so')
+if os.environ.get('GPI_PHASE_TIMING') == '1':      # tools/phase_probe.py: the stamped build of the same kernels
+    LIB_PATH = os.path.join(HERE, 'libgpi_hip_timing.so')
 
 GPI_MAX_GROUPS = 4
 GPI_MAX_CIN = 32

@@ -1,0 +1,74 @@
+"""Per-phase timing of single codec operators (timing build of the library).
+
+usage: GPI_PHASE_TIMING=1 python tools/phase_probe.py [OP_SUBSTRING ...] [--fwd]
+Runs every matching operator of the C64 ELBO step once more after a warm step,
+reads the s_memtime stamps each workgroup wrote at its phase boundaries and
+prints mean cycles per phase, the mean workgroup lifetime, the kernel span on
+the 100 MHz real-time clock and the mean number of workgroups in flight.
+Phases (backward): 0 entry | 1 bases | 2 loads landed + stats | 3 coefficients |
+4 activations | 5 weight gradient | 6 input gradient | 7 sums/atomics; inside phase 1:
+8 LDS-DMA issued | 9 epilogue operands issued | 10 stat loads issued | 11 stats summed.
+"""
+import ctypes as C
+import os
+import sys
+
+os.environ['GPI_PHASE_TIMING'] = '1'
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+import bench  # noqa: E402
+import torch  # noqa: E402
+from gpi import _lib as L  # noqa: E402
+from gpi.train import FusedElboStep  # noqa: E402
+
+
+def main():
+    args = [a for a in sys.argv[1:] if not a.startswith('--')]
+    fwd = '--fwd' in sys.argv
+    dev = torch.device('cuda', 0)
+    model, data, (B_u, N_s), physics = bench.build('c64', dev, seed=1)
+    Xu, Xs, Y, F = data
+    step = FusedElboStep(model, Xu, B_u, Xs, Y, F)
+    step.step_eager()
+    torch.cuda.synchronize()
+    e = step.engine
+    lib = L.lib()
+    stamps = lib.gpi_debug_phase_stamps
+    stamps.restype = C.c_int
+    stamps.argtypes = [C.c_void_p, C.c_void_p]
+    st = L.stream_handle()
+    ph = np.zeros((4096, 16), np.uint64)
+    rt = np.zeros((4096, 2), np.uint64)
+    for prog, descs, ctx in ((e.ep, e.enc_descs, e.ectx), (e.dp, e.dec_descs, e.dctx)):
+        for i, op in enumerate(prog.ops):
+            if args and not any(a in op.name for a in args):
+                continue
+            nb = C.c_int32()
+            L.check(lib.gpi_conv_blocks(C.byref(descs[i]), C.byref(ctx.groups), C.byref(nb)), 'blocks')
+            nb = min(nb.value, 4096)
+            fn = lib.gpi_conv_forward if fwd else lib.gpi_conv_backward
+            torch.cuda.synchronize()
+            L.check(stamps(ph.ctypes.data, rt.ctypes.data), 'stamps')     # clears the device stamps
+            for _ in range(3):     # the last launch's stamps remain
+                L.check(fn(C.byref(descs[i]), C.byref(ctx), st), op.name)
+            torch.cuda.synchronize()
+            L.check(stamps(ph.ctypes.data, rt.ctypes.data), 'stamps')
+            p = ph[:nb].astype(np.int64)
+            r = rt[:nb].astype(np.int64)
+            d = np.diff(p, axis=1)
+            used = [k for k in range(7) if (p[:, k + 1] != 0).all() and (p[:, k] != 0).all()]
+            life = (r[:, 1] - r[:, 0]) * 10.0 / 1e3          # us
+            span = (r[:, 1].max() - r[:, 0].min()) * 10.0 / 1e3
+            inflight = life.sum() / span if span > 0 else 0
+            print('%-44s %s blocks %5d  life %6.2f us  span %6.2f us  in-flight %5.1f' %
+                  (op.name, 'fwd' if fwd else 'bwd', nb, life.mean(), span, inflight))
+            print('    cycles/phase: ' + '  '.join('%d:%6.0f' % (k + 1, d[:, k].mean()) for k in used))
+            sub = [1, 8, 9, 10, 11, 2]     # phase-1 issue points (timing build, backward)
+            if all((p[:, k] != 0).all() for k in sub):
+                print('    phase-1 split: ' + '  '.join('%d->%d:%6.0f' % (sub[k], sub[k + 1],
+                      (p[:, sub[k + 1]] - p[:, sub[k]]).mean()) for k in range(len(sub) - 1)))
+
+
+if __name__ == '__main__':
+    main()
