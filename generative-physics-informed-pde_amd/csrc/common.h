@@ -14,10 +14,24 @@
 
 namespace gpi {
 
+// DPP step: v + (v moved by ctrl within the rows of row_mask; other rows add 0)
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ float dpp_add(float v) {
+    const int t = __builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROW_MASK, 0xf, false);
+    return v + __int_as_float(t);
+}
+
+// Wave64 sum by the DPP ladder (no LDS traffic): quad pairs, quads, rows of 8 and 16
+// by row rotation, then row_bcast15 / row_bcast31 fold rows 0..3 into lane 63,
+// whose value is returned to every lane.
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+    v = dpp_add<0xb1, 0xf>(v);    // quad_perm [1,0,3,2]
+    v = dpp_add<0x4e, 0xf>(v);    // quad_perm [2,3,0,1]
+    v = dpp_add<0x124, 0xf>(v);   // row_ror:4
+    v = dpp_add<0x128, 0xf>(v);   // row_ror:8
+    v = dpp_add<0x142, 0xa>(v);   // row_bcast:15 into rows 1, 3
+    v = dpp_add<0x143, 0xc>(v);   // row_bcast:31 into rows 2, 3
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
 
 __device__ __forceinline__ double wave_sum_d(double v) {

@@ -80,6 +80,7 @@ struct ConvGeom {
     int rh, P;      // input image: rows [iy0, iy0 + rh), pitch P = w_in + 2H
     int gh, PG;     // output-gradient image: rows [gy0, gy0 + gh), pitch PG = w_out + 2H
     int ph;         // owned input rows (backward)
+    const float* zero;   // the zero page (kernel argument: no per-use address reload)
     Div d_in4, d_P4, d_g4, d_PG4, d_cin, d_cout, d_win, d_tp, d_wout;
 };
 
@@ -150,6 +151,7 @@ bool conv_geom(const gpi_conv_desc& d, const gpi_groups& g, ConvGeom& G) {
     if (ein * in4 >= lim || in4 * (G.P / 4) >= lim || eg * g4 >= lim || g4 * (G.PG / 4) >= lim ||
         eo * d.w_in >= lim || 256ull * G.th * d.w_out >= lim)
         return false;
+    G.zero = nullptr;   // set by launch()
     G.d_in4 = mkdiv((int)in4);
     G.d_P4 = mkdiv(G.P / 4);
     G.d_g4 = mkdiv((int)g4);
@@ -175,13 +177,13 @@ __device__ __forceinline__ void glds16(const float* g, float* lds_wave_base) {
 // dst[e] = *src(e) for e in [0, total) by 4-byte LDS-DMA; src(e) == nullptr reads the
 // zero page.  dst is padded to a multiple of 256 floats (whole waves write).
 template <typename Src>
-__device__ __forceinline__ void stage(float* dst, int total, Src src) {
+__device__ __forceinline__ void stage(float* dst, int total, const float* zero, Src src) {
     const int wb = threadIdx.x & ~63;
     for (int e0 = 0; e0 < total; e0 += 256) {
         if (e0 + wb < total) {
             const int e = e0 + (int)threadIdx.x;
             const float* p = e < total ? src(e) : nullptr;
-            glds4(p ? p : g_zero_page, dst + e0 + wb);
+            glds4(p ? p : zero, dst + e0 + wb);
         }
     }
 }
@@ -191,7 +193,7 @@ __device__ __forceinline__ void stage(float* dst, int total, Src src) {
 // halo chunks and rows outside [0, h) read the zero page.  dst padded to 256 floats.
 template <typename Plane>
 __device__ __forceinline__ void stage_img(float* dst, int nq, int nr, int P, Div d_q4, Div d_p4, int r0, int h,
-                                          int w, Plane plane) {
+                                          int w, const float* zero, Plane plane) {
     const int P4 = P >> 2, plane4 = nr * P4, total = nq * plane4;
     const int wb = threadIdx.x & ~63;
     for (int e0 = 0; e0 < total; e0 += 256) {
@@ -204,7 +206,7 @@ __device__ __forceinline__ void stage_img(float* dst, int nq, int nr, int P, Div
                 const int row = r0 + r;
                 if (row >= 0 && row < h && col >= 0 && col < w) p = plane(q) + row * w + col;
             }
-            glds16(p ? p : g_zero_page, dst + 4 * (e0 + wb));
+            glds16(p ? p : zero, dst + 4 * (e0 + wb));
         }
     }
 }
@@ -220,9 +222,9 @@ struct StatLoad {
 };
 
 __device__ __forceinline__ void stat_issue(const gpi_codec_ctx& c, int grp, int64_t sa, int na, double* da,
-                                           int64_t sb, int nb, double* db, StatLoad& L) {
+                                           int64_t sb, int nb, double* db, const float* zero, StatLoad& L) {
     const int t = threadIdx.x, k = t & 3, h = (t >> 2) & 1, ch = t >> 3;
-    const double* p = (const double*)g_zero_page;
+    const double* p = (const double*)zero;
     int64_t step = 0;
     L.out = nullptr;
     const int64_t rstride = c.n_stats * GPI_MAX_GROUPS * 4;   // doubles per replica
@@ -367,13 +369,13 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(gpi_conv_desc d, gpi_code
     PHASE(1);
 
     // ---- phase 1: every global read of the tile in flight together
-    stage(wT, nw, [&](int e) -> const float* {
+    stage(wT, nw, G.zero, [&](int e) -> const float* {
         const int co = e % CP, r = e / CP;
         return co < d.cout ? c.params + d.w_off + (int64_t)co * d.cin * KK + r : nullptr;
     });
     int iy0, rh_;
     in_rows(K, S, UP, d.pad, T.oy0, G.th, iy0, rh_);
-    stage_img(img, d.cin, G.rh, G.P, G.d_in4, G.d_P4, iy0, d.h_in, d.w_in,
+    stage_img(img, d.cin, G.rh, G.P, G.d_in4, G.d_P4, iy0, d.h_in, d.w_in, G.zero,
               [&](int q) -> const float* { return ib + (int64_t)q * HWi; });
     if (d.in_bn) {
         float gam = 0.f, bet = 0.f;
@@ -382,7 +384,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(gpi_conv_desc d, gpi_code
             bet = c.params[d.beta_off + tid];
         }
         StatLoad L;
-        stat_issue(c, T.grp, d.in_stat, d.cin, gst, 0, 0, nullptr, L);
+        stat_issue(c, T.grp, d.in_stat, d.cin, gst, 0, 0, nullptr, G.zero, L);
         stat_finish(L);
         __syncthreads();
         PHASE(2);
@@ -539,22 +541,25 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(gpi_conv_desc d, gpi_code
 
     // ---- phase 1: every global read in flight together
     if (has_gin)
-        stage(wD, nwd, [&](int e) -> const float* {
+        stage(wD, nwd, G.zero, [&](int e) -> const float* {
             const int ci = e & 15, k = e >> 4;
             const int co = k / KK, t = k - co * KK;
             return ci < d.cin ? c.params + d.w_off + ((int64_t)co * d.cin + ci) * KK + t : nullptr;
         });
+    PHASE(12);
     int gy0, gh_;
     g_rows(K, S, d.pad, T.oy0, G.th, gy0, gh_);
     const int64_t gbase = ((int64_t)T.b * d.out_ctot + d.out_c0) * HWo;
-    stage_img(gl, d.cout, G.gh, G.PG, G.d_g4, G.d_PG4, gy0, d.h_out, d.w_out,
+    stage_img(gl, d.cout, G.gh, G.PG, G.d_g4, G.d_PG4, gy0, d.h_out, d.w_out, G.zero,
               [&](int q) -> const float* { return c.ws + d.gout_off + gbase + (int64_t)q * HWo; });
+    PHASE(13);
     if (obn)
-        stage_img(gz, d.cout, G.gh, G.PG, G.d_g4, G.d_PG4, gy0, d.h_out, d.w_out,
+        stage_img(gz, d.cout, G.gh, G.PG, G.d_g4, G.d_PG4, gy0, d.h_out, d.w_out, G.zero,
                   [&](int q) -> const float* { return c.ws + d.out_off + gbase + (int64_t)q * HWo; });
+    PHASE(14);
     int iy0, rh_;
     in_rows(K, S, UP, d.pad, T.oy0, G.th, iy0, rh_);
-    stage_img(al, d.cin, G.rh, G.P, G.d_in4, G.d_P4, iy0, d.h_in, d.w_in,
+    stage_img(al, d.cin, G.rh, G.P, G.d_in4, G.d_P4, iy0, d.h_in, d.w_in, G.zero,
               [&](int q) -> const float* { return ib + (int64_t)q * HWi; });
     PHASE(8);
     // input-gradient epilogue operands (x, previous S_in) of this wave's first four pixel
@@ -571,8 +576,8 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(gpi_conv_desc d, gpi_code
             const int m = wv + 4 * (4 * round + u);
             const bool ok = m < nmblk;
             const int64_t o = ibase + 16 * m + 4 * kq;
-            if (d.in_bn) xv4[u] = *(const float4*)(ok ? c.ws + d.in_off + o : g_zero_page);
-            if (d.gin_accumulate) pv4[u] = *(const float4*)(ok ? c.ws + d.gin_off + o : g_zero_page);
+            if (d.in_bn) xv4[u] = *(const float4*)(ok ? c.ws + d.in_off + o : G.zero);
+            if (d.gin_accumulate) pv4[u] = *(const float4*)(ok ? c.ws + d.gin_off + o : G.zero);
             else pv4[u] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
     };
@@ -586,7 +591,7 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(gpi_conv_desc d, gpi_code
     {
         StatLoad L;
         stat_issue(c, T.grp, d.in_stat, d.in_bn ? d.cin : 0, gst, d.out_stat, obn ? d.cout : 0,
-                   gst + 4 * GPI_MAX_CIN, L);
+                   gst + 4 * GPI_MAX_CIN, G.zero, L);
         PHASE(10);
         stat_finish(L);
         PHASE(11);
@@ -900,6 +905,13 @@ int launch(const gpi_conv_desc& d, const gpi_codec_ctx& c, hipStream_t st, bool 
     const int cp = cp_of(d.cout);
     conv_kernel_t k = select_kernel(d, cp, fwd);
     if (!k) return GPI_ERR_UNSUPPORTED;
+    static const float* zero = nullptr;
+    if (!zero) {
+        void* p = nullptr;
+        if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_zero_page)) != hipSuccess) return GPI_ERR_LAUNCH;
+        zero = (const float*)p;
+    }
+    G.zero = zero;
     const size_t lds = fwd ? fwd_lds(d, G, cp) : bwd_lds(d, G);
     if (lds > 160 * 1024) return GPI_ERR_UNSUPPORTED;
     if (lds > 64 * 1024) {

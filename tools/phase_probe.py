@@ -7,7 +7,8 @@ prints mean cycles per phase, the mean workgroup lifetime, the kernel span on
 the 100 MHz real-time clock and the mean number of workgroups in flight.
 Phases (backward): 0 entry | 1 bases | 2 loads landed + stats | 3 coefficients |
 4 activations | 5 weight gradient | 6 input gradient | 7 sums/atomics; inside phase 1:
-8 LDS-DMA issued | 9 epilogue operands issued | 10 stat loads issued | 11 stats summed.
+12 weights issued | 13 gradient image issued | 14 BN operand image issued | 8 input image issued |
+9 epilogue operands issued | 10 stat loads issued | 11 stats summed.
 """
 import ctypes as C
 import os
@@ -64,7 +65,7 @@ def main():
             print('%-44s %s blocks %5d  life %6.2f us  span %6.2f us  in-flight %5.1f' %
                   (op.name, 'fwd' if fwd else 'bwd', nb, life.mean(), span, inflight))
             print('    cycles/phase: ' + '  '.join('%d:%6.0f' % (k + 1, d[:, k].mean()) for k in used))
-            sub = [1, 8, 9, 10, 11, 2]     # phase-1 issue points (timing build, backward)
+            sub = [1, 12, 13, 14, 8, 9, 10, 11, 2]     # phase-1 issue points (timing build, backward)
             if all((p[:, k] != 0).all() for k in sub):
                 print('    phase-1 split: ' + '  '.join('%d->%d:%6.0f' % (sub[k], sub[k + 1],
                       (p[:, sub[k + 1]] - p[:, sub[k]]).mean()) for k in range(len(sub) - 1)))
