@@ -30,6 +30,10 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+# HBM traffic per launch of the heaviest operators, from two separate rocprofv3 PMC
+# passes (FETCH_SIZE, WRITE_SIZE) over tools/kprobe.py: tools/profile_round.sh +
+# tools/pmc_traffic.py.  Used for roofline.traffic when the dominant operator is listed.
+TRAFFIC_JSON = os.path.join(ROOT, 'profiles', 'r01_traffic.json')
 
 CONFIGS = {
     # name: (factory, B_u, N_s, pool, field params (mean, std, corrlength))
@@ -238,8 +242,13 @@ def main():
                 json.dump([dict(op=n, ms=m, bytes=b, gbs=b / (m * 1e-3) / 1e9) for n, m, b in prof], fh, indent=1)
         name, ms, byts = max(prof, key=lambda t: t[1])
         ach = byts / (ms * 1e-3) / 1e9
+        traffic = None
+        if os.path.exists(TRAFFIC_JSON):
+            with open(TRAFFIC_JSON) as fh:
+                t = json.load(fh)['ops'].get(name)
+            traffic = round(t['traffic_bytes']) if t else None
         roof = dict(bound='hbm', achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit='GB/s',
-                    frac=round(ach / HBM_PEAK_GBS, 4), traffic=None, kernel=name,
+                    frac=round(ach / HBM_PEAK_GBS, 4), traffic=traffic, kernel=name,
                     kernel_ms=round(ms, 5), bytes_per_launch=byts,
                     codec_ms_sum=round(sum(t[1] for t in prof), 4))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -18,6 +18,16 @@ from . import _lib as L
 from .engine import ElboEngine
 
 
+def allreduce_shared(flat, group=None):
+    """Data-parallel gradient exchange: ONE SUM all-reduce
+    (the ELBO is a sum over samples, normalize=False) of the shared-parameter
+    prefix G[:n_shared] of the flat gradient; the per-sample variational rows
+    that follow it are rank-owned and never communicated."""
+    n = flat.n_shared
+    if n > 0:
+        dist.all_reduce(flat.G[:n], op=dist.ReduceOp.SUM, group=group)
+
+
 class FusedElboStep(object):
 
     def __init__(self, model, X_pool, B_u, X_s=None, Y=None, F=None, lr=1e-2, betas=(0.9, 0.999), eps=1e-8,
@@ -70,8 +80,7 @@ class FusedElboStep(object):
 
     def allreduce(self):
         if self.distributed:
-            n = self.flat.n_shared
-            dist.all_reduce(self.flat.G[:n], op=dist.ReduceOp.SUM, group=self.pg)
+            allreduce_shared(self.flat, self.pg)
 
     def update(self, stream=None):
         st = stream if stream is not None else L.stream_handle()
