@@ -46,16 +46,16 @@ __device__ __forceinline__ float c_v(const float* k, int nc, int I, int J) {
 
 __device__ void chol_band(float* L, const RomDims& D) {
     const int w = D.bw + 1;
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x, NT = blockDim.x;
     for (int k = 0; k < D.nI; ++k) {
         const float dkk = sqrtf(L[k * w]);
         __syncthreads();
-        for (int t = 1 + lane; t <= D.bw; t += 64)
+        for (int t = 1 + lane; t <= D.bw; t += NT)
             if (k + t < D.nI) L[(k + t) * w + t] /= dkk;
         if (lane == 0) L[k * w] = dkk;
         __syncthreads();
         const int np = D.bw * (D.bw + 1) / 2;
-        for (int e = lane; e < np; e += 64) {
+        for (int e = lane; e < np; e += NT) {
             // decode e -> (t1 >= t2) in [1, bw]
             int t1 = 1, rem = e;
             while (rem >= t1) { rem -= t1; ++t1; }
@@ -70,11 +70,11 @@ __device__ void chol_band(float* L, const RomDims& D) {
 // solve L L^T x = b in place (b -> x)
 __device__ void solve_band(const float* L, float* b, const RomDims& D) {
     const int w = D.bw + 1;
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x, NT = blockDim.x;
     for (int k = 0; k < D.nI; ++k) {
         const float yk = b[k] / L[k * w];
         __syncthreads();
-        for (int t = 1 + lane; t <= D.bw; t += 64)
+        for (int t = 1 + lane; t <= D.bw; t += NT)
             if (k + t < D.nI) b[k + t] -= L[(k + t) * w + t] * yk;
         if (lane == 0) b[k] = yk;
         __syncthreads();
@@ -82,7 +82,7 @@ __device__ void solve_band(const float* L, float* b, const RomDims& D) {
     for (int k = D.nI - 1; k >= 0; --k) {
         const float xk = b[k] / L[k * w];
         __syncthreads();
-        for (int t = 1 + lane; t <= D.bw; t += 64)
+        for (int t = 1 + lane; t <= D.bw; t += NT)
             if (k - t >= 0) b[k - t] -= L[k * w + t] * xk;
         if (lane == 0) b[k] = xk;
         __syncthreads();
@@ -101,7 +101,10 @@ __device__ __forceinline__ void interp(int i, int j, int r, int nc, int& n00, in
     else { n10 = n00 + (nc + 1); w0 = 1.f - eta; w1 = eta - xi; w2 = xi; }
 }
 
-__global__ __launch_bounds__(64) void rom_kernel(gpi_rom_desc d, RomDims D) {
+constexpr int ROM_NT = 256;      // threads per sample
+constexpr int ROM_U = 8;         // fine nodes per batch of global loads
+
+__global__ __launch_bounds__(ROM_NT) void rom_kernel(gpi_rom_desc d, RomDims D) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int w = D.bw + 1;
     float* kp = sm;                   // [nT] kappa
@@ -110,27 +113,28 @@ __global__ __launch_bounds__(64) void rom_kernel(gpi_rom_desc d, RomDims D) {
     float* b = u + D.nn;              // [nI]
     float* lam = b + D.nI;            // [nn]
     double* du = (double*)(sm + ((D.nT + D.nI * w + 2 * D.nn + D.nI + 1) & ~1));   // [nn] fp64 W^T dmu
+    double* lred = du + D.nn;         // [4] per-wave log-likelihood sums
     const int s = blockIdx.x;
-    const int lane = threadIdx.x;
+    const int tid = threadIdx.x, NT = ROM_NT;
     const int nc = D.nc;
     const float* x = d.x + (int64_t)s * d.x_stride;
     const float* F = d.F + (int64_t)s * D.nn;
 
     bool bad = false;
-    for (int t = lane; t < D.nT; t += 64) {
+    for (int t = tid; t < D.nT; t += NT) {
         const float kv = d.input_kappa ? x[t] : expf(x[t]) + 1e-8f;
         bad |= !(kv > 1e-12f);
         kp[t] = kv;
     }
     if (bad && d.flag) atomicOr(d.flag, 1);
-    for (int e = lane; e < D.nn; e += 64) {
+    for (int e = tid; e < D.nn; e += NT) {
         du[e] = (d.mode == GPI_ROM_BACKWARD && d.duc) ? (double)d.duc[(int64_t)s * D.nn + e] : 0.0;
         lam[e] = 0.f;
     }
     __syncthreads();
 
     // ---- assemble interior system (banded lower) + rhs
-    for (int ii = lane; ii < D.nI; ii += 64) {
+    for (int ii = tid; ii < D.nI; ii += NT) {
         const int J = ii / (nc - 1), I = ii - J * (nc - 1) + 1;
         const int p = I + (nc + 1) * J;
         const float chl = c_h(kp, nc, I - 1, J), chr = c_h(kp, nc, I, J);
@@ -149,61 +153,119 @@ __global__ __launch_bounds__(64) void rom_kernel(gpi_rom_desc d, RomDims D) {
     __syncthreads();
     chol_band(L, D);
     solve_band(L, b, D);
-    for (int e = lane; e < D.nn; e += 64) {
+    for (int e = tid; e < D.nn; e += NT) {
         const int I = e % (nc + 1), J = e / (nc + 1);
         u[e] = (I == 0 || I == nc) ? F[e] : b[J * (nc - 1) + (I - 1)];
     }
     __syncthreads();
-    if (d.uc) for (int e = lane; e < D.nn; e += 64) d.uc[(int64_t)s * D.nn + e] = u[e];
+    if (d.uc) for (int e = tid; e < D.nn; e += NT) d.uc[(int64_t)s * D.nn + e] = u[e];
 
-    // ---- prolongation (+ log-likelihood)
-    const int nf = D.n;
+    // ---- prolongation (+ log-likelihood, + W^T of the output gradient), by coarse square:
+    // four threads share square q = (I, J) and its corner values; each takes every fourth
+    // fine free node the square owns (interp()'s partition), loads its Y / logsigma / dmu
+    // in batches of ROM_U, and accumulates its W^T contributions to the four corners in
+    // registers; one fp64 LDS atomic per corner per square at the end.
+    const int nf = D.n, r = D.r;
+    const float rinv = 1.f / (float)r;
     float Lsum = 0.f;
-    for (int p = lane; p < D.dy; p += 64) {
-        const int j = p / (nf - 1), i = p - j * (nf - 1) + 1;
-        int n00, n10, n11;
-        float w0, w1, w2;
-        interp(i, j, D.r, nc, n00, n10, n11, w0, w1, w2);
-        const float mu = w0 * u[n00] + w1 * u[n10] + w2 * u[n11];
-        if (d.mu_y) d.mu_y[(int64_t)s * D.dy + p] = mu;
-        if (d.mode == GPI_ROM_FORWARD) continue;
-        float g;
-        if (d.mode == GPI_ROM_LOGLIK) {
-            const float ls = d.logsig_y[p];
-            const float e = expf(-2.f * ls);
-            const float rr = d.Y[(int64_t)s * D.dy + p] - mu;
-            Lsum += -0.5f * (2.f * ls + rr * rr * e + GPI_LOG2PI);
-            g = -d.loss_scale * rr * e;
-            atomicAdd(d.gacc_logsig + p, (double)(d.loss_scale * (1.f - rr * rr * e)));
-        } else {
-            if (!d.dmu) continue;
-            g = d.dmu[(int64_t)s * D.dy + p];
+    const bool want_g = d.mode == GPI_ROM_LOGLIK || (d.mode == GPI_ROM_BACKWARD && d.dmu);
+    for (int qb = 0; qb < nc * nc; qb += NT / 4) {
+        const int q = qb + (tid >> 2), sub = tid & 3;
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};   // corners v0, v1 (+x), v2 (+y), v3 (+x+y)
+        int v0 = 0;
+        if (q < nc * nc) {
+            const int I = q % nc, J = q / nc;
+            v0 = I + (nc + 1) * J;
+            const float u0 = u[v0], u1 = u[v0 + 1], u2 = u[v0 + nc + 1], u3 = u[v0 + nc + 2];
+            const int i0 = I == 0 ? 1 : I * r, i1 = (I + 1) * r - 1;           // free columns (inclusive)
+            const int rows = J == nc - 1 ? r + 1 : r;
+            const int ncol = i1 - i0 + 1, total = rows * ncol;
+            for (int e0 = sub; e0 < total; e0 += 4 * ROM_U) {
+                int pp[ROM_U];
+                float yv[ROM_U], lv[ROM_U], gv[ROM_U];
+#pragma unroll
+                for (int k = 0; k < ROM_U; ++k) {
+                    const int e = min(e0 + 4 * k, total - 1);
+                    const int jj = e / ncol, ii = e - jj * ncol;
+                    pp[k] = (J * r + jj) * (nf - 1) + (i0 + ii - 1);
+                }
+                if (d.mode == GPI_ROM_LOGLIK) {
+#pragma unroll
+                    for (int k = 0; k < ROM_U; ++k) {
+                        yv[k] = d.Y[(int64_t)s * D.dy + pp[k]];
+                        lv[k] = d.logsig_y[pp[k]];
+                    }
+                } else if (want_g) {
+#pragma unroll
+                    for (int k = 0; k < ROM_U; ++k) gv[k] = d.dmu[(int64_t)s * D.dy + pp[k]];
+                }
+#pragma unroll
+                for (int k = 0; k < ROM_U; ++k) {
+                    const int e = e0 + 4 * k;
+                    if (e >= total) break;
+                    const int jj = e / ncol, ii = e - jj * ncol;
+                    const float xi = (float)(i0 + ii - I * r) * rinv, eta = (float)jj * rinv;
+                    float w0, w1, w2, w3;
+                    if (xi >= eta) { w0 = 1.f - xi; w1 = xi - eta; w2 = 0.f; w3 = eta; }
+                    else { w0 = 1.f - eta; w1 = 0.f; w2 = eta - xi; w3 = xi; }
+                    const float mu = w0 * u0 + (w1 * u1 + w2 * u2) + w3 * u3;
+                    if (d.mu_y) d.mu_y[(int64_t)s * D.dy + pp[k]] = mu;
+                    if (!want_g) continue;
+                    float g;
+                    if (d.mode == GPI_ROM_LOGLIK) {
+                        const float ee = expf(-2.f * lv[k]);
+                        const float rr = yv[k] - mu;
+                        Lsum += -0.5f * (2.f * lv[k] + rr * rr * ee + GPI_LOG2PI);
+                        g = -d.loss_scale * rr * ee;
+                        atomicAdd(d.gacc_logsig + pp[k], (double)(d.loss_scale * (1.f - rr * rr * ee)));
+                    } else {
+                        g = gv[k];
+                    }
+                    acc[0] += w0 * g;
+                    acc[1] += w1 * g;
+                    acc[2] += w2 * g;
+                    acc[3] += w3 * g;
+                }
+            }
         }
-        atomicAdd(&du[n00], (double)(w0 * g));
-        atomicAdd(&du[n10], (double)(w1 * g));
-        atomicAdd(&du[n11], (double)(w2 * g));
+        if (want_g) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                acc[c] += __shfl_xor(acc[c], 1, 64);
+                acc[c] += __shfl_xor(acc[c], 2, 64);
+            }
+            if (q < nc * nc && sub == 0) {
+                atomicAdd(&du[v0], (double)acc[0]);
+                atomicAdd(&du[v0 + 1], (double)acc[1]);
+                atomicAdd(&du[v0 + nc + 1], (double)acc[2]);
+                atomicAdd(&du[v0 + nc + 2], (double)acc[3]);
+            }
+        }
     }
     if (d.mode == GPI_ROM_LOGLIK) {
         Lsum = wave_sum(Lsum);
-        if (lane == 0 && d.loss_acc) atomicAdd(d.loss_acc + blockIdx.x % GPI_REPLICAS, (double)Lsum);
+        if ((tid & 63) == 0) lred[tid >> 6] = (double)Lsum;
+        __syncthreads();
+        if (tid == 0 && d.loss_acc)
+            atomicAdd(d.loss_acc + blockIdx.x % GPI_REPLICAS, (lred[0] + lred[1]) + (lred[2] + lred[3]));
     }
     if (d.mode == GPI_ROM_FORWARD) return;
     __syncthreads();
 
     // ---- adjoint
-    for (int ii = lane; ii < D.nI; ii += 64) {
+    for (int ii = tid; ii < D.nI; ii += NT) {
         const int J = ii / (nc - 1), I = ii - J * (nc - 1) + 1;
         b[ii] = (float)du[I + (nc + 1) * J];
     }
     __syncthreads();
     solve_band(L, b, D);
-    for (int ii = lane; ii < D.nI; ii += 64) {
+    for (int ii = tid; ii < D.nI; ii += NT) {
         const int J = ii / (nc - 1), I = ii - J * (nc - 1) + 1;
         lam[I + (nc + 1) * J] = b[ii];
     }
     __syncthreads();
     // ---- dJ/dx per coarse triangle
-    for (int t = lane; t < D.nT; t += 64) {
+    for (int t = tid; t < D.nT; t += NT) {
         const int q = t >> 1, ul = t & 1;
         const int I = q % nc, J = q / nc;
         const int v0 = I + (nc + 1) * J, v1 = v0 + 1, v2 = v0 + (nc + 1), v3 = v2 + 1;
@@ -235,8 +297,8 @@ extern "C" int gpi_rom(const gpi_rom_desc* d, void* stream) {
     D.r = d->refine;
     D.n = d->nc * d->refine;
     D.dy = (D.n + 1) * (D.n - 1);
-    const size_t lds = sizeof(float) * (D.nT + D.nI * (D.bw + 1) + 4 * D.nn + D.nI + 8);
-    hipLaunchKernelGGL(rom_kernel, dim3(d->n), dim3(64), lds, (hipStream_t)stream, *d, D);
+    const size_t lds = sizeof(float) * (D.nT + D.nI * (D.bw + 1) + 4 * D.nn + D.nI + 16);
+    hipLaunchKernelGGL(rom_kernel, dim3(d->n), dim3(ROM_NT), lds, (hipStream_t)stream, *d, D);
     GPI_CHECK_LAUNCH();
     return GPI_OK;
 }
