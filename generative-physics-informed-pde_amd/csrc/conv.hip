@@ -81,6 +81,8 @@ struct ConvGeom {
     int gh, PG;     // output-gradient image: rows [gy0, gy0 + gh), pitch PG = w_out + 2H
     int ph;         // owned input rows (backward)
     const float* zero;   // the zero page (kernel argument: no per-use address reload)
+    int in_sq, in_sr, in_sc;   // 256 chunks of the input image = (planes, rows, chunks)
+    int g_sq, g_sr, g_sc;      // ... of the output-gradient image
     Div d_in4, d_P4, d_g4, d_PG4, d_cin, d_cout, d_win, d_tp, d_wout;
 };
 
@@ -152,6 +154,15 @@ bool conv_geom(const gpi_conv_desc& d, const gpi_groups& g, ConvGeom& G) {
         eo * d.w_in >= lim || 256ull * G.th * d.w_out >= lim)
         return false;
     G.zero = nullptr;   // set by launch()
+    {
+        const int P4 = G.P / 4, pl = G.rh * P4, Q4 = G.PG / 4, gl = G.gh * Q4;
+        G.in_sq = 256 / pl;
+        G.in_sr = (256 % pl) / P4;
+        G.in_sc = (256 % pl) % P4;
+        G.g_sq = 256 / gl;
+        G.g_sr = (256 % gl) / Q4;
+        G.g_sc = (256 % gl) % Q4;
+    }
     G.d_in4 = mkdiv((int)in4);
     G.d_P4 = mkdiv(G.P / 4);
     G.d_g4 = mkdiv((int)g4);
@@ -188,26 +199,50 @@ __device__ __forceinline__ void stage(float* dst, int total, const float* zero, 
     }
 }
 
+// Chunk (16 B) e of a row image of planes of nr rows x P4 chunks decomposed as
+// (plane q, row r, chunk c4), advanced by 256 chunks per step with constant carries
+// (sq, sr, sc) = decomposition of 256, so a loop pays no division per chunk.
+struct ChunkIter {
+    int q, r, c4;
+    __device__ __forceinline__ void init(int e, int plane4, int P4, Div d_q4, Div d_p4) {
+        q = dq(e, d_q4);
+        const int rem = e - q * plane4;
+        r = dq(rem, d_p4);
+        c4 = rem - r * P4;
+    }
+    __device__ __forceinline__ void step(int sq, int sr, int sc, int P4, int nr) {
+        c4 += sc;
+        if (c4 >= P4) { c4 -= P4; ++r; }
+        r += sr;
+        if (r >= nr) { r -= nr; ++q; }
+        q += sq;
+    }
+};
+
+// Extra zero chunks staged after every row image: the maskless MFMA loops read up to a
+// few floats past an image's last row.
+constexpr int IMG_MARGIN4 = 16;
+__host__ __device__ inline int img_floats(int nq, int nr, int P) { return pad256(4 * (nq * nr * (P / 4) + IMG_MARGIN4)); }
+
 // Row image of nq planes (plane q at plane(q), an h x w plane): rows [r0, r0 + nr),
-// LDS pitch w + 2H, chunk e (16 B) of plane q = e / (nr * P / 4).  16-byte LDS-DMA;
-// halo chunks and rows outside [0, h) read the zero page.  dst padded to 256 floats.
+// LDS pitch P = w + 2 HALO.  16-byte LDS-DMA; halo chunks, rows outside [0, h) and the
+// IMG_MARGIN4 tail chunks read the zero page.
 template <typename Plane>
-__device__ __forceinline__ void stage_img(float* dst, int nq, int nr, int P, Div d_q4, Div d_p4, int r0, int h,
-                                          int w, const float* zero, Plane plane) {
-    const int P4 = P >> 2, plane4 = nr * P4, total = nq * plane4;
+__device__ __forceinline__ void stage_img(float* dst, int nq, int nr, int P, Div d_q4, Div d_p4, int sq, int sr,
+                                          int sc, int r0, int h, int w, const float* zero, Plane plane) {
+    const int P4 = P >> 2, plane4 = nr * P4, total = nq * plane4 + IMG_MARGIN4;
     const int wb = threadIdx.x & ~63;
+    const int c4lo = HALO / 4, c4hi = HALO / 4 + w / 4;
+    ChunkIter it;
+    it.init(threadIdx.x, plane4, P4, d_q4, d_p4);
     for (int e0 = 0; e0 < total; e0 += 256) {
         if (e0 + wb < total) {
-            const int e = e0 + (int)threadIdx.x;
-            const float* p = nullptr;
-            if (e < total) {
-                const int q = dq(e, d_q4), rem = e - q * plane4;
-                const int r = dq(rem, d_p4), col = 4 * (rem - r * P4) - HALO;
-                const int row = r0 + r;
-                if (row >= 0 && row < h && col >= 0 && col < w) p = plane(q) + row * w + col;
-            }
-            glds16(p ? p : zero, dst + 4 * (e0 + wb));
+            const int row = r0 + it.r;
+            const bool ok = it.q < nq && row >= 0 && row < h && it.c4 >= c4lo && it.c4 < c4hi;
+            const float* p = ok ? plane(it.q) + row * w + 4 * (it.c4 - c4lo) : zero;
+            glds16(p, dst + 4 * (e0 + wb));
         }
+        it.step(sq, sr, sc, P4, nr);
     }
 }
 
@@ -313,23 +348,24 @@ __device__ __forceinline__ const float* input_base(const gpi_conv_desc& d, const
 __device__ __forceinline__ void activate_img(float* img, const ConvGeom& G, const gpi_conv_desc& d, int iy0,
                                              const float* sc, const float* sh) {
     const int P4 = G.P >> 2, plane4 = G.rh * P4, total = d.cin * plane4;
+    const int c4lo = HALO / 4, c4hi = HALO / 4 + d.w_in / 4;
     float4* im4 = reinterpret_cast<float4*>(img);
-    for (int e0 = threadIdx.x; e0 < total; e0 += 1024) {
-        float4 v[4];
-        bool ok[4];
-        int ci[4];
+    ChunkIter it;
+    it.init(threadIdx.x, plane4, P4, G.d_in4, G.d_P4);
+    for (int e0 = threadIdx.x; e0 < total; e0 += 512) {
+        float4 v[2];
+        bool ok[2];
+        int ci[2];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int e = e0 + 256 * u;
-            const int q = dq(e, G.d_in4), rem = e - q * plane4;
-            const int r = dq(rem, G.d_P4), col = 4 * (rem - r * P4) - HALO;
-            const int row = iy0 + r;
-            ok[u] = e < total && row >= 0 && row < d.h_in && col >= 0 && col < d.w_in;
-            ci[u] = q;
-            if (ok[u]) v[u] = im4[e];
+        for (int u = 0; u < 2; ++u) {
+            const int row = iy0 + it.r;
+            ok[u] = e0 + 256 * u < total && row >= 0 && row < d.h_in && it.c4 >= c4lo && it.c4 < c4hi;
+            ci[u] = it.q;
+            if (ok[u]) v[u] = im4[e0 + 256 * u];
+            it.step(G.in_sq, G.in_sr, G.in_sc, P4, G.rh);
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < 2; ++u) {
             if (ok[u]) {
                 const float a = sc[ci[u]], b = sh[ci[u]];
                 float4 o;
@@ -358,7 +394,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(gpi_conv_desc d, gpi_code
     float* red = scratch + 64;           // 2*CP <= 16
     float* wT = smem + pad256(FWD_HDR);  // [cin][KK][CP]
     const int nw = d.cin * KK * CP;
-    float* img = wT + pad256(nw);        // [cin][rh][P]
+    float* img = wT + pad256(nw);        // [cin][rh][P] + zero margin
 
     const int tid = threadIdx.x;
     RTSTAMP(0);
@@ -375,7 +411,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(gpi_conv_desc d, gpi_code
     });
     int iy0, rh_;
     in_rows(K, S, UP, d.pad, T.oy0, G.th, iy0, rh_);
-    stage_img(img, d.cin, G.rh, G.P, G.d_in4, G.d_P4, iy0, d.h_in, d.w_in, G.zero,
+    stage_img(img, d.cin, G.rh, G.P, G.d_in4, G.d_P4, G.in_sq, G.in_sr, G.in_sc, iy0, d.h_in, d.w_in, G.zero,
               [&](int q) -> const float* { return ib + (int64_t)q * HWi; });
     if (d.in_bn) {
         float gam = 0.f, bet = 0.f;
@@ -520,15 +556,17 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(gpi_conv_desc d, gpi_code
     float* o_coef = i_gam + GPI_MAX_CIN;              // [MAX_COUT][4]: mean, inv, mS, mSx
     const bool has_gin = d.gin_off >= 0;
     const bool obn = d.gout_mode == 0;
-    float* wD = smem + pad256(BWD_HDR);               // [cout*KK][16]: W[co][ci][tap] at (co*KK + tap)*16 + ci
-    const int nwd = has_gin ? d.cout * KK * 16 : 0;
-    float* gl = wD + pad256(nwd);                     // [cout][gh][PG]
+    const int KD = d.cout * KK;                       // input-gradient reduction length
+    const int KD4 = (KD + 3) & ~3;
+    float* wD = smem + pad256(BWD_HDR);               // [KD4][16]: W[co][ci][tap] at (co*KK + tap)*16 + ci, zero padded
+    const int nwd = has_gin ? KD4 * 16 : 0;
+    int* ktab = (int*)(wD + pad256(nwd));             // [KD4] output-gradient offset of reduction index k
+    float* gl = (float*)ktab + (has_gin ? pad256(KD4) : 0);   // [cout][gh][PG]
     const int gplane = G.gh * G.PG;
-    const int ngl = d.cout * gplane;
-    float* gz = gl + pad256(ngl);                     // raw z of the output (BN-backward only)
-    float* al = gz + (obn ? pad256(ngl) : 0);         // [cin][rh][P]
-    const int aplane = G.rh * G.P;
-    float* red = al + pad256(d.cin * aplane);
+    const int gimg = img_floats(d.cout, G.gh, G.PG);
+    float* gz = gl + gimg;                            // raw z of the output (BN-backward only)
+    float* al = gz + (obn ? gimg : 0);                // [cin][rh][P]
+    float* red = al + img_floats(d.cin, G.rh, G.P);
 
     const int tid = threadIdx.x;
     const int lane = tid & 63, wv = tid >> 6, kq = lane >> 4, l16 = lane & 15;
@@ -544,22 +582,22 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(gpi_conv_desc d, gpi_code
         stage(wD, nwd, G.zero, [&](int e) -> const float* {
             const int ci = e & 15, k = e >> 4;
             const int co = k / KK, t = k - co * KK;
-            return ci < d.cin ? c.params + d.w_off + ((int64_t)co * d.cin + ci) * KK + t : nullptr;
+            return ci < d.cin && k < KD ? c.params + d.w_off + ((int64_t)co * d.cin + ci) * KK + t : nullptr;
         });
     PHASE(12);
     int gy0, gh_;
     g_rows(K, S, d.pad, T.oy0, G.th, gy0, gh_);
     const int64_t gbase = ((int64_t)T.b * d.out_ctot + d.out_c0) * HWo;
-    stage_img(gl, d.cout, G.gh, G.PG, G.d_g4, G.d_PG4, gy0, d.h_out, d.w_out, G.zero,
+    stage_img(gl, d.cout, G.gh, G.PG, G.d_g4, G.d_PG4, G.g_sq, G.g_sr, G.g_sc, gy0, d.h_out, d.w_out, G.zero,
               [&](int q) -> const float* { return c.ws + d.gout_off + gbase + (int64_t)q * HWo; });
     PHASE(13);
     if (obn)
-        stage_img(gz, d.cout, G.gh, G.PG, G.d_g4, G.d_PG4, gy0, d.h_out, d.w_out, G.zero,
+        stage_img(gz, d.cout, G.gh, G.PG, G.d_g4, G.d_PG4, G.g_sq, G.g_sr, G.g_sc, gy0, d.h_out, d.w_out, G.zero,
                   [&](int q) -> const float* { return c.ws + d.out_off + gbase + (int64_t)q * HWo; });
     PHASE(14);
     int iy0, rh_;
     in_rows(K, S, UP, d.pad, T.oy0, G.th, iy0, rh_);
-    stage_img(al, d.cin, G.rh, G.P, G.d_in4, G.d_P4, iy0, d.h_in, d.w_in, G.zero,
+    stage_img(al, d.cin, G.rh, G.P, G.d_in4, G.d_P4, G.in_sq, G.in_sr, G.in_sc, iy0, d.h_in, d.w_in, G.zero,
               [&](int q) -> const float* { return ib + (int64_t)q * HWi; });
     PHASE(8);
     // input-gradient epilogue operands (x, previous S_in) of this wave's first four pixel
@@ -623,28 +661,42 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(gpi_conv_desc d, gpi_code
     __syncthreads();
     PHASE(3);
 
-    // ---- phase 3: activations in LDS
+    // ---- phase 3: activations in LDS; offset table of the input-gradient reduction
     if (d.in_bn) activate_img(al, G, d, iy0, i_sc, i_sh);
+    if (has_gin && S != 2) {
+        // A operand of reduction index k = (co, ky, kx) for owned pixel (qy, px):
+        // gl[(S1) qy*PG + px | (UP) 2 qy*PG + 2 px] + ktab[k]
+        const int ry0 = (UP ? 2 * py0 : py0) + d.pad - gy0;
+        for (int k = tid; k < KD4; k += 256) {
+            int o = 0;
+            if (k < KD) {
+                const int co = k / KK, tap = k - co * KK, ky = tap / K, kx = tap - ky * K;
+                o = co * gplane + (ry0 - ky) * G.PG + d.pad - kx + HALO;
+            }
+            ktab[k] = o;
+        }
+    }
     if (obn) {
         const int P4 = G.PG >> 2, plane4 = G.gh * P4, total = d.cout * plane4;
+        const int c4lo = HALO / 4, c4hi = HALO / 4 + d.w_out / 4;
         float4* g4 = reinterpret_cast<float4*>(gl);
         const float4* z4 = reinterpret_cast<const float4*>(gz);
+        ChunkIter it;
+        it.init(tid, plane4, P4, G.d_g4, G.d_PG4);
         for (int e0 = tid; e0 < total; e0 += 512) {
             float4 sv[2], zv[2];
             bool ok[2];
             int co[2];
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
-                const int e = e0 + 256 * u;
-                const int q = dq(e, G.d_g4), rem = e - q * plane4;
-                const int r = dq(rem, G.d_PG4), col = 4 * (rem - r * P4) - HALO;
-                const int row = gy0 + r;
-                ok[u] = e < total && row >= 0 && row < d.h_out && col >= 0 && col < d.w_out;
-                co[u] = q;
+                const int row = gy0 + it.r;
+                ok[u] = e0 + 256 * u < total && row >= 0 && row < d.h_out && it.c4 >= c4lo && it.c4 < c4hi;
+                co[u] = it.q;
                 if (ok[u]) {
-                    sv[u] = g4[e];
-                    zv[u] = z4[e];
+                    sv[u] = g4[e0 + 256 * u];
+                    zv[u] = z4[e0 + 256 * u];
                 }
+                it.step(G.g_sq, G.g_sr, G.g_sc, P4, G.gh);
             }
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
@@ -664,7 +716,10 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(gpi_conv_desc d, gpi_code
     __syncthreads();
     PHASE(4);
 
-    // ---- phase 4a: weight gradient (MFMA, column-shift form) -> slab row
+    // ---- phase 4a: weight gradient (MFMA, column-shift form) -> slab row.
+    // Stride 1 / upsampling: no masks in the loop -- the zero halos and tail margins of the
+    // images make every out-of-range read a zero or a finite value multiplied by a zero,
+    // and rows i >= M / columns j >= N of the tile (clamped operands) are never stored.
     const int J = d.cin * KK;
     const int rowlen = d.cout * J + (d.in_bn ? 2 * d.cin : 0);
     float* slab = c.wpart + d.wpart_off + (int64_t)blockIdx.x * rowlen;
@@ -675,47 +730,41 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(gpi_conv_desc d, gpi_code
         const int nxs = (XW + 3) >> 2;
         for (int mb = 0; mb < nmb; ++mb) {
             const int i = 16 * mb + l16;
-            const bool iok = i < MI;
             const int co = min(i / K, d.cout - 1), kx = i - (i / K) * K;
             for (int nb0 = 0; nb0 < nnb; nb0 += 2) {
                 const bool two = nb0 + 1 < nnb;
                 int ci[2], ky[2];
-                bool jok[2];
 #pragma unroll
                 for (int u = 0; u < 2; ++u) {
                     const int j = 16 * (nb0 + u) + l16;
-                    jok[u] = j < NJ;
                     ci[u] = min(j / K, d.cin - 1);
                     ky[u] = j - (j / K) * K;
                 }
                 f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
                 for (int ty = wv; ty < G.th; ty += 4) {
-                    const float* grow = gl + (co * G.gh + (T.oy0 + ty - gy0)) * G.PG + HALO;
+                    const float* grow = gl + (co * G.gh + (T.oy0 + ty - gy0)) * G.PG + HALO - kx;
                     const float* brow[2];
 #pragma unroll
                     for (int u = 0; u < 2; ++u) {
                         const int ry = UP ? fdiv2(T.oy0 + ty - d.pad + ky[u]) - iy0 : ty * S + ky[u];
                         brow[u] = al + (ci[u] * G.rh + ry) * G.P + HALO;
                     }
-                    for (int xs = 0; xs < nxs; ++xs) {
-                        const int xv = 4 * xs + kq;          // virtual column index in [0, XW)
-                        const int t2 = xv - kx;
-                        bool aok = iok && t2 >= 0;
-                        int ox = t2;
-                        if (S == 2) {
-                            aok = aok && !(t2 & 1);
-                            ox = t2 >> 1;
+                    if (S == 2) {
+                        for (int xs = 0; xs < nxs; ++xs) {
+                            const int xv = 4 * xs + kq;          // virtual column, xv - kx = 2 ox
+                            const int t2 = xv - kx;
+                            const float a = (t2 & 1) ? 0.f : grow[kx + (t2 >> 1)];
+                            const int ix = xv - d.pad;
+                            acc[0] = mfma4(a, brow[0][ix], acc[0]);
+                            if (two) acc[1] = mfma4(a, brow[1][ix], acc[1]);
                         }
-                        aok = aok && ox < d.w_out;
-                        const float a = aok ? grow[aok ? ox : 0] : 0.f;
-                        const bool xok = xv < XW;
-                        const int ix = UP ? fdiv2(xv - d.pad) : xv - d.pad;   // input column (halo >= -pad)
-                        const int ixc = xok ? ix : 0;
-                        const float b0 = (jok[0] && xok) ? brow[0][ixc] : 0.f;
-                        acc[0] = mfma4(a, b0, acc[0]);
-                        if (two) {
-                            const float b1 = (jok[1] && xok) ? brow[1][ixc] : 0.f;
-                            acc[1] = mfma4(a, b1, acc[1]);
+                    } else {
+                        for (int xs = 0; xs < nxs; ++xs) {
+                            const int xv = 4 * xs + kq;          // virtual column, ox = xv - kx
+                            const float a = grow[xv];
+                            const int ix = UP ? fdiv2(xv - d.pad) : xv - d.pad;
+                            acc[0] = mfma4(a, brow[0][ix], acc[0]);
+                            if (two) acc[1] = mfma4(a, brow[1][ix], acc[1]);
                         }
                     }
                 }
@@ -756,8 +805,7 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(gpi_conv_desc d, gpi_code
             l_inv = i_inv[ci_l];
             l_gam = i_gam[ci_l];
         }
-        const int KD = d.cout * KK;
-        const int nkd = (KD + 3) >> 2;
+        const int nkd = KD4 >> 2;
         const bool cok = l16 < d.cin;
         for (int round = 0; wv + 16 * round < nmblk; ++round) {
             if (round > 0) own_load(round);
@@ -767,30 +815,29 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(gpi_conv_desc d, gpi_code
                 if (m < nmblk) {
                     const int i = 16 * m + l16;                   // owned pixel of this lane's A row
                     const int qy = dq(i, G.d_win), px = i - qy * d.w_in;
-                    const int py = py0 + qy;
                     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-                    for (int ks = 0; ks < nkd; ++ks) {
-                        const int k = 4 * ks + kq;
-                        const bool kok = k < KD;
-                        const int kc = kok ? k : 0;
-                        const int co = kc / KK, tap = kc - co * KK;
-                        const int ky = tap / K, kx = tap - ky * K;
-                        const float* gc = gl + co * gplane + HALO;
-                        float a;
-                        if (UP) {
-                            const int o = (2 * py + d.pad - ky - gy0) * G.PG + (2 * px + d.pad - kx);
-                            a = (gc[o] + gc[o + 1]) + (gc[o + G.PG] + gc[o + G.PG + 1]);
-                        } else if (S == 2) {
+                    if (S == 2) {
+                        const int py = py0 + qy;
+                        for (int ks = 0; ks < nkd; ++ks) {
+                            const int k = 4 * ks + kq;
+                            const bool kok = k < KD;
+                            const int kc = kok ? k : 0;
+                            const int co = kc / KK, tap = kc - co * KK;
+                            const int ky = tap / K, kx = tap - ky * K;
                             const int oy2 = py + d.pad - ky, ox2 = px + d.pad - kx;
-                            const bool ok2 = !((oy2 | ox2) & 1);
-                            const int o = ok2 ? ((oy2 >> 1) - gy0) * G.PG + (ox2 >> 1) : 0;
-                            a = ok2 ? gc[o] : 0.f;
-                        } else {
-                            a = gc[(py + d.pad - ky - gy0) * G.PG + (px + d.pad - kx)];
+                            const bool ok2 = kok && !((oy2 | ox2) & 1);
+                            const int o = co * gplane + ((oy2 >> 1) - gy0) * G.PG + (ox2 >> 1) + HALO;
+                            const float a = ok2 ? gl[o] : 0.f;
+                            acc = mfma4(a, wD[k * 16 + l16], acc);
                         }
-                        a = kok ? a : 0.f;
-                        const float b = kok ? wD[kc * 16 + l16] : 0.f;
-                        acc = mfma4(a, b, acc);
+                    } else {
+                        const float* gp0 = gl + (UP ? 2 * (qy * G.PG + px) : qy * G.PG + px);
+                        for (int ks = 0; ks < nkd; ++ks) {
+                            const int k = 4 * ks + kq;
+                            const float* ga = gp0 + ktab[k];
+                            const float a = UP ? (ga[0] + ga[1]) + (ga[G.PG] + ga[G.PG + 1]) : ga[0];
+                            acc = mfma4(a, wD[k * 16 + l16], acc);
+                        }
                     }
                     if (cok) {
                         float* gp = c.ws + d.gin_off + ibase + 16 * m + 4 * kq;
@@ -848,13 +895,14 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(gpi_conv_desc d, gpi_code
 
 size_t fwd_lds(const gpi_conv_desc& d, const ConvGeom& G, int cp) {
     return sizeof(float) *
-           ((size_t)pad256(FWD_HDR) + pad256(d.cin * d.k * d.k * cp) + pad256(d.cin * G.rh * G.P));
+           ((size_t)pad256(FWD_HDR) + pad256(d.cin * d.k * d.k * cp) + img_floats(d.cin, G.rh, G.P));
 }
 
 size_t bwd_lds(const gpi_conv_desc& d, const ConvGeom& G) {
-    const int ngl = pad256(d.cout * G.gh * G.PG);
-    size_t f = (size_t)pad256(BWD_HDR) + (d.gin_off >= 0 ? pad256(d.cout * d.k * d.k * 16) : 0) + ngl +
-               (d.gout_mode == 0 ? ngl : 0) + pad256(d.cin * G.rh * G.P) + BWD_RED;
+    const int KD4 = (d.cout * d.k * d.k + 3) & ~3;
+    const int gimg = img_floats(d.cout, G.gh, G.PG);
+    size_t f = (size_t)pad256(BWD_HDR) + (d.gin_off >= 0 ? pad256(KD4 * 16) + pad256(KD4) : 0) + gimg +
+               (d.gout_mode == 0 ? gimg : 0) + img_floats(d.cin, G.rh, G.P) + BWD_RED;
     return f * sizeof(float);
 }
 
