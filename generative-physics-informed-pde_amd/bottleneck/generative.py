@@ -35,7 +35,7 @@ class _ElboFunction(torch.autograd.Function):
         e = ctx.engine
         e.backward()
         tmp = torch.empty_like(e.flat.G)
-        e.finalize(tmp)
+        e.finalize(tmp, zero_acc=True)      # every finalize leaves the fp64 accumulator zeroed
         tmp.mul_(-grad_out)                 # engine gradients are d(-elbo)/dtheta
         e.flat.deliver(tmp)
         return None, None

@@ -256,24 +256,27 @@ struct StatLoad {
     double* out;
 };
 
-__device__ __forceinline__ void stat_issue(const gpi_codec_ctx& c, int grp, int64_t sa, int na, double* da,
-                                           int64_t sb, int nb, double* db, const float* zero, StatLoad& L) {
+__device__ __forceinline__ void stat_issue(const gpi_stat* stats, int64_t n_stats, int grp, int64_t sa, int na,
+                                           double* da, int64_t sb, int nb, double* db, const float* zero, StatLoad& L) {
     const int t = threadIdx.x, k = t & 3, h = (t >> 2) & 1, ch = t >> 3;
     const double* p = (const double*)zero;
     int64_t step = 0;
     L.out = nullptr;
-    const int64_t rstride = c.n_stats * GPI_MAX_GROUPS * 4;   // doubles per replica
+    // layout [GPI_REPLICAS][group][stat]: consecutive channels of one replica share cache lines
+    const int64_t rstride = n_stats * GPI_MAX_GROUPS * 4;   // doubles per replica
+    const gpi_stat* sg = stats + (int64_t)grp * n_stats;
     if (ch < na) {
-        p = &c.stats[(sa + ch) * GPI_MAX_GROUPS + grp].sum + k + h * STAT_HALF * rstride;
+        p = &sg[sa + ch].sum + k + h * STAT_HALF * rstride;
         step = rstride;
         L.out = da + 4 * ch + k;
     } else if (ch - na < nb) {
-        p = &c.stats[(sb + ch - na) * GPI_MAX_GROUPS + grp].sum + k + h * STAT_HALF * rstride;
+        p = &sg[sb + ch - na].sum + k + h * STAT_HALF * rstride;
         step = rstride;
         L.out = db + 4 * (ch - na) + k;
     }
+    const auto g = (const __attribute__((address_space(1))) double*)p;
 #pragma unroll
-    for (int r = 0; r < STAT_HALF; ++r) L.v[r] = p[r * step];
+    for (int r = 0; r < STAT_HALF; ++r) L.v[r] = g[r * step];
 }
 
 __device__ __forceinline__ void stat_finish(StatLoad& L) {
@@ -290,7 +293,7 @@ __device__ __forceinline__ void stat_finish(StatLoad& L) {
 
 __device__ __forceinline__ gpi_stat* stat_slot(const gpi_codec_ctx& c, int64_t stat, int grp) {
     const int r = blockIdx.x % GPI_REPLICAS;
-    return c.stats + ((int64_t)r * c.n_stats + stat) * GPI_MAX_GROUPS + grp;
+    return c.stats + ((int64_t)r * GPI_MAX_GROUPS + grp) * c.n_stats + stat;
 }
 
 __device__ __forceinline__ void mean_invstd(const double* s4, double n, float eps, float& mean, float& invstd) {
@@ -320,6 +323,29 @@ __device__ __forceinline__ void fma_vec(float (&acc)[CP], const float* w, float 
             acc[2 * q + 1] = fmaf(w2.y, v, acc[2 * q + 1]);
         }
     }
+}
+
+// Keep a kernel argument in a register from kernel entry on: the compiler cannot
+// rematerialise the value of an opaque asm, so it never re-reads the (large, by-value)
+// argument block with a dependent s_load + s_waitcnt in the middle of a phase.
+template <typename T>
+__device__ __forceinline__ T pin(T v) {
+    asm volatile("" : "+s"(v));
+    return v;
+}
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// Global-address-space views of (pinned, hence generic) pointers: ordinary loads and
+// stores through them stay global_load / global_store.  A flat access could alias LDS,
+// so the compiler would drain every outstanding LDS-DMA (vmcnt(0)) in front of it.
+template <typename T>
+__device__ __forceinline__ const __attribute__((address_space(1))) T* as_gld(const T* p) {
+    return (const __attribute__((address_space(1))) T*)p;
+}
+template <typename T>
+__device__ __forceinline__ __attribute__((address_space(1))) T* as_gst(T* p) {
+    return (__attribute__((address_space(1))) T*)p;
 }
 
 struct TileIdx {
@@ -399,28 +425,32 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(gpi_conv_desc d, gpi_code
     const int tid = threadIdx.x;
     RTSTAMP(0);
     PHASE(0);
+    float* const ws = pin(c.ws);
+    const float* const params = pin(c.params);
+    const float* const zero = pin(G.zero);
+    const int64_t w_off = pin(d.w_off);
     const TileIdx T = tile_of(G, c.groups);
     const int HWi = d.h_in * d.w_in, HWo = d.h_out * d.w_out;
     const float* ib = input_base(d, c, T.b);
     PHASE(1);
 
     // ---- phase 1: every global read of the tile in flight together
-    stage(wT, nw, G.zero, [&](int e) -> const float* {
+    stage(wT, nw, zero, [&](int e) -> const float* {
         const int co = e % CP, r = e / CP;
-        return co < d.cout ? c.params + d.w_off + (int64_t)co * d.cin * KK + r : nullptr;
+        return co < d.cout ? params + w_off + (int64_t)co * d.cin * KK + r : nullptr;
     });
     int iy0, rh_;
     in_rows(K, S, UP, d.pad, T.oy0, G.th, iy0, rh_);
-    stage_img(img, d.cin, G.rh, G.P, G.d_in4, G.d_P4, G.in_sq, G.in_sr, G.in_sc, iy0, d.h_in, d.w_in, G.zero,
+    stage_img(img, d.cin, G.rh, G.P, G.d_in4, G.d_P4, G.in_sq, G.in_sr, G.in_sc, iy0, d.h_in, d.w_in, zero,
               [&](int q) -> const float* { return ib + (int64_t)q * HWi; });
     if (d.in_bn) {
         float gam = 0.f, bet = 0.f;
         if (tid < d.cin) {
-            gam = c.params[d.gamma_off + tid];
-            bet = c.params[d.beta_off + tid];
+            gam = *as_gld(params + d.gamma_off + tid);
+            bet = *as_gld(params + d.beta_off + tid);
         }
         StatLoad L;
-        stat_issue(c, T.grp, d.in_stat, d.cin, gst, 0, 0, nullptr, G.zero, L);
+        stat_issue(c.stats, c.n_stats, T.grp, d.in_stat, d.cin, gst, 0, 0, nullptr, zero, L);
         stat_finish(L);
         __syncthreads();
         PHASE(2);
@@ -480,12 +510,12 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(gpi_conv_desc d, gpi_code
             const float r = tgt - mu;
             Lv = -0.5f * (2.f * ls + r * r * e + GPI_LOG2PI);
             const float scl = c.loss_scale[T.grp];
-            float* go = c.ws + d.gout_off + (int64_t)T.b * 2 * HWo + oy * d.w_out + ox;
+            auto go = as_gst(ws + d.gout_off + (int64_t)T.b * 2 * HWo + oy * d.w_out + ox);
             go[0] = -scl * r * e;
             go[HWo] = scl * (1.f - r * r * e);
             if (d.out_off >= 0) {
-                float* o = c.ws + d.out_off + (int64_t)T.b * d.out_ctot * HWo + (int64_t)d.out_c0 * HWo +
-                           oy * d.w_out + ox;
+                auto o = as_gst(ws + d.out_off + (int64_t)T.b * d.out_ctot * HWo + (int64_t)d.out_c0 * HWo +
+                             oy * d.w_out + ox);
                 o[0] = mu;
                 o[HWo] = ls;
             }
@@ -500,7 +530,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(gpi_conv_desc d, gpi_code
     }
 
     if (active) {
-        float* o = c.ws + d.out_off + ((int64_t)T.b * d.out_ctot + d.out_c0) * HWo + oy * d.w_out + ox;
+        auto o = as_gst(ws + d.out_off + ((int64_t)T.b * d.out_ctot + d.out_c0) * HWo + oy * d.w_out + ox);
 #pragma unroll
         for (int co = 0; co < CP; ++co)
             if (co < d.cout) o[(int64_t)co * HWo] = acc[co];
@@ -533,8 +563,6 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(gpi_conv_desc d, gpi_code
 //    and summed in LDS in a fixed order;
 //  * input gradient as [owned pixels] x [cin] with reduction over (co, ky, kx):
 //    A = the output-gradient window of the pixel (LDS), B = W (LDS, [co*KK+tap][16]).
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
@@ -572,6 +600,11 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(gpi_conv_desc d, gpi_code
     const int lane = tid & 63, wv = tid >> 6, kq = lane >> 4, l16 = lane & 15;
     RTSTAMP(0);
     PHASE(0);
+    float* const ws = pin(c.ws);
+    const float* const params = pin(c.params);
+    const float* const zero = pin(G.zero);
+    const int64_t w_off = pin(d.w_off), gout_off = pin(d.gout_off), out_off = pin(d.out_off);
+    const int64_t gin_off = pin(d.gin_off);
     const TileIdx T = tile_of(G, c.groups);
     const int HWi = d.h_in * d.w_in, HWo = d.h_out * d.w_out;
     const float* ib = input_base(d, c, T.b);
@@ -579,57 +612,58 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(gpi_conv_desc d, gpi_code
 
     // ---- phase 1: every global read in flight together
     if (has_gin)
-        stage(wD, nwd, G.zero, [&](int e) -> const float* {
+        stage(wD, nwd, zero, [&](int e) -> const float* {
             const int ci = e & 15, k = e >> 4;
             const int co = k / KK, t = k - co * KK;
-            return ci < d.cin && k < KD ? c.params + d.w_off + ((int64_t)co * d.cin + ci) * KK + t : nullptr;
+            return ci < d.cin && k < KD ? params + w_off + ((int64_t)co * d.cin + ci) * KK + t : nullptr;
         });
     PHASE(12);
     int gy0, gh_;
     g_rows(K, S, d.pad, T.oy0, G.th, gy0, gh_);
     const int64_t gbase = ((int64_t)T.b * d.out_ctot + d.out_c0) * HWo;
-    stage_img(gl, d.cout, G.gh, G.PG, G.d_g4, G.d_PG4, G.g_sq, G.g_sr, G.g_sc, gy0, d.h_out, d.w_out, G.zero,
-              [&](int q) -> const float* { return c.ws + d.gout_off + gbase + (int64_t)q * HWo; });
+    stage_img(gl, d.cout, G.gh, G.PG, G.d_g4, G.d_PG4, G.g_sq, G.g_sr, G.g_sc, gy0, d.h_out, d.w_out, zero,
+              [&](int q) -> const float* { return ws + gout_off + gbase + (int64_t)q * HWo; });
     PHASE(13);
     if (obn)
-        stage_img(gz, d.cout, G.gh, G.PG, G.d_g4, G.d_PG4, G.g_sq, G.g_sr, G.g_sc, gy0, d.h_out, d.w_out, G.zero,
-                  [&](int q) -> const float* { return c.ws + d.out_off + gbase + (int64_t)q * HWo; });
+        stage_img(gz, d.cout, G.gh, G.PG, G.d_g4, G.d_PG4, G.g_sq, G.g_sr, G.g_sc, gy0, d.h_out, d.w_out, zero,
+                  [&](int q) -> const float* { return ws + out_off + gbase + (int64_t)q * HWo; });
     PHASE(14);
     int iy0, rh_;
     in_rows(K, S, UP, d.pad, T.oy0, G.th, iy0, rh_);
-    stage_img(al, d.cin, G.rh, G.P, G.d_in4, G.d_P4, G.in_sq, G.in_sr, G.in_sc, iy0, d.h_in, d.w_in, G.zero,
+    stage_img(al, d.cin, G.rh, G.P, G.d_in4, G.d_P4, G.in_sq, G.in_sr, G.in_sc, iy0, d.h_in, d.w_in, zero,
               [&](int q) -> const float* { return ib + (int64_t)q * HWi; });
     PHASE(8);
-    // input-gradient epilogue operands (x, previous S_in) of this wave's first four pixel
-    // blocks: lane (kq, l16) owns channel l16 at the 4 consecutive pixels 16 m + 4 kq + [0, 4)
+    // input-gradient epilogue operand (previous S_in, when accumulating) of this wave's first
+    // four pixel blocks: lane (kq, l16) owns channel l16 at the 4 consecutive pixels
+    // 16 m + 4 kq + [0, 4).  The input itself is read back from the LDS image.
     int py0, ph_;
     owned_rows(S, UP, T.oy0, G.th, py0, ph_);
     const int nmblk = has_gin ? (G.ph * d.w_in) >> 4 : 0;
     const int ci_l = min(l16, d.cin - 1);
+    const bool cok = l16 < d.cin;
     const int64_t ibase = ((int64_t)T.b * d.in_ctot + d.in_c0 + ci_l) * HWi + (int64_t)py0 * d.w_in;
-    float4 xv4[4], pv4[4];
+    f32x4 pv4[4];
     auto own_load = [&](int round) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int m = wv + 4 * (4 * round + u);
-            const bool ok = m < nmblk;
+            const bool ok = m < nmblk && cok;
             const int64_t o = ibase + 16 * m + 4 * kq;
-            if (d.in_bn) xv4[u] = *(const float4*)(ok ? c.ws + d.in_off + o : G.zero);
-            if (d.gin_accumulate) pv4[u] = *(const float4*)(ok ? c.ws + d.gin_off + o : G.zero);
-            else pv4[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (d.gin_accumulate) pv4[u] = *as_gld((const f32x4*)(ok ? ws + gin_off + o : zero));
+            else pv4[u] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
     };
     if (nmblk > 0) own_load(0);
     PHASE(9);
     float gam = 0.f, bet = 0.f;
     if (d.in_bn && tid < d.cin) {
-        gam = c.params[d.gamma_off + tid];
-        bet = c.params[d.beta_off + tid];
+        gam = *as_gld(params + d.gamma_off + tid);
+        bet = *as_gld(params + d.beta_off + tid);
     }
     {
         StatLoad L;
-        stat_issue(c, T.grp, d.in_stat, d.in_bn ? d.cin : 0, gst, d.out_stat, obn ? d.cout : 0,
-                   gst + 4 * GPI_MAX_CIN, G.zero, L);
+        stat_issue(c.stats, c.n_stats, T.grp, d.in_stat, d.in_bn ? d.cin : 0, gst, d.out_stat, obn ? d.cout : 0,
+                   gst + 4 * GPI_MAX_CIN, zero, L);
         PHASE(10);
         stat_finish(L);
         PHASE(11);
@@ -797,16 +831,15 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(gpi_conv_desc d, gpi_code
     // ---- phase 4b: input gradient (MFMA) + BN backward of the input + S_in (+)= gamma * dbn
     float sd = 0.f, sdx = 0.f;   // this lane's channel l16
     if (nmblk > 0) {
-        float l_sc = 0.f, l_sh = 0.f, l_mean = 0.f, l_inv = 0.f, l_gam = 0.f;
+        // x-hat of an active (a > 0) input from its activation a = gamma x-hat + beta
+        float l_bet = 0.f, l_rgam = 0.f, l_gam = 0.f;
         if (d.in_bn) {
-            l_sc = i_sc[ci_l];
-            l_sh = i_sh[ci_l];
-            l_mean = i_mean[ci_l];
-            l_inv = i_inv[ci_l];
             l_gam = i_gam[ci_l];
+            l_bet = i_sh[ci_l] + i_mean[ci_l] * i_sc[ci_l];     // beta
+            l_rgam = 1.f / l_gam;
         }
+        const float* arow0 = al + (ci_l * G.rh + (py0 - iy0)) * G.P + HALO;   // owned row 0 of channel l16
         const int nkd = KD4 >> 2;
-        const bool cok = l16 < d.cin;
         for (int round = 0; wv + 16 * round < nmblk; ++round) {
             if (round > 0) own_load(round);
 #pragma unroll
@@ -840,23 +873,24 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(gpi_conv_desc d, gpi_code
                         }
                     }
                     if (cok) {
-                        float* gp = c.ws + d.gin_off + ibase + 16 * m + 4 * kq;
-                        const float xa[4] = {xv4[u].x, xv4[u].y, xv4[u].z, xv4[u].w};
-                        const float pa[4] = {pv4[u].x, pv4[u].y, pv4[u].z, pv4[u].w};
+                        float* gp = ws + gin_off + ibase + 16 * m + 4 * kq;
+                        const int i0 = 16 * m + 4 * kq;
+                        const int qy0 = dq(i0, G.d_win), px0 = i0 - qy0 * d.w_in;
+                        const f32x4 av = *(const f32x4*)(arow0 + qy0 * G.P + px0);
+                        const float pa[4] = {pv4[u][0], pv4[u][1], pv4[u][2], pv4[u][3]};
                         float o[4];
 #pragma unroll
                         for (int q = 0; q < 4; ++q) {
                             if (d.in_bn) {
-                                const float bnv = fmaf(xa[q], l_sc, l_sh);
-                                const float dbn = bnv > 0.f ? acc[q] : 0.f;
+                                const float dbn = av[q] > 0.f ? acc[q] : 0.f;
                                 o[q] = pa[q] + l_gam * dbn;
                                 sd += dbn;
-                                sdx += dbn * ((xa[q] - l_mean) * l_inv);
+                                sdx += dbn * ((av[q] - l_bet) * l_rgam);
                             } else {
                                 o[q] = pa[q] + acc[q];
                             }
                         }
-                        *(float4*)gp = make_float4(o[0], o[1], o[2], o[3]);
+                        *as_gst((f32x4*)gp) = f32x4{o[0], o[1], o[2], o[3]};
                     }
                 }
             }

@@ -5,13 +5,14 @@ using namespace gpi;
 
 namespace {
 
-__global__ __launch_bounds__(256) void grad_finalize_kernel(const double* __restrict__ gacc, float* grad, int64_t n,
-                                                            int accumulate, int64_t* step) {
+__global__ __launch_bounds__(256) void grad_finalize_kernel(double* __restrict__ gacc, float* grad, int64_t n,
+                                                            int flags, int64_t* step) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (step && i == 0) *step += 1;
     if (i >= n) return;
     const float g = (float)gacc[i];
-    grad[i] = accumulate ? grad[i] + g : g;
+    grad[i] = (flags & GPI_FINALIZE_ACCUMULATE) ? grad[i] + g : g;
+    if (flags & GPI_FINALIZE_ZERO) gacc[i] = 0.0;
 }
 
 // torch.optim.Adam single-tensor math (torch/optim/adam.py, defaults:
@@ -34,6 +35,7 @@ __global__ __launch_bounds__(256) void adam_kernel(gpi_adam_desc d) {
         const float denom = sqrtf(v) / bc2_sqrt + d.eps;
         d.p[i] = d.p[i] - step_size * (m / denom);
     }
+    if (d.rng_offset && blockIdx.x == 0 && threadIdx.x == 0) *d.rng_offset += d.rng_advance;
 }
 
 __global__ __launch_bounds__(256) void randn_kernel(float* out, int64_t n, uint64_t seed, const uint64_t* offset,
@@ -110,12 +112,11 @@ extern "C" const char* gpi_error_string(int code) {
     }
 }
 
-extern "C" int gpi_grad_finalize(const double* gacc, float* grad, int64_t n, int accumulate, int64_t* step,
-                                 void* stream) {
+extern "C" int gpi_grad_finalize(double* gacc, float* grad, int64_t n, int flags, int64_t* step, void* stream) {
     if (!gacc || !grad || n < 0) return GPI_ERR_ARG;
     const int64_t nb = n > 0 ? (n + 255) / 256 : 1;
     hipLaunchKernelGGL(grad_finalize_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, gacc, grad, n,
-                       accumulate, step);
+                       flags, step);
     GPI_CHECK_LAUNCH();
     return GPI_OK;
 }

@@ -20,6 +20,8 @@ GPI_MAX_COUT = 8
 GPI_MAX_REDUCE_ITEMS = 48
 GPI_MAX_GEMM_ITEMS = 12
 GPI_REPLICAS = 32
+FINALIZE_ACCUMULATE = 1
+FINALIZE_ZERO = 2
 
 EPI_STORE, EPI_STORE_STATS, EPI_GAUSS_LOSS = 0, 1, 2
 HEAD_ENC, HEAD_REPARAM, HEAD_QZ, HEAD_LATENT, HEAD_GP = 0x01, 0x02, 0x04, 0x08, 0x10
@@ -88,7 +90,8 @@ class ResidualDesc(C.Structure):
 
 class AdamDesc(C.Structure):
     _fields_ = [('p', vp), ('g', vp), ('m', vp), ('v', vp), ('n', i64), ('lr', vp), ('step', vp),
-                ('beta1', f32), ('beta2', f32), ('eps', f32), ('_pad', f32)]
+                ('beta1', f32), ('beta2', f32), ('eps', f32), ('_pad', f32), ('rng_offset', vp),
+                ('rng_advance', C.c_uint64)]
 
 
 STRUCTS = [Stat, Groups, ConvDesc, CodecCtx, ReduceItem, HeadDesc, GemmItem, RomDesc, ResidualDesc, AdamDesc]

@@ -210,11 +210,9 @@ class ElboEngine(object):
         for gi, scale in enumerate([su] * (self.B_u > 0) + [ss] * (self.N_s > 0)):
             self.dctx.loss_scale[gi] = scale
         # ---- gradient reductions
-        items = []
-        if self.ep is not None:
-            items += self.ep.reduce_items(offE)
-        items += self.dp.reduce_items(offD)
-        self.reduce_items = items
+        self.reduce_enc = self.ep.reduce_items(offE) if self.ep is not None else []
+        self.reduce_dec = self.dp.reduce_items(offD)
+        self.reduce_items = self.reduce_enc + self.reduce_dec
         gi = []
         B = self.B
 
@@ -281,12 +279,14 @@ class ElboEngine(object):
             self.rom.Y = Y.data_ptr()
             self.rom.F = F.data_ptr()
 
-    def forward(self, stream=None, compute_value=True):
-        """Launch the forward; returns the 0-d ELBO tensor (no host sync)."""
+    def forward(self, stream=None, compute_value=True, zero_gacc=True):
+        """Launch the forward; returns the 0-d ELBO tensor (no host sync).  zero_gacc=False
+        when the previous step's finalize already cleared the accumulator (GPI_FINALIZE_ZERO)."""
         lib = _lib()
         st = stream if stream is not None else L.stream_handle()
         self.ws.zero_scratch()
-        self.flat.gacc.zero_()
+        if zero_gacc:
+            self.flat.gacc.zero_()
         if self.ep is not None:
             _run(lib.gpi_codec_forward, self.enc_descs, len(self.enc_descs), C.byref(self.ectx), st,
                  what='encoder forward')
@@ -296,9 +296,7 @@ class ElboEngine(object):
             # the ROM solve only feeds the head backward: run it on a side stream,
             # concurrently with the decoder (fork here, join in backward / value)
             main = torch.cuda.current_stream()
-            if self._side is None:
-                self._side = torch.cuda.Stream(device=main.device)
-                self._ev_fork, self._ev_join = torch.cuda.Event(), torch.cuda.Event()
+            self._side_stream()
             self._ev_fork.record(main)
             self._side.wait_event(self._ev_fork)
             _run(lib.gpi_rom, C.byref(self.rom), C.c_void_p(self._side.cuda_stream), what='rom')
@@ -310,6 +308,13 @@ class ElboEngine(object):
             self._join()
             return self.elbo_value()
         return None
+
+    def _side_stream(self):
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=torch.cuda.current_stream().device)
+            self._ev_fork, self._ev_join = torch.cuda.Event(), torch.cuda.Event()
+            self._ev_fork2, self._ev_join2 = torch.cuda.Event(), torch.cuda.Event()
+        return self._side
 
     def _join(self):
         if self._pending_join:
@@ -355,17 +360,28 @@ class ElboEngine(object):
         self._join()
         _run(lib.gpi_head_backward, C.byref(self.head), C.c_void_p(self.flat.P.data_ptr()),
              C.c_void_p(self.ws.t_ws.data_ptr()), C.c_void_p(self.flat.gacc.data_ptr()), st, what='head backward')
+        # the decoder's slab reduction and the dense weight gradients depend only on what is
+        # done by now: run them on the side stream, concurrently with the encoder backward
+        main = torch.cuda.current_stream()
+        side = self._side_stream()
+        self._ev_fork2.record(main)
+        side.wait_event(self._ev_fork2)
+        sst = C.c_void_p(side.cuda_stream)
+        run_reduce(self.reduce_dec, self.ws, self.flat, sst)
+        _run(lib.gpi_outer_gemm, self.gemm_items, len(self.gemm_items), C.c_void_p(self.ws.t_ws.data_ptr()),
+             C.c_void_p(self.flat.gacc.data_ptr()), sst, what='outer gemm')
+        self._ev_join2.record(side)
         if self.ep is not None:
             _run(lib.gpi_codec_backward, self.enc_descs, len(self.enc_descs), C.byref(self.ectx), st,
                  what='encoder backward')
-        run_reduce(self.reduce_items, self.ws, self.flat, st)
-        _run(lib.gpi_outer_gemm, self.gemm_items, len(self.gemm_items), C.c_void_p(self.ws.t_ws.data_ptr()),
-             C.c_void_p(self.flat.gacc.data_ptr()), st, what='outer gemm')
+            run_reduce(self.reduce_enc, self.ws, self.flat, st)
+        main.wait_event(self._ev_join2)
 
-    def finalize(self, out, accumulate=False, step=None, stream=None):
+    def finalize(self, out, accumulate=False, step=None, stream=None, zero_acc=False):
         st = stream if stream is not None else L.stream_handle()
+        flags = (L.FINALIZE_ACCUMULATE if accumulate else 0) | (L.FINALIZE_ZERO if zero_acc else 0)
         _run(_lib().gpi_grad_finalize, C.c_void_p(self.flat.gacc.data_ptr()), C.c_void_p(out.data_ptr()),
-             self.flat.numel, 1 if accumulate else 0, C.c_void_p(step.data_ptr()) if step is not None else None, st,
+             self.flat.numel, flags, C.c_void_p(step.data_ptr()) if step is not None else None, st,
              what='grad finalize')
 
     def check_flag(self):

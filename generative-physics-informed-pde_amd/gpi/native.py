@@ -49,8 +49,8 @@ def engine_for(module, key, build):
 
 def _deliver(flat, scale=None):
     tmp = torch.empty_like(flat.G)
-    L.check(L.lib().gpi_grad_finalize(L.ptr(flat.gacc), L.ptr(tmp), flat.numel, 0, None, L.stream_handle()),
-            'grad finalize')
+    L.check(L.lib().gpi_grad_finalize(L.ptr(flat.gacc), L.ptr(tmp), flat.numel, L.FINALIZE_ZERO, None,
+                                      L.stream_handle()), 'grad finalize')
     if scale is not None:
         tmp.mul_(scale)
     flat.deliver(tmp)

@@ -57,6 +57,8 @@ class FusedElboStep(object):
         self.n_pool = n_pool
         self.rng_span = max(n_pool, (self.engine.B * self.engine.dz + 3) // 4 + 1,
                             (self.N_s * self.engine.d_x + 3) // 4 + 1)
+        self.adam.rng_offset = self.rng_off.data_ptr()
+        self.adam.rng_advance = self.rng_span
         self.graph = None
 
     # ------------------------------------------------------------------
@@ -74,9 +76,9 @@ class FusedElboStep(object):
     def forward_backward(self, stream=None):
         st = stream if stream is not None else L.stream_handle()
         self._launch_noise(st)
-        self.engine.forward(st, compute_value=False)
+        self.engine.forward(st, compute_value=False, zero_gacc=False)   # finalize left gacc zeroed
         self.engine.backward(st)
-        self.engine.finalize(self.flat.G, step=self.step_ctr, stream=st)
+        self.engine.finalize(self.flat.G, step=self.step_ctr, stream=st, zero_acc=True)
 
     def allreduce(self):
         if self.distributed:
@@ -84,8 +86,7 @@ class FusedElboStep(object):
 
     def update(self, stream=None):
         st = stream if stream is not None else L.stream_handle()
-        L.check(L.lib().gpi_adam(C.byref(self.adam), st), 'adam')
-        L.check(L.lib().gpi_rng_advance(L.ptr(self.rng_off), self.rng_span, st), 'rng advance')
+        L.check(L.lib().gpi_adam(C.byref(self.adam), st), 'adam (+ rng offset advance)')
 
     def step_eager(self):
         self.forward_backward()

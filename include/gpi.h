@@ -101,7 +101,7 @@ typedef struct gpi_conv_desc {
 typedef struct gpi_codec_ctx {
     const float* params;           /* flat fp32 parameters */
     float* ws;                     /* workspace (activations, S / gradient buffers) */
-    gpi_stat* stats;               /* BN statistics records [GPI_REPLICAS][stat][GPI_MAX_GROUPS] */
+    gpi_stat* stats;               /* BN statistics records [GPI_REPLICAS][GPI_MAX_GROUPS][stat] */
     double* gacc;                  /* fp64 gradient accumulator, parallel to params */
     float* wpart;                  /* weight-gradient partial slabs */
     const float* ext_in;           /* external input (e.g. the unlabeled image pool) */
@@ -224,6 +224,8 @@ typedef struct gpi_adam_desc {
     const float* lr;           /* device scalar */
     const int64_t* step;       /* device scalar: step number after increment */
     float beta1, beta2, eps, _pad;
+    uint64_t* rng_offset;      /* optional: device RNG offset advanced by rng_advance after the update */
+    uint64_t rng_advance;      /*           (replaces a separate gpi_rng_advance launch) */
 } gpi_adam_desc;
 
 /* ---------------------------------------------------------------- API */
@@ -250,7 +252,9 @@ int gpi_cgr_residual(const gpi_residual_desc* d, void* stream);
 
 /* Gradient finalisation: grad[i] = (accumulate ? grad[i] : 0) + (float) gacc[i];
  * also increments the device step counter (if non-NULL) for gpi_adam. */
-int gpi_grad_finalize(const double* gacc, float* grad, int64_t n, int accumulate, int64_t* step, void* stream);
+#define GPI_FINALIZE_ACCUMULATE 1   /* grad += gacc (torch .grad accumulation) instead of grad = gacc */
+#define GPI_FINALIZE_ZERO       2   /* zero gacc after reading it (the next step needs no separate fill) */
+int gpi_grad_finalize(double* gacc, float* grad, int64_t n, int flags, int64_t* step, void* stream);
 int gpi_adam(const gpi_adam_desc* d, void* stream);
 
 /* Device Philox4x32-10 normals: out[i] = N(0,1) for counter (*offset + i);
