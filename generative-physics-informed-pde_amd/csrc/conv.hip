@@ -115,7 +115,9 @@ __host__ __device__ inline void owned_rows(int s, int up, int o0, int t, int& p0
     else { p0 = o0; len = t; }
 }
 
-bool conv_geom(const gpi_conv_desc& d, const gpi_groups& g, ConvGeom& G) {
+// Tiles: the forward computes one output pixel per thread (<= 256 per tile); the MFMA
+// backward takes taller tiles (fewer halo rows and per-tile fixed costs per pixel).
+bool conv_geom(const gpi_conv_desc& d, const gpi_groups& g, ConvGeom& G, bool fwd) {
     if (g.n_groups < 1 || g.n_groups > GPI_MAX_GROUPS) return false;
     if (d.cin < 1 || d.cin > GPI_MAX_CIN || d.cout < 1 || d.cout > GPI_MAX_COUT) return false;
     if (d.k != 1 && d.k != 3 && d.k != 5 && d.k != 7) return false;
@@ -131,7 +133,8 @@ bool conv_geom(const gpi_conv_desc& d, const gpi_groups& g, ConvGeom& G) {
     }
     const int B = g.start[g.n_groups] - g.start[0];
     if (g.start[0] != 0 || B <= 0) return false;
-    const int target = d.stride == 2 ? 128 : 256;   // output pixels per tile
+    // output pixels per tile (taller backward tiles only pay on planes >= 64 wide: measured)
+    const int target = d.stride == 2 ? 128 : (!fwd && d.w_out >= 64 ? 512 : 256);
     G.th = target / d.w_out;
     if (G.th < 1) G.th = 1;
     if (G.th > d.h_out) G.th = d.h_out;
@@ -979,7 +982,7 @@ bool aligned_ok(const gpi_conv_desc& d, const gpi_codec_ctx& c, bool fwd) {
 
 int launch(const gpi_conv_desc& d, const gpi_codec_ctx& c, hipStream_t st, bool fwd) {
     ConvGeom G;
-    if (!conv_geom(d, c.groups, G)) return GPI_ERR_UNSUPPORTED;
+    if (!conv_geom(d, c.groups, G, fwd)) return GPI_ERR_UNSUPPORTED;
     if (d.epilogue == GPI_EPI_GAUSS_LOSS && d.cout != 2) return GPI_ERR_ARG;
     if (d.in_off < 0 && !c.ext_in) return GPI_ERR_ARG;
     if (!aligned_ok(d, c, fwd)) return GPI_ERR_UNSUPPORTED;
@@ -1065,7 +1068,7 @@ extern "C" int gpi_debug_phase_stamps(unsigned long long* phase, unsigned long l
 extern "C" int gpi_conv_blocks(const gpi_conv_desc* op, const gpi_groups* groups, int32_t* blocks) {
     if (!op || !groups || !blocks) return GPI_ERR_ARG;
     ConvGeom G;
-    if (!conv_geom(*op, *groups, G)) return GPI_ERR_UNSUPPORTED;
+    if (!conv_geom(*op, *groups, G, false)) return GPI_ERR_UNSUPPORTED;   // backward tiling = slab rows
     *blocks = G.nblocks;
     return GPI_OK;
 }

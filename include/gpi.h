@@ -234,7 +234,7 @@ int gpi_version(void);
 int gpi_struct_sizes(int64_t* out, int n);
 const char* gpi_error_string(int code);
 
-/* Number of workgroups (= partial-slab rows) a conv launch uses. */
+/* Number of workgroups (= partial-slab rows) a conv backward launch uses. */
 int gpi_conv_blocks(const gpi_conv_desc* op, const gpi_groups* groups, int32_t* blocks);
 int gpi_conv_forward(const gpi_conv_desc* op, const gpi_codec_ctx* ctx, void* stream);
 int gpi_conv_backward(const gpi_conv_desc* op, const gpi_codec_ctx* ctx, void* stream);
