@@ -786,23 +786,42 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(gpi_conv_desc d, gpi_code
                         const int ry = UP ? fdiv2(T.oy0 + ty - d.pad + ky[u]) - iy0 : ty * S + ky[u];
                         brow[u] = al + (ci[u] * G.rh + ry) * G.P + HALO;
                     }
-                    if (S == 2) {
-                        for (int xs = 0; xs < nxs; ++xs) {
-                            const int xv = 4 * xs + kq;          // virtual column, xv - kx = 2 ox
-                            const int t2 = xv - kx;
-                            const float a = (t2 & 1) ? 0.f : grow[kx + (t2 >> 1)];
-                            const int ix = xv - d.pad;
-                            acc[0] = mfma4(a, brow[0][ix], acc[0]);
-                            if (two) acc[1] = mfma4(a, brow[1][ix], acc[1]);
-                        }
-                    } else {
-                        for (int xs = 0; xs < nxs; ++xs) {
-                            const int xv = 4 * xs + kq;          // virtual column, ox = xv - kx
-                            const float a = grow[xv];
+                    // operands of four steps are read before their MFMAs (the loop is
+                    // latency-bound otherwise: LDS read -> dependent MFMA each step)
+                    int xs = 0;
+                    for (; xs + 4 <= nxs; xs += 4) {
+                        float a[4], b0[4], b1[4];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const int xv = 4 * (xs + u) + kq;
+                            if (S == 2) {
+                                const int t2 = xv - kx;          // xv - kx = 2 ox
+                                a[u] = (t2 & 1) ? 0.f : grow[kx + (t2 >> 1)];
+                            } else {
+                                a[u] = grow[xv];                 // ox = xv - kx
+                            }
                             const int ix = UP ? fdiv2(xv - d.pad) : xv - d.pad;
-                            acc[0] = mfma4(a, brow[0][ix], acc[0]);
-                            if (two) acc[1] = mfma4(a, brow[1][ix], acc[1]);
+                            b0[u] = brow[0][ix];
+                            b1[u] = two ? brow[1][ix] : 0.f;
                         }
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            acc[0] = mfma4(a[u], b0[u], acc[0]);
+                            if (two) acc[1] = mfma4(a[u], b1[u], acc[1]);
+                        }
+                    }
+                    for (; xs < nxs; ++xs) {
+                        const int xv = 4 * xs + kq;
+                        float a;
+                        if (S == 2) {
+                            const int t2 = xv - kx;
+                            a = (t2 & 1) ? 0.f : grow[kx + (t2 >> 1)];
+                        } else {
+                            a = grow[xv];
+                        }
+                        const int ix = UP ? fdiv2(xv - d.pad) : xv - d.pad;
+                        acc[0] = mfma4(a, brow[0][ix], acc[0]);
+                        if (two) acc[1] = mfma4(a, brow[1][ix], acc[1]);
                     }
                 }
                 // fixed-order sum of the four waves' partial tiles
@@ -868,11 +887,25 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(gpi_conv_desc d, gpi_code
                         }
                     } else {
                         const float* gp0 = gl + (UP ? 2 * (qy * G.PG + px) : qy * G.PG + px);
-                        for (int ks = 0; ks < nkd; ++ks) {
-                            const int k = 4 * ks + kq;
+                        auto aval = [&](int k) -> float {
                             const float* ga = gp0 + ktab[k];
-                            const float a = UP ? (ga[0] + ga[1]) + (ga[G.PG] + ga[G.PG + 1]) : ga[0];
-                            acc = mfma4(a, wD[k * 16 + l16], acc);
+                            return UP ? (ga[0] + ga[1]) + (ga[G.PG] + ga[G.PG + 1]) : ga[0];
+                        };
+                        int ks = 0;
+                        for (; ks + 4 <= nkd; ks += 4) {   // operands of four steps before their MFMAs
+                            float a[4], b[4];
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) {
+                                const int k = 4 * (ks + u) + kq;
+                                a[u] = aval(k);
+                                b[u] = wD[k * 16 + l16];
+                            }
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) acc = mfma4(a[u], b[u], acc);
+                        }
+                        for (; ks < nkd; ++ks) {
+                            const int k = 4 * ks + kq;
+                            acc = mfma4(aval(k), wD[k * 16 + l16], acc);
                         }
                     }
                     if (cok) {
