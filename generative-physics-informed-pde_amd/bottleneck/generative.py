@@ -19,6 +19,8 @@ from gpi.engine import ElboEngine
 from gpi.flat import FlatParameters
 from gpi.native import anchor, set_flat, engine_for
 from gpi import _lib as L
+from gpi import vo as gvo
+from gpi.engine import rom_call, ROM_NN
 
 SHARED_PREFIXES = ('f.', 'g.', 'gp.', 'encoder.')
 
@@ -175,21 +177,34 @@ class GenerativeModel(lamp.modules.BaseModule):
             set_flat(self, self._flat)
         return self._flat
 
-    def _elbo_engine(self, B_u, N_s, normalize):
+    def _elbo_engine(self, B_u, N_s, normalize, N_vo=0, vo_holdoff=False):
         flat = self.native_flat()
-        return engine_for(self, ('elbo', B_u, N_s, bool(normalize), id(flat)),
-                          lambda: ElboEngine(self, B_u, N_s, normalize=normalize))
+        return engine_for(self, ('elbo', B_u, N_s, N_vo, bool(vo_holdoff), bool(normalize), id(flat)),
+                          lambda: ElboEngine(self, B_u, N_s, normalize=normalize, N_vo=N_vo, vo_holdoff=vo_holdoff))
 
-    def _run_engine(self, engine, X_u=None, X_s=None, Y=None, F=None, eps=None):
+    @staticmethod
+    def _host_seed():
+        # Philox seed from torch's CPU generator: torch.manual_seed reproducibility, no device sync
+        return int(torch.randint(0, 2 ** 62, (1,)).item())
+
+    def _run_engine(self, engine, X_u=None, X_s=None, Y=None, F=None, eps=None, X_vo=None, F_vo=None):
+        """eps (optional, injected noise): (eps_z [B, d_z], eps_X [N_s + N_vo, n_T][, eps_y [N_vo, d_y]])."""
         if eps is None:
             engine.eps_z().normal_()
-            if engine.N_s > 0:
+            if engine.N_x > 0:
                 engine.eps_x().normal_()
         else:
             engine.eps_z().copy_(eps[0])
-            if engine.N_s > 0:
+            if engine.N_x > 0:
                 engine.eps_x().copy_(eps[1])
-        engine.bind(X_u=X_u, X_s=X_s, Y=Y, F=F)
+        if engine.N_vo > 0 and not engine.vo_holdoff:
+            # y ~ reparametrize(VO.mean, VO.logsigma) (generative.py:356)
+            if self.VO is None or self.VO.mean is None:
+                raise RuntimeError('the virtual observables have no posterior yet: call update_virtual_observables')
+            gvo.gauss_sample(engine.y_vo(), self.VO.mean, self.VO.logsigma,
+                             eps=eps[2] if (eps is not None and len(eps) > 2) else None, seed=self._host_seed(),
+                             sub=11)
+        engine.bind(X_u=X_u, X_s=X_s, Y=Y, F=F, X_vo=X_vo, F_vo=F_vo)
         return _ElboFunction.apply(anchor(self, engine.flat.P.device), engine)
 
     def _log_terms(self, engine, step, prefix_map=None):
@@ -198,16 +213,73 @@ class GenerativeModel(lamp.modules.BaseModule):
         for k, v in engine.terms().items():
             self.writer.add_scalar('objective/' + k, v, global_step=step)
 
+    # ------------------------------------------------------------ virtual observables
+    @torch.no_grad()
+    def update_virtual_observables(self, N_monte_carlo, Y_mean=None, Y_std=None, return_mean_stddev=False, step=None,
+                                   Resample=True, eps=None):
+        """generative.py:182-222 on the native path.  The per-VO-sample Python loop of MC ROM
+        solves becomes three launches over all N_vo * N_mc samples: q_X['vo'] draws
+        (gpi_gauss_sample), coarse ROM solves (gpi_rom FORWARD, coarse solutions only) and the
+        moments of y = W u + exp(logsigma_y) eps (gpi_vo_moments); VO.update then runs the batched
+        precision / conditioning kernels.  ``eps`` optionally injects (eps_X [N_vo * N_mc, n_T],
+        eps_y [N_vo * N_mc, d_y])."""
+        if step is None:
+            raise ValueError('We now require a step parameter to be passed to update VOs')
+        if Y_mean is None or Y_std is None:
+            if not self._independent_X:
+                raise NotImplementedError('the lockX VO predictive is not on the native path')
+            ds = self._datasets['vo']
+            N, N_mc = ds.N, int(N_monte_carlo)
+            if N_mc > 2048:
+                raise RuntimeError('Batchsize will lead to memory issues')
+            F = ds.get('F_ROM_BC').detach()
+            L.require_device(F)
+            qx = self.q_X['vo']
+            rom = self.g.rom
+            dx = qx.dim
+            xs = torch.empty(N * N_mc, dx, dtype=torch.float32, device=F.device)
+            gvo.gauss_sample(xs, qx.mean.detach().contiguous(), qx.logsigma.detach().contiguous(), rep=N_mc,
+                             eps=eps[0] if eps is not None else None, seed=self._host_seed(), sub=12)
+            key = (F.data_ptr(), N_mc)
+            if getattr(self, '_vo_F_mc_key', None) != key:
+                self._vo_F_mc = F.float().repeat_interleave(N_mc, 0).contiguous()
+                self._vo_F_mc_key = key
+            uc = torch.empty(N * N_mc, ROM_NN(rom.nc), dtype=torch.float32, device=F.device)
+            rom_call(rom.nc, rom.refine, xs, self._vo_F_mc, False, L.ROM_FORWARD, uc=uc)
+            Y_mean, Y_std, PREC = gvo.vo_moments(uc, rom.nc, rom.refine, N, N_mc,
+                                                 logsig_y=self.g.logsigmas_y.detach().contiguous(),
+                                                 eps=eps[1] if eps is not None else None, seed=self._host_seed())
+        else:
+            PREC = 1 / (Y_std ** 2)
+        if Resample:
+            self.VO.resample()
+        self.VO.update(Y_mean, PREC, step, writer=self.writer)
+        if step is not None and self.writer is not None:
+            Yv = self._datasets['vo'].get('Y').detach()
+            err = torch.mean(torch.sqrt(torch.sum((self.VO.mean - Yv) ** 2, 1)) / torch.sqrt(torch.sum(Yv ** 2, 1)))
+            self.writer.add_scalar('vo/q_y_mean_rel_err', err.item(), global_step=step)
+            self.writer.add_scalar('vo/likelihood', torch.mean(DiagonalGaussianLogLikelihood(
+                Yv, self.VO.mean, 2 * self.VO.logsigma)), global_step=step)
+        if return_mean_stddev:
+            return Y_mean, Y_std
+
     # ------------------------------------------------------------ ELBO
     def elbo(self, step, vo_holdoff=False, disable_vo=False, armortized_bs=None, normalize=False, l1_penalty=None,
              l2_penalty=None, eps=None):
-        """Reference generative.py:247-287.  ``eps`` optionally injects the
-        reparametrisation noise as (eps_z [B_u + N_s, d_z], eps_X [N_s, n_T])."""
+        """Reference generative.py:247-287.  ``eps`` optionally injects the reparametrisation
+        noise as (eps_z [B_u + N_s + N_vo, d_z], eps_X [N_s + N_vo, n_T][, eps_y [N_vo, d_y]])."""
         assert not (armortized_bs is not None and self.encoder is None)
         if l1_penalty is not None:
             raise NotImplementedError
+        N_vo = 0
+        X_vo = F_vo = None
         if self._datasets.get('vo') and not disable_vo and not self.disable_elbo_vo:
-            raise NotImplementedError('the virtual-observable ELBO term is not yet on the native path')
+            if not self._independent_X:
+                raise NotImplementedError('the lockX virtual-observable variant is not on the native path')
+            dsv = self._datasets['vo']
+            X_vo = dsv.get('X').detach().contiguous()
+            F_vo = dsv.get('F_ROM_BC').detach().contiguous()
+            N_vo = X_vo.shape[0]
         X_u = None
         B_u = 0
         if self._datasets.get('unsupervised') and not self.disable_elbo_unsupervised:
@@ -227,10 +299,10 @@ class GenerativeModel(lamp.modules.BaseModule):
             if self.preprocess_y_fct is not None:
                 raise NotImplementedError('preprocess_y_fct is not supported on the native path')
             N_s = X_s.shape[0]
-        if B_u == 0 and N_s == 0:
+        if B_u == 0 and N_s == 0 and N_vo == 0:
             return 0
-        engine = self._elbo_engine(B_u, N_s, normalize)
-        elbo = self._run_engine(engine, X_u, X_s, Y, F, eps)
+        engine = self._elbo_engine(B_u, N_s, normalize, N_vo=N_vo, vo_holdoff=vo_holdoff)
+        elbo = self._run_engine(engine, X_u, X_s, Y, F, eps, X_vo=X_vo, F_vo=F_vo)
         if l2_penalty is not None:
             pen = sum(torch.norm(p) for p in self.f.parameters())
             if self.encoder is not None:

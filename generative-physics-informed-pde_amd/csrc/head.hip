@@ -48,13 +48,40 @@ __device__ __forceinline__ void matvec_t(const float* __restrict__ W, const floa
     }
 }
 
+// The variational segment of workspace row q (>= 0): its parameter rows, flags, scales, term slots.
+struct QSeg {
+    int row, flags;
+    int64_t qz_mu, qz_ls, qx_mu, qx_ls;
+    float kl_scale, lx_scale;
+    double* terms;   // [KL_q, logL_X, entropy][GPI_REPLICAS]
+};
+
+__device__ __forceinline__ QSeg qseg(const gpi_head_desc& d, int q) {
+    QSeg g;
+    if (q >= d.n_q) {
+        g.row = q - d.n_q;
+        g.flags = d.flags2;
+        g.qz_mu = d.qz_mu2; g.qz_ls = d.qz_ls2; g.qx_mu = d.qx_mu2; g.qx_ls = d.qx_ls2;
+        g.kl_scale = d.kl_scale_q2; g.lx_scale = d.lx_scale2;
+        g.terms = d.terms2;
+    } else {
+        g.row = q;
+        g.flags = d.flags;
+        g.qz_mu = d.qz_mu; g.qz_ls = d.qz_ls; g.qx_mu = d.qx_mu; g.qx_ls = d.qx_ls;
+        g.kl_scale = d.kl_scale_q; g.lx_scale = d.lx_scale;
+        g.terms = d.terms + GPI_REPLICAS;
+    }
+    return g;
+}
+
 __global__ __launch_bounds__(HT) void head_fwd_kernel(gpi_head_desc d, const float* __restrict__ P, float* ws) {
     __shared__ float v0[VMAX], v1[VMAX], v2[VMAX], v3[VMAX];
     __shared__ float scratch[4];
     const int s = blockIdx.x;
     const int tid = threadIdx.x;
     const bool enc = s < d.n_enc;
-    const int q = s - d.n_enc;
+    const int q = s - d.n_enc;                  // workspace row over both variational segments
+    const QSeg g = qseg(d, q);
     const int dz = d.d_z;
     float* z = v2;
 
@@ -100,10 +127,10 @@ __global__ __launch_bounds__(HT) void head_fwd_kernel(gpi_head_desc d, const flo
             for (int k = tid; k < dz; k += HT) z[k] = ws[d.z + (int64_t)s * dz + k];
         }
     } else {
-        if (d.flags & GPI_HEAD_QZ) {
+        if (g.flags & GPI_HEAD_QZ) {
             float kl = 0.f;
             for (int k = tid; k < dz; k += HT) {
-                const float mu = P[d.qz_mu + (int64_t)q * dz + k], ls = P[d.qz_ls + (int64_t)q * dz + k];
+                const float mu = P[g.qz_mu + (int64_t)g.row * dz + k], ls = P[g.qz_ls + (int64_t)g.row * dz + k];
                 const float e = expf(ls);
                 const float zz = fmaf(e, ws[d.eps_z + (int64_t)s * dz + k], mu);
                 z[k] = zz;
@@ -111,7 +138,7 @@ __global__ __launch_bounds__(HT) void head_fwd_kernel(gpi_head_desc d, const flo
                 kl += 1.f + 2.f * ls - mu * mu - e * e;
             }
             kl = block_sum128(kl, scratch);
-            if (tid == 0) atomicAdd(d.terms + 1 * GPI_REPLICAS + blockIdx.x % GPI_REPLICAS, -0.5 * (double)kl);
+            if (tid == 0) atomicAdd(g.terms + 0 * GPI_REPLICAS + blockIdx.x % GPI_REPLICAS, -0.5 * (double)kl);
         } else {
             for (int k = tid; k < dz; k += HT) z[k] = ws[d.z + (int64_t)s * dz + k];
         }
@@ -126,15 +153,16 @@ __global__ __launch_bounds__(HT) void head_fwd_kernel(gpi_head_desc d, const flo
             lat[j] = a;
         }
     }
-    if (!enc && (d.flags & GPI_HEAD_GP)) {
+    if (!enc && (g.flags & GPI_HEAD_GP)) {
         float lx = 0.f, ent = 0.f;
         for (int t = tid; t < d.d_x; t += HT) {
             float a = P[d.gp_b + t];
             const float* w = P + d.gp_w + (int64_t)t * dz;
             for (int k = 0; k < dz; ++k) a = fmaf(w[k], z[k], a);
-            const int64_t qi = (int64_t)q * d.d_x + t;
-            const float lsq = P[d.qx_ls + qi];
-            const float xs = fmaf(expf(lsq), ws[d.eps_x + qi], P[d.qx_mu + qi]);
+            const int64_t qi = (int64_t)q * d.d_x + t;              // workspace row
+            const int64_t pi = (int64_t)g.row * d.d_x + t;          // q_X parameter row
+            const float lsq = P[g.qx_ls + pi];
+            const float xs = fmaf(expf(lsq), ws[d.eps_x + qi], P[g.qx_mu + pi]);
             ws[d.mux + qi] = a;
             ws[d.xs + qi] = xs;
             const float gls = P[d.gp_ls + t];
@@ -145,8 +173,8 @@ __global__ __launch_bounds__(HT) void head_fwd_kernel(gpi_head_desc d, const flo
         lx = block_sum128(lx, scratch);
         ent = block_sum128(ent, scratch);
         if (tid == 0) {
-            atomicAdd(d.terms + 2 * GPI_REPLICAS + blockIdx.x % GPI_REPLICAS, (double)lx);
-            atomicAdd(d.terms + 3 * GPI_REPLICAS + blockIdx.x % GPI_REPLICAS, (double)ent);
+            atomicAdd(g.terms + 1 * GPI_REPLICAS + blockIdx.x % GPI_REPLICAS, (double)lx);
+            atomicAdd(g.terms + 2 * GPI_REPLICAS + blockIdx.x % GPI_REPLICAS, (double)ent);
         }
     }
 }
@@ -158,6 +186,7 @@ __global__ __launch_bounds__(HT) void head_bwd_kernel(gpi_head_desc d, const flo
     const int tid = threadIdx.x;
     const bool enc = s < d.n_enc;
     const int q = s - d.n_enc;
+    const QSeg g = qseg(d, q);
     const int dz = d.d_z;
     float* dz_ = v0;   // dJ/dz
 
@@ -172,21 +201,22 @@ __global__ __launch_bounds__(HT) void head_bwd_kernel(gpi_head_desc d, const flo
     }
     __syncthreads();
 
-    if (!enc && (d.flags & GPI_HEAD_GP)) {
+    if (!enc && (g.flags & GPI_HEAD_GP)) {
         for (int t = tid; t < d.d_x; t += HT) {
             const int64_t qi = (int64_t)q * d.d_x + t;
+            const int64_t pi = (int64_t)g.row * d.d_x + t;
             const float gls = P[d.gp_ls + t];
             const float e2 = expf(-2.f * gls);
             const float xs = ws[d.xs + qi], mux = ws[d.mux + qi];
             const float r = xs - mux;
-            const float gm = -d.lx_scale * r * e2;            // dJ/dmu_X
+            const float gm = -g.lx_scale * r * e2;            // dJ/dmu_X
             v2[t] = gm;
             ws[d.gmux + qi] = gm;
-            atomicAdd(gacc + d.gp_ls + t, (double)(d.lx_scale * (1.f - r * r * e2)));
-            const float dxs = ws[d.gxs + qi] + d.lx_scale * r * e2;   // dJ/dX~
-            const float lsq = P[d.qx_ls + qi];
-            gacc[d.qx_mu + qi] += (double)dxs;
-            gacc[d.qx_ls + qi] += (double)(dxs * expf(lsq) * ws[d.eps_x + qi] - d.lx_scale);
+            atomicAdd(gacc + d.gp_ls + t, (double)(g.lx_scale * (1.f - r * r * e2)));
+            const float dxs = ws[d.gxs + qi] + g.lx_scale * r * e2;   // dJ/dX~
+            const float lsq = P[g.qx_ls + pi];
+            gacc[g.qx_mu + pi] += (double)dxs;
+            gacc[g.qx_ls + pi] += (double)(dxs * expf(lsq) * ws[d.eps_x + qi] - g.lx_scale);
         }
         __syncthreads();
         matvec_t(P + d.gp_w, v2, d.d_x, dz, dz_, true);
@@ -194,14 +224,14 @@ __global__ __launch_bounds__(HT) void head_bwd_kernel(gpi_head_desc d, const flo
     }
 
     if (!enc) {
-        if (d.flags & GPI_HEAD_QZ) {
+        if (g.flags & GPI_HEAD_QZ) {
             for (int k = tid; k < dz; k += HT) {
-                const int64_t qi = (int64_t)q * dz + k;
-                const float mu = P[d.qz_mu + qi], ls = P[d.qz_ls + qi];
+                const int64_t qi = (int64_t)g.row * dz + k;
+                const float mu = P[g.qz_mu + qi], ls = P[g.qz_ls + qi];
                 const float e = expf(ls);
-                gacc[d.qz_mu + qi] += (double)(dz_[k] + d.kl_scale_q * mu);
-                gacc[d.qz_ls + qi] += (double)(dz_[k] * e * ws[d.eps_z + (int64_t)s * dz + k] +
-                                               d.kl_scale_q * (e * e - 1.f));
+                gacc[g.qz_mu + qi] += (double)(dz_[k] + g.kl_scale * mu);
+                gacc[g.qz_ls + qi] += (double)(dz_[k] * e * ws[d.eps_z + (int64_t)s * dz + k] +
+                                               g.kl_scale * (e * e - 1.f));
             }
         }
         return;
@@ -294,14 +324,15 @@ __global__ __launch_bounds__(256) void outer_gemm_kernel(GemmArgs a, const float
 
 bool head_ok(const gpi_head_desc* d) {
     return d && d->d_z > 0 && d->d_z <= VMAX && d->d_feat <= VMAX && d->d_lat <= VMAX && d->d_x <= VMAX &&
-           d->n_enc >= 0 && d->n_q >= 0 && (d->n_enc + d->n_q) > 0 && d->terms;
+           d->n_enc >= 0 && d->n_q >= 0 && d->n_q2 >= 0 && (d->n_enc + d->n_q + d->n_q2) > 0 && d->terms &&
+           (d->n_q2 == 0 || d->terms2);
 }
 
 }  // namespace
 
 extern "C" int gpi_head_forward(const gpi_head_desc* d, const float* params, float* ws, void* stream) {
     if (!head_ok(d) || !params || !ws) return GPI_ERR_ARG;
-    hipLaunchKernelGGL(head_fwd_kernel, dim3(d->n_enc + d->n_q), dim3(HT), 0, (hipStream_t)stream, *d, params, ws);
+    hipLaunchKernelGGL(head_fwd_kernel, dim3(d->n_enc + d->n_q + d->n_q2), dim3(HT), 0, (hipStream_t)stream, *d, params, ws);
     GPI_CHECK_LAUNCH();
     return GPI_OK;
 }
@@ -309,7 +340,7 @@ extern "C" int gpi_head_forward(const gpi_head_desc* d, const float* params, flo
 extern "C" int gpi_head_backward(const gpi_head_desc* d, const float* params, float* ws, double* gacc,
                                  void* stream) {
     if (!head_ok(d) || !params || !ws || !gacc) return GPI_ERR_ARG;
-    hipLaunchKernelGGL(head_bwd_kernel, dim3(d->n_enc + d->n_q), dim3(HT), 0, (hipStream_t)stream, *d, params, ws,
+    hipLaunchKernelGGL(head_bwd_kernel, dim3(d->n_enc + d->n_q + d->n_q2), dim3(HT), 0, (hipStream_t)stream, *d, params, ws,
                        gacc);
     GPI_CHECK_LAUNCH();
     return GPI_OK;

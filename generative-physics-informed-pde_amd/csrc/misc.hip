@@ -95,7 +95,9 @@ extern "C" int gpi_struct_sizes(int64_t* out, int n) {
     const int64_t s[] = {(int64_t)sizeof(gpi_stat), (int64_t)sizeof(gpi_groups), (int64_t)sizeof(gpi_conv_desc),
                          (int64_t)sizeof(gpi_codec_ctx), (int64_t)sizeof(gpi_reduce_item), (int64_t)sizeof(gpi_head_desc),
                          (int64_t)sizeof(gpi_gemm_item), (int64_t)sizeof(gpi_rom_desc), (int64_t)sizeof(gpi_residual_desc),
-                         (int64_t)sizeof(gpi_adam_desc)};
+                         (int64_t)sizeof(gpi_adam_desc), (int64_t)sizeof(gpi_vo_query_desc),
+                         (int64_t)sizeof(gpi_vo_moments_desc), (int64_t)sizeof(gpi_vo_condition_desc),
+                         (int64_t)sizeof(gpi_vo_precision_desc)};
     const int k = (int)(sizeof(s) / sizeof(s[0]));
     if (!out || n < k) return GPI_ERR_ARG;
     for (int i = 0; i < k; ++i) out[i] = s[i];

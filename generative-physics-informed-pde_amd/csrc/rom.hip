@@ -159,6 +159,7 @@ __global__ __launch_bounds__(ROM_NT) void rom_kernel(gpi_rom_desc d, RomDims D) 
     }
     __syncthreads();
     if (d.uc) for (int e = tid; e < D.nn; e += NT) d.uc[(int64_t)s * D.nn + e] = u[e];
+    if (d.mode == GPI_ROM_FORWARD && !d.mu_y) return;   // coarse solutions only (VO MC predictive)
 
     // ---- prolongation (+ log-likelihood, + W^T of the output gradient), by coarse square:
     // four threads share square q = (I, J) and its corner values; each takes every fourth

@@ -1,0 +1,573 @@
+// Virtual observables (bottleneck/VirtualObservables.py) for gfx950.
+//
+// Reference: per VO sample, FEniCS assembles K_ff / f_eff once
+// (QuerryPoint._assemble_system, VirtualObservables.py:57-59), the CGR sampler
+// forms W^T K_ff and W^T f_eff densely with numpy (:61-69,297-321), the flux
+// sampler runs one FEniCS facet assembly per coarse cell (flux.py:81-158); the
+// MC predictive runs the ROM once per VO sample in a Python loop
+// (generative.py:198-207) and the conditioning is a torch fp64 Cholesky per
+// VO sample in another Python loop (VirtualObservables.py:642-669,891-898).
+// Here every step is one batched launch over all VO samples:
+//   vo_query_columns / vo_query_flux  Gamma, alpha from the closed-form P1 stencil
+//                                     (one thread per fine free node = Gamma column)
+//   vo_moments_kernel                 MC mean / std of W u_s + sigma eps from the
+//                                     coarse ROM solutions (no [n_mc, d_y] sample matrix)
+//   vo_lambda_kernel                  Lambda = Gamma C Gamma^T + diag(v), 32x32 fp64 tiles
+//   vo_chol_kernel                    Cholesky + (Gamma g - alpha) + solve, one workgroup per sample
+//   vo_columns_kernel                 posterior mean / variance per column (|L^-1 Gamma_i|^2)
+//   vo_precision_kernel               beta / mean VO variances (deterministic row reductions)
+#include "common.h"
+
+using namespace gpi;
+
+namespace {
+
+// ---------------------------------------------------------------- fine grid helpers
+struct FineGrid {
+    int n, nc, r, dy, nn_c, nT_c;
+};
+
+__device__ __forceinline__ double kcell(const double* lk, int n, int i, int j, int ul) {
+    return exp(lk[2 * (i + n * j) + ul]);
+}
+// conductance of the horizontal edge (i,j)-(i+1,j): the lower-right triangle of square (i,j)
+// and the upper-left triangle of square (i,j-1) (P1 on right triangles: -1/2 kappa per leg)
+__device__ __forceinline__ double ch_(const double* lk, int n, int i, int j) {
+    double c = 0.0;
+    if (j < n) c += kcell(lk, n, i, j, 0);
+    if (j > 0) c += kcell(lk, n, i, j - 1, 1);
+    return 0.5 * c;
+}
+// vertical edge (i,j)-(i,j+1): upper-left of square (i,j), lower-right of square (i-1,j)
+__device__ __forceinline__ double cv_(const double* lk, int n, int i, int j) {
+    double c = 0.0;
+    if (i < n) c += kcell(lk, n, i, j, 1);
+    if (i > 0) c += kcell(lk, n, i - 1, j, 0);
+    return 0.5 * c;
+}
+
+// P1 prolongation weights of fine node (i,j) onto the coarse "/" mesh (components.py:42-60)
+__device__ __forceinline__ void interp_w(int i, int j, int r, int nc, int (&k)[3], double (&w)[3]) {
+    int I = i / r, J = j / r;
+    if (I > nc - 1) I = nc - 1;
+    if (J > nc - 1) J = nc - 1;
+    const double xi = (double)(i - I * r) / (double)r, eta = (double)(j - J * r) / (double)r;
+    const int n00 = I + (nc + 1) * J;
+    k[0] = n00;
+    k[2] = n00 + (nc + 1) + 1;
+    if (xi >= eta) { k[1] = n00 + 1; w[0] = 1.0 - xi; w[1] = xi - eta; w[2] = eta; }
+    else { k[1] = n00 + (nc + 1); w[0] = 1.0 - eta; w[1] = eta - xi; w[2] = xi; }
+}
+
+__device__ __forceinline__ double bc_value(const double* u, int i, int j, int n) {
+    const double y = (double)j / (double)n;
+    return i == 0 ? u[0] * (1.0 - y) + u[1] * y : u[2] * (1.0 - y) + u[3] * y;
+}
+
+constexpr int NZ = 16;   // nonzeros of one CGR column: 5 stencil nodes x 3 coarse weights
+
+struct SparseCol {
+    int k[NZ];
+    double v[NZ];
+    int n;
+    __device__ void add(int kk, double vv) {
+        for (int t = 0; t < n; ++t)
+            if (k[t] == kk) { v[t] += vv; return; }
+        if (n < NZ) { k[n] = kk; v[n] = vv; ++n; }
+    }
+};
+
+// Gamma column of fine free node p (all rows; flux rows zero here, added by vo_query_flux)
+// and, in workgroup 0 of each field, alpha.
+__global__ __launch_bounds__(256) void vo_query_columns(gpi_vo_query_desc d, FineGrid G, int m) {
+    extern __shared__ __attribute__((aligned(16))) double sacc[];   // [nn_c]
+    const int f = blockIdx.y;
+    const int n = G.n, nc = G.nc, r = G.r;
+    const double* lk = d.logkappa + (int64_t)f * 2 * n * n;
+    double* gam = d.gamma + (int64_t)f * m * G.dy;
+    const bool cgr = d.flags & GPI_VO_CGR;
+    const int p = blockIdx.x * 256 + threadIdx.x;
+    if (p < G.dy) {
+        const int jj = p / (n - 1), ii = p - jj * (n - 1) + 1;
+        SparseCol col;
+        col.n = 0;
+        if (cgr) {
+            const double chl = ch_(lk, n, ii - 1, jj), chr = ch_(lk, n, ii, jj);
+            const double cvd = jj > 0 ? cv_(lk, n, ii, jj - 1) : 0.0;
+            const double cvu = jj < n ? cv_(lk, n, ii, jj) : 0.0;
+            // column i of K_ff: K[j, i] for the free nodes j of the 5-point star
+            const int ni[5] = {ii, ii - 1, ii + 1, ii, ii};
+            const int nj[5] = {jj, jj, jj, jj - 1, jj + 1};
+            const double kv[5] = {chl + chr + cvd + cvu, -chl, -chr, -cvd, -cvu};
+            for (int t = 0; t < 5; ++t) {
+                const int a = ni[t], b = nj[t];
+                if (a < 1 || a > n - 1 || b < 0 || b > n) continue;
+                if (t >= 3 && kv[t] == 0.0) continue;
+                int kk[3];
+                double w[3];
+                interp_w(a, b, r, nc, kk, w);
+                for (int c = 0; c < 3; ++c)
+                    if (w[c] != 0.0) col.add(kk[c], w[c] * kv[t]);
+            }
+        }
+        for (int row = 0; row < m; ++row) {
+            double v = 0.0;
+            for (int t = 0; t < col.n; ++t) v = col.k[t] == row ? col.v[t] : v;
+            gam[(int64_t)row * G.dy + p] = v;
+        }
+    }
+    if (blockIdx.x != 0) return;
+    // alpha: W^T f_eff, f_eff[j] = sum over the Dirichlet neighbours c of j of c_jc g_c (zero source)
+    const int m_cgr = cgr ? G.nn_c : 0;
+    for (int e = threadIdx.x; e < G.nn_c; e += 256) sacc[e] = 0.0;
+    __syncthreads();
+    if (cgr) {
+        const double* u = d.bc + 4 * f;
+        for (int e = threadIdx.x; e < 2 * (n + 1); e += 256) {
+            const int side = e / (n + 1), jj = e - side * (n + 1);
+            const int ii = side == 0 ? 1 : n - 1;
+            const int ic = side == 0 ? 0 : n;
+            const double c = ch_(lk, n, side == 0 ? 0 : n - 1, jj);
+            double fe = c * bc_value(u, ic, jj, n);
+            if (n == 2) {   // a single interior column touches both sides
+                if (side == 1) continue;
+                fe += ch_(lk, n, n - 1, jj) * bc_value(u, n, jj, n);
+            }
+            int kk[3];
+            double w[3];
+            interp_w(ii, jj, r, nc, kk, w);
+            for (int t = 0; t < 3; ++t)
+                if (w[t] != 0.0) atomicAdd(&sacc[kk[t]], w[t] * fe);
+        }
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < m; e += 256) d.alpha[(int64_t)f * m + e] = e < m_cgr ? sacc[e] : 0.0;
+}
+
+// Flux rows: one thread per (field, coarse triangle k) owns row k and walks the 3r fine
+// facets of its edges.  Per facet of fine square (i,j), corners u0=(i,j), u1=(i+1,j),
+// u2=(i,j+1), u3=(i+1,j+1), |e| kappa grad(u).n_out on the fine triangle inside k:
+//   lower-right (cells 2q): bottom k(u1-u3), right k(u1-u0), diagonal k(u0-2u1+u3)
+//   upper-left  (2q+1)    : left k(u2-u3),  top k(u2-u0),   diagonal k(u0-2u2+u3)
+// Edges on y=0 / y=1 are interior-facet (dS) measures over boundary facets in the
+// reference and contribute nothing; x=0 / x=1 edges are ds, all others dS with the
+// '+' side inside coarse cell k (flux.py:24-31,123-126).  Constrained fine nodes are
+// dropped (Gamma_reduced keeps the free columns, alpha = 0: flux.py:151-156).
+__device__ __forceinline__ void flux_add(double* row, int n, int i, int j, int dy, double coef) {
+    if (i < 1 || i > n - 1 || coef == 0.0) return;
+    row[(int64_t)(j * (n - 1) + i - 1)] += coef;
+    (void)dy;
+}
+
+__global__ __launch_bounds__(64) void vo_query_flux(gpi_vo_query_desc d, FineGrid G, int m, int row0) {
+    const int f = blockIdx.y;
+    const int k = blockIdx.x * 64 + threadIdx.x;
+    if (k >= G.nT_c) return;
+    const int n = G.n, nc = G.nc, r = G.r;
+    const double* lk = d.logkappa + (int64_t)f * 2 * n * n;
+    double* row = d.gamma + ((int64_t)f * m + row0 + k) * G.dy;
+    const int Q = k >> 1, ul = k & 1;
+    const int I = Q % nc, J = Q / nc;
+    for (int e = 0; e < 3; ++e) {
+        if (ul == 0 && e == 0 && J == 0) continue;            // bottom edge on y = 0
+        if (ul == 1 && e == 1 && J == nc - 1) continue;       // top edge on y = 1
+        for (int t = 0; t < r; ++t) {
+            int i, j;
+            if (ul == 0) {
+                if (e == 0) { i = I * r + t; j = J * r; }
+                else if (e == 1) { i = (I + 1) * r - 1; j = J * r + t; }
+                else { i = I * r + t; j = J * r + t; }
+            } else {
+                if (e == 0) { i = I * r; j = J * r + t; }
+                else if (e == 1) { i = I * r + t; j = (J + 1) * r - 1; }
+                else { i = I * r + t; j = J * r + t; }
+            }
+            const double kap = kcell(lk, n, i, j, ul);
+            double c0 = 0.0, c1 = 0.0, c2 = 0.0, c3 = 0.0;
+            if (ul == 0) {
+                if (e == 0) { c1 = kap; c3 = -kap; }
+                else if (e == 1) { c1 = kap; c0 = -kap; }
+                else { c0 = kap; c1 = -2.0 * kap; c3 = kap; }
+            } else {
+                if (e == 0) { c2 = kap; c3 = -kap; }
+                else if (e == 1) { c2 = kap; c0 = -kap; }
+                else { c0 = kap; c2 = -2.0 * kap; c3 = kap; }
+            }
+            flux_add(row, n, i, j, G.dy, c0);
+            flux_add(row, n, i + 1, j, G.dy, c1);
+            flux_add(row, n, i, j + 1, G.dy, c2);
+            flux_add(row, n, i + 1, j + 1, G.dy, c3);
+        }
+    }
+}
+
+// ---------------------------------------------------------------- MC predictive moments
+constexpr int MOM_CH = 64;   // MC samples staged in LDS per chunk
+
+__device__ __forceinline__ float normal_at(uint64_t ctr, uint64_t sub, uint64_t seed) {
+    const uint4_ q = philox(ctr, sub, seed);
+    const float u0 = u01(q.x), u1 = u01(q.y);
+    return sqrtf(-2.f * logf(u0)) * cosf(6.2831853071795864f * u1);
+}
+
+__global__ __launch_bounds__(256) void vo_moments_kernel(gpi_vo_moments_desc d, FineGrid G) {
+    extern __shared__ __attribute__((aligned(16))) float su[];   // [MOM_CH][nn_c]
+    const int j = blockIdx.y;
+    const int n = G.n, nn = G.nn_c;
+    const int p = blockIdx.x * 256 + threadIdx.x;
+    const bool act = p < G.dy;
+    int kk[3] = {0, 0, 0};
+    float w[3] = {0.f, 0.f, 0.f};
+    float sig = 0.f;
+    if (act) {
+        const int jj = p / (n - 1), ii = p - jj * (n - 1) + 1;
+        double wd[3];
+        interp_w(ii, jj, G.r, G.nc, kk, wd);
+        for (int t = 0; t < 3; ++t) w[t] = (float)wd[t];
+        if (d.logsig_y) sig = expf(d.logsig_y[p]);
+    }
+    const uint64_t base = d.offset ? *d.offset : 0;
+    const int64_t row0 = (int64_t)j * d.n_mc;
+    double mean = 0.0, ssd = 0.0;
+    for (int pass = 0; pass < 2; ++pass) {
+        double acc = 0.0;
+        for (int s0 = 0; s0 < d.n_mc; s0 += MOM_CH) {
+            const int ns = min(MOM_CH, d.n_mc - s0);
+            __syncthreads();
+            for (int e = threadIdx.x; e < ns * nn; e += 256) su[e] = d.uc[(row0 + s0) * nn + e];
+            __syncthreads();
+            if (!act) continue;
+            for (int s = 0; s < ns; ++s) {
+                const float* us = su + s * nn;
+                float y = w[0] * us[kk[0]] + w[1] * us[kk[1]] + w[2] * us[kk[2]];
+                if (d.logsig_y) {
+                    const int64_t rr = row0 + s0 + s;
+                    const float e = d.eps ? d.eps[rr * G.dy + p]
+                                          : normal_at(base + (uint64_t)(rr * G.dy + p), d.sub, d.seed);
+                    y = fmaf(sig, e, y);
+                }
+                if (pass == 0) acc += (double)y;
+                else { const double t = (double)y - mean; acc += t * t; }
+            }
+        }
+        if (pass == 0) mean = acc / (double)d.n_mc;
+        else ssd = acc;
+    }
+    if (!act) return;
+    const float sd = (float)sqrt(ssd / (double)(d.n_mc - 1));
+    const int64_t o = (int64_t)j * G.dy + p;
+    d.mean[o] = (float)mean;
+    if (d.std) d.std[o] = sd;
+    if (d.prec) d.prec[o] = 1.f / (sd * sd);
+}
+
+// ---------------------------------------------------------------- conditioning
+constexpr int LT = 32;   // Lambda tile
+
+// Lambda[a][b] = sum_i Gamma[a][i] cov_i Gamma[b][i] (+ vo_var on the diagonal), lower tiles
+// (ta >= tb) computed and mirrored.  cov_i = 1 / (double) prec_i.
+__global__ __launch_bounds__(256) void vo_lambda_kernel(gpi_vo_condition_desc d) {
+    __shared__ double As[LT][LT + 1], Bs[LT][LT + 1];
+    const int j = blockIdx.y;
+    int t = blockIdx.x, ta = 0;
+    while (t > ta) { t -= ta + 1; ++ta; }
+    const int tb = t;
+    const int m = d.m, dy = d.d_y;
+    const double* gam = d.gamma + (int64_t)j * m * dy;
+    const float* prec = d.prec + (int64_t)j * dy;
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+    double acc[2][2] = {{0.0, 0.0}, {0.0, 0.0}};
+    for (int k0 = 0; k0 < dy; k0 += LT) {
+        for (int e = threadIdx.x; e < LT * LT; e += 256) {
+            const int rr = e / LT, cc = e - rr * LT;
+            const int i = k0 + cc;
+            const int a = ta * LT + rr, b = tb * LT + rr;
+            double av = 0.0, bv = 0.0;
+            if (i < dy) {
+                const double cov = 1.0 / (double)prec[i];
+                if (a < m) av = gam[(int64_t)a * dy + i] * cov;
+                if (b < m) bv = gam[(int64_t)b * dy + i];
+            }
+            As[rr][cc] = av;
+            Bs[rr][cc] = bv;
+        }
+        __syncthreads();
+#pragma unroll 8
+        for (int c = 0; c < LT; ++c) {
+            const double a0 = As[ty][c], a1 = As[ty + 16][c];
+            const double b0 = Bs[tx][c], b1 = Bs[tx + 16][c];
+            acc[0][0] = fma(a0, b0, acc[0][0]);
+            acc[0][1] = fma(a0, b1, acc[0][1]);
+            acc[1][0] = fma(a1, b0, acc[1][0]);
+            acc[1][1] = fma(a1, b1, acc[1][1]);
+        }
+        __syncthreads();
+    }
+    double* lam = d.lam + (int64_t)j * m * m;
+    for (int u = 0; u < 2; ++u)
+        for (int v = 0; v < 2; ++v) {
+            const int a = ta * LT + ty + 16 * u, b = tb * LT + tx + 16 * v;
+            if (a >= m || b >= m || b > a) continue;
+            double val = acc[u][v];
+            if (a == b) val += d.vo_var[a];
+            lam[(int64_t)a * m + b] = val;
+            lam[(int64_t)b * m + a] = val;
+        }
+}
+
+// In-place lower Cholesky of one m x m matrix A (row-major) by the 256 threads of the block.
+__device__ void chol_block(double* A, int m, bool& bad) {
+    const int tid = threadIdx.x;
+    for (int k = 0; k < m; ++k) {
+        const double akk = A[k * m + k];
+        if (!(akk > 0.0)) bad = true;
+        const double dk = sqrt(akk);
+        __syncthreads();
+        for (int i = k + 1 + tid; i < m; i += 256) A[i * m + k] /= dk;
+        if (tid == 0) A[k * m + k] = dk;
+        __syncthreads();
+        for (int i = k + 1 + (tid >> 4); i < m; i += 16) {
+            const double lik = A[i * m + k];
+            for (int jj = k + 1 + (tid & 15); jj <= i; jj += 16) A[i * m + jj] -= lik * A[jj * m + k];
+        }
+        __syncthreads();
+    }
+}
+
+template <bool LDS>
+__global__ __launch_bounds__(256) void vo_chol_kernel(gpi_vo_condition_desc d) {
+    extern __shared__ __attribute__((aligned(16))) double sm[];   // [m] rhs (+ [m*m] matrix if LDS)
+    const int j = blockIdx.x;
+    const int m = d.m, dy = d.d_y;
+    double* lam = d.lam + (int64_t)j * m * m;
+    double* b = sm;
+    double* A = LDS ? sm + m : lam;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    if (LDS) {
+        for (int e = tid; e < m * m; e += 256) A[e] = lam[e];
+        __syncthreads();
+    }
+    bool bad = false;
+    chol_block(A, m, bad);
+    if (bad && d.flag && tid == 0) atomicOr(d.flag, 1);
+    // b = Gamma g - alpha
+    const double* gam = d.gamma + (int64_t)j * m * dy;
+    const float* g = d.g + (int64_t)j * dy;
+    for (int a = wid; a < m; a += 4) {
+        double s = 0.0;
+        for (int i = lane; i < dy; i += 64) s = fma(gam[(int64_t)a * dy + i], (double)g[i], s);
+        s = wave_sum_d(s);
+        if (lane == 0) b[a] = s - d.alpha[(int64_t)j * m + a];
+    }
+    __syncthreads();
+    // L z = b, L^T x = z
+    for (int k = 0; k < m; ++k) {
+        const double zk = b[k] / A[k * m + k];
+        __syncthreads();
+        for (int i = k + 1 + tid; i < m; i += 256) b[i] -= A[i * m + k] * zk;
+        if (tid == 0) b[k] = zk;
+        __syncthreads();
+    }
+    for (int k = m - 1; k >= 0; --k) {
+        const double xk = b[k] / A[k * m + k];
+        __syncthreads();
+        for (int i = tid; i < k; i += 256) b[i] -= A[k * m + i] * xk;
+        if (tid == 0) b[k] = xk;
+        __syncthreads();
+    }
+    for (int e = tid; e < m; e += 256) d.solvec[(int64_t)j * m + e] = b[e];
+    if (LDS)
+        for (int e = tid; e < m * m; e += 256) lam[e] = A[e];
+}
+
+// One lane per column i of Gamma: q = L^{-1} Gamma_i (forward substitution, q in LDS),
+// mean_i = g_i - cov_i Gamma_i . solvec, vars_i = cov_i - cov_i^2 |q|^2.
+__global__ __launch_bounds__(64) void vo_columns_kernel(gpi_vo_condition_desc d) {
+    extern __shared__ __attribute__((aligned(16))) double sq[];   // [m][64]
+    const int j = blockIdx.y;
+    const int m = d.m, dy = d.d_y;
+    const int lane = threadIdx.x;
+    const int i = blockIdx.x * 64 + lane;
+    const bool act = i < dy;
+    const int ic = act ? i : dy - 1;
+    const double* gam = d.gamma + (int64_t)j * m * dy;
+    const double* L = d.lam + (int64_t)j * m * m;
+    const double* sv = d.solvec + (int64_t)j * m;
+    double qn = 0.0, sm = 0.0;
+    for (int a = 0; a < m; ++a) {
+        const double ga = gam[(int64_t)a * dy + ic];
+        const double* La = L + (int64_t)a * m;
+        double acc = ga;
+        int bb = 0;
+        for (; bb + 4 <= a; bb += 4) {
+            acc -= La[bb] * sq[bb * 64 + lane];
+            acc -= La[bb + 1] * sq[(bb + 1) * 64 + lane];
+            acc -= La[bb + 2] * sq[(bb + 2) * 64 + lane];
+            acc -= La[bb + 3] * sq[(bb + 3) * 64 + lane];
+        }
+        for (; bb < a; ++bb) acc -= La[bb] * sq[bb * 64 + lane];
+        const double qa = acc / La[a];
+        sq[a * 64 + lane] = qa;
+        qn = fma(qa, qa, qn);
+        sm = fma(ga, sv[a], sm);
+    }
+    if (!act) return;
+    const int64_t o = (int64_t)j * dy + i;
+    const double cov = 1.0 / (double)d.prec[o];
+    const double mean = (double)d.g[o] - cov * sm;
+    const double var = cov - cov * cov * qn;
+    d.mean[o] = mean;
+    d.vars[o] = var;
+    if (d.mean32) d.mean32[o] = (float)mean;
+    if (d.logsig32) d.logsig32[o] = 0.5f * logf((float)var);
+}
+
+// ---------------------------------------------------------------- precision
+__global__ __launch_bounds__(256) void vo_precision_kernel(gpi_vo_precision_desc d) {
+    __shared__ double red[4];
+    const int a = blockIdx.x;
+    const int m = d.m, dy = d.d_y;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    double tot = 0.0;
+    for (int j = 0; j < d.n; ++j) {
+        const double* row = d.gamma + ((int64_t)j * m + a) * dy;
+        const double* mu = d.mean + (int64_t)j * dy;
+        const double* va = d.vars + (int64_t)j * dy;
+        double s1 = 0.0, s2 = 0.0;
+        for (int i = tid; i < dy; i += 256) {
+            const double gv = row[i];
+            s1 = fma(gv, mu[i], s1);
+            s2 = fma(gv * gv, va[i], s2);
+        }
+        s1 = wave_sum_d(s1);
+        s2 = wave_sum_d(s2);
+        __syncthreads();
+        if (lane == 0) { red[wid] = s1; }
+        __syncthreads();
+        const double r1 = (red[0] + red[1]) + (red[2] + red[3]) - d.alpha[(int64_t)j * m + a];
+        __syncthreads();
+        if (lane == 0) red[wid] = s2;
+        __syncthreads();
+        const double r2 = (red[0] + red[1]) + (red[2] + red[3]);
+        tot += r1 * r1 + r2;
+    }
+    if (tid == 0) {
+        const double beta = 0.5 * tot + d.beta0;
+        d.beta[a] = beta;
+        d.vo_var[a] = (d.infinite && d.infinite[a]) ? 0.0 : beta / (0.5 * (double)d.n + d.alpha0 + 1.0);
+    }
+}
+
+// ---------------------------------------------------------------- reparametrised rows
+__global__ __launch_bounds__(256) void gauss_sample_kernel(float* out, const float* mean, const float* ls,
+                                                           int64_t total, int32_t dim, int32_t rep,
+                                                           const float* eps, uint64_t seed,
+                                                           const uint64_t* offset, uint64_t sub) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= total) return;
+    const int64_t r = e / dim;
+    const int t = (int)(e - r * dim);
+    const int64_t src = (r / rep) * dim + t;
+    const float z = eps ? eps[e] : normal_at((offset ? *offset : 0) + (uint64_t)e, sub, seed);
+    out[e] = fmaf(expf(ls[src]), z, mean[src]);
+}
+
+bool grid_of(int n_fine, int nc, FineGrid& G) {
+    if (n_fine < 2 || nc < 1 || n_fine % nc) return false;
+    G.n = n_fine;
+    G.nc = nc;
+    G.r = n_fine / nc;
+    G.dy = (n_fine + 1) * (n_fine - 1);
+    G.nn_c = (nc + 1) * (nc + 1);
+    G.nT_c = 2 * nc * nc;
+    return true;
+}
+
+}  // namespace
+
+extern "C" int gpi_vo_rows(int32_t n_fine, int32_t nc, int32_t flags) {
+    FineGrid G;
+    if (!grid_of(n_fine, nc, G) || !(flags & (GPI_VO_CGR | GPI_VO_FLUX)) || (flags & ~(GPI_VO_CGR | GPI_VO_FLUX)))
+        return GPI_ERR_ARG;
+    return ((flags & GPI_VO_CGR) ? G.nn_c : 0) + ((flags & GPI_VO_FLUX) ? G.nT_c : 0);
+}
+
+extern "C" int gpi_vo_query(const gpi_vo_query_desc* d, void* stream) {
+    if (!d || !d->logkappa || !d->bc || !d->gamma || !d->alpha || d->n < 0) return GPI_ERR_ARG;
+    const int m = gpi_vo_rows(d->n_fine, d->nc, d->flags);
+    if (m < 0) return m;
+    if (d->n == 0) return GPI_OK;
+    FineGrid G;
+    grid_of(d->n_fine, d->nc, G);
+    const hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(vo_query_columns, dim3((G.dy + 255) / 256, d->n), dim3(256), sizeof(double) * G.nn_c, st, *d,
+                       G, m);
+    GPI_CHECK_LAUNCH();
+    if (d->flags & GPI_VO_FLUX) {
+        const int row0 = (d->flags & GPI_VO_CGR) ? G.nn_c : 0;
+        hipLaunchKernelGGL(vo_query_flux, dim3((G.nT_c + 63) / 64, d->n), dim3(64), 0, st, *d, G, m, row0);
+        GPI_CHECK_LAUNCH();
+    }
+    return GPI_OK;
+}
+
+extern "C" int gpi_vo_moments(const gpi_vo_moments_desc* d, void* stream) {
+    FineGrid G;
+    if (!d || !d->uc || !d->mean || d->n < 0 || d->n_mc < 2 || d->refine < 1) return GPI_ERR_ARG;
+    if (!grid_of(d->nc * d->refine, d->nc, G)) return GPI_ERR_ARG;
+    if (d->n == 0) return GPI_OK;
+    const size_t lds = sizeof(float) * MOM_CH * G.nn_c;
+    if (lds > 64 * 1024) return GPI_ERR_UNSUPPORTED;
+    hipLaunchKernelGGL(vo_moments_kernel, dim3((G.dy + 255) / 256, d->n), dim3(256), lds, (hipStream_t)stream, *d,
+                       G);
+    GPI_CHECK_LAUNCH();
+    return GPI_OK;
+}
+
+extern "C" int gpi_vo_condition(const gpi_vo_condition_desc* d, void* stream) {
+    if (!d || !d->gamma || !d->alpha || !d->g || !d->prec || !d->vo_var || !d->lam || !d->solvec || !d->mean ||
+        !d->vars || d->n < 0 || d->m < 1 || d->d_y < 1)
+        return GPI_ERR_ARG;
+    if (d->n == 0) return GPI_OK;
+    const size_t col_lds = sizeof(double) * 64 * d->m;
+    if (col_lds > 160 * 1024) return GPI_ERR_UNSUPPORTED;
+    const hipStream_t st = (hipStream_t)stream;
+    const int T = (d->m + LT - 1) / LT;
+    hipLaunchKernelGGL(vo_lambda_kernel, dim3(T * (T + 1) / 2, d->n), dim3(256), 0, st, *d);
+    GPI_CHECK_LAUNCH();
+    const size_t lds_small = sizeof(double) * ((size_t)d->m * d->m + d->m);
+    if (lds_small <= 64 * 1024) {
+        hipLaunchKernelGGL(vo_chol_kernel<true>, dim3(d->n), dim3(256), lds_small, st, *d);
+    } else {
+        hipLaunchKernelGGL(vo_chol_kernel<false>, dim3(d->n), dim3(256), sizeof(double) * d->m, st, *d);
+    }
+    GPI_CHECK_LAUNCH();
+    if (col_lds > 64 * 1024 &&
+        hipFuncSetAttribute((const void*)vo_columns_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)col_lds) != hipSuccess)
+        return GPI_ERR_LAUNCH;
+    hipLaunchKernelGGL(vo_columns_kernel, dim3((d->d_y + 63) / 64, d->n), dim3(64), col_lds, st, *d);
+    GPI_CHECK_LAUNCH();
+    return GPI_OK;
+}
+
+extern "C" int gpi_vo_precision(const gpi_vo_precision_desc* d, void* stream) {
+    if (!d || !d->gamma || !d->alpha || !d->mean || !d->vars || !d->beta || !d->vo_var || d->n < 0 || d->m < 1 ||
+        d->d_y < 1)
+        return GPI_ERR_ARG;
+    hipLaunchKernelGGL(vo_precision_kernel, dim3(d->m), dim3(256), 0, (hipStream_t)stream, *d);
+    GPI_CHECK_LAUNCH();
+    return GPI_OK;
+}
+
+extern "C" int gpi_gauss_sample(float* out, const float* mean, const float* logsigma, int64_t rows, int32_t dim,
+                                int32_t rep, const float* eps, uint64_t seed, const uint64_t* offset, uint64_t sub,
+                                void* stream) {
+    if (!out || !mean || !logsigma || rows < 0 || dim < 1 || rep < 1) return GPI_ERR_ARG;
+    const int64_t total = rows * dim;
+    if (total == 0) return GPI_OK;
+    hipLaunchKernelGGL(gauss_sample_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, out, mean, logsigma, total, dim, rep, eps, seed, offset, sub);
+    GPI_CHECK_LAUNCH();
+    return GPI_OK;
+}

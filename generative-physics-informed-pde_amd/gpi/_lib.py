@@ -26,6 +26,7 @@ FINALIZE_ZERO = 2
 EPI_STORE, EPI_STORE_STATS, EPI_GAUSS_LOSS = 0, 1, 2
 HEAD_ENC, HEAD_REPARAM, HEAD_QZ, HEAD_LATENT, HEAD_GP = 0x01, 0x02, 0x04, 0x08, 0x10
 ROM_FORWARD, ROM_LOGLIK, ROM_BACKWARD = 0, 1, 2
+VO_CGR, VO_FLUX = 0x1, 0x2
 
 i32, i64, f32, u64 = C.c_int32, C.c_int64, C.c_float, C.c_uint64
 vp = C.c_void_p
@@ -68,7 +69,9 @@ class HeadDesc(C.Structure):
                                    'gp_ls', 'qz_mu', 'qz_ls', 'qx_mu', 'qx_ls', 'feat', 'gfeat', 'hpre', 'zmu',
                                    'zls', 'eps_z', 'z', 'gz', 'lat', 'glat', 'eps_x', 'xs', 'mux', 'gxs', 'gmux',
                                    'dzmu', 'dzls', 'dhpre')] + \
-               [('kl_scale_enc', f32), ('kl_scale_q', f32), ('lx_scale', f32), ('_fpad', f32), ('terms', vp)]
+               [('kl_scale_enc', f32), ('kl_scale_q', f32), ('lx_scale', f32), ('_fpad', f32), ('terms', vp),
+                ('n_q2', i32), ('flags2', i32), ('qz_mu2', i64), ('qz_ls2', i64), ('qx_mu2', i64), ('qx_ls2', i64),
+                ('kl_scale_q2', f32), ('lx_scale2', f32), ('terms2', vp)]
 
 
 class GemmItem(C.Structure):
@@ -94,7 +97,31 @@ class AdamDesc(C.Structure):
                 ('rng_advance', C.c_uint64)]
 
 
-STRUCTS = [Stat, Groups, ConvDesc, CodecCtx, ReduceItem, HeadDesc, GemmItem, RomDesc, ResidualDesc, AdamDesc]
+class VoQueryDesc(C.Structure):
+    _fields_ = [('n_fine', i32), ('nc', i32), ('n', i32), ('flags', i32),
+                ('logkappa', vp), ('bc', vp), ('gamma', vp), ('alpha', vp)]
+
+
+class VoMomentsDesc(C.Structure):
+    _fields_ = [('nc', i32), ('refine', i32), ('n', i32), ('n_mc', i32),
+                ('uc', vp), ('logsig_y', vp), ('eps', vp), ('seed', u64), ('offset', vp), ('sub', u64),
+                ('mean', vp), ('std', vp), ('prec', vp)]
+
+
+class VoConditionDesc(C.Structure):
+    _fields_ = [('n', i32), ('m', i32), ('d_y', i32), ('_pad', i32),
+                ('gamma', vp), ('alpha', vp), ('g', vp), ('prec', vp), ('vo_var', vp), ('lam', vp), ('solvec', vp),
+                ('mean', vp), ('vars', vp), ('mean32', vp), ('logsig32', vp), ('flag', vp)]
+
+
+class VoPrecisionDesc(C.Structure):
+    _fields_ = [('n', i32), ('m', i32), ('d_y', i32), ('_pad', i32),
+                ('gamma', vp), ('alpha', vp), ('mean', vp), ('vars', vp), ('infinite', vp),
+                ('alpha0', C.c_double), ('beta0', C.c_double), ('beta', vp), ('vo_var', vp)]
+
+
+STRUCTS = [Stat, Groups, ConvDesc, CodecCtx, ReduceItem, HeadDesc, GemmItem, RomDesc, ResidualDesc, AdamDesc,
+           VoQueryDesc, VoMomentsDesc, VoConditionDesc, VoPrecisionDesc]
 
 # name -> (restype, argtypes)
 SIGNATURES = {
@@ -117,6 +144,12 @@ SIGNATURES = {
     'gpi_randn': (C.c_int, [vp, i64, u64, vp, u64, vp]),
     'gpi_rng_advance': (C.c_int, [vp, u64, vp]),
     'gpi_random_subset': (C.c_int, [vp, i32, i32, u64, vp, u64, vp]),
+    'gpi_vo_rows': (C.c_int, [i32, i32, i32]),
+    'gpi_vo_query': (C.c_int, [C.POINTER(VoQueryDesc), vp]),
+    'gpi_vo_moments': (C.c_int, [C.POINTER(VoMomentsDesc), vp]),
+    'gpi_vo_condition': (C.c_int, [C.POINTER(VoConditionDesc), vp]),
+    'gpi_vo_precision': (C.c_int, [C.POINTER(VoPrecisionDesc), vp]),
+    'gpi_gauss_sample': (C.c_int, [vp, vp, vp, i64, i32, i32, vp, u64, vp, u64, vp]),
 }
 
 _LIB = None

@@ -4,12 +4,13 @@ pre-planned workspaces.  No host synchronisation anywhere on the path.
 
 ElboEngine = GenerativeModel.elbo (generative.py:247-287) for the armortized
 unsupervised term (generative.py:546-585) + the supervised freeX term
-(generative.py:461-500), and its backward:
+(generative.py:461-500) + the virtual-observable freeX term
+(generative.py:341-392, hold-off variant included), and its backward:
 
   forward   encoder program (B_u)            conv.hip  (11 launches at C64)
             dense head (all samples)          head.hip  (1)
-            decoder program (B_u + N_s, two BN groups, fused Gaussian loss)  (12)
-            ROM solve + log-lik + adjoint     rom.hip   (1)
+            decoder program (B_u + N_s + N_vo, one BN group per term, fused Gaussian loss)  (12)
+            ROM solve + log-lik + adjoint     rom.hip   (1 per labeled / VO term)
   backward  decoder program (reverse), dense head, encoder program (reverse),
             weight-gradient slab reduction, outer-product GEMMs, finalize.
 """
@@ -26,7 +27,9 @@ N_TERMS = 16
 R = L.GPI_REPLICAS
 # term slots in the fp64 scratch
 T_LX0 = 0          # decoder Gaussian log-lik per group (0..3)
-T_KL_ENC, T_KL_Q, T_LOGL_X, T_ENT, T_LOGL_Y = 4, 5, 6, 7, 8
+T_KL_ENC, T_KL_Q, T_LOGL_X, T_ENT = 4, 5, 6, 7           # head terms (supervised segment)
+T_KL_Q2, T_LOGL_X2, T_ENT2 = 8, 9, 10                   # head terms (VO segment)
+T_LOGL_Y, T_LOGL_Y2 = 11, 12                            # ROM log-lik (supervised, VO)
 
 
 def groups_struct(sizes):
@@ -123,16 +126,23 @@ def _run(fn, *args, what=None):
 
 
 class ElboEngine(object):
-    """Fused armortized-unsupervised + supervised-freeX ELBO of a GenerativeModel."""
+    """Fused armortized-unsupervised + supervised-freeX (+ virtual-observable freeX) ELBO of a
+    GenerativeModel.  N_vo > 0 adds the VO term (its own decoder BN group, q_z['vo'] / q_X['vo']
+    rows as the head's second variational segment, a second ROM launch against targets sampled
+    from the VO posterior); vo_holdoff keeps only its logL_x - KL part (generative.py:349-364)."""
 
-    def __init__(self, model, B_u, N_s, normalize=False):
+    def __init__(self, model, B_u, N_s, normalize=False, N_vo=0, vo_holdoff=False):
         self.model = model
         flat = model._flat
         self.flat = flat
         dev = flat.P.device
-        self.B_u, self.N_s = int(B_u), int(N_s)
-        self.B = self.B_u + self.N_s
+        self.B_u, self.N_s, self.N_vo = int(B_u), int(N_s), int(N_vo)
+        self.vo_holdoff = bool(vo_holdoff) and self.N_vo > 0
+        self.N_q = self.N_s + self.N_vo
+        self.B = self.B_u + self.N_q
         self.normalize = bool(normalize)
+        # q samples whose X~ enters the ROM / gp likelihood (hold-off VO samples do not)
+        self.N_x = self.N_s + (self.N_vo if not self.vo_holdoff else 0)
         enc, dec, gp, g = model.encoder, model.f, model.gp, model.g
         self.enc, self.dec = enc, dec
         ws = Workspace()
@@ -150,21 +160,25 @@ class ElboEngine(object):
         else:
             self.ep = None
             d_feat = 1
-        # ---- decoder program (groups: unsup, sup)
+        # ---- decoder program (groups: unsup, sup, vo)
         dc = dec.native_config()
         self.dp = decoder_program(final_epilogue=L.EPI_GAUSS_LOSS, **dc)
-        self.dec_sizes = [n for n in (self.B_u, self.N_s) if n > 0]
+        self.dec_sizes = [n for n in (self.B_u, self.N_s, self.N_vo) if n > 0]
+        self.g_sup = (1 if self.B_u > 0 else 0) if self.N_s > 0 else None
+        self.g_vo = ((self.B_u > 0) + (self.N_s > 0)) if self.N_vo > 0 else None
         self.dec_descs = self.dp.layout(self.B, ws.ws, ws.stats, ws.parts, groups_struct(self.dec_sizes), offD)
         # ---- dense head buffers
         d_lat = self.dp.input.per_sample
-        d_x = g.dim_effective_property if self.N_s > 0 else 1
+        d_x = g.dim_effective_property if self.N_q > 0 else 1
         self.d_x = d_x
+        self.d_y = g.dim_out
         hb = {}
         for name, n in (('hpre', self.B_u * d_feat), ('dhpre', self.B_u * d_feat),
                         ('zmu', self.B * dz), ('zls', self.B * dz), ('eps_z', self.B * dz), ('z', self.B * dz),
                         ('gz', self.B * dz), ('dzmu', self.B * dz), ('dzls', self.B * dz),
-                        ('eps_x', self.N_s * d_x), ('xs', self.N_s * d_x), ('mux', self.N_s * d_x),
-                        ('gxs', self.N_s * d_x), ('gmux', self.N_s * d_x)):
+                        ('eps_x', self.N_q * d_x), ('xs', self.N_q * d_x), ('mux', self.N_q * d_x),
+                        ('gxs', self.N_q * d_x), ('gmux', self.N_q * d_x),
+                        ('y_vo', (self.N_vo if not self.vo_holdoff else 0) * self.d_y)):
             hb[name] = ws.alloc(max(n, 1))
         self.hb = hb
         ws.materialize(dev)
@@ -175,7 +189,9 @@ class ElboEngine(object):
             h.flags |= L.HEAD_ENC | L.HEAD_REPARAM
         if self.N_s > 0:
             h.flags |= L.HEAD_QZ | L.HEAD_GP
-        h.n_enc, h.n_q = self.B_u, self.N_s
+        h.n_enc, h.n_q, h.n_q2 = self.B_u, self.N_s, self.N_vo
+        if self.N_vo > 0:
+            h.flags2 = L.HEAD_QZ | (0 if self.vo_holdoff else L.HEAD_GP)
         h.d_feat, h.d_z, h.d_lat, h.d_x = d_feat, dz, d_lat, d_x
         if self.B_u > 0:
             h.fc_w, h.fc_b = P(enc, 'features.FC.weight'), P(enc, 'features.FC.bias')
@@ -186,28 +202,37 @@ class ElboEngine(object):
             h.fc_w = h.fc_b = h.mu_w = h.mu_b = h.ls_w = h.ls_b = -1
             h.feat = h.gfeat = 0
         h.lat_w, h.lat_b = P(dec, 'latent_map.weight'), P(dec, 'latent_map.bias')
+        h.gp_w = h.gp_b = h.gp_ls = h.qz_mu = h.qz_ls = h.qx_mu = h.qx_ls = -1
+        h.qz_mu2 = h.qz_ls2 = h.qx_mu2 = h.qx_ls2 = -1
+        if self.N_x > 0:
+            h.gp_w, h.gp_b, h.gp_ls = P(gp, 'fc.weight'), P(gp, 'fc.bias'), P(gp, 'logsigmas_X')
         if self.N_s > 0:
             qz, qx = model.q_z['supervised'], model.q_X['supervised']
-            h.gp_w, h.gp_b, h.gp_ls = P(gp, 'fc.weight'), P(gp, 'fc.bias'), P(gp, 'logsigmas_X')
             h.qz_mu, h.qz_ls = flat.offset(qz._mean), flat.offset(qz._logsigma)
             h.qx_mu, h.qx_ls = flat.offset(qx._mean), flat.offset(qx._logsigma)
-        else:
-            h.gp_w = h.gp_b = h.gp_ls = h.qz_mu = h.qz_ls = h.qx_mu = h.qx_ls = -1
+        if self.N_vo > 0:
+            qz, qx = model.q_z['vo'], model.q_X['vo']
+            h.qz_mu2, h.qz_ls2 = flat.offset(qz._mean), flat.offset(qz._logsigma)
+            if not self.vo_holdoff:
+                h.qx_mu2, h.qx_ls2 = flat.offset(qx._mean), flat.offset(qx._logsigma)
         for k, v in hb.items():
             setattr(h, k, v)
         h.lat, h.glat = self.dp.input.off, self.dp.input.s_off
         su = 1.0 / self.B_u if (self.normalize and self.B_u) else 1.0
         ss = 1.0 / self.N_s if (self.normalize and self.N_s) else 1.0
-        self.su, self.ss = su, ss
+        sv = 1.0 / self.N_vo if (self.normalize and self.N_vo) else 1.0
+        self.su, self.ss, self.sv = su, ss, sv
         h.kl_scale_enc, h.kl_scale_q, h.lx_scale = su, ss, ss
+        h.kl_scale_q2, h.lx_scale2 = sv, sv
         h.terms = ws.term_ptr(T_KL_ENC).value
+        h.terms2 = ws.term_ptr(T_KL_Q2).value
         self.head = h
         # ---- contexts
         if self.ep is not None:
             self.ectx = make_ctx(ws, flat, [self.B_u])
             self.ectx.ext_stride = self.ep.input.per_sample
         self.dctx = make_ctx(ws, flat, self.dec_sizes)
-        for gi, scale in enumerate([su] * (self.B_u > 0) + [ss] * (self.N_s > 0)):
+        for gi, scale in enumerate([su] * (self.B_u > 0) + [ss] * (self.N_s > 0) + [sv] * (self.N_vo > 0)):
             self.dctx.loss_scale[gi] = scale
         # ---- gradient reductions
         self.reduce_enc = self.ep.reduce_items(offE) if self.ep is not None else []
@@ -223,33 +248,43 @@ class ElboEngine(object):
             gi.append(it)
 
         gemm(self.dp.input.s_off, hb['z'], B, d_lat, dz, d_lat, dz, h.lat_w, h.lat_b)
-        if self.N_s > 0:
-            gemm(hb['gmux'], hb['z'] + self.B_u * dz, self.N_s, d_x, dz, d_x, dz, h.gp_w, h.gp_b)
+        if self.N_x > 0:
+            gemm(hb['gmux'], hb['z'] + self.B_u * dz, self.N_x, d_x, dz, d_x, dz, h.gp_w, h.gp_b)
         if self.B_u > 0:
             gemm(hb['dzmu'], hb['hpre'], self.B_u, dz, d_feat, dz, d_feat, h.mu_w, h.mu_b, 1)
             gemm(hb['dzls'], hb['hpre'], self.B_u, dz, d_feat, dz, d_feat, h.ls_w, h.ls_b, 1)
             gemm(hb['dhpre'], h.feat, self.B_u, d_feat, d_feat, d_feat, d_feat, h.fc_w, h.fc_b)
         self.gemm_items = (L.GemmItem * len(gi))(*gi)
-        # ---- ROM
-        if self.N_s > 0:
+        # ---- ROM (one launch per labeled / VO term; both on the side stream)
+        def rom_desc(row0, n, scale, slot):
             r = L.RomDesc()
             rom = g.rom
-            r.nc, r.refine, r.n, r.mode = rom.nc, rom.refine, self.N_s, L.ROM_LOGLIK
-            r.x = ws.fptr(hb['xs']).value
+            r.nc, r.refine, r.n, r.mode = rom.nc, rom.refine, n, L.ROM_LOGLIK
+            r.x = ws.fptr(hb['xs'] + row0 * d_x).value
             r.x_stride = d_x
             r.logsig_y = flat.P.data_ptr() + 4 * flat.offset(g.logsigmas_y)
-            r.loss_scale = ss
+            r.loss_scale = scale
             r.gx_accumulate = 0
-            r.gx = ws.fptr(hb['gxs']).value
+            r.gx = ws.fptr(hb['gxs'] + row0 * d_x).value
             r.gx_stride = d_x
             r.gacc_logsig = flat.gacc.data_ptr() + 8 * flat.offset(g.logsigmas_y)
-            r.loss_acc = ws.term_ptr(T_LOGL_Y).value
+            r.loss_acc = ws.term_ptr(slot).value
             r.flag = ws.t_flag.data_ptr()
             r.mu_y = None
             r.uc = None
             r.dmu = None
-            self.rom = r
-        self._fixed = (self.B_u, self.N_s)
+            return r
+
+        self.roms = []
+        self.rom = self.rom_vo = None
+        if self.N_s > 0:
+            self.rom = rom_desc(0, self.N_s, ss, T_LOGL_Y)
+            self.roms.append(self.rom)
+        if self.N_vo > 0 and not self.vo_holdoff:
+            self.rom_vo = rom_desc(self.N_s, self.N_vo, sv, T_LOGL_Y2)
+            self.rom_vo.Y = ws.fptr(hb['y_vo']).value
+            self.roms.append(self.rom_vo)
+        self._fixed = (self.B_u, self.N_s, self.N_vo)
         self._side = None
         self._pending_join = False
 
@@ -258,9 +293,14 @@ class ElboEngine(object):
         return self.ws.view(self.hb['eps_z'], self.B, self.dz)
 
     def eps_x(self):
-        return self.ws.view(self.hb['eps_x'], self.N_s, self.d_x)
+        """[N_x, d_x] q_X noise (supervised rows, then VO rows unless held off)."""
+        return self.ws.view(self.hb['eps_x'], self.N_x, self.d_x)
 
-    def bind(self, X_u=None, u_index=None, X_s=None, Y=None, F=None):
+    def y_vo(self):
+        """[N_vo, d_y] VO targets y ~ N(VO.mean, VO.var) of this step (generative.py:356)."""
+        return self.ws.view(self.hb['y_vo'], self.N_vo if not self.vo_holdoff else 0, self.d_y)
+
+    def bind(self, X_u=None, u_index=None, X_s=None, Y=None, F=None, X_vo=None, F_vo=None):
         """Point the launch descriptors at this step's data tensors."""
         if self.B_u > 0:
             L.require_device(X_u)
@@ -278,6 +318,16 @@ class ElboEngine(object):
             self.dctx.tgt_idx[gs] = None
             self.rom.Y = Y.data_ptr()
             self.rom.F = F.data_ptr()
+        if self.N_vo > 0:
+            for t in (X_vo,) + ((F_vo,) if not self.vo_holdoff else ()):
+                L.require_device(t)
+                assert t.dtype == torch.float32 and t.is_contiguous()
+            assert X_vo.shape[0] == self.N_vo
+            self.dctx.tgt[self.g_vo] = X_vo.data_ptr()
+            self.dctx.tgt_idx[self.g_vo] = None
+            if not self.vo_holdoff:
+                assert F_vo.shape[0] == self.N_vo
+                self.rom_vo.F = F_vo.data_ptr()
 
     def forward(self, stream=None, compute_value=True, zero_gacc=True):
         """Launch the forward; returns the 0-d ELBO tensor (no host sync).  zero_gacc=False
@@ -292,14 +342,15 @@ class ElboEngine(object):
                  what='encoder forward')
         _run(lib.gpi_head_forward, C.byref(self.head), C.c_void_p(self.flat.P.data_ptr()),
              C.c_void_p(self.ws.t_ws.data_ptr()), st, what='head forward')
-        if self.N_s > 0:
+        if self.roms:
             # the ROM solve only feeds the head backward: run it on a side stream,
             # concurrently with the decoder (fork here, join in backward / value)
             main = torch.cuda.current_stream()
             self._side_stream()
             self._ev_fork.record(main)
             self._side.wait_event(self._ev_fork)
-            _run(lib.gpi_rom, C.byref(self.rom), C.c_void_p(self._side.cuda_stream), what='rom')
+            for r in self.roms:
+                _run(lib.gpi_rom, C.byref(r), C.c_void_p(self._side.cuda_stream), what='rom')
             self._ev_join.record(self._side)
             self._pending_join = True
         _run(lib.gpi_codec_forward, self.dec_descs, len(self.dec_descs), C.byref(self.dctx), st,
@@ -323,15 +374,18 @@ class ElboEngine(object):
 
     def elbo_value(self):
         t = self.ws.terms
-        su, ss = self.su, self.ss
+        su, ss, sv = self.su, self.ss, self.sv
         val = t.new_zeros(())
-        gi = 0
         if self.B_u > 0:
-            val = val + su * (t[T_LX0 + gi] - t[T_KL_ENC])
-            gi += 1
+            val = val + su * (t[T_LX0] - t[T_KL_ENC])
         if self.N_s > 0:
-            val = val + ss * (t[T_LX0 + gi] + t[T_LOGL_Y] + t[T_LOGL_X] + t[T_ENT] + self.N_s * ENT_CONST
+            val = val + ss * (t[T_LX0 + self.g_sup] + t[T_LOGL_Y] + t[T_LOGL_X] + t[T_ENT] + self.N_s * ENT_CONST
                               - t[T_KL_Q])
+        if self.N_vo > 0:
+            v = t[T_LX0 + self.g_vo] - t[T_KL_Q2]
+            if not self.vo_holdoff:
+                v = v + t[T_LOGL_Y2] + t[T_LOGL_X2] + t[T_ENT2] + self.N_vo * ENT_CONST
+            val = val + sv * v
         return val.to(torch.float32)
 
     def terms(self):
@@ -349,6 +403,13 @@ class ElboEngine(object):
             out['supervised_logL_y'] = float(t[T_LOGL_Y])
             out['supervised_DKL_z'] = float(t[T_KL_Q])
             out['supervised_entropy_X'] = float(t[T_ENT]) + self.N_s * ENT_CONST
+        if self.N_vo > 0:
+            out['vo_logL_x'] = float(t[T_LX0 + self.g_vo])
+            out['vo_DKL'] = float(t[T_KL_Q2])
+            if not self.vo_holdoff:
+                out['vo_logL_X'] = float(t[T_LOGL_X2])
+                out['vo_logL_y'] = float(t[T_LOGL_Y2])
+                out['vo_entropy'] = float(t[T_ENT2]) + self.N_vo * ENT_CONST
         return out
 
     def backward(self, stream=None):

@@ -1,0 +1,120 @@
+"""Launchers of the virtual-observable kernels (csrc/vo.hip, include/gpi.h).
+
+Every function takes device tensors, launches on the current stream and never
+synchronises the host; shapes are checked here, before any launch, against
+what the kernels assume.
+"""
+import ctypes as C
+
+import torch
+
+from . import _lib as L
+
+ALPHA0 = 1e-6    # VirtualObservablesEnsemble._alpha_0 (VirtualObservables.py:919)
+BETA0 = 1e-6     # ._beta_0 (:920)
+
+
+def _p(t):
+    return t.data_ptr() if t is not None else None
+
+
+def _dev(*ts):
+    for t in ts:
+        if t is not None:
+            L.require_device(t)
+
+
+def vo_rows(n_fine, nc, flags):
+    m = L.lib().gpi_vo_rows(int(n_fine), int(nc), int(flags))
+    if m < 0:
+        L.check(m, 'gpi_vo_rows')
+    return m
+
+
+def vo_query(x_dg, bc, n_fine, nc, flags):
+    """Gamma [N, m, d_y], alpha [N, m] (fp64) of the CGR / flux samplers for a batch of
+    DG0 log-conductivities x_dg [N, 2 n_fine^2] (fp64) and NDP BCs [N, 4]."""
+    _dev(x_dg, bc)
+    N = x_dg.shape[0]
+    assert x_dg.shape == (N, 2 * n_fine * n_fine) and bc.shape == (N, 4)
+    m = vo_rows(n_fine, nc, flags)
+    dy = (n_fine + 1) * (n_fine - 1)
+    x_dg = x_dg.contiguous().double()
+    bc = bc.contiguous().double()
+    gamma = torch.empty(N, m, dy, dtype=torch.float64, device=x_dg.device)
+    alpha = torch.empty(N, m, dtype=torch.float64, device=x_dg.device)
+    d = L.VoQueryDesc(n_fine=n_fine, nc=nc, n=N, flags=flags, logkappa=_p(x_dg), bc=_p(bc), gamma=_p(gamma),
+                      alpha=_p(alpha))
+    L.check(L.lib().gpi_vo_query(C.byref(d), L.stream_handle()), 'vo query')
+    return gamma, alpha
+
+
+def vo_moments(uc, nc, refine, n, n_mc, logsig_y=None, eps=None, seed=0, offset=None, sub=7, want_std=True):
+    """MC mean / std / precision of y_s = W u_s + exp(logsig_y) eps_s per VO sample
+    (generative.py:198-207).  uc [n * n_mc, (nc+1)^2] fp32."""
+    _dev(uc, logsig_y, eps, offset)
+    nf = nc * refine
+    dy = (nf + 1) * (nf - 1)
+    assert uc.shape == (n * n_mc, (nc + 1) ** 2) and uc.dtype == torch.float32 and uc.is_contiguous()
+    if logsig_y is not None:
+        assert logsig_y.numel() == dy and logsig_y.dtype == torch.float32
+        logsig_y = logsig_y.contiguous()
+    if eps is not None:
+        assert eps.shape == (n * n_mc, dy) and eps.dtype == torch.float32
+        eps = eps.contiguous()
+    mean = torch.empty(n, dy, dtype=torch.float32, device=uc.device)
+    std = torch.empty_like(mean) if want_std else None
+    prec = torch.empty_like(mean)
+    d = L.VoMomentsDesc(nc=nc, refine=refine, n=n, n_mc=n_mc, uc=_p(uc), logsig_y=_p(logsig_y), eps=_p(eps),
+                        seed=seed, offset=_p(offset), sub=sub, mean=_p(mean), std=_p(std), prec=_p(prec))
+    L.check(L.lib().gpi_vo_moments(C.byref(d), L.stream_handle()), 'vo moments')
+    return mean, std, prec
+
+
+class ConditionWorkspace(object):
+    def __init__(self, N, m, dy, device):
+        self.lam = torch.empty(N, m, m, dtype=torch.float64, device=device)
+        self.solvec = torch.empty(N, m, dtype=torch.float64, device=device)
+        self.flag = torch.zeros(1, dtype=torch.int32, device=device)
+
+
+def vo_condition(gamma, alpha, g, prec, vo_var, mean, vars_, mean32=None, logsig32=None, ws=None):
+    """VirtualObservable.update for every VO sample (VirtualObservables.py:642-669)."""
+    _dev(gamma, alpha, g, prec, vo_var, mean, vars_, mean32, logsig32)
+    N, m, dy = gamma.shape
+    assert alpha.shape == (N, m) and vo_var.shape == (m,)
+    assert g.shape == (N, dy) and prec.shape == (N, dy) and g.dtype == torch.float32 and prec.dtype == torch.float32
+    assert mean.shape == (N, dy) and vars_.shape == (N, dy) and mean.dtype == torch.float64
+    for t in (gamma, alpha, g, prec, vo_var, mean, vars_, mean32, logsig32):
+        assert t is None or t.is_contiguous()
+    if ws is None:
+        ws = ConditionWorkspace(N, m, dy, gamma.device)
+    d = L.VoConditionDesc(n=N, m=m, d_y=dy, gamma=_p(gamma), alpha=_p(alpha), g=_p(g), prec=_p(prec),
+                          vo_var=_p(vo_var), lam=_p(ws.lam), solvec=_p(ws.solvec), mean=_p(mean), vars=_p(vars_),
+                          mean32=_p(mean32), logsig32=_p(logsig32), flag=_p(ws.flag))
+    L.check(L.lib().gpi_vo_condition(C.byref(d), L.stream_handle()), 'vo condition')
+    return ws
+
+
+def vo_precision(gamma, alpha, mean, vars_, infinite, beta, vo_var, alpha0=ALPHA0, beta0=BETA0):
+    """update_vo_precision + _get_mean_vo_variances (VirtualObservables.py:960-998)."""
+    _dev(gamma, alpha, mean, vars_, infinite, beta, vo_var)
+    N, m, dy = gamma.shape
+    assert mean.shape == (N, dy) and vars_.shape == (N, dy) and infinite.shape == (m,)
+    assert infinite.dtype == torch.int32 and beta.shape == (m,) and vo_var.shape == (m,)
+    d = L.VoPrecisionDesc(n=N, m=m, d_y=dy, gamma=_p(gamma), alpha=_p(alpha), mean=_p(mean), vars=_p(vars_),
+                          infinite=_p(infinite), alpha0=alpha0, beta0=beta0, beta=_p(beta), vo_var=_p(vo_var))
+    L.check(L.lib().gpi_vo_precision(C.byref(d), L.stream_handle()), 'vo precision')
+
+
+def gauss_sample(out, mean, logsigma, rep=1, eps=None, seed=0, offset=None, sub=0, stream=None):
+    """out[r] = mean[r // rep] + exp(logsigma[r // rep]) * N(0, 1) (float32 rows)."""
+    _dev(out, mean, logsigma, eps, offset)
+    rows, dim = out.shape
+    assert mean.shape == logsigma.shape and mean.shape[-1] == dim and mean.numel() * rep == out.numel()
+    for t in (out, mean, logsigma):
+        assert t.dtype == torch.float32 and t.is_contiguous()
+    st = stream if stream is not None else L.stream_handle()
+    L.check(L.lib().gpi_gauss_sample(_p(out), _p(mean), _p(logsigma), rows, dim, rep, _p(eps), seed, _p(offset), sub,
+                                     st), 'gauss sample')
+    return out

@@ -130,7 +130,8 @@ typedef struct gpi_reduce_item {
  * and the effective-property map with its Gaussian log-likelihood
  * (components.py:201-256, generative.py:469-470).
  * Samples [0, n_enc) take the amortised-encoder path, samples
- * [n_enc, n_enc + n_q) the per-sample variational path. */
+ * [n_enc, n_enc + n_q) the per-sample variational path (and
+ * [n_enc + n_q, + n_q2) a second variational segment, see n_q2). */
 #define GPI_HEAD_ENC      0x01  /* feat -> FC -> relu -> (mu, logsigma) for encoder samples */
 #define GPI_HEAD_REPARAM  0x02  /* z = mu + exp(logsigma) eps, KL (encoder samples) */
 #define GPI_HEAD_QZ       0x04  /* z from q_z params, KL (q samples) */
@@ -157,6 +158,14 @@ typedef struct gpi_head_desc {
     float kl_scale_enc, kl_scale_q, lx_scale, _fpad;
     /* fp64 term accumulators (terms[0..]): KL_enc, KL_q, logL_X, entropy */
     double* terms;                   /* [4][GPI_REPLICAS] */
+    /* Second per-sample variational segment: samples [n_enc + n_q, n_enc + n_q + n_q2), e.g. the
+     * virtual-observable term (generative.py:341-392) next to the supervised one, with its own
+     * q_z / q_X rows, flags (GPI_HEAD_QZ [| GPI_HEAD_GP]; GP off = VO hold-off), scales and
+     * term slots.  Workspace rows eps_x / xs / mux / gxs / gmux run over both segments. */
+    int32_t n_q2, flags2;
+    int64_t qz_mu2, qz_ls2, qx_mu2, qx_ls2;
+    float kl_scale_q2, lx_scale2;
+    double* terms2;                  /* [3][GPI_REPLICAS]: KL_q, logL_X, entropy of segment 2 */
 } gpi_head_desc;
 
 /* Batched outer-product GEMM for shared dense-layer gradients:
@@ -212,8 +221,93 @@ typedef struct gpi_residual_desc {
     const float* y;            /* [n, d_y] fine free values */
     const float* bc;           /* [n, 4] u0..u3 */
     float* r;                  /* [n, (nc+1)^2] CGR residual */
-    float* r_flux;             /* [n, 2 nc^2] flux residual (or NULL), bottleneck/flux.py */
+    float* r_flux;             /* [n, 2 nc^2] flux residual Gamma_fc y (alpha_fc = 0), or NULL;
+                                  bottleneck/flux.py:81-158, rows as GPI_VO_FLUX */
 } gpi_residual_desc;
+
+/* ------------------------------------------------------------------------
+ * Virtual observables (bottleneck/VirtualObservables.py).
+ *
+ * Query rows of one VO sample (LinearQuerry.Gamma / .alpha, fp64 as the
+ * reference asserts at VirtualObservables.py:396-407), rows in the order the
+ * reference concatenates its samplers (QuerryEnsemble.FromQuerryPointEnsemble,
+ * VirtualObservables.py:519-539):
+ *   GPI_VO_CGR   (nc+1)^2 rows: CoarseGrainedResidualSampler, Gamma = W^T K_ff,
+ *                alpha = W^T f_eff (VirtualObservables.py:57-69,297-321);
+ *   GPI_VO_FLUX  2 nc^2 rows: FluxConstrainSampler / FluxConstraintReducedOrderModel,
+ *                Gamma[k, free i] = d/du_i of the outward flux of kappa grad u over the
+ *                boundary of coarse triangle k (top/bottom domain edges excluded),
+ *                alpha = 0 (bottleneck/flux.py:81-158, incl. the alpha quirk at :153).
+ * Conductivity per DG0 cell of the fine mesh (QuerryPoint.x = X_DG, cell 2q the
+ * lower-right and 2q+1 the upper-left triangle of fine square q = i + n j). */
+#define GPI_VO_CGR  0x1
+#define GPI_VO_FLUX 0x2
+
+typedef struct gpi_vo_query_desc {
+    int32_t n_fine, nc, n, flags;
+    const double* logkappa;    /* [n, 2 n_fine^2] log conductivity per DG0 cell (X_DG) */
+    const double* bc;          /* [n, 4] NDP boundary values u0..u3 */
+    double* gamma;             /* [n, m, d_y] out (every entry written), m = gpi_vo_rows(...) */
+    double* alpha;             /* [n, m] out */
+} gpi_vo_query_desc;
+
+/* MC predictive moments of the ROM (GenerativeModel.update_virtual_observables,
+ * generative.py:198-207): for VO sample j and its n_mc coarse solutions u_s
+ * (gpi_rom FORWARD with uc), y_s = W u_s + exp(logsig_y) eps_s
+ * (ReducedOrderModelOperator.propagate_samples, components.py:304-311);
+ * mean = torch.mean(y_s), std = torch.std(y_s) (unbiased), prec = 1 / std^2 (fp32). */
+typedef struct gpi_vo_moments_desc {
+    int32_t nc, refine, n, n_mc;
+    const float* uc;           /* [n * n_mc, (nc+1)^2] */
+    const float* logsig_y;     /* [d_y] or NULL (no observation noise) */
+    const float* eps;          /* optional injected noise [n * n_mc, d_y]; NULL: device Philox */
+    uint64_t seed;
+    const uint64_t* offset;    /* device Philox offset (may be NULL = 0) */
+    uint64_t sub;
+    float* mean;               /* [n, d_y] out */
+    float* std;                /* [n, d_y] out (optional) */
+    float* prec;               /* [n, d_y] out (optional) */
+} gpi_vo_moments_desc;
+
+/* Gaussian conditioning of every VO sample (VirtualObservable.update,
+ * VirtualObservables.py:642-669): prior N(g, diag(1/prec)), observation
+ * Gamma y = alpha + N(0, diag(vo_var)):
+ *   Lambda = Gamma C Gamma^T + diag(vo_var), L = chol(Lambda),
+ *   mean = g - C Gamma^T Lambda^{-1} (Gamma g - alpha),
+ *   vars = diag(C) - diag(C)^2 |L^{-1} Gamma_i|^2   (= cov - postcov_diag_subtractor).
+ * fp64 throughout (prior casts as the reference: g, prec -> double). */
+typedef struct gpi_vo_condition_desc {
+    int32_t n, m, d_y, _pad;
+    const double* gamma;       /* [n, m, d_y] */
+    const double* alpha;       /* [n, m] */
+    const float* g;            /* [n, d_y] prior mean */
+    const float* prec;         /* [n, d_y] prior precision */
+    const double* vo_var;      /* [m] */
+    double* lam;               /* workspace [n, m, m] (holds L on return) */
+    double* solvec;            /* workspace [n, m] */
+    double* mean;              /* [n, d_y] out */
+    double* vars;              /* [n, d_y] out */
+    float* mean32;             /* optional [n, d_y] out: (float) mean  (ensemble .mean, model dtype) */
+    float* logsig32;           /* optional [n, d_y] out: 0.5 log((float) vars)  (ensemble .logsigma) */
+    int32_t* flag;             /* optional: set to 1 if a Lambda is not positive definite
+                                  (torch.cholesky raises there; checked lazily by the caller) */
+} gpi_vo_condition_desc;
+
+/* VO precision update (VirtualObservablesEnsemble.update_vo_precision,
+ * VirtualObservables.py:971-998 + _get_mean_vo_variances :960-964):
+ *   beta = 0.5 sum_j [(Gamma_j mean_j - alpha_j)^2 + Gamma_j^2 vars_j] + beta0,
+ *   vo_var = beta / (0.5 n + alpha0 + 1), 0 on rows with infinite precision. */
+typedef struct gpi_vo_precision_desc {
+    int32_t n, m, d_y, _pad;
+    const double* gamma;       /* [n, m, d_y] */
+    const double* alpha;       /* [n, m] */
+    const double* mean;        /* [n, d_y] */
+    const double* vars;        /* [n, d_y] */
+    const int32_t* infinite;   /* [m] 1 = infinite precision row */
+    double alpha0, beta0;
+    double* beta;              /* [m] out (prec_beta) */
+    double* vo_var;            /* [m] out (mean VO variances) */
+} gpi_vo_precision_desc;
 
 /* Flat Adam (torch.optim.Adam semantics, no weight decay / amsgrad),
  * training.py:254,417.  step and lr are read from device memory so the
@@ -249,6 +343,18 @@ int gpi_outer_gemm(const gpi_gemm_item* items, int n_items, const float* ws, dou
 
 int gpi_rom(const gpi_rom_desc* d, void* stream);
 int gpi_cgr_residual(const gpi_residual_desc* d, void* stream);
+
+/* Virtual observables: rows per VO sample for a flag set (or a negative error). */
+int gpi_vo_rows(int32_t n_fine, int32_t nc, int32_t flags);
+int gpi_vo_query(const gpi_vo_query_desc* d, void* stream);
+int gpi_vo_moments(const gpi_vo_moments_desc* d, void* stream);
+int gpi_vo_condition(const gpi_vo_condition_desc* d, void* stream);
+int gpi_vo_precision(const gpi_vo_precision_desc* d, void* stream);
+/* Reparametrised Gaussian rows (bottleneck/utils.py:216-219, components.py:174-180):
+ * out[r, t] = mean[r / rep, t] + exp(logsigma[r / rep, t]) * N(0,1), normals from
+ * Philox counter (*offset + r * dim + t) in stream `sub` (or eps[r, t] if eps != NULL). */
+int gpi_gauss_sample(float* out, const float* mean, const float* logsigma, int64_t rows, int32_t dim, int32_t rep,
+                     const float* eps, uint64_t seed, const uint64_t* offset, uint64_t sub, void* stream);
 
 /* Gradient finalisation: grad[i] = (accumulate ? grad[i] : 0) + (float) gacc[i];
  * also increments the device step counter (if non-NULL) for gpi_adam. */

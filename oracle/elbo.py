@@ -120,3 +120,18 @@ def vo_mean_variances(prec_beta, N, infinite_mask, alpha0=1e-6):
     v = v.clone()
     v[infinite_mask] = 0
     return v
+
+
+def vo_predictive(W, M, bc_dofs, qx_mean, qx_logsigma, F, logsigmas_y, eps_X, eps_y):
+    """update_virtual_observables' MC predictive (generative.py:191-207): per VO sample n,
+    X_s = q_X mean + exp(logsigma) eps_X (components.py:174-180), y_s = rom mean(X_s) +
+    exp(logsigmas_y) eps_y (components.py:304-311); returns torch.mean / torch.std (unbiased).
+    eps_X [N, N_mc, dx], eps_y [N, N_mc, d_y]."""
+    means, stds = [], []
+    for n in range(qx_mean.shape[0]):
+        X = qx_mean[n] + torch.exp(qx_logsigma[n]) * eps_X[n]
+        mu, ls = rom_operator(W, M, bc_dofs, X, F[n].expand(X.shape[0], -1), logsigmas_y)
+        y = mu + torch.exp(ls) * eps_y[n]
+        means.append(torch.mean(y, 0))
+        stds.append(torch.std(y, 0))
+    return torch.stack(means), torch.stack(stds)

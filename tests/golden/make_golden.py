@@ -17,6 +17,9 @@ Outputs (small .npz, float32 unless noted) -- inputs, outputs and gradients:
   rom_c32.npz                     ROM solve + ReducedOrderModelOperator bwd
   elbo_c32.npz                    GenerativeModel.elbo (armortized + freeX) + bwd
   vo_c32.npz                      VirtualObservable.update / precision (fp64)
+  vo_elbo_c32.npz                 GenerativeModel.update_virtual_observables (x2, CGR + flux
+                                  queries through the reference's own sampler / LinearQuerry /
+                                  VirtualObservablesEnsemble classes) + elbo with the VO term + bwd
   terms.npz                       DGLL / KL known values
 """
 import os
@@ -273,6 +276,191 @@ def make_vo():
     print('vo ok')
 
 
+# --------------------------------------------------------------------------
+class _FakePhysics(object):
+    """What QuerryPoint / CoarseGrainedResidualSampler read from a FEniCS physics object;
+    the operators come from the oracle's generic P1 assembly."""
+
+    def __init__(self, mesh):
+        self.mesh = mesh
+        c, f = fem.dirichlet_split(mesh)
+        self.dim_out = f.size
+        self.Vc = mock.MagicMock()
+        self.Vc.dim.return_value = mesh.num_cells
+
+    def assemble_system(self, x, bc=None, only_free_dofs=True):
+        return fem.assemble_system(self.mesh, x, bc.u)
+
+
+class _FakeBC(object):
+    def __init__(self, u):
+        self.u = u
+
+
+class _FakeFlux(object):
+    """FluxConstraintReducedOrderModel stand-in: oracle flux rows reduced to the free dofs, alpha = 0."""
+
+    initialized = True
+
+    def __init__(self, mc, mf):
+        self.mc, self.mf = mc, mf
+        self.free = fem.dirichlet_split(mf)[1]
+
+    def assemble_reduced(self, x, bc):
+        G, a = fem.flux_rows(self.mc, self.mf, x)
+        return G[:, self.free], a
+
+
+def make_vo_elbo():
+    nc, r, mc, mf, M, W, cdofs, fdofs = c32_physics()
+    n = nc * r
+    rng = np.random.default_rng(8)
+    Nu, bs, Ns, Nvo, Nmc = 8, 4, 3, 3, 6
+    dz = 16
+    torch.manual_seed(0)
+    gen = torch.Generator().manual_seed(9)
+    enc = CNNEncoder(n, dz, [1, 1], 4, 4, drop_rate=0)
+    dec = CNNDecoder(n, dz, (8, 8), 1, 4, [1, 1], False, 4, drop_rate=0., upsample='nearest',
+                     force_single_output=False, homoscedastic=False)
+    randomize_bn(enc, gen)
+    randomize_bn(dec, gen)
+    rom = R_ROM.ROM(_Phys(cdofs, fdofs), torch.tensor(M, dtype=torch.float32), torch.float32, 'cpu')
+    g = R_comp.ReducedOrderModelOperator(rom, torch.tensor(W, dtype=torch.float32), dtype=torch.float32,
+                                         device='cpu')
+    gp = R_comp.EffectivePropertyMap(dz, M.shape[2], num_hidden_layers=0, independent_X=True,
+                                     dtype=torch.float32, device='cpu')
+    model = R_gen.GenerativeModel(f=dec, g=g, gp=gp, dtype=torch.float32, device='cpu')
+    model.encoder = enc
+
+    def labeled(k):
+        img = random_fields(rng, k, n)
+        U = rng.uniform(-0.5, 0.5, (k, 4))
+        Y = np.stack([fem.solve_fom(mf, np.exp(fem.image_to_cells(x)), u) for x, u in zip(img, U)])
+        F = np.stack([fem.f_rom_bc(mc, u) for u in U])
+        return img, U, Y, F
+
+    Xu = random_fields(rng, Nu, n)
+    Xs, Us, Ys, Fs = labeled(Ns)
+    Xv, Uv, Yv, Fv = labeled(Nvo)
+    t32 = lambda a: torch.tensor(a, dtype=torch.float32)
+    ds_sup = _DS(X=t32(Xs), Y=t32(Ys), F_ROM_BC=t32(Fs))
+    ds_uns = _DS(X=t32(Xu))
+    ds_vo = _DS(X=t32(Xv), Y=t32(Yv), F_ROM_BC=t32(Fv))
+
+    # the reference's own query / ensemble classes over oracle operators
+    phys = _FakePhysics(mf)
+    QPs = [R_VO.QuerryPoint(phys, fem.image_to_cells(x), _FakeBC(u)) for x, u in zip(Xv, Uv)]
+    QPE = R_VO.QuerryPointEnsemble(QPs)
+    flux = _FakeFlux(mc, mf)
+    querries = []
+    for qp in QPs:
+        sampler = R_VO.ConcatenatedSamplers([R_VO.CoarseGrainedResidualSampler(qp=qp, W=W),
+                                             R_VO.FluxConstrainSampler(qp, flux)])
+        querries.append(R_VO.LinearQuerry(qp, sampler, dtype=torch.float32, device='cpu'))
+    QE = R_VO.QuerryEnsemble(querries, dtype=torch.float32, device='cpu')
+    VO = R_VO.VirtualObservablesEnsemble(QPE, QE, dtype=torch.float32, device=torch.device('cpu'))
+
+    model.register_datasets({'supervised': ds_sup, 'unsupervised': ds_uns, 'vo': ds_vo}, VO,
+                            create_unsupervised_variational_approximation=False)
+    with torch.no_grad():
+        for key in ('supervised', 'vo'):
+            for q in (model.q_z[key], model.q_X[key]):
+                q._mean.copy_(torch.tensor(rng.normal(0, 0.5, q._mean.shape)))
+                q._logsigma.copy_(torch.tensor(rng.normal(-1.0, 0.3, q._logsigma.shape)))
+        g.logsigmas_y.copy_(torch.tensor(rng.normal(-2.0, 0.2, g.logsigmas_y.shape)))
+    state0 = {k: v.detach().cpu().numpy().copy() for k, v in model.state_dict().items()}
+    dx = M.shape[2]
+    dy = W.shape[0]
+
+    # two VO updates (the second one exercises the learnable flux-row precisions)
+    upd = []
+    for it in range(2):
+        ex = rng.normal(size=(Nvo, Nmc, dx))
+        ey = rng.normal(size=(Nvo, Nmc, dy))
+        q_randn = [torch.tensor(e, dtype=torch.float32) for e in ex]
+        q_like = [torch.tensor(e, dtype=torch.float32) for e in ey]
+
+        def fake_randn(*size, **k):
+            e = q_randn.pop(0)
+            assert tuple(e.shape) == tuple(size), (e.shape, size)
+            return e
+
+        def fake_randn_like(t, *a, **k):
+            e = q_like.pop(0)
+            assert e.shape == t.shape
+            return e
+
+        with mock.patch('torch.randn', fake_randn), mock.patch('torch.randn_like', fake_randn_like), \
+                mock.patch('torch.cholesky', torch.linalg.cholesky):
+            Ym, Ysd = model.update_virtual_observables(Nmc, return_mean_stddev=True, step=it)
+        assert not q_randn and not q_like
+        upd.append(dict(eps_X=ex.reshape(Nvo * Nmc, dx), eps_y=ey.reshape(Nvo * Nmc, dy), Y_mean=Ym.numpy(),
+                        Y_std=Ysd.numpy(), mean=VO.mean.numpy(), vars=VO.vars.numpy(),
+                        vo_var=VO._mean_vo_variances.numpy(), prec_beta=VO._prec_beta.numpy()))
+
+    perm = torch.tensor(rng.permutation(Nu), dtype=torch.long)
+    shapes = [(bs, dz), (Ns, dz), (Ns, dx), (Nvo, dz), (Nvo, dx), (Nvo, dy)]
+    eps = [torch.tensor(rng.normal(size=sh), dtype=torch.float32) for sh in shapes]
+    queue = list(eps)
+
+    def fake_randn_like(t, *a, **k):
+        e = queue.pop(0)
+        assert e.shape == t.shape, (e.shape, t.shape)
+        return e.to(dtype=t.dtype)
+
+    class _Writer(object):
+        def __init__(self):
+            self.d = {}
+
+        def add_scalar(self, k, v, global_step=None):
+            self.d[k] = float(v)
+
+    model.writer = _Writer()
+    with mock.patch('torch.randperm', lambda N, **k: perm.clone()), mock.patch('torch.randn_like', fake_randn_like):
+        elbo = model.elbo(step=0, armortized_bs=bs)
+    assert not queue
+    terms_main = dict(model.writer.d)
+    model.writer = _Writer()
+    (-elbo).backward()
+    grads_main = {'grad.' + k: p.grad.detach().numpy().copy() for k, p in model.named_parameters()
+                  if p.grad is not None}
+    # hold-off variant (generative.py:361-364): only q_z['vo'] is sampled for the VO term
+    model.zero_grad()
+    eps_h = [torch.tensor(rng.normal(size=sh), dtype=torch.float32) for sh in shapes[:4]]
+    queue = list(eps_h)
+    with mock.patch('torch.randperm', lambda N, **k: perm.clone()), mock.patch('torch.randn_like', fake_randn_like):
+        elbo_h = model.elbo(step=0, armortized_bs=bs, vo_holdoff=True)
+    assert not queue
+    terms_h = dict(model.writer.d)
+    model.writer = None
+    out = {'state.' + k: v for k, v in state0.items()}
+    out.update(grads_main)
+    out.update(Xu=Xu.astype(np.float32), Xs=Xs.astype(np.float32), Ys=Ys.astype(np.float32),
+               Fs=Fs.astype(np.float32), Us=Us, Xv=Xv.astype(np.float32), Yv=Yv.astype(np.float32),
+               Fv=Fv.astype(np.float32), Uv=Uv, Xv_dg=np.stack([qp.x for qp in QPs]), perm=perm.numpy(),
+               M=M.astype(np.float32), W=W.astype(np.float32), bc_dofs=cdofs,
+               cfg=np.array([n, nc, dz, Nu, bs, Ns, Nvo, Nmc]),
+               Gamma=np.stack([q.Gamma.numpy() for q in querries]), alpha=np.stack([q.alpha.numpy() for q in querries]),
+               elbo=np.float64(elbo.item()), elbo_holdoff=np.float64(elbo_h.item()))
+    for k, v in terms_main.items():
+        out['term.' + k] = np.float64(v)
+    for k, v in terms_h.items():
+        out['termh.' + k] = np.float64(v)
+    for i, e in enumerate(eps):
+        out['eps%d' % i] = e.numpy()
+    for i, e in enumerate(eps_h):
+        out['epsh%d' % i] = e.numpy()
+    for it, u in enumerate(upd):
+        for k, v in u.items():
+            out['upd%d.%s' % (it, k)] = v
+    (-elbo_h).backward()
+    out.update({'gradh.' + k: p.grad.detach().numpy().copy() for k, p in model.named_parameters()
+                if p.grad is not None})
+    np.savez_compressed(os.path.join(HERE, 'vo_elbo_c32.npz'), **out)
+    print('vo elbo ok', elbo.item(), elbo_h.item())
+    return elbo
+
+
 def make_terms():
     rng = np.random.default_rng(7)
     t = torch.tensor(rng.normal(size=(5, 7)))
@@ -290,3 +478,4 @@ if __name__ == '__main__':
     make_rom()
     make_elbo()
     make_vo()
+    make_vo_elbo()

@@ -62,3 +62,13 @@ def test_conv_blocks_host_query(lib):
     assert nb.value == 288 * 4          # full-width tiles of 8 rows on a 32 x 32 plane
     d.k = 4                             # unsupported kernel size -> error code, no crash
     assert L.gpi_conv_blocks(C.byref(d), C.byref(g), C.byref(nb)) != 0
+
+
+def test_vo_rows_host_query(lib):
+    L = lib.lib()
+    assert L.gpi_vo_rows(64, 8, lib.VO_CGR) == 81
+    assert L.gpi_vo_rows(64, 8, lib.VO_FLUX) == 128
+    assert L.gpi_vo_rows(64, 8, lib.VO_CGR | lib.VO_FLUX) == 209
+    assert L.gpi_vo_rows(32, 4, lib.VO_CGR | lib.VO_FLUX) == 25 + 32
+    assert L.gpi_vo_rows(64, 7, lib.VO_CGR) < 0        # fine grid must refine the coarse one
+    assert L.gpi_vo_rows(64, 8, 0) < 0

@@ -119,3 +119,82 @@ def test_vo_update():
     beta = oelbo.vo_precision_beta([torch.tensor(g) for g in d['Gamma']], [torch.tensor(a) for a in d['alpha']],
                                    [torch.tensor(m) for m in d['mean']], [torch.tensor(v) for v in d['vars']])
     np.testing.assert_allclose(beta.numpy(), d['prec_beta'], rtol=1e-9)
+
+
+def _vo_fixture_state(d):
+    st = {k[len('state.'):]: torch.tensor(v, dtype=torch.float64, requires_grad=True)
+          for k, v in d.items() if k.startswith('state.') and
+          not k.endswith(('running_mean', 'running_var', 'num_batches_tracked'))}
+    return st
+
+
+def test_vo_pipeline_and_vo_elbo():
+    """update_virtual_observables x2 (MC predictive, precision update, conditioning) and the ELBO
+    with the VO term (generative.py:182-222,341-392), oracle vs the reference's own classes."""
+    d = load('vo_elbo_c32.npz')
+    n, nc, dz, Nu, bs, Ns, Nvo, Nmc = [int(v) for v in d['cfg']]
+    st = _vo_fixture_state(d)
+    M = torch.tensor(d['M'], dtype=torch.float64)
+    W = torch.tensor(d['W'], dtype=torch.float64)
+    bc = torch.tensor(d['bc_dofs'])
+    t64 = lambda k: torch.tensor(d[k], dtype=torch.float64)
+    G, A = t64('Gamma'), t64('alpha')
+    m = G.shape[1]
+    assert m == (nc + 1) ** 2 + 2 * nc * nc
+    infinite = torch.zeros(m, dtype=torch.bool)
+    infinite[:(nc + 1) ** 2] = True                       # CGR rows: infinite precision, flux rows learnable
+    vo_var = oelbo.vo_mean_variances(torch.ones(m, dtype=torch.float64), Nvo, infinite)
+    with torch.no_grad():
+        for it in range(2):
+            ex = t64('upd%d.eps_X' % it).view(Nvo, Nmc, -1).float().double()
+            ey = t64('upd%d.eps_y' % it).view(Nvo, Nmc, -1).float().double()
+            Ym, Ysd = oelbo.vo_predictive(W, M, bc, st['q_X.vo._mean'], st['q_X.vo._logsigma'], t64('Fv'),
+                                          st['g.logsigmas_y'], ex, ey)
+            np.testing.assert_allclose(Ym.numpy(), d['upd%d.Y_mean' % it], rtol=1e-5, atol=1e-5)
+            np.testing.assert_allclose(Ysd.numpy(), d['upd%d.Y_std' % it], rtol=1e-4, atol=1e-6)
+            # the reference conditions on its fp32 Y_mean / 1/Y_std^2
+            g32 = torch.tensor(d['upd%d.Y_mean' % it]).double()
+            p32 = (1 / torch.tensor(d['upd%d.Y_std' % it]) ** 2).double()
+            if it == 1:
+                beta = oelbo.vo_precision_beta(list(G), list(A), list(mean_prev), list(vars_prev))
+                np.testing.assert_allclose(beta.numpy(), d['upd1.prec_beta'], rtol=1e-9)
+                vo_var = oelbo.vo_mean_variances(beta, Nvo, infinite)
+            np.testing.assert_allclose(vo_var.numpy(), d['upd%d.vo_var' % it], rtol=1e-9)
+            res = [oelbo.vo_condition(G[i], A[i], g32[i], p32[i], vo_var) for i in range(Nvo)]
+            mean_prev = torch.stack([r[0] for r in res])
+            vars_prev = torch.stack([r[1] for r in res])
+            np.testing.assert_allclose(mean_prev.numpy(), d['upd%d.mean' % it], rtol=1e-6, atol=1e-6)
+            np.testing.assert_allclose(vars_prev.numpy(), d['upd%d.vars' % it], rtol=1e-5, atol=1e-9)
+
+    # ELBO: armortized + supervised + VO terms
+    enc_p = {k[len('encoder.'):]: v for k, v in st.items() if k.startswith('encoder.')}
+    dec_p = {k[len('f.'):]: v for k, v in st.items() if k.startswith('f.')}
+    enc = lambda x: ocodec.encoder_forward(enc_p, x, n, [1, 1], 4, 4)
+    dec = lambda z: ocodec.decoder_forward(dec_p, z, 8, [1, 1], 4, 4)
+    gp = lambda z: torch.nn.functional.linear(z, st['gp.fc.weight'], st['gp.fc.bias'])
+    rom = lambda x, F: oelbo.rom_operator(W, M, bc, x, F, st['g.logsigmas_y'])
+    e = [t64('eps%d' % i) for i in range(6)]
+    Xu = t64('Xu')[torch.tensor(d['perm'][:bs])]
+    e1, _ = oelbo.elbo_unsupervised_armortized(enc, dec, Xu, e[0])
+    qz = lambda key: (st['q_z.%s._mean' % key], st['q_z.%s._logsigma' % key])
+    qx = lambda key: (st['q_X.%s._mean' % key], st['q_X.%s._logsigma' % key])
+    e2, _ = oelbo.elbo_supervised_freeX(dec, gp, st['gp.logsigmas_X'], rom, qz('supervised'), qx('supervised'),
+                                        t64('Xs'), t64('Ys'), t64('Fs'), e[1], e[2])
+    # VO targets: reparametrize(VO.mean, VO.logsigma) in fp32 (generative.py:356)
+    vmean = torch.tensor(d['upd1.mean'])
+    vls = 0.5 * torch.log(torch.tensor(d['upd1.vars']))
+    y = (vmean + torch.exp(vls) * torch.tensor(d['eps5'])).double()
+    e3, terms = oelbo.elbo_supervised_freeX(dec, gp, st['gp.logsigmas_X'], rom, qz('vo'), qx('vo'), t64('Xv'), y,
+                                            t64('Fv'), e[3], e[4])
+    np.testing.assert_allclose(terms['logL_y'].item(), d['term.objective/vo_logL_y'], rtol=1e-4)
+    np.testing.assert_allclose(terms['logL_x'].item(), d['term.objective/vo_logL_x'], rtol=2e-5)
+    elbo = e1 + e2 + e3
+    np.testing.assert_allclose(elbo.item(), float(d['elbo']), rtol=2e-5)
+    (-elbo).backward()
+    for k, p in st.items():
+        ref = d.get('grad.' + k)
+        if ref is None:
+            assert p.grad is None or not p.grad.abs().any(), k
+            continue
+        scale = max(np.abs(ref).max(), 1.0)
+        np.testing.assert_allclose(p.grad.numpy() / scale, ref / scale, atol=2e-4, err_msg=k)
