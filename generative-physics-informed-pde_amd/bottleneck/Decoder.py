@@ -5,6 +5,7 @@ Linear latent map -> 1 x 8 x 8 image -> conv0 -> [DenseBlock -> TransitionUp]
 the reference; ``forward`` runs the latent map and the whole conv stack as
 native kernels.
 """
+import torch
 import torch.nn as nn
 
 import lamp.modules
@@ -20,6 +21,13 @@ class BaseDecoder(lamp.modules.BaseModule):
     @property
     def dim_out(self):
         raise NotImplementedError
+
+    def propagate_samples(self, Z):
+        """Decoder.py:29-37: a sample of the decoder's Gaussian for each z."""
+        means, logsigmas = self.forward(Z)
+        if means.shape != logsigmas.shape:
+            raise RuntimeError('Implementation assumes that full logsigmas matrix is given; check for broadcasting')
+        return means + torch.exp(logsigmas) * torch.randn_like(logsigmas)
 
 
 class CNNDecoder(BaseDecoder):

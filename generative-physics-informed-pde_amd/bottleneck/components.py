@@ -1,5 +1,5 @@
 """Variational approximations, effective-property map, ROM operator, W interpolator,
-prediction ensemble (reference bottleneck/components.py:13-393)."""
+prediction ensemble, predictive analysis (reference bottleneck/components.py:13-654)."""
 import copy
 
 import numpy as np
@@ -221,7 +221,10 @@ class ReducedOrderModelOperator(lamp.modules.BaseModule):
 
 
 class PredictionEnsemble(object):
-    """Validation q_z fitted against the frozen decoder (components.py:326-393)."""
+    """Validation q_z fitted against the frozen decoder (components.py:326-393).  update() runs the
+    native PredictionEnsembleEngine (gpi/predictive.py): decoder-only ELBO + backward + Adam on the
+    q_z rows, no host sync unless a writer records the values.  The torch Adam object is kept for
+    the scheduler wrapper, which reads and rescales its learning rate."""
 
     def __init__(self, model, dataset, scheduler_wrapper, lr=1e-2, writer=None):
         self._model = model
@@ -232,6 +235,10 @@ class PredictionEnsemble(object):
         self._scheduler_wrapper = scheduler_wrapper
         self._scheduler_wrapper.register_optimizer(self._optimizer, 'validation')
         self.writer = writer
+        self._engine = None
+
+    def set_lr_manually(self, lr):
+        raise NotImplementedError
 
     @property
     def q_z(self):
@@ -245,25 +252,179 @@ class PredictionEnsemble(object):
     def dataset(self):
         return self._dataset
 
-    def _elbo(self, X):
-        Z = self._q_z.sample()
-        logL = self._model.random_field_likelihood(self._model.f(Z), X)
-        return logL, self._q_z.KLD()
+    def _native(self):
+        if self._engine is None:
+            from gpi.predictive import PredictionEnsembleEngine
+            self._engine = PredictionEnsembleEngine(self._model, self._q_z, self._dataset.get('X'),
+                                                    lambda: self._optimizer.param_groups[0]['lr'])
+        return self._engine
 
-    def update(self, numIter=1, record=True, step=None):
-        X = self._dataset.get('X')
+    def update(self, numIter=1, record=True, step=None, eps=None):
+        """components.py:365-388.  ``eps`` optionally injects the q_z noise per iteration
+        (a list of numIter [N, d_z] tensors)."""
+        e = self._native()
         for n in range(numIter):
-            logL, KLD = self._elbo(X.detach())
-            elbo = logL - KLD
-            self._optimizer.zero_grad()
-            (-elbo).backward()
-            self._optimizer.step()
+            elbo, logL, KLD = e.update(eps=eps[n] if eps is not None else None)
             if n == numIter - 1:
                 if record and self.writer is not None:
                     self.writer.add_scalar('PredictionEnsemble/elbo', elbo.item(), global_step=step)
                     self.writer.add_scalar('PredictionEnsemble/logL', logL.item(), global_step=step)
                     self.writer.add_scalar('PredictionEnsemble/KLD', KLD.item(), global_step=step)
+                    self.writer.add_scalar('PredictionEnsemble/AvgLatentStddev',
+                                           torch.mean(torch.exp(self._q_z.logsigma)), global_step=step)
                 self._scheduler_wrapper.step('validation', None, None, None, elbo)
+        return elbo
 
     def __repr__(self):
         return 'PredictionEnsemble | Wraps a dataset with {} points for validation purposes'.format(self._dataset.N)
+
+
+class DataPair(object):
+
+    def __init__(self, writer=None, label='', name=None):
+        if writer is not None and name is None:
+            raise ValueError('Required to provide a name for the writer')
+        self.iteration = list()
+        self.value = list()
+        self._writer = writer
+        self._label = label
+        self._name = name
+
+    def append(self, iteration, value):
+        self.iteration.append(iteration)
+        self.value.append(value)
+        if self._writer is not None:
+            self._writer.add_scalar(self._label + '/' + self._name, value, global_step=iteration)
+
+    def min(self):
+        return min(self.value)
+
+    def max(self):
+        return max(self.value)
+
+    def final(self):
+        return self.value[-1]
+
+
+class Analysis(object):
+    """Predictive evaluation of a q (components.py:427-654).  eval_all_y runs every sample's MC
+    predictive at once on the native path (gpi/predictive.py: gp draws, ROM, moments, scores);
+    the per-index methods keep the reference's sample-level semantics."""
+
+    def __init__(self, q, model, dataset, identifier=''):
+        self._q = q
+        self._model = model
+        self._dataset = dataset
+        self.description = None
+        self.data = dict()
+        for item in ['relerr_x', 'relerr_y', 'logscore_x', 'logscore_y', 'r2_y']:
+            self.data[item] = DataPair(writer=self._model.writer, label=getattr(dataset, 'label', ''), name=item)
+
+    @property
+    def dataset(self):
+        return self._dataset
+
+    @classmethod
+    def FromPredictionEnsemble(cls, pe):
+        return cls(pe.q_z, pe.model, pe.dataset)
+
+    @classmethod
+    def FromEncoder(cls, model, dataset):
+        with torch.no_grad():
+            Z_mean, Z_logsigma = model.encoder(dataset.get('X'))
+        q = VariationalApproximation(Z_mean.shape[1], Z_mean.shape[0], dataset.get('X'), dtype=Z_mean.dtype,
+                                     device=Z_mean.device, requires_grad=False)
+        q.init(Z_mean, Z_logsigma)
+        return cls(q, model, dataset)
+
+    @property
+    def X(self):
+        return self._dataset.get('X')
+
+    @property
+    def Y(self):
+        return self._dataset.get('Y')
+
+    @property
+    def F(self):
+        return self._dataset.get('F_ROM_BC')
+
+    @torch.no_grad()
+    def sample_predictive_y(self, N_monte_carlo, index):
+        Z_samples = self._q.sample_batch_component(index, batch_size=N_monte_carlo)
+        X_samples = self._model.gp.propagate_samples(Z_samples)
+        return self._model.g.propagate_samples(X_samples, self.F[index, :].unsqueeze(0).expand(
+            N_monte_carlo, self.F.shape[1]).contiguous())
+
+    @torch.no_grad()
+    def sample_predictive_x(self, N_monte_carlo, index):
+        Z_samples = self._q.sample_batch_component(index, batch_size=N_monte_carlo)
+        return self._model.f.propagate_samples(Z_samples)
+
+    def eval_all(self, N_monte_carlo, iteration):
+        self.relative_error_x(N_monte_carlo, iteration)
+        self.eval_all_y(N_monte_carlo, iteration)
+        self.predictive_log_probability_x(N_monte_carlo, iteration)
+
+    @torch.no_grad()
+    def eval_all_y(self, N_monte_carlo, iteration=None, return_mean_std=False, eps=None):
+        """components.py:493-524 for all samples at once; ``eps`` optionally injects
+        (eps_z [N*N_mc, d_z], eps_x [N*N_mc, d_x], eps_y [N*N_mc, d_y])."""
+        from gpi.predictive import predictive_y, predictive_scores
+        Y = self.Y.detach().float().contiguous()
+        y_mean, y_std = predictive_y(self._model, self._q.mean, self._q.logsigma, self.F.detach(), N_monte_carlo,
+                                     eps=eps)
+        relerr_y, logscore_y, r2_y = predictive_scores(Y, y_mean, y_std)
+        if iteration is None:
+            if return_mean_std:
+                raise RuntimeError('nope')
+            return logscore_y, r2_y, relerr_y
+        self.data['relerr_y'].append(iteration, relerr_y)
+        self.data['logscore_y'].append(iteration, logscore_y)
+        self.data['r2_y'].append(iteration, r2_y)
+        if return_mean_std:
+            return y_mean, y_std
+
+    @torch.no_grad()
+    def relative_error_y(self, N_monte_carlo, iteration=None, ReturnValue=False):
+        relerr = self.eval_all_y(N_monte_carlo)[2]
+        if iteration is None:
+            return relerr
+        self.data['relerr_y'].append(iteration, relerr)
+        if ReturnValue:
+            return relerr
+
+    @torch.no_grad()
+    def predictive_log_probability_y(self, N_monte_carlo, iteration=None):
+        logp = self.eval_all_y(N_monte_carlo)[0]
+        if iteration is None:
+            return logp
+        self.data['logscore_y'].append(iteration, logp)
+
+    @torch.no_grad()
+    def relative_error_x(self, N_monte_carlo, iteration=None, ReturnValue=False):
+        relerrs = np.zeros(self._q.N)
+        for index in range(self._q.N):
+            mean_x = torch.mean(self.sample_predictive_x(N_monte_carlo, index), 0)
+            relerrs[index] = (torch.norm(mean_x.flatten() - self.X[index].flatten()) /
+                              torch.norm(self.X[index].flatten())).item()
+        relerr = float(np.mean(relerrs))
+        if iteration is None:
+            return relerr
+        self.data['relerr_x'].append(iteration, relerr)
+        if ReturnValue:
+            return relerr
+
+    @torch.no_grad()
+    def predictive_log_probability_x(self, N_monte_carlo, iteration=None):
+        logp = np.zeros(self._q.N)
+        for index in range(self._q.N):
+            X_pred = self.sample_predictive_x(N_monte_carlo, index)
+            x_mean = torch.mean(X_pred, 0).flatten()
+            x_std = torch.std(X_pred, 0).flatten()
+            logp[index] = torch.mean(-torch.log(x_std) - 0.5 * ((self.X[index, :].flatten() - x_mean) ** 2 /
+                                                                x_std ** 2) - 0.5 * np.log(2 * np.pi)).item()
+        logp = float(np.mean(logp))
+        if iteration is None:
+            return logp
+        self.data['logscore_x'].append(iteration, logp)

@@ -472,6 +472,85 @@ __global__ __launch_bounds__(256) void gauss_sample_kernel(float* out, const flo
     out[e] = fmaf(expf(ls[src]), z, mean[src]);
 }
 
+
+// ---------------------------------------------------------------- predictive (Analysis)
+constexpr int GPT = 128;   // threads per predictive row
+
+__global__ __launch_bounds__(GPT) void gp_sample_kernel(gpi_gp_sample_desc d) {
+    __shared__ float zs[512];
+    const int r = blockIdx.x;
+    const int j = r / d.rep;
+    const uint64_t base = d.offset ? *d.offset : 0;
+    for (int k = threadIdx.x; k < d.d_z; k += GPT) {
+        const int64_t e = (int64_t)r * d.d_z + k;
+        const float ez = d.eps_z ? d.eps_z[e] : normal_at(base + (uint64_t)e, d.sub, d.seed);
+        zs[k] = fmaf(expf(d.qz_ls[(int64_t)j * d.d_z + k]), ez, d.qz_mu[(int64_t)j * d.d_z + k]);
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < d.d_x; t += GPT) {
+        float a = d.gp_b[t];
+        const float* w = d.gp_w + (int64_t)t * d.d_z;
+        for (int k = 0; k < d.d_z; ++k) a = fmaf(w[k], zs[k], a);
+        if (d.gp_ls) {
+            const int64_t e = (int64_t)r * d.d_x + t;
+            const float ex = d.eps_x ? d.eps_x[e] : normal_at(base + (uint64_t)e, d.sub + 1, d.seed);
+            a = fmaf(expf(d.gp_ls[t]), ex, a);
+        }
+        d.x[(int64_t)r * d.d_x + t] = a;
+    }
+}
+
+// per sample: relative error and log score (one workgroup per sample)
+__global__ __launch_bounds__(256) void scores_rows_kernel(const float* Y, const float* mean, const float* std,
+                                                          int d_y, double* out) {
+    __shared__ double red[3][4];
+    const int n = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    double se = 0.0, sy = 0.0, ls = 0.0;
+    for (int p = tid; p < d_y; p += 256) {
+        const int64_t o = (int64_t)n * d_y + p;
+        const double y = Y[o], mu = mean[o], sd = std[o];
+        const double r = y - mu;
+        se += r * r;
+        sy += y * y;
+        ls += -log(sd) - 0.5 * r * r / (sd * sd) - 0.91893853320467274;
+    }
+    se = wave_sum_d(se);
+    sy = wave_sum_d(sy);
+    ls = wave_sum_d(ls);
+    if (lane == 0) { red[0][wid] = se; red[1][wid] = sy; red[2][wid] = ls; }
+    __syncthreads();
+    if (tid == 0) {
+        const double a = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+        const double b = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+        const double c = (red[2][0] + red[2][1]) + (red[2][2] + red[2][3]);
+        atomicAdd(out + 0, sqrt(a) / sqrt(b));
+        atomicAdd(out + 1, c / (double)d_y);
+    }
+}
+
+// per output p: 1 - sum_n (Y - mean)^2 / sum_n (Y - Ybar)^2 (one thread per output)
+__global__ __launch_bounds__(256) void scores_cols_kernel(const float* Y, const float* mean, int n, int d_y,
+                                                          double* out) {
+    const int p = blockIdx.x * 256 + threadIdx.x;
+    double v = 0.0;
+    if (p < d_y) {
+        double yb = 0.0;
+        for (int k = 0; k < n; ++k) yb += (double)Y[(int64_t)k * d_y + p];
+        yb /= (double)n;
+        double num = 0.0, den = 0.0;
+        for (int k = 0; k < n; ++k) {
+            const double y = Y[(int64_t)k * d_y + p];
+            const double r = y - (double)mean[(int64_t)k * d_y + p], c = y - yb;
+            num += r * r;
+            den += c * c;
+        }
+        v = 1.0 - num / den;
+    }
+    v = wave_sum_d(v);
+    if ((threadIdx.x & 63) == 0) atomicAdd(out + 2, v);
+}
+
 bool grid_of(int n_fine, int nc, FineGrid& G) {
     if (n_fine < 2 || nc < 1 || n_fine % nc) return false;
     G.n = n_fine;
@@ -568,6 +647,28 @@ extern "C" int gpi_gauss_sample(float* out, const float* mean, const float* logs
     if (total == 0) return GPI_OK;
     hipLaunchKernelGGL(gauss_sample_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
                        (hipStream_t)stream, out, mean, logsigma, total, dim, rep, eps, seed, offset, sub);
+    GPI_CHECK_LAUNCH();
+    return GPI_OK;
+}
+
+extern "C" int gpi_gp_sample(const gpi_gp_sample_desc* d, void* stream) {
+    if (!d || !d->qz_mu || !d->qz_ls || !d->gp_w || !d->gp_b || !d->x || d->rows < 0 || d->rep < 1 || d->d_z < 1 ||
+        d->d_z > 512 || d->d_x < 1)
+        return GPI_ERR_ARG;
+    if (d->rows == 0) return GPI_OK;
+    hipLaunchKernelGGL(gp_sample_kernel, dim3(d->rows), dim3(GPT), 0, (hipStream_t)stream, *d);
+    GPI_CHECK_LAUNCH();
+    return GPI_OK;
+}
+
+extern "C" int gpi_predictive_scores(const float* Y, const float* mean, const float* std, int32_t n, int32_t d_y,
+                                     double* out, void* stream) {
+    if (!Y || !mean || !std || !out || n < 1 || d_y < 1) return GPI_ERR_ARG;
+    const hipStream_t st = (hipStream_t)stream;
+    if (hipMemsetAsync(out, 0, 3 * sizeof(double), st) != hipSuccess) return GPI_ERR_LAUNCH;
+    hipLaunchKernelGGL(scores_rows_kernel, dim3(n), dim3(256), 0, st, Y, mean, std, d_y, out);
+    GPI_CHECK_LAUNCH();
+    hipLaunchKernelGGL(scores_cols_kernel, dim3((d_y + 255) / 256), dim3(256), 0, st, Y, mean, n, d_y, out);
     GPI_CHECK_LAUNCH();
     return GPI_OK;
 }

@@ -120,8 +120,14 @@ class VoPrecisionDesc(C.Structure):
                 ('alpha0', C.c_double), ('beta0', C.c_double), ('beta', vp), ('vo_var', vp)]
 
 
+class GpSampleDesc(C.Structure):
+    _fields_ = [('rows', i32), ('rep', i32), ('d_z', i32), ('d_x', i32),
+                ('qz_mu', vp), ('qz_ls', vp), ('gp_w', vp), ('gp_b', vp), ('gp_ls', vp), ('eps_z', vp), ('eps_x', vp),
+                ('seed', u64), ('offset', vp), ('sub', u64), ('x', vp)]
+
+
 STRUCTS = [Stat, Groups, ConvDesc, CodecCtx, ReduceItem, HeadDesc, GemmItem, RomDesc, ResidualDesc, AdamDesc,
-           VoQueryDesc, VoMomentsDesc, VoConditionDesc, VoPrecisionDesc]
+           VoQueryDesc, VoMomentsDesc, VoConditionDesc, VoPrecisionDesc, GpSampleDesc]
 
 # name -> (restype, argtypes)
 SIGNATURES = {
@@ -150,6 +156,8 @@ SIGNATURES = {
     'gpi_vo_condition': (C.c_int, [C.POINTER(VoConditionDesc), vp]),
     'gpi_vo_precision': (C.c_int, [C.POINTER(VoPrecisionDesc), vp]),
     'gpi_gauss_sample': (C.c_int, [vp, vp, vp, i64, i32, i32, vp, u64, vp, u64, vp]),
+    'gpi_gp_sample': (C.c_int, [C.POINTER(GpSampleDesc), vp]),
+    'gpi_predictive_scores': (C.c_int, [vp, vp, vp, i32, i32, vp, vp]),
 }
 
 _LIB = None

@@ -1,0 +1,171 @@
+"""Native monitoring / validation paths around the ELBO step.
+
+PredictionEnsembleEngine -- PredictionEnsemble.update (components.py:365-388), the
+    decoder-only ELBO of the validation set with its own Adam, called 3x per step by
+    training.py:419.  It is the ElboEngine with a single hold-off variational segment
+    (q_z sample -> latent map -> decoder with fused Gaussian log-lik -> KL), run on a
+    private flat buffer: [shadow copy of the decoder weights | the ensemble's q_z]; the
+    shadow is refreshed from the model with one device copy per update, and Adam
+    (gpi_adam) updates the q_z rows only.  The decoder weight gradients the reference
+    leaves in f.*.grad (cleared by the trainer's next zero_grad) are not delivered.
+
+predictive_y -- Analysis.sample_predictive_y for every sample at once
+    (components.py:472-478,493-524): q_z draws -> gp mean (+ exp(logsigma_X) noise)
+    (gpi_gp_sample) -> ROM coarse solves (gpi_rom) -> mean / std of W u + exp(logsigma_y)
+    eps (gpi_vo_moments), i.e. N * N_mc MC samples in three launches instead of a
+    Python loop of N ROM calls; predictive_scores -> relerr / logscore / R^2 sums.
+"""
+import copy
+import ctypes as C
+
+import torch
+
+from . import _lib as L
+from . import vo as V
+from .engine import ElboEngine, rom_call, ROM_NN
+from .flat import FlatParameters
+
+
+def _p(t):
+    return t.data_ptr() if t is not None else None
+
+
+def host_seed():
+    return int(torch.randint(0, 2 ** 62, (1,)).item())
+
+
+# ---------------------------------------------------------------- predictive y
+def predictive_y(model, q_mean, q_logsigma, F, N_mc, eps=None, seed=None):
+    """(mean, std) [N, d_y] of the MC predictive y of every row of q (Analysis.eval_all_y).
+    eps (optional, injected): (eps_z [N*N_mc, d_z], eps_x [N*N_mc, d_x], eps_y [N*N_mc, d_y])."""
+    for t in (q_mean, q_logsigma, F):
+        L.require_device(t)
+    gp, g = model.gp, model.g
+    N, dz = q_mean.shape
+    dx = g.dim_effective_property
+    rom = g.rom
+    rows = N * int(N_mc)
+    dev = q_mean.device
+    seed = host_seed() if seed is None else seed
+    x = torch.empty(rows, dx, dtype=torch.float32, device=dev)
+    w, b = gp.fc.weight.detach().contiguous(), gp.fc.bias.detach().contiguous()
+    assert w.shape == (dx, dz)
+    ls = gp.logsigmas_X.detach().contiguous() if gp.independent_X else None
+    d = L.GpSampleDesc(rows=rows, rep=int(N_mc), d_z=dz, d_x=dx, qz_mu=_p(q_mean.detach().contiguous()),
+                       qz_ls=_p(q_logsigma.detach().contiguous()), gp_w=_p(w), gp_b=_p(b), gp_ls=_p(ls),
+                       eps_z=_p(eps[0]) if eps is not None else None, eps_x=_p(eps[1]) if eps is not None else None,
+                       seed=seed, offset=None, sub=21, x=_p(x))
+    keep = (q_mean, q_logsigma, w, b, ls)
+    L.check(L.lib().gpi_gp_sample(C.byref(d), L.stream_handle()), 'gp sample')
+    F_mc = F.float().repeat_interleave(int(N_mc), 0).contiguous()
+    uc = torch.empty(rows, ROM_NN(rom.nc), dtype=torch.float32, device=dev)
+    rom_call(rom.nc, rom.refine, x, F_mc, False, L.ROM_FORWARD, uc=uc)
+    mean, std, _ = V.vo_moments(uc, rom.nc, rom.refine, N, int(N_mc), logsig_y=g.logsigmas_y.detach().contiguous(),
+                                eps=eps[2] if eps is not None else None, seed=seed, sub=23)
+    del keep
+    return mean, std
+
+
+def predictive_scores(Y, mean, std):
+    """(mean relerr, mean logscore, R^2) -- Analysis.eval_all_y's three numbers (host sync)."""
+    for t in (Y, mean, std):
+        L.require_device(t)
+        assert t.dtype == torch.float32 and t.is_contiguous()
+    N, dy = Y.shape
+    out = torch.empty(3, dtype=torch.float64, device=Y.device)
+    L.check(L.lib().gpi_predictive_scores(_p(Y), _p(mean), _p(std), N, dy, _p(out), L.stream_handle()),
+            'predictive scores')
+    o = out.cpu()
+    return float(o[0]) / N, float(o[1]) / N, float(o[2]) / dy
+
+
+# ---------------------------------------------------------------- prediction ensemble
+class _EngineModel(object):
+    """The attributes ElboEngine reads from a GenerativeModel."""
+
+    def __init__(self, f, gp, g, q_z, flat):
+        self.f, self.gp, self.g = f, gp, g
+        self.encoder = None
+        self.q_z = {'vo': q_z}
+        self.q_X = {'vo': None}
+        self._flat = flat
+
+
+class PredictionEnsembleEngine(object):
+
+    def __init__(self, model, q_z, X, lr_source, betas=(0.9, 0.999), eps=1e-8):
+        L.require_device(X)
+        self.model = model
+        self.q_z = q_z
+        self.X = X.detach().contiguous().float()
+        self.N = self.X.shape[0]
+        self.shadow = copy.deepcopy(model.f)
+        self._src = [p for _, p in model.f.named_parameters()]
+        named = [('f.' + n, p) for n, p in self.shadow.named_parameters()] + \
+                [('q.' + n, p) for n, p in q_z.named_parameters()]
+        dev = X.device
+        self.flat = FlatParameters(named, dev)
+        self.n_dec = sum(p.numel() for p in self._src)
+        self.q_off = min(self.flat.offset(q_z._mean), self.flat.offset(q_z._logsigma))
+        self.q_n = self.flat.numel - self.q_off
+        assert self.q_off == self.n_dec and self.q_n == 2 * q_z._mean.numel()
+        em = _EngineModel(self.shadow, model.gp, model.g, q_z, self.flat)
+        self.engine = ElboEngine(em, 0, 0, N_vo=self.N, vo_holdoff=True)
+        self.engine.bind(X_vo=self.X)
+        self.m = torch.zeros(self.q_n, dtype=torch.float32, device=dev)
+        self.v = torch.zeros_like(self.m)
+        self.step_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.lr = torch.zeros(1, dtype=torch.float32, device=dev)
+        self._lr_host = None
+        self._lr_source = lr_source
+        P, G = self.flat.P, self.flat.G
+        self.adam = L.AdamDesc(p=P.data_ptr() + 4 * self.q_off, g=G.data_ptr() + 4 * self.q_off, m=self.m.data_ptr(),
+                               v=self.v.data_ptr(), n=self.q_n, lr=self.lr.data_ptr(), step=self.step_ctr.data_ptr(),
+                               beta1=betas[0], beta2=betas[1], eps=eps)
+        self.seed = host_seed()
+        self.rng_off = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.adam.rng_offset = self.rng_off.data_ptr()
+        self.adam.rng_advance = (self.N * self.engine.dz + 3) // 4 + 1
+
+    def _sync_decoder(self):
+        src_flat = getattr(self.model.f, '_gpi_flat', None)
+        if src_flat is not None and all(src_flat.owns(p) for p in self._src):
+            o = src_flat.offset(self._src[0])
+            if all(src_flat.offset(p) == o + k for p, k in zip(self._src, self._cum())):
+                self.flat.P[:self.n_dec].copy_(src_flat.P[o:o + self.n_dec])
+                return
+        with torch.no_grad():
+            for d, s in zip(self.shadow.parameters(), self._src):
+                d.copy_(s)
+
+    def _cum(self):
+        out, c = [], 0
+        for p in self._src:
+            out.append(c)
+            c += p.numel()
+        return out
+
+    def _sync_lr(self):
+        lr = float(self._lr_source())
+        if lr != self._lr_host:
+            self.lr.fill_(lr)
+            self._lr_host = lr
+
+    def update(self, eps=None):
+        """One PredictionEnsemble iteration; returns (elbo, logL, KLD) device scalars (no host sync)."""
+        lib, st = L.lib(), L.stream_handle()
+        self._sync_decoder()
+        self._sync_lr()
+        ez = self.engine.eps_z()
+        if eps is not None:
+            ez.copy_(eps)
+        else:
+            L.check(lib.gpi_randn(L.ptr(ez), ez.numel(), self.seed, L.ptr(self.rng_off), 5, st), 'randn pe')
+        self.engine.forward(st, compute_value=False)
+        t = self.engine.ws.terms
+        from .engine import T_LX0, T_KL_Q2
+        logL, kld = t[T_LX0].float(), t[T_KL_Q2].float()
+        self.engine.backward(st)
+        self.engine.finalize(self.flat.G, step=self.step_ctr, stream=st, zero_acc=True)
+        L.check(lib.gpi_adam(C.byref(self.adam), st), 'pe adam')
+        return logL - kld, logL, kld

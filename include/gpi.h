@@ -309,6 +309,35 @@ typedef struct gpi_vo_precision_desc {
     double* vo_var;            /* [m] out (mean VO variances) */
 } gpi_vo_precision_desc;
 
+/* Predictive effective properties (Analysis.sample_predictive_y's first two stages,
+ * components.py:472-478 + EffectivePropertyMap.propagate_samples :238-249): for row r,
+ * j = r / rep,  z = qz_mu[j] + exp(qz_ls[j]) eps_z,  x = gp_w z + gp_b (+ exp(gp_ls) eps_x when
+ * gp_ls != NULL, independent_X).  Normals from Philox (counter *offset + r * dim + t; streams
+ * sub, sub + 1) unless eps_z / eps_x are given.  Parameters are plain device pointers. */
+typedef struct gpi_gp_sample_desc {
+    int32_t rows, rep, d_z, d_x;
+    const float* qz_mu;        /* [rows / rep, d_z] */
+    const float* qz_ls;
+    const float* gp_w;         /* [d_x, d_z] */
+    const float* gp_b;         /* [d_x] */
+    const float* gp_ls;        /* [d_x] or NULL */
+    const float* eps_z;        /* optional [rows, d_z] */
+    const float* eps_x;        /* optional [rows, d_x] */
+    uint64_t seed;
+    const uint64_t* offset;
+    uint64_t sub;
+    float* x;                  /* [rows, d_x] out */
+} gpi_gp_sample_desc;
+
+/* Predictive scores of Analysis.eval_all_y (components.py:493-524): per sample n
+ *   relerr_n   = |mean_n - Y_n| / |Y_n|                             (bottleneck/utils.py relative_error)
+ *   logscore_n = mean_p [-log std - (Y - mean)^2 / (2 std^2) - log(2 pi) / 2]
+ * and per output p (lamp/utils.py:5-20, global_average = False)
+ *   r2_p = 1 - sum_n (Y - mean)^2 / sum_n (Y - Ybar_p)^2.
+ * out[0] = sum_n relerr_n, out[1] = sum_n logscore_n, out[2] = sum_p r2_p (fp64; caller divides). */
+int gpi_predictive_scores(const float* Y, const float* mean, const float* std, int32_t n, int32_t d_y,
+                          double* out, void* stream);
+
 /* Flat Adam (torch.optim.Adam semantics, no weight decay / amsgrad),
  * training.py:254,417.  step and lr are read from device memory so the
  * update can be replayed from a captured graph. */
@@ -353,6 +382,7 @@ int gpi_vo_precision(const gpi_vo_precision_desc* d, void* stream);
 /* Reparametrised Gaussian rows (bottleneck/utils.py:216-219, components.py:174-180):
  * out[r, t] = mean[r / rep, t] + exp(logsigma[r / rep, t]) * N(0,1), normals from
  * Philox counter (*offset + r * dim + t) in stream `sub` (or eps[r, t] if eps != NULL). */
+int gpi_gp_sample(const gpi_gp_sample_desc* d, void* stream);
 int gpi_gauss_sample(float* out, const float* mean, const float* logsigma, int64_t rows, int32_t dim, int32_t rep,
                      const float* eps, uint64_t seed, const uint64_t* offset, uint64_t sub, void* stream);
 

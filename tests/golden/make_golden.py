@@ -20,6 +20,8 @@ Outputs (small .npz, float32 unless noted) -- inputs, outputs and gradients:
   vo_elbo_c32.npz                 GenerativeModel.update_virtual_observables (x2, CGR + flux
                                   queries through the reference's own sampler / LinearQuerry /
                                   VirtualObservablesEnsemble classes) + elbo with the VO term + bwd
+  pe_analysis_c32.npz             PredictionEnsemble.update (3 iterations, own Adam) and
+                                  Analysis.eval_all_y (relerr / logscore / R^2)
   terms.npz                       DGLL / KL known values
 """
 import os
@@ -45,6 +47,7 @@ import bottleneck.ROM as R_ROM                # noqa: E402
 import bottleneck.components as R_comp        # noqa: E402
 import bottleneck.generative as R_gen         # noqa: E402
 import bottleneck.VirtualObservables as R_VO  # noqa: E402
+import lamp.optimization as R_opt             # noqa: E402
 from bottleneck.Encoder import CNNEncoder     # noqa: E402
 from bottleneck.Decoder import CNNDecoder     # noqa: E402
 
@@ -461,6 +464,97 @@ def make_vo_elbo():
     return elbo
 
 
+def make_pe_analysis():
+    nc, r, mc, mf, M, W, cdofs, fdofs = c32_physics()
+    n = nc * r
+    rng = np.random.default_rng(10)
+    Nval, dz, Nmc, iters = 5, 16, 6, 3
+    torch.manual_seed(0)
+    gen = torch.Generator().manual_seed(11)
+    dec = CNNDecoder(n, dz, (8, 8), 1, 4, [1, 1], False, 4, drop_rate=0., upsample='nearest',
+                     force_single_output=False, homoscedastic=False)
+    randomize_bn(dec, gen)
+    rom = R_ROM.ROM(_Phys(cdofs, fdofs), torch.tensor(M, dtype=torch.float32), torch.float32, 'cpu')
+    g = R_comp.ReducedOrderModelOperator(rom, torch.tensor(W, dtype=torch.float32), dtype=torch.float32,
+                                         device='cpu')
+    gp = R_comp.EffectivePropertyMap(dz, M.shape[2], num_hidden_layers=0, independent_X=True,
+                                     dtype=torch.float32, device='cpu')
+    model = R_gen.GenerativeModel(f=dec, g=g, gp=gp, dtype=torch.float32, device='cpu')
+    with torch.no_grad():
+        g.logsigmas_y.copy_(torch.tensor(rng.normal(-2.0, 0.2, g.logsigmas_y.shape)))
+        gp.logsigmas_X.copy_(torch.tensor(rng.normal(-1.0, 0.2, gp.logsigmas_X.shape)))
+    img = random_fields(rng, Nval, n)
+    U = rng.uniform(-0.5, 0.5, (Nval, 4))
+    Y = np.stack([fem.solve_fom(mf, np.exp(fem.image_to_cells(x)), u) for x, u in zip(img, U)])
+    F = np.stack([fem.f_rom_bc(mc, u) for u in U])
+    t32 = lambda a: torch.tensor(a, dtype=torch.float32)
+    ds = _DS(X=t32(img), Y=t32(Y), F_ROM_BC=t32(F))
+    ds.label = 'validation'
+
+    class _Writer(object):
+        def __init__(self):
+            self.d = {}
+
+        def add_scalar(self, k, v, global_step=None):
+            self.d[k] = float(v)
+
+    state0 = {k: v.detach().cpu().numpy().copy() for k, v in model.state_dict().items()}
+    pe = R_comp.PredictionEnsemble(model, ds, R_opt.LearningScheduleWrapper.Dummy(), lr=1e-2, writer=_Writer())
+    eps = [torch.tensor(rng.normal(size=(Nval, dz)), dtype=torch.float32) for _ in range(iters)]
+    queue = list(eps)
+
+    def fake_randn_like(t, *a, **k):
+        e = queue.pop(0)
+        assert e.shape == t.shape, (e.shape, t.shape)
+        return e
+
+    with mock.patch('torch.randn_like', fake_randn_like):
+        pe.update(numIter=iters, record=True, step=0)
+    assert not queue
+    pe_terms = dict(pe.writer.d)
+
+    # Analysis.eval_all_y on a spread-out q (the PE's q after 3 steps is still near the prior)
+    q = R_comp.VariationalApproximation(dz, Nval, t32(img))
+    with torch.no_grad():
+        q._mean.copy_(torch.tensor(rng.normal(0, 0.7, q._mean.shape)))
+        q._logsigma.copy_(torch.tensor(rng.normal(-1.5, 0.3, q._logsigma.shape)))
+    ez = rng.normal(size=(Nval, Nmc, dz))
+    ex = rng.normal(size=(Nval, Nmc, M.shape[2]))
+    ey = rng.normal(size=(Nval, Nmc, W.shape[0]))
+    qr = [torch.tensor(e, dtype=torch.float32) for e in ez]
+    ql = []
+    for i in range(Nval):
+        ql += [torch.tensor(ex[i], dtype=torch.float32), torch.tensor(ey[i], dtype=torch.float32)]
+
+    def fake_randn(*size, **k):
+        e = qr.pop(0)
+        assert tuple(e.shape) == tuple(size)
+        return e
+
+    def fake_randn_like2(t, *a, **k):
+        e = ql.pop(0)
+        assert e.shape == t.shape
+        return e
+
+    an = R_comp.Analysis(q, model, ds)
+    with mock.patch('torch.randn', fake_randn), mock.patch('torch.randn_like', fake_randn_like2):
+        logscore, r2, relerr = an.eval_all_y(Nmc)
+    assert not qr and not ql
+    out = {'state.' + k: v for k, v in state0.items()}
+    out.update(X=img.astype(np.float32), Y=Y.astype(np.float32), F=F.astype(np.float32), W=W.astype(np.float32),
+               cfg=np.array([n, nc, dz, Nval, Nmc, iters]), pe_eps=np.stack([e.numpy() for e in eps]),
+               pe_mean=pe.q_z._mean.detach().numpy(), pe_logsigma=pe.q_z._logsigma.detach().numpy(),
+               pe_elbo=np.float64(pe_terms['PredictionEnsemble/elbo']),
+               pe_logL=np.float64(pe_terms['PredictionEnsemble/logL']),
+               pe_KLD=np.float64(pe_terms['PredictionEnsemble/KLD']),
+               q_mean=q._mean.detach().numpy(), q_logsigma=q._logsigma.detach().numpy(),
+               an_eps_z=ez.reshape(Nval * Nmc, -1), an_eps_x=ex.reshape(Nval * Nmc, -1),
+               an_eps_y=ey.reshape(Nval * Nmc, -1), logscore=np.float64(logscore), r2=np.float64(r2),
+               relerr=np.float64(relerr))
+    np.savez_compressed(os.path.join(HERE, 'pe_analysis_c32.npz'), **out)
+    print('pe/analysis ok', pe_terms, logscore, r2, relerr)
+
+
 def make_terms():
     rng = np.random.default_rng(7)
     t = torch.tensor(rng.normal(size=(5, 7)))
@@ -479,3 +573,4 @@ if __name__ == '__main__':
     make_elbo()
     make_vo()
     make_vo_elbo()
+    make_pe_analysis()

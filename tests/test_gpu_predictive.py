@@ -1,0 +1,97 @@
+"""GPU parity of the monitoring / validation paths: the native
+PredictionEnsemble.update (decoder-only ELBO + Adam on the validation q_z) and the batched
+Analysis.eval_all_y, against the reference run recorded in pe_analysis_c32.npz
+(injected noise).  Tolerances: q_z after 3 Adam steps 1e-4 relative, ELBO terms 2e-5,
+predictive scores 1e-4."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), 'golden')
+
+
+def load(name):
+    return dict(np.load(os.path.join(GOLD, name), allow_pickle=False))
+
+
+def cuda(a, dtype=torch.float32):
+    return torch.tensor(np.asarray(a), dtype=dtype, device='cuda')
+
+
+def rel(a, b):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    return np.abs(a - b).max() / max(np.abs(b).max(), 1e-30)
+
+
+class _DS(object):
+    label = 'validation'
+
+    def __init__(self, **t):
+        self.t = t
+        self.N = next(iter(t.values())).shape[0]
+
+    def __bool__(self):
+        return True
+
+    def get(self, key, random_subset=None):
+        return self.t[key]
+
+
+class _Writer(object):
+    def __init__(self):
+        self.d = {}
+
+    def add_scalar(self, k, v, global_step=None):
+        self.d[k] = float(v)
+
+
+def build(d):
+    from bottleneck.Decoder import CNNDecoder
+    from bottleneck.components import EffectivePropertyMap, ReducedOrderModelOperator
+    from bottleneck.ROM import ROM
+    from bottleneck.generative import GenerativeModel
+    from physics.grid import StructuredGrid
+    n, nc, dz, Nval, Nmc, iters = [int(v) for v in d['cfg']]
+    dec = CNNDecoder(n, dz, (8, 8), 1, 4, [1, 1], False, 4, drop_rate=0.)
+    rom = ROM(StructuredGrid(nc), n // nc)
+    g = ReducedOrderModelOperator(rom, torch.tensor(d['W']), dtype=torch.float32, device='cuda')
+    gp = EffectivePropertyMap(dz, 2 * nc * nc, dtype=torch.float32, device='cuda')
+    model = GenerativeModel(f=dec.cuda(), g=g, gp=gp, dtype=torch.float32, device=torch.device('cuda'))
+    model.load_state_dict({k[6:]: torch.tensor(v) for k, v in d.items() if k.startswith('state.')})
+    model.cuda()
+    ds = _DS(X=cuda(d['X']), Y=cuda(d['Y']), F_ROM_BC=cuda(d['F']))
+    return model, ds
+
+
+def test_prediction_ensemble_update(device):
+    from bottleneck.components import PredictionEnsemble
+    from lamp.optimization import LearningScheduleWrapper
+    d = load('pe_analysis_c32.npz')
+    model, ds = build(d)
+    pe = PredictionEnsemble(model, ds, LearningScheduleWrapper.Dummy(), lr=1e-2, writer=_Writer())
+    iters = int(d['cfg'][5])
+    pe.update(numIter=iters, record=True, step=0, eps=[cuda(e) for e in d['pe_eps']])
+    w = pe.writer.d
+    for k in ('elbo', 'logL', 'KLD'):
+        ref = float(d['pe_' + k])
+        assert abs(w['PredictionEnsemble/' + k] - ref) <= 2e-5 * max(abs(ref), 1.0), (k, w, ref)
+    assert rel(pe.q_z.mean.detach().cpu(), d['pe_mean']) < 1e-4
+    assert rel(pe.q_z.logsigma.detach().cpu(), d['pe_logsigma']) < 1e-4
+
+
+def test_analysis_eval_all_y(device):
+    from bottleneck.components import Analysis, VariationalApproximation
+    d = load('pe_analysis_c32.npz')
+    model, ds = build(d)
+    n, nc, dz, Nval, Nmc, iters = [int(v) for v in d['cfg']]
+    q = VariationalApproximation(dz, Nval, ds.get('X'))
+    q.init(cuda(d['q_mean']), cuda(d['q_logsigma']))
+    an = Analysis(q, model, ds)
+    logscore, r2, relerr = an.eval_all_y(Nmc, eps=(cuda(d['an_eps_z']), cuda(d['an_eps_x']), cuda(d['an_eps_y'])))
+    assert abs(logscore - float(d['logscore'])) <= 1e-4 * abs(float(d['logscore']))
+    assert abs(r2 - float(d['r2'])) <= 1e-4 * abs(float(d['r2']))
+    assert abs(relerr - float(d['relerr'])) <= 1e-4 * abs(float(d['relerr']))
