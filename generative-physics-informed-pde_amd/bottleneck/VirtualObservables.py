@@ -14,10 +14,11 @@ updated by gpi_vo_precision + gpi_vo_condition in one launch set; the
 per-sample objects hold views of it.  No host synchronisation, no CPU
 fallback (gpi/_lib.py raises without a GPU).
 
-Samplers on the native path: CoarseGrainedResidualSampler (infinite
-precision rows) and FluxConstrainSampler (learnable precision rows), alone or
-concatenated in the reference's order.  GaussianSketchingSampler /
-RadialBasisFunctionSampler and the energy VOs are not native yet and raise.
+Samplers on the native path, concatenated in the reference's order:
+CoarseGrainedResidualSampler (infinite precision), FluxConstrainSampler
+(learnable precision), GaussianSketchingSampler and RadialBasisFunctionSampler
+(infinite precision, test functions redrawn on the device at every resample).
+The energy VOs (host numpy loops in the reference) are not native and raise.
 """
 import numpy as np
 import torch
@@ -32,6 +33,11 @@ BETA0 = V.BETA0
 def _grid_sizes(physics):
     """(n_fine, nc) of a physics dict {'fom', 'rom', 'W'} or of a fom physics + W."""
     return physics['fom'].grid.n, physics['rom'].grid.n
+
+
+def _host_seed():
+    # device Philox seeded from torch's CPU generator (torch.manual_seed reproducible, no device sync)
+    return int(torch.randint(0, 2 ** 62, (1,)).item())
 
 
 def _same_device(a, b):
@@ -266,18 +272,63 @@ class FluxConstrainSampler(BaseSampler):
         raise NotImplementedError
 
 
-class GaussianSketchingSampler(BaseSampler):
-    """V ~ N(0, 1) test functions (VirtualObservables.py:230-258): not on the native path yet."""
+class _TestFunctionSampler(BaseSampler):
+    """Galerkin rows V^T K_ff / V^T f_eff from random test functions, redrawn on every resample
+    (not constant), infinite precision.  V is drawn on the device (gpi_vo_galerkin)."""
 
-    def __init__(self, qp, N_aux):
-        raise NotImplementedError('GaussianSketchingSampler is not on the native path yet')
+    kind = None
+
+    def __init__(self, qp, N_aux, length=0.0, device=None):
+        super().__init__(qp=qp)
+        self._N = int(N_aux)
+        self._length = float(length)
+        self._device = device if device is not None else torch.device('cuda')
+
+    @property
+    def m(self):
+        return self._N
+
+    @property
+    def is_constant(self):
+        return False
+
+    @property
+    def precision_mask(self):
+        return -np.ones(self.m)
+
+    def sample(self):
+        qp = self._qp
+        n = int(round(np.sqrt(qp.dim_in / 2)))
+        x = torch.tensor(qp.x, dtype=torch.float64, device=self._device).view(1, -1)
+        u = torch.tensor(qp.u, dtype=torch.float64, device=self._device).view(1, 4)
+        dy = (n + 1) * (n - 1)
+        g = torch.empty(1, self._N, dy, dtype=torch.float64, device=self._device)
+        a = torch.empty(1, self._N, dtype=torch.float64, device=self._device)
+        V.vo_galerkin(g, a, 0, self._N, x, u, n, self.kind, length=self._length, seed=_host_seed())
+        return g[0], a[0]
+
+    def _sample(self):
+        raise NotImplementedError('test functions are drawn on the device and not materialised')
 
 
-class RadialBasisFunctionSampler(BaseSampler):
-    """RBF test functions (VirtualObservables.py:172-228): not on the native path yet."""
+class GaussianSketchingSampler(_TestFunctionSampler):
+    """V ~ N(0, 1) on the free nodes (VirtualObservables.py:230-258)."""
 
-    def __init__(self, qp, l, N_aux):
-        raise NotImplementedError('RadialBasisFunctionSampler is not on the native path yet')
+    kind = L.VO_TEST_GAUSS
+
+    def __init__(self, qp, N_aux, device=None):
+        super().__init__(qp, N_aux, device=device)
+
+
+class RadialBasisFunctionSampler(_TestFunctionSampler):
+    """V = exp(-|x - r0|^2 / l^2) at the free nodes, r0 ~ U(0,1)^2 per test function
+    (VirtualObservables.py:172-228, fawkes/Expressions.py:26-31)."""
+
+    kind = L.VO_TEST_RBF
+
+    def __init__(self, qp, l, N_aux, device=None):
+        assert l is not None
+        super().__init__(qp, N_aux, length=l() if callable(l) else l, device=device)
 
 
 class ConcatenatedSamplers(BaseSampler):
@@ -318,9 +369,10 @@ class ConcatenatedSamplers(BaseSampler):
 class LinearQuerry(object):
     """Gamma / alpha of one VO sample (VirtualObservables.py:353-448); fp64 device tensors."""
 
-    def __init__(self, querry_point, sampler, dtype, device, Gamma=None, alpha=None):
+    def __init__(self, querry_point, sampler, dtype, device, Gamma=None, alpha=None, ensemble=None, index=None):
         self._sampler = sampler
         self._querry_point = querry_point
+        self._ensemble, self._index = ensemble, index
         self._Gamma = None
         self._GammaTransposed = None
         self._alpha = None
@@ -372,6 +424,11 @@ class LinearQuerry(object):
         return self.Gamma.shape[0]
 
     def resample(self, ForceResample=False):
+        if self._ensemble is not None:
+            # rows live in the ensemble's batched layout: redraw this sample's random rows in place
+            if not self._sampler.is_constant:
+                self._ensemble._draw_aux(index=self._index)
+            return
         if not self._sampler.is_constant or ForceResample:
             Gamma, alpha = self._sampler()
             self.Gamma = torch.as_tensor(Gamma, dtype=torch.double, device=self.device)
@@ -403,6 +460,7 @@ class QuerryEnsemble(object):
         self._device = device
         self._gamma = gamma
         self._alpha = alpha
+        self._aux = []
 
     def __len__(self):
         return len(self._querries)
@@ -441,8 +499,19 @@ class QuerryEnsemble(object):
         return self._alpha
 
     def resample(self, ForceResample=False):
+        if self._aux:
+            self._draw_aux()
+            return
         for q in self:
             q.resample(ForceResample=ForceResample)
+
+    def _draw_aux(self, index=None):
+        """Redraw the test-function rows (Gaussian sketch / RBF) of all samples, or of one, on the device."""
+        x, u = self._qpe.device_batch(self._device)
+        sl = slice(None) if index is None else slice(index, index + 1)
+        g, a = self._gamma[sl], self._alpha[sl]
+        for row0, m_aux, kind, length in self._aux:
+            V.vo_galerkin(g, a, row0, m_aux, x[sl], u[sl], self._n_fine, kind, length=length, seed=_host_seed())
 
     @property
     def dim_out(self):
@@ -457,8 +526,8 @@ class QuerryEnsemble(object):
     @classmethod
     def FromQuerryPointEnsemble(cls, QuerryPointEnsemble, physics, CGR, flux, N_gaussian, N_rbf, l_rbf=None, *,
                                 dtype=None, device=None):
-        """VirtualObservables.py:498-543: sampler rows CGR, flux (, Gaussian, RBF) per VO sample,
-        assembled for the whole ensemble by ONE gpi_vo_query launch."""
+        """VirtualObservables.py:498-543: sampler rows CGR, flux, Gaussian sketch, RBF per VO sample,
+        assembled for the whole ensemble in one launch per sampler kind."""
         assert isinstance(physics, dict)
         W = physics['W']
         if W is None:
@@ -466,29 +535,51 @@ class QuerryEnsemble(object):
         assert W.shape[0] > W.shape[1]
         assert dtype is not None
         assert device is not None
-        if N_gaussian > 0 or N_rbf > 0:
-            raise NotImplementedError('Gaussian-sketch / RBF test functions are not on the native path yet')
-        if not (CGR or flux):
-            raise ValueError('no sampler selected')
+        if N_rbf > 0:
+            assert l_rbf is not None
         n_fine, nc = _grid_sizes(physics)
+        dy = (n_fine + 1) * (n_fine - 1)
         flags = (L.VO_CGR if CGR else 0) | (L.VO_FLUX if flux else 0)
+        m0 = V.vo_rows(n_fine, nc, flags) if flags else 0
+        m = m0 + N_gaussian + N_rbf
+        if m == 0:
+            raise ValueError('no sampler selected')
         x, u = QuerryPointEnsemble.device_batch(device)
-        gamma, alpha = V.vo_query(x, u, n_fine, nc, flags)
+        N = len(QuerryPointEnsemble)
+        gamma = torch.empty(N, m, dy, dtype=torch.float64, device=device)
+        alpha = torch.empty(N, m, dtype=torch.float64, device=device)
+        if m0:
+            g0, a0 = V.vo_query(x, u, n_fine, nc, flags)
+            gamma[:, :m0].copy_(g0)
+            alpha[:, :m0].copy_(a0)
+        aux = []
+        if N_gaussian > 0:
+            aux.append((m0, N_gaussian, L.VO_TEST_GAUSS, 0.0))
+        if N_rbf > 0:
+            aux.append((m0 + N_gaussian, N_rbf, L.VO_TEST_RBF, float(l_rbf() if callable(l_rbf) else l_rbf)))
         fluxconstr = None
         if flux:
             from bottleneck.flux import FluxConstraintReducedOrderModel
             fluxconstr = FluxConstraintReducedOrderModel(physics)
             fluxconstr.create_measures()
-        querries = []
+        ens = cls([], dtype=dtype, device=device, gamma=gamma, alpha=alpha)
+        ens._qpe, ens._n_fine, ens._aux = QuerryPointEnsemble, n_fine, aux
         for n, qp in enumerate(QuerryPointEnsemble):
             samplers = []
             if CGR:
                 samplers.append(CoarseGrainedResidualSampler(qp=qp, W=W, device=device))
             if flux:
                 samplers.append(FluxConstrainSampler(qp, fluxconstr, device=device))
+            if N_gaussian > 0:
+                samplers.append(GaussianSketchingSampler(qp=qp, N_aux=N_gaussian, device=device))
+            if N_rbf > 0:
+                samplers.append(RadialBasisFunctionSampler(qp=qp, l=l_rbf, N_aux=N_rbf, device=device))
             sampler = samplers[0] if len(samplers) == 1 else ConcatenatedSamplers(samplers)
-            querries.append(LinearQuerry(qp, sampler, dtype=dtype, device=device, Gamma=gamma[n], alpha=alpha[n]))
-        return cls(querries, dtype=dtype, device=device, gamma=gamma, alpha=alpha)
+            ens._querries.append(LinearQuerry(qp, sampler, dtype=dtype, device=device, Gamma=gamma[n],
+                                              alpha=alpha[n], ensemble=ens, index=n))
+        if aux:
+            ens._draw_aux()
+        return ens
 
 
 # ---------------------------------------------------------------------------
@@ -740,6 +831,9 @@ class VirtualObservablesEnsemble(BaseVirtualObservablesEnsemble):
         self._has_posterior = True
         self._bind_members()
         self.flush_cache()
+
+    def resample(self, ForceResample=False):
+        self._QuerryEnsemble.resample(ForceResample=ForceResample)
 
     def check_flag(self):
         """Lazy replacement of torch.cholesky's error (host sync)."""

@@ -201,6 +201,75 @@ __global__ __launch_bounds__(64) void vo_query_flux(gpi_vo_query_desc d, FineGri
     }
 }
 
+
+// ---------------------------------------------------------------- Galerkin rows from test functions
+__device__ __forceinline__ double test_value(const gpi_vo_galerkin_desc& d, int f, int a, int p, int n,
+                                             uint64_t base, double cx, double cy) {
+    const int dy = (n + 1) * (n - 1);
+    if (d.V) return d.V[((int64_t)f * d.m_aux + a) * dy + p];
+    if (d.kind == GPI_VO_TEST_GAUSS) {
+        const uint4_ q = philox(base + (uint64_t)(((int64_t)f * d.m_aux + a) * dy + p), d.sub, d.seed);
+        const double u0 = ((double)q.x + 1.0) * 2.3283064365386963e-10;   // (0, 1]
+        const double u1 = (double)q.y * 2.3283064365386963e-10;
+        return sqrt(-2.0 * log(u0)) * cos(6.283185307179586 * u1);
+    }
+    const int jj = p / (n - 1), ii = p - jj * (n - 1) + 1;
+    const double x = (double)ii / n - cx, y = (double)jj / n - cy;
+    return exp(-(x * x + y * y) / (d.length * d.length));
+}
+
+__device__ __forceinline__ void rbf_center(const gpi_vo_galerkin_desc& d, int f, int a, uint64_t base, double& cx,
+                                           double& cy) {
+    if (d.centers) {
+        cx = d.centers[((int64_t)f * d.m_aux + a) * 2];
+        cy = d.centers[((int64_t)f * d.m_aux + a) * 2 + 1];
+    } else {
+        // a separate counter range (above every Gaussian counter) for the centres
+        const uint4_ q = philox(base + ((uint64_t)1 << 62) + (uint64_t)((int64_t)f * d.m_aux + a), d.sub, d.seed);
+        cx = (double)q.x * 2.3283064365386963e-10;
+        cy = (double)q.y * 2.3283064365386963e-10;
+    }
+}
+
+__global__ __launch_bounds__(256) void vo_galerkin_kernel(gpi_vo_galerkin_desc d) {
+    __shared__ double red[4];
+    const int a = blockIdx.y, f = blockIdx.z;
+    const int n = d.n_fine, dy = (n + 1) * (n - 1);
+    const double* lk = d.logkappa + (int64_t)f * 2 * n * n;
+    const uint64_t base = d.offset ? *d.offset : 0;
+    double cx = 0.0, cy = 0.0;
+    if (d.kind == GPI_VO_TEST_RBF) rbf_center(d, f, a, base, cx, cy);
+    const int p = blockIdx.x * 256 + threadIdx.x;
+    if (p < dy) {
+        const int jj = p / (n - 1), ii = p - jj * (n - 1) + 1;
+        const double chl = ch_(lk, n, ii - 1, jj), chr = ch_(lk, n, ii, jj);
+        const double cvd = jj > 0 ? cv_(lk, n, ii, jj - 1) : 0.0;
+        const double cvu = jj < n ? cv_(lk, n, ii, jj) : 0.0;
+        double g = (chl + chr + cvd + cvu) * test_value(d, f, a, p, n, base, cx, cy);
+        if (ii > 1) g -= chl * test_value(d, f, a, p - 1, n, base, cx, cy);
+        if (ii < n - 1) g -= chr * test_value(d, f, a, p + 1, n, base, cx, cy);
+        if (jj > 0) g -= cvd * test_value(d, f, a, p - (n - 1), n, base, cx, cy);
+        if (jj < n) g -= cvu * test_value(d, f, a, p + (n - 1), n, base, cx, cy);
+        d.gamma[((int64_t)f * d.m + d.row0 + a) * dy + p] = g;
+    }
+    if (blockIdx.x != 0) return;
+    // alpha = V_a . f_eff: only the free nodes next to x = 0 / x = 1 carry f_eff
+    const double* u = d.bc + 4 * f;
+    double s = 0.0;
+    for (int e = threadIdx.x; e < 2 * (n + 1); e += 256) {
+        const int side = e / (n + 1), jj = e - side * (n + 1);
+        if (n == 2 && side == 1) continue;
+        const int ii = side == 0 ? 1 : n - 1;
+        double fe = ch_(lk, n, side == 0 ? 0 : n - 1, jj) * bc_value(u, side == 0 ? 0 : n, jj, n);
+        if (n == 2) fe += ch_(lk, n, n - 1, jj) * bc_value(u, n, jj, n);
+        s += fe * test_value(d, f, a, jj * (n - 1) + ii - 1, n, base, cx, cy);
+    }
+    s = wave_sum_d(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) d.alpha[(int64_t)f * d.m + d.row0 + a] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
 // ---------------------------------------------------------------- MC predictive moments
 constexpr int MOM_CH = 64;   // MC samples staged in LDS per chunk
 
@@ -669,6 +738,19 @@ extern "C" int gpi_predictive_scores(const float* Y, const float* mean, const fl
     hipLaunchKernelGGL(scores_rows_kernel, dim3(n), dim3(256), 0, st, Y, mean, std, d_y, out);
     GPI_CHECK_LAUNCH();
     hipLaunchKernelGGL(scores_cols_kernel, dim3((d_y + 255) / 256), dim3(256), 0, st, Y, mean, n, d_y, out);
+    GPI_CHECK_LAUNCH();
+    return GPI_OK;
+}
+
+extern "C" int gpi_vo_galerkin(const gpi_vo_galerkin_desc* d, void* stream) {
+    if (!d || !d->logkappa || !d->bc || !d->gamma || !d->alpha || d->n < 0 || d->n_fine < 2 || d->m_aux < 1 ||
+        d->row0 < 0 || d->row0 + d->m_aux > d->m || (d->kind != GPI_VO_TEST_GAUSS && d->kind != GPI_VO_TEST_RBF) ||
+        (d->kind == GPI_VO_TEST_RBF && !d->V && !(d->length > 0.0)))
+        return GPI_ERR_ARG;
+    if (d->n == 0) return GPI_OK;
+    const int dy = (d->n_fine + 1) * (d->n_fine - 1);
+    hipLaunchKernelGGL(vo_galerkin_kernel, dim3((dy + 255) / 256, d->m_aux, d->n), dim3(256), 0, (hipStream_t)stream,
+                       *d);
     GPI_CHECK_LAUNCH();
     return GPI_OK;
 }

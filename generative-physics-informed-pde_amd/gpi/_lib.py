@@ -27,6 +27,7 @@ EPI_STORE, EPI_STORE_STATS, EPI_GAUSS_LOSS = 0, 1, 2
 HEAD_ENC, HEAD_REPARAM, HEAD_QZ, HEAD_LATENT, HEAD_GP = 0x01, 0x02, 0x04, 0x08, 0x10
 ROM_FORWARD, ROM_LOGLIK, ROM_BACKWARD = 0, 1, 2
 VO_CGR, VO_FLUX = 0x1, 0x2
+VO_TEST_GAUSS, VO_TEST_RBF = 0, 1
 
 i32, i64, f32, u64 = C.c_int32, C.c_int64, C.c_float, C.c_uint64
 vp = C.c_void_p
@@ -126,8 +127,15 @@ class GpSampleDesc(C.Structure):
                 ('seed', u64), ('offset', vp), ('sub', u64), ('x', vp)]
 
 
+class VoGalerkinDesc(C.Structure):
+    _fields_ = [('n_fine', i32), ('n', i32), ('m_aux', i32), ('kind', i32),
+                ('logkappa', vp), ('bc', vp), ('V', vp), ('centers', vp), ('length', C.c_double),
+                ('seed', u64), ('offset', vp), ('sub', u64), ('gamma', vp), ('alpha', vp), ('m', i32), ('row0', i32)]
+
+
 STRUCTS = [Stat, Groups, ConvDesc, CodecCtx, ReduceItem, HeadDesc, GemmItem, RomDesc, ResidualDesc, AdamDesc,
-           VoQueryDesc, VoMomentsDesc, VoConditionDesc, VoPrecisionDesc, GpSampleDesc]
+           VoQueryDesc, VoMomentsDesc, VoConditionDesc, VoPrecisionDesc, GpSampleDesc,
+           VoGalerkinDesc]
 
 # name -> (restype, argtypes)
 SIGNATURES = {
@@ -153,6 +161,7 @@ SIGNATURES = {
     'gpi_vo_rows': (C.c_int, [i32, i32, i32]),
     'gpi_vo_query': (C.c_int, [C.POINTER(VoQueryDesc), vp]),
     'gpi_vo_moments': (C.c_int, [C.POINTER(VoMomentsDesc), vp]),
+    'gpi_vo_galerkin': (C.c_int, [C.POINTER(VoGalerkinDesc), vp]),
     'gpi_vo_condition': (C.c_int, [C.POINTER(VoConditionDesc), vp]),
     'gpi_vo_precision': (C.c_int, [C.POINTER(VoPrecisionDesc), vp]),
     'gpi_gauss_sample': (C.c_int, [vp, vp, vp, i64, i32, i32, vp, u64, vp, u64, vp]),

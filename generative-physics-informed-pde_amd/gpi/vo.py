@@ -49,6 +49,28 @@ def vo_query(x_dg, bc, n_fine, nc, flags):
     return gamma, alpha
 
 
+def vo_galerkin(gamma, alpha, row0, m_aux, x_dg, bc, n_fine, kind, V=None, centers=None, length=0.0, seed=0,
+                sub=31):
+    """Rows row0 .. row0 + m_aux of gamma [N, m, d_y] / alpha [N, m] from test functions: given V
+    [N, m_aux, d_y] or drawn on the device (VO_TEST_GAUSS / VO_TEST_RBF)."""
+    _dev(gamma, alpha, x_dg, bc, V, centers)
+    N, m, dy = gamma.shape
+    assert dy == (n_fine + 1) * (n_fine - 1) and alpha.shape == (N, m) and 0 <= row0 and row0 + m_aux <= m
+    assert x_dg.shape == (N, 2 * n_fine * n_fine) and bc.shape == (N, 4)
+    assert gamma.dtype == torch.float64 and gamma.is_contiguous() and alpha.is_contiguous()
+    if V is not None:
+        assert V.shape == (N, m_aux, dy) and V.dtype == torch.float64
+        V = V.contiguous()
+    if centers is not None:
+        assert centers.shape == (N, m_aux, 2) and centers.dtype == torch.float64
+        centers = centers.contiguous()
+    x_dg, bc = x_dg.contiguous().double(), bc.contiguous().double()
+    d = L.VoGalerkinDesc(n_fine=n_fine, n=N, m_aux=m_aux, kind=kind, logkappa=_p(x_dg), bc=_p(bc), V=_p(V),
+                         centers=_p(centers), length=float(length), seed=seed, offset=None, sub=sub, gamma=_p(gamma),
+                         alpha=_p(alpha), m=m, row0=row0)
+    L.check(L.lib().gpi_vo_galerkin(C.byref(d), L.stream_handle()), 'vo galerkin')
+
+
 def vo_moments(uc, nc, refine, n, n_mc, logsig_y=None, eps=None, seed=0, offset=None, sub=7, want_std=True):
     """MC mean / std / precision of y_s = W u_s + exp(logsig_y) eps_s per VO sample
     (generative.py:198-207).  uc [n * n_mc, (nc+1)^2] fp32."""

@@ -251,6 +251,32 @@ typedef struct gpi_vo_query_desc {
     double* alpha;             /* [n, m] out */
 } gpi_vo_query_desc;
 
+/* Galerkin query rows from test functions V on the fine free nodes
+ * (QuerryPoint.construct_querry_weak_galerkin, VirtualObservables.py:61-69):
+ *   Gamma[row0 + a] = V_a^T K_ff  (= K_ff V_a, K symmetric),  alpha[row0 + a] = V_a^T f_eff,
+ * with V given, or drawn per (sample, a) as
+ *   GPI_VO_TEST_GAUSS  V ~ N(0, 1) i.i.d.       (GaussianSketchingSampler, :230-258)
+ *   GPI_VO_TEST_RBF    V_j = exp(-|x_j - r0|^2 / l^2), r0 ~ U(0,1)^2 per row
+ *                      (RadialBasisFunctionSampler + fawkes FastRadialBasisFunction, :172-228)
+ * from Philox (counter *offset + ((sample * m_aux + a) * d_y + j), stream sub) or `centers`. */
+#define GPI_VO_TEST_GAUSS 0
+#define GPI_VO_TEST_RBF   1
+
+typedef struct gpi_vo_galerkin_desc {
+    int32_t n_fine, n, m_aux, kind;
+    const double* logkappa;    /* [n, 2 n_fine^2] */
+    const double* bc;          /* [n, 4] */
+    const double* V;           /* optional [n, m_aux, d_y] test functions */
+    const double* centers;     /* optional [n, m_aux, 2] RBF centres */
+    double length;             /* RBF length scale l */
+    uint64_t seed;
+    const uint64_t* offset;
+    uint64_t sub;
+    double* gamma;             /* [n, m, d_y]: rows row0 .. row0 + m_aux - 1 written */
+    double* alpha;             /* [n, m] */
+    int32_t m, row0;
+} gpi_vo_galerkin_desc;
+
 /* MC predictive moments of the ROM (GenerativeModel.update_virtual_observables,
  * generative.py:198-207): for VO sample j and its n_mc coarse solutions u_s
  * (gpi_rom FORWARD with uc), y_s = W u_s + exp(logsig_y) eps_s
@@ -376,6 +402,7 @@ int gpi_cgr_residual(const gpi_residual_desc* d, void* stream);
 /* Virtual observables: rows per VO sample for a flag set (or a negative error). */
 int gpi_vo_rows(int32_t n_fine, int32_t nc, int32_t flags);
 int gpi_vo_query(const gpi_vo_query_desc* d, void* stream);
+int gpi_vo_galerkin(const gpi_vo_galerkin_desc* d, void* stream);
 int gpi_vo_moments(const gpi_vo_moments_desc* d, void* stream);
 int gpi_vo_condition(const gpi_vo_condition_desc* d, void* stream);
 int gpi_vo_precision(const gpi_vo_precision_desc* d, void* stream);

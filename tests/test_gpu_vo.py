@@ -284,3 +284,97 @@ def test_vo_update_and_vo_elbo_match_reference(device):
             continue
         err = np.abs(got - ref).max() / max(np.abs(ref).max(), 1.0)
         assert err < 2e-3, (k, err)
+
+
+# ---------------------------------------------------------------- random test functions
+def test_vo_galerkin_rows_given_test_functions(device):
+    """V^T K_ff, V^T f_eff (QuerryPoint.construct_querry_weak_galerkin) for explicit V and for RBF
+    centres, vs the oracle's assembled K_ff / f_eff (fp64, 1e-12)."""
+    from gpi import _lib as L
+    from gpi.vo import vo_galerkin
+    rng = np.random.default_rng(21)
+    nc, r, N, ma = 4, 8, 2, 3
+    n = nc * r
+    mf = fem.unit_square_mesh(n)
+    dy = (n + 1) * (n - 1)
+    x = rng.normal(0.3, 0.9, (N, 2 * n * n))
+    u = rng.uniform(-0.5, 0.5, (N, 4))
+    Vt = rng.normal(size=(N, ma, dy))
+    cen = rng.uniform(0, 1, (N, ma, 2))
+    m = 2 * ma + 1
+    g = torch.full((N, m, dy), 7.0, dtype=torch.float64, device='cuda')
+    a = torch.full((N, m), 7.0, dtype=torch.float64, device='cuda')
+    xg, ug = cuda(x, torch.float64), cuda(u, torch.float64)
+    vo_galerkin(g, a, 1, ma, xg, ug, n, L.VO_TEST_GAUSS, V=cuda(Vt, torch.float64))
+    vo_galerkin(g, a, 1 + ma, ma, xg, ug, n, L.VO_TEST_RBF, centers=cuda(cen, torch.float64), length=0.15)
+    free = fem.dirichlet_split(mf)[1]
+    P = mf.coords[free]
+    for i in range(N):
+        K, f = fem.assemble_system(mf, np.exp(x[i]), u[i])
+        Vr = np.exp(-((P[None, :, 0] - cen[i, :, 0:1]) ** 2 + (P[None, :, 1] - cen[i, :, 1:2]) ** 2) / 0.15 ** 2)
+        Vall = np.concatenate([Vt[i], Vr])
+        assert rel(g[i, 1:].cpu(), Vall @ K) < 1e-12
+        assert np.abs(a[i, 1:].cpu().numpy() - Vall @ f).max() <= 1e-12 * max(np.abs(Vall @ f).max(), 1.0)
+        assert float(g[i, 0, 0]) == 7.0 and float(a[i, 0]) == 7.0          # other rows untouched
+
+
+def test_vo_galerkin_device_draws(device):
+    """Device-drawn test functions: Gaussian V recovered from Gamma = V^T K (K SPD) is N(0,1);
+    RBF rows are bounded by the RBF's own row of K (0 < V <= 1); redraws differ."""
+    from gpi import _lib as L
+    from gpi.vo import vo_galerkin
+    rng = np.random.default_rng(22)
+    nc, r, N, ma = 4, 8, 2, 8
+    n = nc * r
+    mf = fem.unit_square_mesh(n)
+    dy = (n + 1) * (n - 1)
+    x = rng.normal(0.3, 0.9, (N, 2 * n * n))
+    u = rng.uniform(-0.5, 0.5, (N, 4))
+    xg, ug = cuda(x, torch.float64), cuda(u, torch.float64)
+    g = torch.empty(N, ma, dy, dtype=torch.float64, device='cuda')
+    a = torch.empty(N, ma, dtype=torch.float64, device='cuda')
+    vo_galerkin(g, a, 0, ma, xg, ug, n, L.VO_TEST_GAUSS, seed=5)
+    K, _ = fem.assemble_system(mf, np.exp(x[0]), u[0])
+    Vrec = np.linalg.solve(K, g[0].cpu().numpy().T).T            # K symmetric
+    assert abs(Vrec.mean()) < 0.03 and abs(Vrec.std() - 1) < 0.03
+    g2 = g.clone()
+    vo_galerkin(g2, a, 0, ma, xg, ug, n, L.VO_TEST_GAUSS, seed=6)
+    assert (g2 - g).abs().max().item() > 1.0
+    vo_galerkin(g, a, 0, ma, xg, ug, n, L.VO_TEST_RBF, length=0.15, seed=5)
+    Vrbf = np.linalg.solve(K, g[0].cpu().numpy().T).T
+    assert Vrbf.min() > -1e-9 and Vrbf.max() <= 1 + 1e-9 and Vrbf.max() > 0.3
+
+
+def test_vo_ensemble_with_random_test_functions(device):
+    """QuerryEnsemble with CGR + flux + Gaussian + RBF rows; resample redraws only the random rows,
+    and the batched conditioning runs on the full row set."""
+    from bottleneck import VirtualObservables as VO
+    from physics.LinearElliptic import LinearEllipticPhysics
+    from physics.BoundaryConditions import BoundaryCondition
+    rng = np.random.default_rng(23)
+    nc, r, N = 4, 8, 3
+    n = nc * r
+    physics = {'fom': LinearEllipticPhysics('fom', 'NDP', n), 'rom': LinearEllipticPhysics('rom', 'NDP', nc)}
+    physics['W'] = physics['fom'].grid.prolongation_from(physics['rom'].grid)
+    QPE = VO.QuerryPointEnsemble([VO.QuerryPoint(physics['fom'], rng.normal(0.4, 0.8, 2 * n * n),
+                                                 BoundaryCondition(rng.uniform(-0.5, 0.5, 4))) for _ in range(N)])
+    QE = VO.QuerryEnsemble.FromQuerryPointEnsemble(QPE, physics, True, True, 4, 3, l_rbf=0.15,
+                                                   dtype=torch.float32, device=torch.device('cuda'))
+    m0 = (nc + 1) ** 2 + 2 * nc * nc
+    assert QE.gamma.shape[1] == m0 + 7
+    assert (QE.precision_mask < 0).sum() == (nc + 1) ** 2 + 7
+    before = QE.gamma.clone()
+    ens = VO.VirtualObservablesEnsemble(QPE, QE, dtype=torch.float32, device=torch.device('cuda'))
+    ens.resample()
+    assert torch.equal(QE.gamma[:, :m0], before[:, :m0])
+    assert (QE.gamma[:, m0:] - before[:, m0:]).abs().max().item() > 0
+    assert QE[1].Gamma.data_ptr() == QE.gamma[1].data_ptr()
+    dy = (n + 1) * (n - 1)
+    G = cuda(rng.normal(0, 0.3, (N, dy)))
+    P = cuda(1.0 / rng.uniform(0.01, 0.1, (N, dy)) ** 2)
+    ens.update(G, P, 0)
+    ens.check_flag()
+    for i in range(N):
+        mo, vo = oelbo.vo_condition(QE.gamma[i].cpu(), QE.alpha[i].cpu(), G[i].cpu().double(), P[i].cpu().double(),
+                                    ens._mean_vo_variances.cpu())
+        assert rel(ens._mean64[i].cpu(), mo) < 1e-7
