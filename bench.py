@@ -40,6 +40,7 @@ CONFIGS = {
     'c64': ('highres', 256, 32, 1024, (0.4, 0.8, 0.04)),
     'c32': ('highres32', 64, 16, 256, (0.4, 0.8, 0.15)),
     'c128': ('highres128', 256, 32, 512, (0.4, 0.8, 0.04)),
+    'c256': ('highres256', 128, 32, 256, (0.4, 0.8, 0.04)),
 }
 
 

@@ -138,6 +138,7 @@ bool conv_geom(const gpi_conv_desc& d, const gpi_groups& g, ConvGeom& G, bool fw
     G.th = target / d.w_out;
     if (G.th < 1) G.th = 1;
     if (G.th > d.h_out) G.th = d.h_out;
+    if (d.upsample && G.th < 2) G.th = 2;   // upsampled tiles pair output rows (256-wide planes)
     while (d.h_out % G.th) --G.th;
     if (d.upsample && (G.th & 1)) return false;
     G.tiles = d.h_out / G.th;
@@ -471,58 +472,82 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(gpi_conv_desc d, gpi_code
     __syncthreads();
     PHASE(4);
 
-    // ---- phase 4: compute (the loss target load is in flight meanwhile)
+    // ---- phase 4: compute, one output pixel per thread and pass (two passes only for the
+    // 256-wide upsampled planes, whose tiles pair output rows)
     const int tp = G.th * d.w_out;
-    const int ty = dq(tid, G.d_wout), tx = tid - ty * d.w_out;
-    const int oy = T.oy0 + ty, ox = tx;
-    const bool active = tid < tp;
-    float tgt = 0.f;
-    if (d.epilogue == GPI_EPI_GAUSS_LOSS && active) {
-        int row = T.b - c.groups.start[T.grp];
-        if (c.tgt_idx[T.grp]) row = c.tgt_idx[T.grp][row];
-        tgt = c.tgt[T.grp][(int64_t)row * HWo + oy * d.w_out + ox];
-    }
-    PHASE(5);
-    float acc[CP];
+    float Lv = 0.f;
+    float vst[2 * CP];
 #pragma unroll
-    for (int co = 0; co < CP; ++co) acc[co] = 0.f;
-    if (active) {
-        const int plane = G.rh * G.P;
-        for (int ci = 0; ci < d.cin; ++ci) {
-            const float* tci = img + ci * plane;
-            const float* wci = wT + ci * KK * CP;
+    for (int q = 0; q < 2 * CP; ++q) vst[q] = 0.f;
+    for (int pbase = 0; pbase < tp; pbase += 256) {
+        const int pix = pbase + tid;
+        const int ty = dq(pix, G.d_wout), tx = pix - ty * d.w_out;
+        const int oy = T.oy0 + ty, ox = tx;
+        const bool active = pix < tp;
+        float tgt = 0.f;
+        if (d.epilogue == GPI_EPI_GAUSS_LOSS && active) {
+            int row = T.b - c.groups.start[T.grp];
+            if (c.tgt_idx[T.grp]) row = c.tgt_idx[T.grp][row];
+            tgt = c.tgt[T.grp][(int64_t)row * HWo + oy * d.w_out + ox];
+        }
+        PHASE(5);
+        float acc[CP];
 #pragma unroll
-            for (int ky = 0; ky < K; ++ky) {
-                const int ry = UP ? (fdiv2(oy - d.pad + ky) - iy0) : (ty * S + ky);
-                const float* trow = tci + ry * G.P;
+        for (int co = 0; co < CP; ++co) acc[co] = 0.f;
+        if (active) {
+            const int plane = G.rh * G.P;
+            for (int ci = 0; ci < d.cin; ++ci) {
+                const float* tci = img + ci * plane;
+                const float* wci = wT + ci * KK * CP;
 #pragma unroll
-                for (int kx = 0; kx < K; ++kx) {
-                    const int col = UP ? fdiv2(ox - d.pad + kx) + HALO : ox * S - d.pad + kx + HALO;
-                    fma_vec<CP>(acc, wci + (ky * K + kx) * CP, trow[col]);
+                for (int ky = 0; ky < K; ++ky) {
+                    const int ry = UP ? (fdiv2(oy - d.pad + ky) - iy0) : (ty * S + ky);
+                    const float* trow = tci + ry * G.P;
+#pragma unroll
+                    for (int kx = 0; kx < K; ++kx) {
+                        const int col = UP ? fdiv2(ox - d.pad + kx) + HALO : ox * S - d.pad + kx + HALO;
+                        fma_vec<CP>(acc, wci + (ky * K + kx) * CP, trow[col]);
+                    }
                 }
             }
         }
-    }
-    PHASE(6);
-
-    if (d.epilogue == GPI_EPI_GAUSS_LOSS) {
-        float Lv = 0.f;
+        PHASE(6);
+        if (d.epilogue == GPI_EPI_GAUSS_LOSS) {
+            if (active) {
+                const float mu = acc[0], ls = acc[1];
+                const float e = expf(-2.f * ls);
+                const float r = tgt - mu;
+                Lv += -0.5f * (2.f * ls + r * r * e + GPI_LOG2PI);
+                const float scl = c.loss_scale[T.grp];
+                auto go = as_gst(ws + d.gout_off + (int64_t)T.b * 2 * HWo + oy * d.w_out + ox);
+                go[0] = -scl * r * e;
+                go[HWo] = scl * (1.f - r * r * e);
+                if (d.out_off >= 0) {
+                    auto o = as_gst(ws + d.out_off + (int64_t)T.b * d.out_ctot * HWo + (int64_t)d.out_c0 * HWo +
+                                 oy * d.w_out + ox);
+                    o[0] = mu;
+                    o[HWo] = ls;
+                }
+            }
+            continue;
+        }
         if (active) {
-            const float mu = acc[0], ls = acc[1];
-            const float e = expf(-2.f * ls);
-            const float r = tgt - mu;
-            Lv = -0.5f * (2.f * ls + r * r * e + GPI_LOG2PI);
-            const float scl = c.loss_scale[T.grp];
-            auto go = as_gst(ws + d.gout_off + (int64_t)T.b * 2 * HWo + oy * d.w_out + ox);
-            go[0] = -scl * r * e;
-            go[HWo] = scl * (1.f - r * r * e);
-            if (d.out_off >= 0) {
-                auto o = as_gst(ws + d.out_off + (int64_t)T.b * d.out_ctot * HWo + (int64_t)d.out_c0 * HWo +
-                             oy * d.w_out + ox);
-                o[0] = mu;
-                o[HWo] = ls;
+            auto o = as_gst(ws + d.out_off + ((int64_t)T.b * d.out_ctot + d.out_c0) * HWo + oy * d.w_out + ox);
+#pragma unroll
+            for (int co = 0; co < CP; ++co)
+                if (co < d.cout) o[(int64_t)co * HWo] = acc[co];
+        }
+        if (d.epilogue == GPI_EPI_STORE_STATS) {
+#pragma unroll
+            for (int co = 0; co < CP; ++co) {
+                const float a = (active && co < d.cout) ? acc[co] : 0.f;
+                vst[2 * co] += a;
+                vst[2 * co + 1] += a * a;
             }
         }
+    }
+
+    if (d.epilogue == GPI_EPI_GAUSS_LOSS) {
         float v[1] = {Lv};
         block_sum<1>(v, scratch, red);
         __syncthreads();
@@ -531,22 +556,8 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(gpi_conv_desc d, gpi_code
         RTSTAMP(1);
         return;
     }
-
-    if (active) {
-        auto o = as_gst(ws + d.out_off + ((int64_t)T.b * d.out_ctot + d.out_c0) * HWo + oy * d.w_out + ox);
-#pragma unroll
-        for (int co = 0; co < CP; ++co)
-            if (co < d.cout) o[(int64_t)co * HWo] = acc[co];
-    }
     if (d.epilogue == GPI_EPI_STORE_STATS) {
-        float v[2 * CP];
-#pragma unroll
-        for (int co = 0; co < CP; ++co) {
-            const float a = (active && co < d.cout) ? acc[co] : 0.f;
-            v[2 * co] = a;
-            v[2 * co + 1] = a * a;
-        }
-        block_sum<2 * CP>(v, scratch, red);
+        block_sum<2 * CP>(vst, scratch, red);
         __syncthreads();
         if (tid < 2 * d.cout) {
             gpi_stat* st = stat_slot(c, d.out_stat + (tid >> 1), T.grp);

@@ -46,7 +46,7 @@ class ModelFactory(object):
 
     @classmethod
     def FromIdentifier(cls, identifier, *args, **kwargs):
-        classes = {c.__name__: c for c in (highres, highres32, highres128)}
+        classes = {c.__name__: c for c in (highres, highres32, highres128, highres256)}
         return classes[identifier](*args, **kwargs)
 
     @property
@@ -142,4 +142,16 @@ class highres128(ModelFactory):
         self.params.update(ptype='NDP', dim_latent=64, dtype='float32', device='best', nx_rom=8, ny_rom=8,
                            eff_property_map_hidden_layers=0, num_refines=4, droprate=0.0)
         self._identifier = 'highres128'
+        self.set(kwargs)
+
+
+class highres256(ModelFactory):
+    """256 x 256 scale-up (BASELINE config 5): blocks [1, 2, 2, 2, 1], ROM 8x8 with 5 refinements."""
+    CODEC = dict(latent=8, latent_features=1, f_dec=6, f_enc=6, blocks=[1, 2, 2, 2, 1], growth=4)
+
+    def __init__(self, **kwargs):
+        super().__init__()
+        self.params.update(ptype='NDP', dim_latent=64, dtype='float32', device='best', nx_rom=8, ny_rom=8,
+                           eff_property_map_hidden_layers=0, num_refines=5, droprate=0.0)
+        self._identifier = 'highres256'
         self.set(kwargs)

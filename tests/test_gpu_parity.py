@@ -262,3 +262,70 @@ def test_device_rng(device):
     L.check(L.lib().gpi_random_subset(L.ptr(idx), 2048, 256, 99, L.ptr(off), 3, L.stream_handle()), 'subset')
     v = idx.cpu().numpy()
     assert len(set(v.tolist())) == 256 and v.min() >= 0 and v.max() < 2048
+
+
+# ---------------------------------------------------------------- larger grids (BASELINE configs 4 / 5)
+def _codec_case(imsize, blocks, B, seed, dz=64, growth=4, f0=6):
+    """Per-tensor relative gradient errors (and forward errors) of the native encoder / decoder vs
+    the fp64 oracle for one seeded model + input."""
+    from bottleneck.Encoder import CNNEncoder
+    from bottleneck.Decoder import CNNDecoder
+    from oracle import codec as ocodec
+    torch.manual_seed(seed)
+    enc = CNNEncoder(imsize, dz, blocks, growth, f0, drop_rate=0)
+    dec = CNNDecoder(imsize, dz, (8, 8), 1, f0, blocks, False, growth, drop_rate=0.)
+    gen = torch.Generator().manual_seed(seed + 1)
+    with torch.no_grad():
+        for m in list(enc.modules()) + list(dec.modules()):
+            if isinstance(m, torch.nn.BatchNorm2d):
+                m.weight.copy_(1.0 + 0.3 * torch.randn(m.weight.shape, generator=gen))
+                m.bias.copy_(0.2 * torch.randn(m.bias.shape, generator=gen))
+    sd_e = {k: v.clone().double() for k, v in enc.state_dict().items()}
+    sd_d = {k: v.clone().double() for k, v in dec.state_dict().items()}
+    enc, dec = enc.cuda(), dec.cuda()
+    X = torch.randn(B, imsize, imsize, generator=gen).double() * 0.8 + 0.4
+    wm, ws = torch.randn(B, dz, generator=gen).double(), torch.randn(B, dz, generator=gen).double()
+    mu, ls = enc(X.float().cuda())
+    (torch.sum(mu * wm.float().cuda()) + torch.sum(ls * ws.float().cuda())).backward()
+    pe = {k: v.requires_grad_(True) for k, v in sd_e.items() if v.is_floating_point() and 'running' not in k}
+    mu_o, ls_o = ocodec.encoder_forward(pe, X, imsize, blocks, growth, f0)
+    (torch.sum(mu_o * wm) + torch.sum(ls_o * ws)).backward()
+    fwd = max(rel(mu.detach().cpu(), mu_o.detach()), rel(ls.detach().cpu(), ls_o.detach()))
+    errs = {'enc.' + k: rel(q.grad.cpu(), pe[k].grad) for k, q in enc.named_parameters()}
+    Z = torch.randn(B, dz, generator=gen).double()
+    vm, vs = torch.randn(B, imsize, imsize, generator=gen).double(), torch.randn(B, imsize, imsize, generator=gen).double()
+    Zc = Z.float().cuda().requires_grad_(True)
+    mx, lsx = dec(Zc)
+    (torch.sum(mx * vm.float().cuda()) + torch.sum(lsx * vs.float().cuda())).backward()
+    pd = {k: v.requires_grad_(True) for k, v in sd_d.items() if v.is_floating_point() and 'running' not in k}
+    Zo = Z.clone().requires_grad_(True)
+    mx_o, lsx_o = ocodec.decoder_forward(pd, Zo, 8, blocks, growth, f0)
+    (torch.sum(mx_o * vm) + torch.sum(lsx_o * vs)).backward()
+    fwd = max(fwd, rel(mx.detach().cpu(), mx_o.detach()), rel(lsx.detach().cpu(), lsx_o.detach()))
+    errs.update({'dec.' + k: rel(q.grad.cpu(), pd[k].grad) for k, q in dec.named_parameters()})
+    errs['dec.Z'] = rel(Zc.grad.cpu(), Zo.grad)
+    return fwd, errs
+
+
+@pytest.mark.parametrize('imsize,blocks,B', [(128, [1, 2, 2, 1], 3), (256, [1, 2, 2, 2, 1], 2)])
+def test_codec_large_grids_vs_oracle(device, imsize, blocks, B):
+    """Encoder / decoder forward + backward at 128^2 (highres128) and 256^2 (deeper codec) against
+    the fp64 oracle restatement (pinned by the reference fixtures at 32^2 / 64^2).
+
+    ReLU near-ties: at these sizes the fp64 oracle has BN outputs within ~1e-7..1e-6 of 0 (measured
+    minima per seed), below the fp32 forward error, so any fp32 implementation may take the other
+    ReLU branch at such a pixel and move that pixel's share of the upstream gradients (up to a few
+    1e-3 of a tensor at the 8x8 latent resolution; a perturbation of the input by 1e-3 makes the
+    same kernels agree to ~1e-6: tools/flip_probe.py; a flip at the 8x8 latent level moved
+    latent_map.weight by 3.8e-2 in one seed).  Hence, over six seeds: forward within 1e-4 always,
+    every gradient tensor within 1e-1 always, and every gradient tensor within 2e-4 in at least
+    one seed -- a systematic kernel error fails every seed."""
+    best = {}
+    for seed in range(6):
+        fwd, errs = _codec_case(imsize, blocks, B, seed)
+        assert fwd < 1e-4, (seed, fwd)
+        for k, e in errs.items():
+            assert e < 1e-1, (seed, k, e)
+            best[k] = min(best.get(k, 1.0), e)
+    bad = {k: e for k, e in best.items() if e >= 2e-4}
+    assert not bad, bad
