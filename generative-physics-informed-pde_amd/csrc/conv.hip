@@ -22,6 +22,7 @@
 // reduced by gpi_wgrad_reduce with the dgamma/dbeta partials) and the input
 // gradient with the ReLU mask and S_in (+)= gamma * dbn.
 #include "common.h"
+#include <stdlib.h>
 
 using namespace gpi;
 
@@ -117,6 +118,11 @@ __host__ __device__ inline void owned_rows(int s, int up, int o0, int t, int& p0
 
 // Tiles: the forward computes one output pixel per thread (<= 256 per tile); the MFMA
 // backward takes taller tiles (fewer halo rows and per-tile fixed costs per pixel).
+int env_int(const char* name, int dflt) {
+    const char* v = getenv(name);
+    return v && *v ? atoi(v) : dflt;
+}
+
 bool conv_geom(const gpi_conv_desc& d, const gpi_groups& g, ConvGeom& G, bool fwd) {
     if (g.n_groups < 1 || g.n_groups > GPI_MAX_GROUPS) return false;
     if (d.cin < 1 || d.cin > GPI_MAX_CIN || d.cout < 1 || d.cout > GPI_MAX_COUT) return false;
@@ -133,8 +139,11 @@ bool conv_geom(const gpi_conv_desc& d, const gpi_groups& g, ConvGeom& G, bool fw
     }
     const int B = g.start[g.n_groups] - g.start[0];
     if (g.start[0] != 0 || B <= 0) return false;
-    // output pixels per tile (taller backward tiles only pay on planes >= 64 wide: measured)
-    const int target = d.stride == 2 ? 128 : (!fwd && d.w_out >= 64 ? 512 : 256);
+    // output pixels per tile (taller backward tiles only pay on planes >= 64 wide: measured);
+    // GPI_TILE_FWD / GPI_TILE_BWD / GPI_TILE_S2 override the targets (tuning runs only)
+    static const int t_fwd = env_int("GPI_TILE_FWD", 512), t_bwd = env_int("GPI_TILE_BWD", 512),
+                     t_s2 = env_int("GPI_TILE_S2", 128);
+    const int target = d.stride == 2 ? t_s2 : (!fwd && d.w_out >= 64 ? t_bwd : (fwd ? t_fwd : 256));
     G.th = target / d.w_out;
     if (G.th < 1) G.th = 1;
     if (G.th > d.h_out) G.th = d.h_out;

@@ -15,6 +15,21 @@ __global__ __launch_bounds__(256) void grad_finalize_kernel(double* __restrict__
     if (flags & GPI_FINALIZE_ZERO) gacc[i] = 0.0;
 }
 
+__global__ __launch_bounds__(256) void step_epilogue_kernel(gpi_step_epilogue_desc d) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (d.step && i == 0) *d.step += 1;
+    if (i < d.n) {
+        const float g = (float)d.gacc[i];
+        d.grad[i] = (d.flags & GPI_FINALIZE_ACCUMULATE) ? d.grad[i] + g : g;
+        if (d.flags & GPI_FINALIZE_ZERO) d.gacc[i] = 0.0;
+    }
+    if (i < d.n_scratch) {
+        if (i < d.n_terms) d.terms_dst[i] = d.scratch[i];
+        d.scratch[i] = 0.0;
+    }
+    if (i < d.n_idx) d.idx_dst[i] = d.idx_src[i];
+}
+
 // torch.optim.Adam single-tensor math (torch/optim/adam.py, defaults:
 // no weight decay, no amsgrad, maximize=False).
 __global__ __launch_bounds__(256) void adam_kernel(gpi_adam_desc d) {
@@ -98,7 +113,7 @@ extern "C" int gpi_struct_sizes(int64_t* out, int n) {
                          (int64_t)sizeof(gpi_adam_desc), (int64_t)sizeof(gpi_vo_query_desc),
                          (int64_t)sizeof(gpi_vo_moments_desc), (int64_t)sizeof(gpi_vo_condition_desc),
                          (int64_t)sizeof(gpi_vo_precision_desc), (int64_t)sizeof(gpi_gp_sample_desc),
-                         (int64_t)sizeof(gpi_vo_galerkin_desc)};
+                         (int64_t)sizeof(gpi_vo_galerkin_desc), (int64_t)sizeof(gpi_step_epilogue_desc)};
     const int k = (int)(sizeof(s) / sizeof(s[0]));
     if (!out || n < k) return GPI_ERR_ARG;
     for (int i = 0; i < k; ++i) out[i] = s[i];
@@ -120,6 +135,19 @@ extern "C" int gpi_grad_finalize(double* gacc, float* grad, int64_t n, int flags
     const int64_t nb = n > 0 ? (n + 255) / 256 : 1;
     hipLaunchKernelGGL(grad_finalize_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, gacc, grad, n,
                        flags, step);
+    GPI_CHECK_LAUNCH();
+    return GPI_OK;
+}
+
+extern "C" int gpi_step_epilogue(const gpi_step_epilogue_desc* d, void* stream) {
+    if (!d || d->n < 0 || d->n_scratch < 0 || d->n_idx < 0 || d->n_terms < 0 || d->n_terms > d->n_scratch) return GPI_ERR_ARG;
+    if ((d->n && (!d->gacc || !d->grad)) || (d->n_scratch && !d->scratch) || (d->n_terms && !d->terms_dst) ||
+        (d->n_idx && (!d->idx_src || !d->idx_dst)))
+        return GPI_ERR_ARG;
+    int64_t m = d->n > d->n_scratch ? d->n : d->n_scratch;
+    if (d->n_idx > m) m = d->n_idx;
+    const int64_t nb = m > 0 ? (m + 255) / 256 : 1;
+    hipLaunchKernelGGL(step_epilogue_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, *d);
     GPI_CHECK_LAUNCH();
     return GPI_OK;
 }

@@ -133,9 +133,15 @@ class VoGalerkinDesc(C.Structure):
                 ('seed', u64), ('offset', vp), ('sub', u64), ('gamma', vp), ('alpha', vp), ('m', i32), ('row0', i32)]
 
 
+class StepEpilogueDesc(C.Structure):
+    _fields_ = [('gacc', vp), ('grad', vp), ('n', i64), ('flags', i32), ('n_terms', i32), ('step', vp),
+                ('scratch', vp), ('n_scratch', i64), ('terms_dst', vp), ('idx_src', vp), ('idx_dst', vp),
+                ('n_idx', i64)]
+
+
 STRUCTS = [Stat, Groups, ConvDesc, CodecCtx, ReduceItem, HeadDesc, GemmItem, RomDesc, ResidualDesc, AdamDesc,
            VoQueryDesc, VoMomentsDesc, VoConditionDesc, VoPrecisionDesc, GpSampleDesc,
-           VoGalerkinDesc]
+           VoGalerkinDesc, StepEpilogueDesc]
 
 # name -> (restype, argtypes)
 SIGNATURES = {
@@ -155,6 +161,7 @@ SIGNATURES = {
     'gpi_cgr_residual': (C.c_int, [C.POINTER(ResidualDesc), vp]),
     'gpi_grad_finalize': (C.c_int, [vp, vp, i64, C.c_int, vp, vp]),
     'gpi_adam': (C.c_int, [C.POINTER(AdamDesc), vp]),
+    'gpi_step_epilogue': (C.c_int, [C.POINTER(StepEpilogueDesc), vp]),
     'gpi_randn': (C.c_int, [vp, i64, u64, vp, u64, vp]),
     'gpi_rng_advance': (C.c_int, [vp, u64, vp]),
     'gpi_random_subset': (C.c_int, [vp, i32, i32, u64, vp, u64, vp]),
@@ -187,8 +194,8 @@ def lib():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        sizes = (i64 * 16)()
-        k = L.gpi_struct_sizes(sizes, 16)
+        sizes = (i64 * 64)()
+        k = L.gpi_struct_sizes(sizes, 64)
         if k != len(STRUCTS):
             raise NativeError('ABI mismatch: %d structs in the library, %d in the binding' % (k, len(STRUCTS)))
         for s, cls in zip(sizes[:k], STRUCTS):

@@ -329,12 +329,14 @@ class ElboEngine(object):
                 assert F_vo.shape[0] == self.N_vo
                 self.rom_vo.F = F_vo.data_ptr()
 
-    def forward(self, stream=None, compute_value=True, zero_gacc=True):
-        """Launch the forward; returns the 0-d ELBO tensor (no host sync).  zero_gacc=False
-        when the previous step's finalize already cleared the accumulator (GPI_FINALIZE_ZERO)."""
+    def forward(self, stream=None, compute_value=True, zero_gacc=True, zero_scratch=True):
+        """Launch the forward; returns the 0-d ELBO tensor (no host sync).  zero_gacc / zero_scratch
+        False when the previous step's epilogue already cleared the accumulator / the statistics
+        and term scratch (gpi_step_epilogue)."""
         lib = _lib()
         st = stream if stream is not None else L.stream_handle()
-        self.ws.zero_scratch()
+        if zero_scratch:
+            self.ws.zero_scratch()
         if zero_gacc:
             self.flat.gacc.zero_()
         if self.ep is not None:
@@ -372,8 +374,9 @@ class ElboEngine(object):
             torch.cuda.current_stream().wait_event(self._ev_join)
             self._pending_join = False
 
-    def elbo_value(self):
-        t = self.ws.terms
+    def elbo_value(self, terms=None):
+        """0-d ELBO from the term accumulators (or from a saved copy ``terms`` [N_TERMS * R])."""
+        t = self.ws.terms if terms is None else terms.view(N_TERMS, R).sum(1)
         su, ss, sv = self.su, self.ss, self.sv
         val = t.new_zeros(())
         if self.B_u > 0:
@@ -412,8 +415,10 @@ class ElboEngine(object):
                 out['vo_entropy'] = float(t[T_ENT2]) + self.N_vo * ENT_CONST
         return out
 
-    def backward(self, stream=None):
-        """Gradients of -ELBO into flat.gacc (fp64)."""
+    def backward(self, stream=None, side_extra=None):
+        """Gradients of -ELBO into flat.gacc (fp64).  side_extra(side_stream_handle) is launched on
+        the side stream after the decoder's reductions, concurrently with the encoder backward
+        (the fused step draws the next step's noise there)."""
         lib = _lib()
         st = stream if stream is not None else L.stream_handle()
         _run(lib.gpi_codec_backward, self.dec_descs, len(self.dec_descs), C.byref(self.dctx), st,
@@ -431,6 +436,8 @@ class ElboEngine(object):
         run_reduce(self.reduce_dec, self.ws, self.flat, sst)
         _run(lib.gpi_outer_gemm, self.gemm_items, len(self.gemm_items), C.c_void_p(self.ws.t_ws.data_ptr()),
              C.c_void_p(self.flat.gacc.data_ptr()), sst, what='outer gemm')
+        if side_extra is not None:
+            side_extra(sst)
         self._ev_join2.record(side)
         if self.ep is not None:
             _run(lib.gpi_codec_backward, self.enc_descs, len(self.enc_descs), C.byref(self.ectx), st,

@@ -52,6 +52,7 @@ class FusedElboStep(object):
         self.adam = L.AdamDesc(p=self.flat.P.data_ptr(), g=self.flat.G.data_ptr(), m=self.m.data_ptr(),
                                v=self.v.data_ptr(), n=self.flat.numel, lr=self.lr.data_ptr(),
                                step=self.step_ctr.data_ptr(), beta1=betas[0], beta2=betas[1], eps=eps)
+        self.idx_next = torch.zeros_like(self.idx)
         self.engine.bind(X_u=self.X_pool, u_index=self.idx if self.B_u else None, X_s=X_s, Y=Y, F=F)
         n_pool = self.X_pool.shape[0] if self.X_pool is not None else 0
         self.n_pool = n_pool
@@ -59,26 +60,43 @@ class FusedElboStep(object):
                             (self.N_s * self.engine.d_x + 3) // 4 + 1)
         self.adam.rng_offset = self.rng_off.data_ptr()
         self.adam.rng_advance = self.rng_span
+        ws = self.engine.ws
+        self.last_terms = torch.zeros(L.GPI_REPLICAS * 16, dtype=torch.float64, device=dev)
+        self.epi = L.StepEpilogueDesc(gacc=self.flat.gacc.data_ptr(), grad=self.flat.G.data_ptr(), n=self.flat.numel,
+                                      flags=L.FINALIZE_ZERO, n_terms=self.last_terms.numel(),
+                                      step=self.step_ctr.data_ptr(), scratch=ws.t_scr.data_ptr(),
+                                      n_scratch=ws.t_scr.numel(), terms_dst=self.last_terms.data_ptr(),
+                                      idx_src=self.idx_next.data_ptr(), idx_dst=self.idx.data_ptr(),
+                                      n_idx=self.B_u)
         self.graph = None
+        # the first step's noise; every step then draws the next step's during its backward
+        self._launch_noise(L.stream_handle(), self.idx, sub0=100)
 
     # ------------------------------------------------------------------
-    def _launch_noise(self, st):
+    def _launch_noise(self, st, idx, sub0=0):
+        """Random subset into ``idx`` and the reparametrisation noise into the engine's eps
+        buffers.  Philox streams: the step's offset (advanced by Adam at the end of every step)
+        and sub ids sub0 + {1, 2, 3}; the noise drawn during step k (for step k+1) therefore
+        differs from step k's own, which was drawn during step k-1 or by the prologue (sub0 = 100)."""
         lib = L.lib()
         if self.B_u:
-            L.check(lib.gpi_random_subset(L.ptr(self.idx), self.n_pool, self.B_u, self.seed, L.ptr(self.rng_off), 1,
-                                          st), 'random subset')
+            L.check(lib.gpi_random_subset(L.ptr(idx), self.n_pool, self.B_u, self.seed, L.ptr(self.rng_off),
+                                          sub0 + 1, st), 'random subset')
         ez = self.engine.eps_z()
-        L.check(lib.gpi_randn(L.ptr(ez), ez.numel(), self.seed, L.ptr(self.rng_off), 2, st), 'randn z')
+        L.check(lib.gpi_randn(L.ptr(ez), ez.numel(), self.seed, L.ptr(self.rng_off), sub0 + 2, st), 'randn z')
         if self.N_s:
             ex = self.engine.eps_x()
-            L.check(lib.gpi_randn(L.ptr(ex), ex.numel(), self.seed, L.ptr(self.rng_off), 3, st), 'randn x')
+            L.check(lib.gpi_randn(L.ptr(ex), ex.numel(), self.seed, L.ptr(self.rng_off), sub0 + 3, st), 'randn x')
 
     def forward_backward(self, stream=None):
+        """One step without the parameter update.  The step's noise and subset were drawn by the
+        previous step (off the critical path); the next step's are drawn on the side stream once
+        the head backward has consumed this step's; the epilogue (gradient finalisation, scratch
+        reset, subset hand-over) is one launch."""
         st = stream if stream is not None else L.stream_handle()
-        self._launch_noise(st)
-        self.engine.forward(st, compute_value=False, zero_gacc=False)   # finalize left gacc zeroed
-        self.engine.backward(st)
-        self.engine.finalize(self.flat.G, step=self.step_ctr, stream=st, zero_acc=True)
+        self.engine.forward(st, compute_value=False, zero_gacc=False, zero_scratch=False)
+        self.engine.backward(st, side_extra=lambda sst: self._launch_noise(sst, self.idx_next))
+        L.check(L.lib().gpi_step_epilogue(C.byref(self.epi), st), 'step epilogue')
 
     def allreduce(self):
         if self.distributed:
@@ -126,5 +144,5 @@ class FusedElboStep(object):
             self.g_up.replay()
 
     def elbo(self):
-        """Current ELBO value of the last forward (0-d tensor)."""
-        return self.engine.elbo_value()
+        """ELBO value of the last completed step (0-d tensor)."""
+        return self.engine.elbo_value(self.last_terms)

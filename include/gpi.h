@@ -418,6 +418,27 @@ int gpi_gauss_sample(float* out, const float* mean, const float* logsigma, int64
 #define GPI_FINALIZE_ACCUMULATE 1   /* grad += gacc (torch .grad accumulation) instead of grad = gacc */
 #define GPI_FINALIZE_ZERO       2   /* zero gacc after reading it (the next step needs no separate fill) */
 int gpi_grad_finalize(double* gacc, float* grad, int64_t n, int flags, int64_t* step, void* stream);
+
+/* End-of-step epilogue of the fused training step (one launch instead of four): gradient
+ * finalisation as gpi_grad_finalize, then the per-step scratch (BN statistics + ELBO term
+ * accumulators) is zeroed for the next step after its first n_terms doubles were saved to
+ * terms_dst (the value of the step just run), and the next step's random-subset indices
+ * (drawn during this step's backward, off the critical path) are moved into place. */
+typedef struct gpi_step_epilogue_desc {
+    double* gacc;
+    float* grad;
+    int64_t n;
+    int32_t flags;             /* GPI_FINALIZE_* */
+    int32_t n_terms;
+    int64_t* step;
+    double* scratch;
+    int64_t n_scratch;
+    double* terms_dst;         /* [n_terms] */
+    const int32_t* idx_src;
+    int32_t* idx_dst;
+    int64_t n_idx;
+} gpi_step_epilogue_desc;
+int gpi_step_epilogue(const gpi_step_epilogue_desc* d, void* stream);
 int gpi_adam(const gpi_adam_desc* d, void* stream);
 
 /* Device Philox4x32-10 normals: out[i] = N(0,1) for counter (*offset + i);

@@ -329,3 +329,43 @@ def test_codec_large_grids_vs_oracle(device, imsize, blocks, B):
             best[k] = min(best.get(k, 1.0), e)
     bad = {k: e for k, e in best.items() if e >= 2e-4}
     assert not bad, bad
+
+
+# ---------------------------------------------------------------- fused training step
+def test_fused_step_matches_module_path(device):
+    """FusedElboStep (graph-capturable step: noise and subset drawn one step ahead, fused epilogue)
+    against GenerativeModel.elbo + backward with the same noise / subset and parameters, over two
+    steps with the native Adam update in between (training.py:405-417; Adam itself is checked by
+    test_flat_adam_matches_torch)."""
+    import copy
+    from gpi.train import FusedElboStep
+    d = load('elbo_c32.npz')
+    model, bs = build_golden_model(d)
+    ref_model = copy.deepcopy(model)
+    Xu, Xs, Y, F = cuda(d['Xu']), cuda(d['Xs']), cuda(d['Y']), cuda(d['F'])
+    step = FusedElboStep(model, Xu, bs, Xs, Y, F, lr=1e-3, seed=7)
+    for it in range(2):
+        with torch.no_grad():
+            for (k, p), (k2, q) in zip(model.named_parameters(), ref_model.named_parameters()):
+                assert k == k2
+                q.copy_(p)
+        e = step.engine
+        eps = (e.eps_z().clone(), e.eps_x().clone())
+        idx = step.idx.clone().long()
+        ref_model._datasets['unsupervised'].perm = idx
+        ref_model.zero_grad()
+        ref = ref_model.elbo(step=it, armortized_bs=bs, eps=eps)
+        (-ref).backward()
+        step.forward_backward()
+        torch.cuda.synchronize()
+        assert abs(step.elbo().item() - ref.item()) <= 1e-5 * abs(ref.item()), (it, step.elbo().item(), ref.item())
+        G = step.flat.G
+        for k, p in ref_model.named_parameters():
+            g = G[step.flat.name_offsets[k]:step.flat.name_offsets[k] + p.numel()].view(p.shape)
+            err = (g - p.grad).abs().max().item() / max(p.grad.abs().max().item(), 1.0)
+            assert err < 1e-4, (it, k, err)
+        assert not torch.equal(step.engine.eps_z(), eps[0])        # next step's noise drawn during this one
+        assert len(set(step.idx.tolist())) == bs
+        step.update()
+        torch.cuda.synchronize()
+    assert step.step_ctr.item() == 2
