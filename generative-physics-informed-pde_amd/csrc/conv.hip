@@ -84,7 +84,8 @@ struct ConvGeom {
     const float* zero;   // the zero page (kernel argument: no per-use address reload)
     int in_sq, in_sr, in_sc;   // 256 chunks of the input image = (planes, rows, chunks)
     int g_sq, g_sr, g_sc;      // ... of the output-gradient image
-    Div d_in4, d_P4, d_g4, d_PG4, d_cin, d_cout, d_win, d_tp, d_wout;
+    Div d_in4, d_P4, d_g4, d_PG4, d_cin, d_cout, d_win, d_tp, d_wout, d_w2;
+    int dbg;   // GPI_DBG_SKIP (timing experiments only, results invalid): 1 skip wgrad, 2 skip dgrad
 };
 
 // first input row and row count of the input image of output rows [o0, o0 + t)
@@ -167,6 +168,8 @@ bool conv_geom(const gpi_conv_desc& d, const gpi_groups& g, ConvGeom& G, bool fw
         eo * d.w_in >= lim || 256ull * G.th * d.w_out >= lim)
         return false;
     G.zero = nullptr;   // set by launch()
+    static const int dbg = env_int("GPI_DBG_SKIP", 0);
+    G.dbg = dbg;
     {
         const int P4 = G.P / 4, pl = G.rh * P4, Q4 = G.PG / 4, gl = G.gh * Q4;
         G.in_sq = 256 / pl;
@@ -185,6 +188,7 @@ bool conv_geom(const gpi_conv_desc& d, const gpi_groups& g, ConvGeom& G, bool fw
     G.d_win = mkdiv(d.w_in);
     G.d_tp = mkdiv(G.th * d.w_out);
     G.d_wout = mkdiv(d.w_out);
+    G.d_w2 = mkdiv(d.w_in >= 2 ? d.w_in / 2 : 1);
     return true;
 }
 
@@ -611,8 +615,10 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(gpi_conv_desc d, gpi_code
     const int KD4 = (KD + 3) & ~3;
     float* wD = smem + pad256(BWD_HDR);               // [KD4][16]: W[co][ci][tap] at (co*KK + tap)*16 + ci, zero padded
     const int nwd = has_gin ? KD4 * 16 : 0;
-    int* ktab = (int*)(wD + pad256(nwd));             // [KD4] output-gradient offset of reduction index k
-    float* gl = (float*)ktab + (has_gin ? pad256(KD4) : 0);   // [cout][gh][PG]
+    // S1 / UP: [KD4] output-gradient offset of reduction index k; S2: per parity class of the input
+    // pixel [4][2][KD4]: (output-gradient offset, weight row) of the class's k-th valid tap
+    int* ktab = (int*)(wD + pad256(nwd));
+    float* gl = (float*)ktab + (has_gin ? pad256((S == 2 ? 8 : 1) * KD4) : 0);   // [cout][gh][PG]
     const int gplane = G.gh * G.PG;
     const int gimg = img_floats(d.cout, G.gh, G.PG);
     float* gz = gl + gimg;                            // raw z of the output (BN-backward only)
@@ -661,7 +667,10 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(gpi_conv_desc d, gpi_code
     // 16 m + 4 kq + [0, 4).  The input itself is read back from the LDS image.
     int py0, ph_;
     owned_rows(S, UP, T.oy0, G.th, py0, ph_);
-    const int nmblk = has_gin ? (G.ph * d.w_in) >> 4 : 0;
+    // cin <= 4 at stride 1: the input gradient runs on the VALU (phase 4b'), the MFMA form would
+    // leave >= 3/4 of its N = 16 columns empty
+    const bool vdg = K == 5 && S == 1 && !UP && has_gin && d.cin <= 4;
+    const int nmblk = (has_gin && !vdg && !(G.dbg & 2)) ? (G.ph * d.w_in) >> 4 : 0;
     const int ci_l = min(l16, d.cin - 1);
     const bool cok = l16 < d.cin;
     const int64_t ibase = ((int64_t)T.b * d.in_ctot + d.in_c0 + ci_l) * HWi + (int64_t)py0 * d.w_in;
@@ -676,7 +685,7 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(gpi_conv_desc d, gpi_code
             else pv4[u] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
     };
-    if (nmblk > 0) own_load(0);
+    if (nmblk > 0 && S != 2) own_load(0);
     PHASE(9);
     float gam = 0.f, bet = 0.f;
     if (d.in_bn && tid < d.cin) {
@@ -720,6 +729,27 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(gpi_conv_desc d, gpi_code
 
     // ---- phase 3: activations in LDS; offset table of the input-gradient reduction
     if (d.in_bn) activate_img(al, G, d, iy0, i_sc, i_sh);
+    if (has_gin && S == 2) {
+        // input pixel (py, px) = (py0 + 2a + ry, 2b + rx) receives output (oy, ox) through tap (ky, kx)
+        // iff 2 oy = py + pad - ky, 2 ox = px + pad - kx: the valid taps depend on the parity class
+        // (ry, rx) only.  Class table entry k: A = gl offset (co, dy = (ry + pad - ky) / 2,
+        // dx = (rx + pad - kx) / 2) relative to (a, b); B = weight row co * KK + ky * K + kx.
+        for (int e = tid; e < 4 * KD4; e += 256) {
+            const int cls = e / KD4, k = e - cls * KD4;
+            const int ry = cls >> 1, rx = cls & 1;
+            const int ky0 = (ry + d.pad) & 1, kx0 = (rx + d.pad) & 1;
+            const int nky = (K - ky0 + 1) >> 1, nkx = (K - kx0 + 1) >> 1;
+            int oa = 0, ob = 0;
+            if (k < d.cout * nky * nkx) {
+                const int co = k / (nky * nkx), r = k - co * nky * nkx, jy = r / nkx, jx = r - jy * nkx;
+                const int ky = ky0 + 2 * jy, kx = kx0 + 2 * jx;
+                oa = co * gplane + ((ry + d.pad - ky) >> 1) * G.PG + ((rx + d.pad - kx) >> 1);
+                ob = co * KK + ky * K + kx;
+            }
+            ktab[cls * 2 * KD4 + k] = oa;
+            ktab[cls * 2 * KD4 + KD4 + k] = ob;
+        }
+    }
     if (has_gin && S != 2) {
         // A operand of reduction index k = (co, ky, kx) for owned pixel (qy, px):
         // gl[(S1) qy*PG + px | (UP) 2 qy*PG + 2 px] + ktab[k]
@@ -782,7 +812,7 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(gpi_conv_desc d, gpi_code
     float* slab = c.wpart + d.wpart_off + (int64_t)blockIdx.x * rowlen;
     {
         const int MI = d.cout * K, NJ = d.cin * K;
-        const int nmb = (MI + 15) >> 4, nnb = (NJ + 15) >> 4;
+        const int nmb = (G.dbg & 1) ? 0 : (MI + 15) >> 4, nnb = (NJ + 15) >> 4;
         const int XW = UP ? d.w_out + K - 1 : S * (d.w_out - 1) + K;   // virtual input columns
         const int nxs = (XW + 3) >> 2;
         for (int mb = 0; mb < nmb; ++mb) {
@@ -883,7 +913,7 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(gpi_conv_desc d, gpi_code
         const float* arow0 = al + (ci_l * G.rh + (py0 - iy0)) * G.P + HALO;   // owned row 0 of channel l16
         const int nkd = KD4 >> 2;
         for (int round = 0; wv + 16 * round < nmblk; ++round) {
-            if (round > 0) own_load(round);
+            if (round > 0 && S != 2) own_load(round);
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const int m = wv + 4 * (4 * round + u);
@@ -892,18 +922,21 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(gpi_conv_desc d, gpi_code
                     const int qy = dq(i, G.d_win), px = i - qy * d.w_in;
                     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
                     if (S == 2) {
-                        const int py = py0 + qy;
-                        for (int ks = 0; ks < nkd; ++ks) {
+                        // parity-class blocks: block m covers 16 consecutive pixels (a, b) of class
+                        // cls = m / nbc, i.e. input pixels (py0 + 2a + ry, 2b + rx); only the class's
+                        // valid taps enter the reduction (1 / 2 / 2 / 4 of the 9 at K = 3)
+                        const int nbc = nmblk >> 2, cls = m / nbc, mb = m - cls * nbc;
+                        const int ry = cls >> 1, rx = cls & 1;
+                        const int nky = (K - ((ry + d.pad) & 1) + 1) >> 1, nkx = (K - ((rx + d.pad) & 1) + 1) >> 1;
+                        const int nk = d.cout * nky * nkx;
+                        const int cp = 16 * mb + l16, a2 = dq(cp, G.d_w2), b2 = cp - a2 * (d.w_in >> 1);
+                        const float* ab = gl + ((py0 >> 1) - gy0 + a2) * G.PG + b2 + HALO;
+                        const int* tA = ktab + cls * 2 * KD4;
+                        const int* tB = tA + KD4;
+                        for (int ks = 0; 4 * ks < nk; ++ks) {
                             const int k = 4 * ks + kq;
-                            const bool kok = k < KD;
-                            const int kc = kok ? k : 0;
-                            const int co = kc / KK, tap = kc - co * KK;
-                            const int ky = tap / K, kx = tap - ky * K;
-                            const int oy2 = py + d.pad - ky, ox2 = px + d.pad - kx;
-                            const bool ok2 = kok && !((oy2 | ox2) & 1);
-                            const int o = co * gplane + ((oy2 >> 1) - gy0) * G.PG + (ox2 >> 1) + HALO;
-                            const float a = ok2 ? gl[o] : 0.f;
-                            acc = mfma4(a, wD[k * 16 + l16], acc);
+                            const float a = k < nk ? ab[tA[k]] : 0.f;
+                            acc = mfma4(a, wD[tB[k] * 16 + l16], acc);
                         }
                     } else {
                         const float* gp0 = gl + (UP ? 2 * (qy * G.PG + px) : qy * G.PG + px);
@@ -928,7 +961,29 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(gpi_conv_desc d, gpi_code
                             acc = mfma4(aval(k), wD[k * 16 + l16], acc);
                         }
                     }
-                    if (cok) {
+                    if (cok && S == 2) {
+                        const int nbc = nmblk >> 2, cls = m / nbc, mb = m - cls * nbc;
+                        const int ry = cls >> 1, rx = cls & 1;
+                        const int cp0 = 16 * mb + 4 * kq, a2 = dq(cp0, G.d_w2), b2 = cp0 - a2 * (d.w_in >> 1);
+                        const int qy = 2 * a2 + ry;
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            const int px = 2 * (b2 + q) + rx;
+                            const int64_t go = ibase + (int64_t)qy * d.w_in + px;
+                            const float pa = d.gin_accumulate ? *as_gld(ws + gin_off + go) : 0.f;
+                            float o;
+                            if (d.in_bn) {
+                                const float av = arow0[qy * G.P + px];
+                                const float dbn = av > 0.f ? acc[q] : 0.f;
+                                o = pa + l_gam * dbn;
+                                sd += dbn;
+                                sdx += dbn * ((av - l_bet) * l_rgam);
+                            } else {
+                                o = pa + acc[q];
+                            }
+                            *as_gst(ws + gin_off + go) = o;
+                        }
+                    } else if (cok) {
                         float* gp = ws + gin_off + ibase + 16 * m + 4 * kq;
                         const int i0 = 16 * m + 4 * kq;
                         const int qy0 = dq(i0, G.d_win), px0 = i0 - qy0 * d.w_in;
@@ -952,16 +1007,100 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(gpi_conv_desc d, gpi_code
             }
         }
     }
+    // ---- phase 4b': input gradient on the VALU (cin <= 4, 5x5, stride 1): two consecutive pixels of
+    // an owned row per thread, all (<= 4) input channels at once; weights are LDS broadcasts of
+    // the same zero-padded [co * KK + tap][16] table the MFMA path uses.
+    float vsd[4] = {0.f, 0.f, 0.f, 0.f}, vsdx[4] = {0.f, 0.f, 0.f, 0.f};
+    if (vdg && !(G.dbg & 2)) {
+        const int np2 = (G.ph * d.w_in) >> 1;
+        float lg[4], lb[4], lr[4];
+#pragma unroll
+        for (int ci = 0; ci < 4; ++ci) {
+            const int cc = min(ci, d.cin - 1);
+            lg[ci] = d.in_bn ? i_gam[cc] : 0.f;
+            lb[ci] = d.in_bn ? i_sh[cc] + i_mean[cc] * i_sc[cc] : 0.f;
+            lr[ci] = d.in_bn ? 1.f / lg[ci] : 0.f;
+        }
+        for (int gq = tid; gq < np2; gq += 256) {
+            const int qy = dq(2 * gq, G.d_win), px0 = 2 * gq - qy * d.w_in;
+            const int64_t pix = (int64_t)(py0 + qy) * d.w_in + px0;
+            const int64_t gbase_in = ((int64_t)T.b * d.in_ctot + d.in_c0) * HWi + pix;
+            float acc[4][2];
+#pragma unroll
+            for (int ci = 0; ci < 4; ++ci) acc[ci][0] = acc[ci][1] = 0.f;
+            for (int co = 0; co < d.cout; ++co) {
+#pragma unroll 1
+                for (int ky = 0; ky < K; ++ky) {
+                    const float* grow = gl + co * gplane + (qy + py0 + d.pad - ky - gy0) * G.PG + HALO + px0 +
+                                        d.pad - (K - 1);
+                    float gw[K + 1];
+#pragma unroll
+                    for (int t = 0; t < K + 1; ++t) gw[t] = grow[t];
+#pragma unroll
+                    for (int kx = 0; kx < K; ++kx) {
+                        const f32x4 w4 = *(const f32x4*)(wD + (co * KK + ky * K + kx) * 16);
+#pragma unroll
+                        for (int q = 0; q < 2; ++q) {
+                            const float gv = gw[q + K - 1 - kx];
+                            acc[0][q] = fmaf(w4[0], gv, acc[0][q]);
+                            acc[1][q] = fmaf(w4[1], gv, acc[1][q]);
+                            acc[2][q] = fmaf(w4[2], gv, acc[2][q]);
+                            acc[3][q] = fmaf(w4[3], gv, acc[3][q]);
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (int ci = 0; ci < 4; ++ci) {
+                if (ci >= d.cin) break;
+                const float* ap = al + (ci * G.rh + (py0 - iy0 + qy)) * G.P + HALO + px0;
+                const float av[2] = {ap[0], ap[1]};
+                float pv[2] = {0.f, 0.f};
+                if (d.gin_accumulate) {
+                    auto pp = as_gld(ws + gin_off + gbase_in + (int64_t)ci * HWi);
+                    pv[0] = pp[0];
+                    pv[1] = pp[1];
+                }
+                float o[2];
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    if (d.in_bn) {
+                        const float dbn = av[q] > 0.f ? acc[ci][q] : 0.f;
+                        o[q] = pv[q] + lg[ci] * dbn;
+                        vsd[ci] += dbn;
+                        vsdx[ci] += dbn * ((av[q] - lb[ci]) * lr[ci]);
+                    } else {
+                        o[q] = pv[q] + acc[ci][q];
+                    }
+                }
+                auto op = as_gst(ws + gin_off + gbase_in + (int64_t)ci * HWi);
+                op[0] = o[0];
+                op[1] = o[1];
+            }
+        }
+    }
     PHASE(6);
     if (d.in_bn) {
-        // lanes 16 apart share a channel: fold them, then the four waves in a fixed order
-        sd += __shfl_xor(sd, 16, 64);
-        sdx += __shfl_xor(sdx, 16, 64);
-        sd += __shfl_xor(sd, 32, 64);
-        sdx += __shfl_xor(sdx, 32, 64);
-        if (kq == 0) {
-            red[wv * 32 + l16] = sd;
-            red[128 + wv * 32 + l16] = sdx;
+        if (vdg) {
+            // per-thread channel sums: wave sums, then the four waves in a fixed order below
+#pragma unroll
+            for (int ci = 0; ci < 4; ++ci) {
+                const float a = wave_sum(vsd[ci]), b = wave_sum(vsdx[ci]);
+                if (lane == 0 && ci < d.cin) {
+                    red[wv * 32 + ci] = a;
+                    red[128 + wv * 32 + ci] = b;
+                }
+            }
+        } else {
+            // lanes 16 apart share a channel: fold them, then the four waves in a fixed order
+            sd += __shfl_xor(sd, 16, 64);
+            sdx += __shfl_xor(sdx, 16, 64);
+            sd += __shfl_xor(sd, 32, 64);
+            sdx += __shfl_xor(sdx, 32, 64);
+            if (kq == 0) {
+                red[wv * 32 + l16] = sd;
+                red[128 + wv * 32 + l16] = sdx;
+            }
         }
         __syncthreads();
         if (tid < d.cin) {
@@ -991,7 +1130,7 @@ size_t fwd_lds(const gpi_conv_desc& d, const ConvGeom& G, int cp) {
 size_t bwd_lds(const gpi_conv_desc& d, const ConvGeom& G) {
     const int KD4 = (d.cout * d.k * d.k + 3) & ~3;
     const int gimg = img_floats(d.cout, G.gh, G.PG);
-    size_t f = (size_t)pad256(BWD_HDR) + (d.gin_off >= 0 ? pad256(KD4 * 16) + pad256(KD4) : 0) + gimg +
+    size_t f = (size_t)pad256(BWD_HDR) + (d.gin_off >= 0 ? pad256(KD4 * 16) + pad256((d.stride == 2 ? 8 : 1) * KD4) : 0) + gimg +
                (d.gout_mode == 0 ? gimg : 0) + img_floats(d.cin, G.rh, G.P) + BWD_RED;
     return f * sizeof(float);
 }
@@ -1040,6 +1179,7 @@ int launch(const gpi_conv_desc& d, const gpi_codec_ctx& c, hipStream_t st, bool 
     if (d.in_off < 0 && !c.ext_in) return GPI_ERR_ARG;
     if (!aligned_ok(d, c, fwd)) return GPI_ERR_UNSUPPORTED;
     if (!fwd && d.gin_off >= 0 && ((G.ph * d.w_in) & 15)) return GPI_ERR_UNSUPPORTED;
+    if (!fwd && d.gin_off >= 0 && d.stride == 2 && ((d.w_in & 7) || (G.ph & 1))) return GPI_ERR_UNSUPPORTED;
     const int cp = cp_of(d.cout);
     conv_kernel_t k = select_kernel(d, cp, fwd);
     if (!k) return GPI_ERR_UNSUPPORTED;
