@@ -23,6 +23,7 @@
 // gradient with the ReLU mask and S_in (+)= gamma * dbn.
 #include "common.h"
 #include <stdlib.h>
+#include <stdio.h>
 
 using namespace gpi;
 
@@ -564,7 +565,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(gpi_conv_desc d, gpi_code
         float v[1] = {Lv};
         block_sum<1>(v, scratch, red);
         __syncthreads();
-        if (tid == 0) atomicAdd(c.loss_acc + T.grp * GPI_REPLICAS + blockIdx.x % GPI_REPLICAS, (double)red[0]);
+        if (tid == 0 && !(G.dbg & 4)) atomicAdd(c.loss_acc + T.grp * GPI_REPLICAS + blockIdx.x % GPI_REPLICAS, (double)red[0]);
         PHASE(7);
         RTSTAMP(1);
         return;
@@ -572,7 +573,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(gpi_conv_desc d, gpi_code
     if (d.epilogue == GPI_EPI_STORE_STATS) {
         block_sum<2 * CP>(vst, scratch, red);
         __syncthreads();
-        if (tid < 2 * d.cout) {
+        if (tid < 2 * d.cout && !(G.dbg & 4)) {
             gpi_stat* st = stat_slot(c, d.out_stat + (tid >> 1), T.grp);
             atomicAdd((tid & 1) ? &st->sumsq : &st->sum, (double)red[tid]);
         }
@@ -838,29 +839,38 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(gpi_conv_desc d, gpi_code
                     }
                     // operands of four steps are read before their MFMAs (the loop is
                     // latency-bound otherwise: LDS read -> dependent MFMA each step)
-                    int xs = 0;
-                    for (; xs + 4 <= nxs; xs += 4) {
-                        float a[4], b0[4], b1[4];
+                    if (UP) {
+                        // nearest x2 upsampling: virtual columns 2p + pad and 2p + pad + 1 both read
+                        // input column p, so their gradient columns are summed first and the
+                        // reduction runs over the (half as many) input columns p
+                        const int plo = fdiv2(-d.pad), nps = (fdiv2(XW - 1 - d.pad) - plo + 4) >> 2;
+                        int ps = 0;
+                        for (; ps + 4 <= nps; ps += 4) {
+                            float a[4], b0[4], b1[4];
 #pragma unroll
-                        for (int u = 0; u < 4; ++u) {
-                            const int xv = 4 * (xs + u) + kq;
-                            if (S == 2) {
-                                const int t2 = xv - kx;          // xv - kx = 2 ox
-                                a[u] = (t2 & 1) ? 0.f : grow[kx + (t2 >> 1)];
-                            } else {
-                                a[u] = grow[xv];                 // ox = xv - kx
+                            for (int u = 0; u < 4; ++u) {
+                                const int pc = plo + 4 * (ps + u) + kq;
+                                const int xv = 2 * pc + d.pad;
+                                a[u] = grow[xv] + grow[xv + 1];
+                                b0[u] = brow[0][pc];
+                                b1[u] = two ? brow[1][pc] : 0.f;
                             }
-                            const int ix = UP ? fdiv2(xv - d.pad) : xv - d.pad;
-                            b0[u] = brow[0][ix];
-                            b1[u] = two ? brow[1][ix] : 0.f;
-                        }
 #pragma unroll
-                        for (int u = 0; u < 4; ++u) {
-                            acc[0] = mfma4(a[u], b0[u], acc[0]);
-                            if (two) acc[1] = mfma4(a[u], b1[u], acc[1]);
+                            for (int u = 0; u < 4; ++u) {
+                                acc[0] = mfma4(a[u], b0[u], acc[0]);
+                                if (two) acc[1] = mfma4(a[u], b1[u], acc[1]);
+                            }
                         }
+                        for (; ps < nps; ++ps) {
+                            const int pc = plo + 4 * ps + kq;
+                            const int xv = 2 * pc + d.pad;
+                            const float a = grow[xv] + grow[xv + 1];
+                            acc[0] = mfma4(a, brow[0][pc], acc[0]);
+                            if (two) acc[1] = mfma4(a, brow[1][pc], acc[1]);
+                        }
+                        continue;
                     }
-                    for (; xs < nxs; ++xs) {
+                    int xs = 0;                    for (; xs < nxs; ++xs) {
                         const int xv = 4 * xs + kq;
                         float a;
                         if (S == 2) {
@@ -1114,8 +1124,10 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(gpi_conv_desc d, gpi_code
             slab[d.cout * J + d.cin + tid] = (float)s_d;     // dbeta
             gpi_stat* st = stat_slot(c, d.in_stat + tid, T.grp);
             const double gm = i_gam[tid];
-            atomicAdd(&st->ssum, gm * s_d);
-            atomicAdd(&st->sxsum, gm * s_dx);
+            if (!(G.dbg & 4)) {
+                atomicAdd(&st->ssum, gm * s_d);
+                atomicAdd(&st->sxsum, gm * s_dx);
+            }
         }
     }
     PHASE(7);
@@ -1192,6 +1204,11 @@ int launch(const gpi_conv_desc& d, const gpi_codec_ctx& c, hipStream_t st, bool 
     G.zero = zero;
     const size_t lds = fwd ? fwd_lds(d, G, cp) : bwd_lds(d, G);
     if (lds > 160 * 1024) return GPI_ERR_UNSUPPORTED;
+    static const int dbg_print = env_int("GPI_DBG_PRINT", 0);
+    if (dbg_print)
+        fprintf(stderr, "conv %s k%d s%d up%d cin%d cout%d in%dx%d out%dx%d th%d blocks %d lds %zu\n",
+                fwd ? "fwd" : "bwd", d.k, d.stride, d.upsample, d.cin, d.cout, d.h_in, d.w_in, d.h_out, d.w_out, G.th,
+                G.nblocks, lds);
     if (lds > 64 * 1024) {
         if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
             return GPI_ERR_LAUNCH;
