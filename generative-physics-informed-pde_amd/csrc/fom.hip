@@ -1,0 +1,299 @@
+// FOM data generation on the device: labels Y and log-conductivity fields.
+//
+// Reference: DataLoader.assemble (utils/data.py:72-103) solves, per sample, the FEniCS system
+// a = kappa grad u . grad v dx with the NDP boundary data (physics/LinearElliptic.py:85-101, PETSc LU)
+// for Y on the fine free nodes; NormalRandomFieldSampler (physics/RandomField.py:162-209) draws the
+// log-conductivity images from a dense squared-exponential covariance factor.
+//
+// gpi_fom_solve: the Dirichlet-reduced operator K_ff is the 5-point stencil of physics/grid.py
+// (edge conductance c = (kappa_a + kappa_b) / 2 of the two triangles having the edge as a leg), SPD.
+// One workgroup of 1024 threads per sample runs Jacobi-preconditioned CG in the Chronopoulos-Gear
+// form, so that every iteration has ONE fused block reduction ((r,u), (Au,u), (r,r)) and one more
+// barrier (the preconditioned residual u is read by the neighbours' stencil).  The per-sample
+// vectors live in the caller's workspace (L2 / MALL resident at 64^2: 10 doubles per node).
+//
+// gpi_random_field: separable restatement x = mean + sigma L_y (S o G) L_x^T of the KL sampler (the SE
+// kernel on a tensor grid is C_y (x) C_x), two batched fp64 products with 16-row panels in LDS.
+#include "common.h"
+
+using namespace gpi;
+
+namespace {
+
+constexpr int FT = 1024;   // threads per FOM workgroup
+constexpr int FW = FT / 64;
+
+struct FomGeom {
+    int n, dy, ne_h, ne_v;
+    int64_t ws;
+};
+
+__device__ __forceinline__ double bcv(const double* u, int side_right, int j, int n) {
+    const double y = (double)j / (double)n;
+    return side_right ? u[2] * (1.0 - y) + u[3] * y : u[0] * (1.0 - y) + u[1] * y;
+}
+
+__device__ __forceinline__ double kc(const double* lk, int n, int i, int j, int ul) {
+    return exp(lk[2 * (i + n * j) + ul]);
+}
+
+// four fused wave + block sums; every thread receives the totals (fixed summation order)
+__device__ __forceinline__ void block_sum4(double (&v)[4], double* red) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = wave_sum_d(v[k]);
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) red[wv * 4 + k] = v[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        double s = 0.0;
+        for (int w = 0; w < FW; ++w) s += red[w * 4 + k];
+        v[k] = s;
+    }
+}
+
+__global__ __launch_bounds__(FT) void fom_pcg_kernel(gpi_fom_desc d, FomGeom G) {
+    __shared__ double red[FW * 4];
+    const int f = blockIdx.x, tid = threadIdx.x;
+    const int n = G.n, nm = n - 1, dy = G.dy;
+    const double* lk = d.logkappa + (int64_t)f * 2 * n * n;
+    const double* ub = d.bc + 4 * f;
+    double* W = d.work + (int64_t)f * G.ws;
+    double* ch = W;                 // [(n+1) n]: edge (i,j)-(i+1,j) at j n + i
+    double* cv = ch + G.ne_h;       // [n (n+1)]: edge (i,j)-(i,j+1) at j (n+1) + i
+    double* dinv = cv + G.ne_v;     // [dy]
+    double* r = dinv + dy;
+    double* pd = r + dy;
+    double* s = pd + dy;
+    double* u = s + dy;
+    double* w = u + dy;
+    double* x = d.y + (int64_t)f * dy;
+
+    // ---- conductances: horizontal edges are legs of T_lr(i,j) / T_ul(i,j-1), vertical ones of
+    // T_ul(i,j) / T_lr(i-1,j) (P1 element matrix kappa/2 [[2,-1,-1],[-1,1,0],[-1,0,1]])
+    for (int e = tid; e < G.ne_h; e += FT) {
+        const int j = e / n, i = e - j * n;
+        double c = 0.0;
+        if (j < n) c += kc(lk, n, i, j, 0);
+        if (j > 0) c += kc(lk, n, i, j - 1, 1);
+        ch[e] = 0.5 * c;
+    }
+    for (int e = tid; e < G.ne_v; e += FT) {
+        const int j = e / (n + 1), i = e - j * (n + 1);
+        double c = 0.0;
+        if (i < n) c += kc(lk, n, i, j, 1);
+        if (i > 0) c += kc(lk, n, i - 1, j, 0);
+        cv[e] = 0.5 * c;
+    }
+    __syncthreads();
+
+    struct Star {
+        int i, j;
+        double cl, cr, cd, cu;
+    };
+    auto star = [&](int p) {
+        Star t;
+        t.j = p / nm;
+        t.i = p - t.j * nm + 1;
+        t.cl = ch[t.j * n + t.i - 1];
+        t.cr = ch[t.j * n + t.i];
+        t.cd = t.j > 0 ? cv[(t.j - 1) * (n + 1) + t.i] : 0.0;
+        t.cu = t.j < n ? cv[t.j * (n + 1) + t.i] : 0.0;
+        return t;
+    };
+    // (K_ff v)_p with v = 0 on the Dirichlet columns
+    auto apply = [&](const double* v, int p, const Star& t) {
+        double a = (t.cl + t.cr + t.cd + t.cu) * v[p];
+        if (t.i > 1) a -= t.cl * v[p - 1];
+        if (t.i < nm) a -= t.cr * v[p + 1];
+        if (t.j > 0) a -= t.cd * v[p - nm];
+        if (t.j < n) a -= t.cu * v[p + nm];
+        return a;
+    };
+    // f_eff = -K_fc g: the Dirichlet neighbours of the first / last free column
+    auto rhs = [&](const Star& t) {
+        double b = 0.0;
+        if (t.i == 1) b += t.cl * bcv(ub, 0, t.j, n);
+        if (t.i == nm) b += t.cr * bcv(ub, 1, t.j, n);
+        return b;
+    };
+
+    const bool warm = d.flags & GPI_FOM_WARM;
+    for (int p = tid; p < dy; p += FT) {
+        const Star t = star(p);
+        dinv[p] = 1.0 / (t.cl + t.cr + t.cd + t.cu);
+        if (!warm) {
+            const double gl = bcv(ub, 0, t.j, n), gr = bcv(ub, 1, t.j, n);
+            x[p] = gl + (gr - gl) * ((double)t.i / (double)n);
+        }
+    }
+    __syncthreads();
+    double bb = 0.0;
+    for (int p = tid; p < dy; p += FT) {
+        const Star t = star(p);
+        const double b = rhs(t);
+        bb += b * b;
+        const double rv = b - apply(x, p, t);
+        r[p] = rv;
+        u[p] = dinv[p] * rv;
+    }
+    __syncthreads();
+    double v4[4] = {0.0, 0.0, 0.0, bb};
+    for (int p = tid; p < dy; p += FT) {
+        const Star t = star(p);
+        const double wv = apply(u, p, t), rv = r[p], uv = u[p];
+        w[p] = wv;
+        v4[0] += rv * uv;
+        v4[1] += wv * uv;
+        v4[2] += rv * rv;
+    }
+    block_sum4(v4, red);
+    const double tol2 = d.rtol * d.rtol * v4[3];
+    double gam = v4[0], alpha = v4[0] / v4[1], beta = 0.0;
+    bool conv = v4[2] <= tol2;
+    int it = 0;
+    while (!conv && it < d.max_iter) {
+        for (int p = tid; p < dy; p += FT) {
+            const double pv = it == 0 ? u[p] : u[p] + beta * pd[p];
+            const double sv = it == 0 ? w[p] : w[p] + beta * s[p];
+            pd[p] = pv;
+            s[p] = sv;
+            x[p] += alpha * pv;
+            const double rv = r[p] - alpha * sv;
+            r[p] = rv;
+            u[p] = dinv[p] * rv;
+        }
+        __syncthreads();
+        double q[4] = {0.0, 0.0, 0.0, 0.0};
+        for (int p = tid; p < dy; p += FT) {
+            const Star t = star(p);
+            const double wv = apply(u, p, t), rv = r[p], uv = u[p];
+            w[p] = wv;
+            q[0] += rv * uv;
+            q[1] += wv * uv;
+            q[2] += rv * rv;
+        }
+        block_sum4(q, red);
+        ++it;
+        conv = q[2] <= tol2;
+        if (!conv) {
+            beta = q[0] / gam;
+            alpha = q[0] / (q[1] - beta * q[0] / alpha);
+            gam = q[0];
+        }
+    }
+    if (tid == 0) {
+        if (d.iters) d.iters[f] = it;
+        if (!conv && d.flag) atomicAdd(d.flag, 1);
+    }
+}
+
+// ---------------------------------------------------------------- random field
+constexpr int RB = 16;   // output rows per workgroup
+
+__device__ __forceinline__ double u01d(uint32_t v) {   // (0, 1]
+    return ((double)v + 1.0) * 2.3283064365386963e-10;
+}
+
+// work[b] = (S o G_b) L_x^T: panel of RB rows of G (given or Philox) in LDS, L_x^T streamed (coalesced in c)
+__global__ __launch_bounds__(256) void rf_rows_kernel(gpi_random_field_desc d) {
+    extern __shared__ __attribute__((aligned(16))) double gp[];   // [RB][px]
+    const int b = blockIdx.y, r0 = blockIdx.x * RB, px = d.px, py = d.py;
+    const int64_t P = (int64_t)py * px, q4 = (P + 3) / 4;
+    const int nr = min(RB, py - r0);
+    for (int e = threadIdx.x; e < RB * px; e += 256) {
+        const int64_t g = (int64_t)r0 * px + e;
+        double v = 0.0;
+        if (e >= nr * px) {
+        } else if (d.gamma) {
+            v = d.gamma[(int64_t)b * P + g];
+        } else {
+            const uint4_ h = philox((uint64_t)b * q4 + (uint64_t)(g >> 2), d.sub, d.seed);
+            const int k = (int)(g & 3);
+            const double ua = u01d(k < 2 ? h.x : h.z), ub = u01d(k < 2 ? h.y : h.w);
+            const double rad = sqrt(-2.0 * log(ua)), th = 6.283185307179586 * ub;
+            v = (k & 1) ? rad * sin(th) : rad * cos(th);
+        }
+        if (d.scale && e < nr * px) v *= d.scale[g];
+        gp[e] = v;
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < px; c += 256) {
+        double acc[RB];
+#pragma unroll
+        for (int t = 0; t < RB; ++t) acc[t] = 0.0;
+        for (int k = 0; k < px; ++k) {
+            const double l = d.lxt[(int64_t)k * px + c];
+#pragma unroll
+            for (int t = 0; t < RB; ++t) acc[t] = fma(gp[t * px + k], l, acc[t]);
+        }
+        for (int t = 0; t < nr; ++t) d.work[(int64_t)b * P + (int64_t)(r0 + t) * px + c] = acc[t];
+    }
+}
+
+// x[b] = mean + sigma L_y work[b]: panel of RB rows of L_y in LDS, work[b] streamed (coalesced in c)
+__global__ __launch_bounds__(256) void rf_cols_kernel(gpi_random_field_desc d) {
+    extern __shared__ __attribute__((aligned(16))) double lp[];   // [RB][py]
+    const int b = blockIdx.y, r0 = blockIdx.x * RB, px = d.px, py = d.py;
+    const int64_t P = (int64_t)py * px;
+    const int nr = min(RB, py - r0);
+    for (int e = threadIdx.x; e < RB * py; e += 256) {
+        const int t = e / py, k = e - t * py;
+        lp[e] = t < nr ? d.ly[(int64_t)(r0 + t) * py + k] : 0.0;
+    }
+    __syncthreads();
+    const double* T = d.work + (int64_t)b * P;
+    for (int c = threadIdx.x; c < px; c += 256) {
+        double acc[RB];
+#pragma unroll
+        for (int t = 0; t < RB; ++t) acc[t] = 0.0;
+        for (int k = 0; k < py; ++k) {
+            const double v = T[(int64_t)k * px + c];
+#pragma unroll
+            for (int t = 0; t < RB; ++t) acc[t] = fma(lp[t * py + k], v, acc[t]);
+        }
+        for (int t = 0; t < nr; ++t) d.x[(int64_t)b * P + (int64_t)(r0 + t) * px + c] = d.mean + d.stddev * acc[t];
+    }
+}
+
+}  // namespace
+
+extern "C" int64_t gpi_fom_workspace(int32_t n_fine) {
+    if (n_fine < 2) return -1;
+    const int64_t n = n_fine, dy = (n + 1) * (n - 1);
+    return 2 * n * (n + 1) + 6 * dy;
+}
+
+extern "C" int gpi_fom_solve(const gpi_fom_desc* d, void* stream) {
+    if (!d || !d->logkappa || !d->bc || !d->y || !d->work || d->n < 0 || d->n_fine < 2 || d->max_iter < 0 ||
+        !(d->rtol >= 0.0))
+        return GPI_ERR_ARG;
+    if (d->n == 0) return GPI_OK;
+    FomGeom G;
+    G.n = d->n_fine;
+    G.dy = (d->n_fine + 1) * (d->n_fine - 1);
+    G.ne_h = (d->n_fine + 1) * d->n_fine;
+    G.ne_v = d->n_fine * (d->n_fine + 1);
+    G.ws = gpi_fom_workspace(d->n_fine);
+    hipLaunchKernelGGL(fom_pcg_kernel, dim3(d->n), dim3(FT), 0, (hipStream_t)stream, *d, G);
+    GPI_CHECK_LAUNCH();
+    return GPI_OK;
+}
+
+extern "C" int gpi_random_field(const gpi_random_field_desc* d, void* stream) {
+    if (!d || !d->ly || !d->lxt || !d->work || !d->x || d->n < 0 || d->py < 1 || d->px < 1 || !(d->stddev > 0.0))
+        return GPI_ERR_ARG;
+    if (d->n == 0) return GPI_OK;
+    const size_t lds_r = sizeof(double) * RB * d->px, lds_c = sizeof(double) * RB * d->py;
+    if (lds_r > 64 * 1024 || lds_c > 64 * 1024) return GPI_ERR_UNSUPPORTED;
+    const hipStream_t st = (hipStream_t)stream;
+    const dim3 grid((d->py + RB - 1) / RB, d->n);
+    hipLaunchKernelGGL(rf_rows_kernel, grid, dim3(256), lds_r, st, *d);
+    GPI_CHECK_LAUNCH();
+    hipLaunchKernelGGL(rf_cols_kernel, grid, dim3(256), lds_c, st, *d);
+    GPI_CHECK_LAUNCH();
+    return GPI_OK;
+}

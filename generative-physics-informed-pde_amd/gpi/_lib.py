@@ -27,6 +27,7 @@ EPI_STORE, EPI_STORE_STATS, EPI_GAUSS_LOSS = 0, 1, 2
 HEAD_ENC, HEAD_REPARAM, HEAD_QZ, HEAD_LATENT, HEAD_GP = 0x01, 0x02, 0x04, 0x08, 0x10
 ROM_FORWARD, ROM_LOGLIK, ROM_BACKWARD = 0, 1, 2
 VO_CGR, VO_FLUX = 0x1, 0x2
+FOM_WARM = 1
 VO_TEST_GAUSS, VO_TEST_RBF = 0, 1
 
 i32, i64, f32, u64 = C.c_int32, C.c_int64, C.c_float, C.c_uint64
@@ -139,9 +140,19 @@ class StepEpilogueDesc(C.Structure):
                 ('n_idx', i64)]
 
 
+class FomDesc(C.Structure):
+    _fields_ = [('n_fine', i32), ('n', i32), ('flags', i32), ('max_iter', i32), ('logkappa', vp), ('bc', vp),
+                ('rtol', C.c_double), ('y', vp), ('work', vp), ('iters', vp), ('flag', vp)]
+
+
+class RandomFieldDesc(C.Structure):
+    _fields_ = [('py', i32), ('px', i32), ('n', i32), ('pad0', i32), ('mean', C.c_double), ('stddev', C.c_double),
+                ('ly', vp), ('lxt', vp), ('scale', vp), ('gamma', vp), ('seed', u64), ('sub', u64), ('work', vp), ('x', vp)]
+
+
 STRUCTS = [Stat, Groups, ConvDesc, CodecCtx, ReduceItem, HeadDesc, GemmItem, RomDesc, ResidualDesc, AdamDesc,
            VoQueryDesc, VoMomentsDesc, VoConditionDesc, VoPrecisionDesc, GpSampleDesc,
-           VoGalerkinDesc, StepEpilogueDesc]
+           VoGalerkinDesc, StepEpilogueDesc, FomDesc, RandomFieldDesc]
 
 # name -> (restype, argtypes)
 SIGNATURES = {
@@ -162,6 +173,9 @@ SIGNATURES = {
     'gpi_grad_finalize': (C.c_int, [vp, vp, i64, C.c_int, vp, vp]),
     'gpi_adam': (C.c_int, [C.POINTER(AdamDesc), vp]),
     'gpi_step_epilogue': (C.c_int, [C.POINTER(StepEpilogueDesc), vp]),
+    'gpi_fom_workspace': (i64, [i32]),
+    'gpi_fom_solve': (C.c_int, [C.POINTER(FomDesc), vp]),
+    'gpi_random_field': (C.c_int, [C.POINTER(RandomFieldDesc), vp]),
     'gpi_randn': (C.c_int, [vp, i64, u64, vp, u64, vp]),
     'gpi_rng_advance': (C.c_int, [vp, u64, vp]),
     'gpi_random_subset': (C.c_int, [vp, i32, i32, u64, vp, u64, vp]),

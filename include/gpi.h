@@ -448,6 +448,48 @@ int gpi_rng_advance(uint64_t* offset, uint64_t by, void* stream);
 /* Uniform random subset (randperm(n)[:k] semantics, utils/data.py:444). */
 int gpi_random_subset(int32_t* out, int32_t n, int32_t k, uint64_t seed, const uint64_t* offset, uint64_t sub, void* stream);
 
+/* ---- FOM data generation (setup side; reference utils/data.py:72-103 DataLoader.assemble ->
+ * physics/LinearElliptic.py:85-101 solve, one PETSc LU per sample).  Batched Jacobi-preconditioned
+ * conjugate gradients (Chronopoulos-Gear form: one fused reduction per iteration) on the matrix-free
+ * 5-point stencil of the NDP problem, one workgroup per sample, fp64 throughout. */
+#define GPI_FOM_WARM 1   /* y holds the initial guess (default: linear interpolation of the BCs in x) */
+typedef struct gpi_fom_desc {
+    int32_t n_fine;            /* squares per side */
+    int32_t n;                 /* samples */
+    int32_t flags;             /* GPI_FOM_* */
+    int32_t max_iter;
+    const double* logkappa;    /* [n, 2 n_fine^2] DG0 log-conductivity (X_DG layout, cells 2q / 2q+1, q = i + n_fine j) */
+    const double* bc;          /* [n, 4] NDP u0..u3 */
+    double rtol;               /* stop at ||b - A y|| <= rtol ||b|| (recurrence residual) */
+    double* y;                 /* [n, d_y] free-node solution */
+    double* work;              /* [n, gpi_fom_workspace(n_fine)] caller-owned scratch */
+    int32_t* iters;            /* [n] iterations used, or NULL */
+    int32_t* flag;             /* [1] += samples not converged within max_iter, or NULL */
+} gpi_fom_desc;
+int64_t gpi_fom_workspace(int32_t n_fine);   /* doubles per sample */
+int gpi_fom_solve(const gpi_fom_desc* d, void* stream);
+
+/* Separable Gaussian random field (physics/RandomField.py:162-209 on the tensor grid of pixel
+ * centres): the squared-exponential covariance is sigma^2 C_y (x) C_x, whose eigenpairs are products
+ * of the 1-D ones, so the reference's KL sampler (eigh of the dense C + 1e-12 I, optional truncation)
+ * is x[b] = mean + stddev * L_y (S o G_b) L_x^T with L = the 1-D eigenvectors and S[i,j] =
+ * sqrt(sigma^2 lambda_i mu_j + 1e-12) on the retained modes, 0 elsewhere.  G_b ~ N(0, I) given, or
+ * drawn with Philox(seed, counter b * ceil(py px / 4) + q, sub): 4 fp64 Box-Muller normals per counter. */
+typedef struct gpi_random_field_desc {
+    int32_t py, px;
+    int32_t n;
+    int32_t pad0;
+    double mean, stddev;
+    const double* ly;          /* [py, py] */
+    const double* lxt;         /* [px, px] = L_x^T */
+    const double* scale;       /* [py, px] S, or NULL (all ones) */
+    const double* gamma;       /* [n, py, px] or NULL */
+    uint64_t seed, sub;
+    double* work;              /* [n, py, px] scratch ((S o G) L_x^T) */
+    double* x;                 /* [n, py, px] */
+} gpi_random_field_desc;
+int gpi_random_field(const gpi_random_field_desc* d, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -14,6 +14,8 @@ fem      generic P1 finite-element restatement (numpy, fp64) of the FEniCS
 elbo     numpy/torch restatement of the reference's ELBO algebra: Gaussian
          log-likelihood, KL, reparametrisation, the ROM solve with
          Dirichlet-row replacement and the virtual-observable conditioning.
+field    dense restatement of the reference's random-field sampler (covariance,
+         KL / Cholesky factor with the adaptive truncation).
 codec    torch.nn.functional restatement of the DenseNet conv encoder /
          decoder (train-mode BatchNorm) used as the fp32 reference for the
          HIP codec kernels.

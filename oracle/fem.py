@@ -135,6 +135,24 @@ def assemble_stiffness(mesh, kappa_cells):
     return K
 
 
+def apply_stiffness(mesh, kappa_cells, u_full):
+    """K u without forming K: vectorised element loop (same element algebra as
+    assemble_stiffness), usable at 128^2 / 256^2 where a dense K does not fit."""
+    P = mesh.coords[mesh.cells]                              # [nc, 3, 2]
+    x0, y0 = P[:, 0, 0], P[:, 0, 1]
+    x1, y1 = P[:, 1, 0], P[:, 1, 1]
+    x2, y2 = P[:, 2, 0], P[:, 2, 1]
+    det = (x1 - x0) * (y2 - y0) - (x2 - x0) * (y1 - y0)
+    g = np.stack([np.stack([y1 - y2, x2 - x1], -1), np.stack([y2 - y0, x0 - x2], -1),
+                  np.stack([y0 - y1, x1 - x0], -1)], 1) / det[:, None, None]
+    Ke = (0.5 * np.abs(det) * np.asarray(kappa_cells, dtype=np.float64))[:, None, None] * np.einsum(
+        'cad,cbd->cab', g, g)
+    contrib = np.einsum('cab,cb->ca', Ke, np.asarray(u_full, dtype=np.float64)[mesh.cells])
+    out = np.zeros(mesh.num_vertices)
+    np.add.at(out, mesh.cells, contrib)
+    return out
+
+
 def rom_stiffness_tensor(mesh):
     """M[:, :, t] = d a / d kappa_t  (bottleneck/ROM.py:46-53)."""
     nv = mesh.num_vertices
@@ -182,6 +200,16 @@ def solve_fom(mesh, kappa_cells, u_bc):
     """FOM label y on free dofs (physics/LinearElliptic.py:85-101)."""
     K, f = assemble_system(mesh, kappa_cells, u_bc)
     return np.linalg.solve(K, f)
+
+
+def fom_residual(mesh, kappa_cells, u_bc, y_free):
+    """(K yhat)_free = K_ff y - f_eff with yhat = y on the free nodes, g on the Dirichlet nodes
+    (the FOM residual of physics/LinearElliptic.py:137-159, f = 0), any mesh size."""
+    c, fr = dirichlet_split(mesh)
+    u = np.zeros(mesh.num_vertices)
+    u[c] = dirichlet_values(mesh, c, u_bc)
+    u[fr] = y_free
+    return apply_stiffness(mesh, kappa_cells, u)[fr]
 
 
 def full_solution(mesh, y_free, u_bc):

@@ -14,7 +14,7 @@ HEADER = os.path.join(ROOT, 'include', 'gpi.h')
 
 def declared():
     src = open(HEADER).read()
-    return sorted(set(re.findall(r'^\s*(?:int|const char\s*\*)\s+(gpi_\w+)\s*\(', src, re.M)))
+    return sorted(set(re.findall(r'^\s*(?:int|int64_t|const char\s*\*)\s+(gpi_\w+)\s*\(', src, re.M)))
 
 
 @pytest.fixture(scope='module')
@@ -72,3 +72,13 @@ def test_vo_rows_host_query(lib):
     assert L.gpi_vo_rows(32, 4, lib.VO_CGR | lib.VO_FLUX) == 25 + 32
     assert L.gpi_vo_rows(64, 7, lib.VO_CGR) < 0        # fine grid must refine the coarse one
     assert L.gpi_vo_rows(64, 8, 0) < 0
+
+
+def test_fom_workspace_host_query(lib):
+    L = lib.lib()
+    assert L.gpi_fom_workspace(64) == 2 * 64 * 65 + 6 * 65 * 63
+    assert L.gpi_fom_workspace(1) < 0
+    d = lib.FomDesc()                   # missing buffers -> argument error, nothing launched
+    assert L.gpi_fom_solve(C.byref(d), None) != 0
+    r = lib.RandomFieldDesc()
+    assert L.gpi_random_field(C.byref(r), None) != 0
