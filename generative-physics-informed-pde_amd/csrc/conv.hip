@@ -143,9 +143,13 @@ bool conv_geom(const gpi_conv_desc& d, const gpi_groups& g, ConvGeom& G, bool fw
     if (g.start[0] != 0 || B <= 0) return false;
     // output pixels per tile (taller backward tiles only pay on planes >= 64 wide: measured);
     // GPI_TILE_FWD / GPI_TILE_BWD / GPI_TILE_S2 override the targets (tuning runs only)
+    // Stride 2: the single-channel input conv (no input gradient) takes larger tiles, the backward of
+    // the transition convs small ones (more workgroups for the parity-class input gradient).
     static const int t_fwd = env_int("GPI_TILE_FWD", 512), t_bwd = env_int("GPI_TILE_BWD", 512),
-                     t_s2 = env_int("GPI_TILE_S2", 128);
-    const int target = d.stride == 2 ? t_s2 : (!fwd && d.w_out >= 64 ? t_bwd : (fwd ? t_fwd : 256));
+                     t_s2 = env_int("GPI_TILE_S2", 128), t_s2b = env_int("GPI_TILE_S2B", 64),
+                     t_s2c1 = env_int("GPI_TILE_S2C1", 256);
+    const int target = d.stride == 2 ? (d.cin == 1 ? t_s2c1 : (fwd ? t_s2 : t_s2b))
+                                     : (!fwd && d.w_out >= 64 ? t_bwd : (fwd ? t_fwd : 256));
     G.th = target / d.w_out;
     if (G.th < 1) G.th = 1;
     if (G.th > d.h_out) G.th = d.h_out;
@@ -811,9 +815,59 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(gpi_conv_desc d, gpi_code
     const int J = d.cin * KK;
     const int rowlen = d.cout * J + (d.in_bn ? 2 * d.cin : 0);
     float* slab = c.wpart + d.wpart_off + (int64_t)blockIdx.x * rowlen;
+    // single-channel 7x7 / stride-2 input conv: VALU weight gradient (the MFMA form below would
+    // compute ~6x the useful products: zero-interleaved stride-2 columns, 42 x 7 padded to 48 x 16)
+    const bool vwg = K == 7 && S == 2 && !UP && d.cin == 1 && !has_gin;
+    if constexpr (K == 7 && S == 2 && !UP) {
+        if (vwg && !(G.dbg & 1)) {
+            // lane: 4 consecutive output pixels of the tile; wave: kernel row ky; 4 output channels
+            // per pass (acc 4 x 7); one register window of 16 input columns per lane and row
+            constexpr int PADC = K / 2, CH = 4;
+            const int tp = G.th * d.w_out;
+            for (int ky = wv; ky < K; ky += 4) {
+                for (int c0 = 0; c0 < d.cout; c0 += CH) {
+                    float acc[CH * K];
+#pragma unroll
+                    for (int a = 0; a < CH * K; ++a) acc[a] = 0.f;
+                    for (int q = lane; 4 * q < tp; q += 64) {
+                        const int p0 = 4 * q;
+                        const int ty = dq(p0, G.d_wout), ox0 = p0 - ty * d.w_out;
+                        // input columns 2 ox0 - 4 .. 2 ox0 + 11 of row 2 ty + ky (16-B aligned)
+                        const float* xr = al + (ty * S + ky) * G.P + HALO + S * ox0 - 4;
+                        float xv[16];
+#pragma unroll
+                        for (int v = 0; v < 4; ++v) {
+                            const float4 t = *reinterpret_cast<const float4*>(xr + 4 * v);
+                            xv[4 * v] = t.x; xv[4 * v + 1] = t.y; xv[4 * v + 2] = t.z; xv[4 * v + 3] = t.w;
+                        }
+                        const float* gr = gl + (T.oy0 + ty - gy0) * G.PG + HALO + ox0;
+#pragma unroll
+                        for (int a = 0; a < CH; ++a) {
+                            if (c0 + a < d.cout) {
+                                const float4 g4 = *reinterpret_cast<const float4*>(gr + (c0 + a) * gplane);
+                                const float g[4] = {g4.x, g4.y, g4.z, g4.w};
+#pragma unroll
+                                for (int j = 0; j < 4; ++j)
+#pragma unroll
+                                    for (int b = 0; b < K; ++b)
+                                        acc[a * K + b] = fmaf(g[j], xv[2 * j + b + 4 - PADC], acc[a * K + b]);
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int a = 0; a < CH; ++a)
+#pragma unroll
+                        for (int b = 0; b < K; ++b) {
+                            const float v = wave_sum(acc[a * K + b]);
+                            if (lane == 0 && c0 + a < d.cout) slab[(c0 + a) * J + ky * K + b] = v;
+                        }
+                }
+            }
+        }
+    }
     {
         const int MI = d.cout * K, NJ = d.cin * K;
-        const int nmb = (G.dbg & 1) ? 0 : (MI + 15) >> 4, nnb = (NJ + 15) >> 4;
+        const int nmb = ((G.dbg & 1) || vwg) ? 0 : (MI + 15) >> 4, nnb = (NJ + 15) >> 4;
         const int XW = UP ? d.w_out + K - 1 : S * (d.w_out - 1) + K;   // virtual input columns
         const int nxs = (XW + 3) >> 2;
         for (int mb = 0; mb < nmb; ++mb) {
