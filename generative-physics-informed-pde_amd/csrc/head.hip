@@ -27,14 +27,26 @@ __device__ __forceinline__ float block_sum128(float v, float* scratch) {
     return scratch[0] + scratch[1];
 }
 
+// The weight reads are the latency chain of these kernels (one sample per workgroup, weights
+// from L2): each thread issues UL loads before their FMAs.
+constexpr int UL = 16;
+
 // y[j] = b[j] + sum_k W[j*K + k] x[k]
 __device__ __forceinline__ void matvec(const float* __restrict__ W, const float* __restrict__ b, const float* x,
                                        int J, int K, float* y) {
     for (int j = threadIdx.x; j < J; j += HT) {
-        float a = b ? b[j] : 0.f;
+        float a[4] = {b ? b[j] : 0.f, 0.f, 0.f, 0.f};
         const float* w = W + (int64_t)j * K;
-        for (int k = 0; k < K; ++k) a = fmaf(w[k], x[k], a);
-        y[j] = a;
+        int k = 0;
+        for (; k + UL <= K; k += UL) {
+            float wv[UL];
+#pragma unroll
+            for (int u = 0; u < UL; ++u) wv[u] = w[k + u];
+#pragma unroll
+            for (int u = 0; u < UL; ++u) a[u & 3] = fmaf(wv[u], x[k + u], a[u & 3]);
+        }
+        for (; k < K; ++k) a[0] = fmaf(w[k], x[k], a[0]);
+        y[j] = (a[0] + a[1]) + (a[2] + a[3]);
     }
 }
 
@@ -42,9 +54,17 @@ __device__ __forceinline__ void matvec(const float* __restrict__ W, const float*
 __device__ __forceinline__ void matvec_t(const float* __restrict__ W, const float* d, int J, int K, float* y,
                                          bool accumulate) {
     for (int k = threadIdx.x; k < K; k += HT) {
-        float a = accumulate ? y[k] : 0.f;
-        for (int j = 0; j < J; ++j) a = fmaf(W[(int64_t)j * K + k], d[j], a);
-        y[k] = a;
+        float a[4] = {accumulate ? y[k] : 0.f, 0.f, 0.f, 0.f};
+        int j = 0;
+        for (; j + UL <= J; j += UL) {
+            float wv[UL];
+#pragma unroll
+            for (int u = 0; u < UL; ++u) wv[u] = W[(int64_t)(j + u) * K + k];
+#pragma unroll
+            for (int u = 0; u < UL; ++u) a[u & 3] = fmaf(wv[u], d[j + u], a[u & 3]);
+        }
+        for (; j < J; ++j) a[0] = fmaf(W[(int64_t)j * K + k], d[j], a[0]);
+        y[k] = (a[0] + a[1]) + (a[2] + a[3]);
     }
 }
 
