@@ -1300,9 +1300,19 @@ __global__ __launch_bounds__(256) void wgrad_reduce(ReduceArgs a, const float* _
     const int r0 = rc * RROWS, r1 = min(it.blocks, r0 + RROWS);
     float s = 0.f;
     if (p < P) {
+        // 16 slab loads in flight per thread (the reduction is latency-bound, not bandwidth-bound)
         const float* base = wpart + it.part_off + w0 + w;
-#pragma unroll 4
-        for (int r = r0 + p; r < r1; r += P) s += base[(int64_t)r * it.row_stride];
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+        int r = r0 + p;
+        for (; r + 15 * P < r1; r += 16 * P) {
+            float v[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) v[u] = base[(int64_t)(r + u * P) * it.row_stride];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) acc[u & 3] += v[u];
+        }
+        for (; r < r1; r += P) acc[0] += base[(int64_t)r * it.row_stride];
+        s = (acc[0] + acc[1]) + (acc[2] + acc[3]);
     }
     red[tid] = s;
     __syncthreads();

@@ -346,17 +346,20 @@ class ElboEngine(object):
              C.c_void_p(self.ws.t_ws.data_ptr()), st, what='head forward')
         if self.roms:
             # the ROM solve only feeds the head backward: run it on a side stream,
-            # concurrently with the decoder (fork here, join in backward / value)
+            # concurrently with the decoder (fork here, join in backward / value).  The decoder
+            # is enqueued first so that, in a captured graph, the main chain is the fork's first
+            # branch and keeps its hardware queue (each cross-queue dependency costs ~10 us).
             main = torch.cuda.current_stream()
             self._side_stream()
             self._ev_fork.record(main)
+        _run(lib.gpi_codec_forward, self.dec_descs, len(self.dec_descs), C.byref(self.dctx), st,
+             what='decoder forward')
+        if self.roms:
             self._side.wait_event(self._ev_fork)
             for r in self.roms:
                 _run(lib.gpi_rom, C.byref(r), C.c_void_p(self._side.cuda_stream), what='rom')
             self._ev_join.record(self._side)
             self._pending_join = True
-        _run(lib.gpi_codec_forward, self.dec_descs, len(self.dec_descs), C.byref(self.dctx), st,
-             what='decoder forward')
         if compute_value:
             self._join()
             return self.elbo_value()
@@ -428,9 +431,14 @@ class ElboEngine(object):
              C.c_void_p(self.ws.t_ws.data_ptr()), C.c_void_p(self.flat.gacc.data_ptr()), st, what='head backward')
         # the decoder's slab reduction and the dense weight gradients depend only on what is
         # done by now: run them on the side stream, concurrently with the encoder backward
+        # (enqueued after it, so the encoder stays on the main chain's queue in a graph)
         main = torch.cuda.current_stream()
         side = self._side_stream()
         self._ev_fork2.record(main)
+        if self.ep is not None:
+            _run(lib.gpi_codec_backward, self.enc_descs, len(self.enc_descs), C.byref(self.ectx), st,
+                 what='encoder backward')
+            run_reduce(self.reduce_enc, self.ws, self.flat, st)
         side.wait_event(self._ev_fork2)
         sst = C.c_void_p(side.cuda_stream)
         run_reduce(self.reduce_dec, self.ws, self.flat, sst)
@@ -439,10 +447,6 @@ class ElboEngine(object):
         if side_extra is not None:
             side_extra(sst)
         self._ev_join2.record(side)
-        if self.ep is not None:
-            _run(lib.gpi_codec_backward, self.enc_descs, len(self.enc_descs), C.byref(self.ectx), st,
-                 what='encoder backward')
-            run_reduce(self.reduce_enc, self.ws, self.flat, st)
         main.wait_event(self._ev_join2)
 
     def finalize(self, out, accumulate=False, step=None, stream=None, zero_acc=False):
