@@ -145,14 +145,25 @@ bool conv_geom(const gpi_conv_desc& d, const gpi_groups& g, ConvGeom& G, bool fw
     // GPI_TILE_FWD / GPI_TILE_BWD / GPI_TILE_S2 override the targets (tuning runs only)
     // Stride 2: the single-channel input conv (no input gradient) takes larger tiles, the backward of
     // the transition convs small ones (more workgroups for the parity-class input gradient).
-    static const int t_fwd = env_int("GPI_TILE_FWD", 512), t_bwd = env_int("GPI_TILE_BWD", 512),
-                     t_s2 = env_int("GPI_TILE_S2", 128), t_s2b = env_int("GPI_TILE_S2B", 64),
-                     t_s2c1 = env_int("GPI_TILE_S2C1", 256);
+    // Forward: 1024-pixel tiles on planes >= 64 wide, 512 below, halved while the input row image
+    // exceeds 28 KB of LDS (keeps >= 5 workgroups per CU on the wide-channel 32x32 convs).
+    static const int t_fwd = env_int("GPI_TILE_FWD", 512), t_fwd64 = env_int("GPI_TILE_FWD64", 1024),
+                     t_bwd = env_int("GPI_TILE_BWD", 512), t_s2 = env_int("GPI_TILE_S2", 128),
+                     t_s2b = env_int("GPI_TILE_S2B", 64), t_s2c1 = env_int("GPI_TILE_S2C1", 256);
     const int target = d.stride == 2 ? (d.cin == 1 ? t_s2c1 : (fwd ? t_s2 : t_s2b))
-                                     : (!fwd && d.w_out >= 64 ? t_bwd : (fwd ? t_fwd : 256));
+                                     : (fwd ? (d.w_out >= 64 ? t_fwd64 : t_fwd) : (d.w_out >= 64 ? t_bwd : 256));
     G.th = target / d.w_out;
     if (G.th < 1) G.th = 1;
     if (G.th > d.h_out) G.th = d.h_out;
+    if (fwd && d.stride == 1 && !d.upsample) {
+        for (;;) {
+            int y0, rh;
+            in_rows(d.k, 1, 0, d.pad, 0, G.th, y0, rh);
+            const int half = G.th / 2;
+            if (4 * d.cin * rh * (d.w_in + 2 * HALO) <= 28 * 1024 || half < 1 || d.h_out % half) break;
+            G.th = half;
+        }
+    }
     if (d.upsample && G.th < 2) G.th = 2;   // upsampled tiles pair output rows (256-wide planes)
     while (d.h_out % G.th) --G.th;
     if (d.upsample && (G.th & 1)) return false;
