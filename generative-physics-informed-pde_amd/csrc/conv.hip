@@ -144,16 +144,16 @@ bool conv_geom(const gpi_conv_desc& d, const gpi_groups& g, ConvGeom& G, bool fw
     // output pixels per tile (taller backward tiles only pay on planes >= 64 wide: measured);
     // GPI_TILE_FWD / GPI_TILE_BWD / GPI_TILE_S2 override the targets (tuning runs only)
     // Stride 2: the single-channel input conv (no input gradient) takes larger tiles, the backward of
-    // the transition convs small ones (more workgroups for the parity-class input gradient).
+    // the transition convs 4 output rows (more workgroups for the parity-class input gradient).
     // Forward: 1024-pixel tiles on planes >= 64 wide, 512 below, halved while the input row image
     // exceeds 28 KB of LDS (keeps >= 5 workgroups per CU on the wide-channel 32x32 convs).
     // Backward: 8 output rows below 64 wide; 512 px on 64-wide planes, 1024 for the upsampling conv
     // (per-operator sweeps, tools/tile_sweep.sh).
     static const int t_fwd = env_int("GPI_TILE_FWD", 512), t_fwd64 = env_int("GPI_TILE_FWD64", 1024),
                      t_bwd = env_int("GPI_TILE_BWD", 512), t_s2 = env_int("GPI_TILE_S2", 128),
-                     t_s2b = env_int("GPI_TILE_S2B", 64), t_s2c1 = env_int("GPI_TILE_S2C1", 256),
+                     t_s2brows = env_int("GPI_TILE_S2BROWS", 4), t_s2c1 = env_int("GPI_TILE_S2C1", 256),
                      t_bwdup = env_int("GPI_TILE_BWDUP", 1024), t_bwdrows = env_int("GPI_TILE_BWDROWS", 8);
-    const int target = d.stride == 2 ? (d.cin == 1 ? t_s2c1 : (fwd ? t_s2 : t_s2b))
+    const int target = d.stride == 2 ? (d.cin == 1 ? t_s2c1 : (fwd ? t_s2 : t_s2brows * d.w_out))
                                      : (fwd ? (d.w_out >= 64 ? t_fwd64 : t_fwd)
                                             : (d.w_out >= 64 ? (d.upsample ? t_bwdup : t_bwd) : t_bwdrows * d.w_out));
     G.th = target / d.w_out;
