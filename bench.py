@@ -221,6 +221,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step.step()
+    t_enq = time.perf_counter()          # host time to enqueue the K steps (graph launches)
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
@@ -271,6 +272,7 @@ def main():
                        'global_batch': world * per_step, 'grid': physics['fom'].grid.n,
                        'parallelism': 'dp%d' % world, 'graph': not args.no_graph},
             'elbo_last': elbo,
+            'host_enqueue_ms_per_step': round(1e3 * (t_enq - t0) / args.steps, 4),
             'roofline': roof,
             'cpu_baseline': cpu,
         }

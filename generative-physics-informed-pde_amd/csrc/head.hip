@@ -200,9 +200,9 @@ __global__ __launch_bounds__(HT) void head_fwd_kernel(gpi_head_desc d, const flo
 }
 
 __global__ __launch_bounds__(HT) void head_bwd_kernel(gpi_head_desc d, const float* __restrict__ P, float* ws,
-                                                      double* gacc) {
+                                                      double* gacc, int s_off) {
     __shared__ float v0[VMAX], v1[VMAX], v2[VMAX], v3[VMAX];
-    const int s = blockIdx.x;
+    const int s = blockIdx.x + s_off;
     const int tid = threadIdx.x;
     const bool enc = s < d.n_enc;
     const int q = s - d.n_enc;
@@ -360,8 +360,12 @@ extern "C" int gpi_head_forward(const gpi_head_desc* d, const float* params, flo
 extern "C" int gpi_head_backward(const gpi_head_desc* d, const float* params, float* ws, double* gacc,
                                  void* stream) {
     if (!head_ok(d) || !params || !ws || !gacc) return GPI_ERR_ARG;
-    hipLaunchKernelGGL(head_bwd_kernel, dim3(d->n_enc + d->n_q + d->n_q2), dim3(HT), 0, (hipStream_t)stream, *d, params, ws,
-                       gacc);
+    const bool pe = d->flags & GPI_HEAD_PART_ENC, pq = d->flags & GPI_HEAD_PART_Q;
+    if (pe && pq) return GPI_ERR_ARG;
+    const int nq = d->n_q + d->n_q2;
+    const int nb = pe ? d->n_enc : (pq ? nq : d->n_enc + nq), s_off = pq ? d->n_enc : 0;
+    if (nb == 0) return GPI_OK;
+    hipLaunchKernelGGL(head_bwd_kernel, dim3(nb), dim3(HT), 0, (hipStream_t)stream, *d, params, ws, gacc, s_off);
     GPI_CHECK_LAUNCH();
     return GPI_OK;
 }

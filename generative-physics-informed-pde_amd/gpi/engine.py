@@ -426,14 +426,23 @@ class ElboEngine(object):
         st = stream if stream is not None else L.stream_handle()
         _run(lib.gpi_codec_backward, self.dec_descs, len(self.dec_descs), C.byref(self.dctx), st,
              what='decoder backward')
-        self._join()
-        _run(lib.gpi_head_backward, C.byref(self.head), C.c_void_p(self.flat.P.data_ptr()),
-             C.c_void_p(self.ws.t_ws.data_ptr()), C.c_void_p(self.flat.gacc.data_ptr()), st, what='head backward')
+        P_, W_, G_ = (C.c_void_p(self.flat.P.data_ptr()), C.c_void_p(self.ws.t_ws.data_ptr()),
+                      C.c_void_p(self.flat.gacc.data_ptr()))
+        main = torch.cuda.current_stream()
+        side = self._side_stream()
+        # With the ROM still pending on the side stream, only the encoder samples' head backward
+        # runs on the main stream; the variational samples' (which need the ROM adjoint) follow
+        # the ROM on the side stream, so the main chain never waits for the ROM.
+        split = self._pending_join
+        if split:
+            hd = L.HeadDesc.from_buffer_copy(self.head)
+            hd.flags |= L.HEAD_PART_ENC
+            _run(lib.gpi_head_backward, C.byref(hd), P_, W_, G_, st, what='head backward (encoder samples)')
+        else:
+            _run(lib.gpi_head_backward, C.byref(self.head), P_, W_, G_, st, what='head backward')
         # the decoder's slab reduction and the dense weight gradients depend only on what is
         # done by now: run them on the side stream, concurrently with the encoder backward
         # (enqueued after it, so the encoder stays on the main chain's queue in a graph)
-        main = torch.cuda.current_stream()
-        side = self._side_stream()
         self._ev_fork2.record(main)
         if self.ep is not None:
             _run(lib.gpi_codec_backward, self.enc_descs, len(self.enc_descs), C.byref(self.ectx), st,
@@ -441,6 +450,11 @@ class ElboEngine(object):
             run_reduce(self.reduce_enc, self.ws, self.flat, st)
         side.wait_event(self._ev_fork2)
         sst = C.c_void_p(side.cuda_stream)
+        if split:
+            hq = L.HeadDesc.from_buffer_copy(self.head)
+            hq.flags |= L.HEAD_PART_Q
+            _run(lib.gpi_head_backward, C.byref(hq), P_, W_, G_, sst, what='head backward (variational samples)')
+            self._pending_join = False          # joined below with the rest of the side work
         run_reduce(self.reduce_dec, self.ws, self.flat, sst)
         _run(lib.gpi_outer_gemm, self.gemm_items, len(self.gemm_items), C.c_void_p(self.ws.t_ws.data_ptr()),
              C.c_void_p(self.flat.gacc.data_ptr()), sst, what='outer gemm')

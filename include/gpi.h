@@ -137,6 +137,10 @@ typedef struct gpi_reduce_item {
 #define GPI_HEAD_QZ       0x04  /* z from q_z params, KL (q samples) */
 #define GPI_HEAD_LATENT   0x08  /* lat = latent_map(z) for all samples */
 #define GPI_HEAD_GP       0x10  /* gp(z), X-sample from q_X, log-lik + entropy (q samples) */
+/* launch subsets (gpi_head_backward): only the encoder samples / only the variational ones, so the
+ * two halves can run on different streams (the variational half needs the ROM adjoint) */
+#define GPI_HEAD_PART_ENC 0x100
+#define GPI_HEAD_PART_Q   0x200
 
 typedef struct gpi_head_desc {
     int32_t flags;
