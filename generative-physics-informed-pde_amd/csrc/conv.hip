@@ -643,7 +643,9 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(gpi_conv_desc d, gpi_code
     const int gimg = img_floats(d.cout, G.gh, G.PG);
     float* gz = gl + gimg;                            // raw z of the output (BN-backward only)
     float* al = gz + (obn ? gimg : 0);                // [cin][rh][P]
-    float* red = al + img_floats(d.cin, G.rh, G.P);
+    // reduction scratch: aliases gz (dead after phase 3) when it is large enough -- 8 KB less LDS
+    // per workgroup, one more resident workgroup per CU on the 32x32 planes
+    float* red = (obn && gimg >= BWD_RED) ? gz : al + img_floats(d.cin, G.rh, G.P);
 
     const int tid = threadIdx.x;
     const int lane = tid & 63, wv = tid >> 6, kq = lane >> 4, l16 = lane & 15;
@@ -1211,8 +1213,9 @@ size_t fwd_lds(const gpi_conv_desc& d, const ConvGeom& G, int cp) {
 size_t bwd_lds(const gpi_conv_desc& d, const ConvGeom& G) {
     const int KD4 = (d.cout * d.k * d.k + 3) & ~3;
     const int gimg = img_floats(d.cout, G.gh, G.PG);
+    const bool alias = d.gout_mode == 0 && gimg >= BWD_RED;   // red inside gz (conv_bwd_kernel)
     size_t f = (size_t)pad256(BWD_HDR) + (d.gin_off >= 0 ? pad256(KD4 * 16) + pad256((d.stride == 2 ? 8 : 1) * KD4) : 0) + gimg +
-               (d.gout_mode == 0 ? gimg : 0) + img_floats(d.cin, G.rh, G.P) + BWD_RED;
+               (d.gout_mode == 0 ? gimg : 0) + img_floats(d.cin, G.rh, G.P) + (alias ? 0 : BWD_RED);
     return f * sizeof(float);
 }
 
