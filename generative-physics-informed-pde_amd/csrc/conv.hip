@@ -616,6 +616,11 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
 
 // header floats: gst fp64 [4*(MAX_CIN+MAX_COUT)] | i_sc i_sh i_mean i_inv i_gam [MAX_CIN] | o_coef [4*MAX_COUT]
 constexpr int BWD_HDR = 8 * (GPI_MAX_CIN + GPI_MAX_COUT) + 5 * GPI_MAX_CIN + 4 * GPI_MAX_COUT;
+template <bool B>
+struct BoolC {
+    static constexpr bool value = B;
+};
+
 constexpr int BWD_RED = 2048;   // [4 waves][2 column blocks][4][64] partial dW / per-wave channel sums
 
 template <int K, int S, int UP>
@@ -899,62 +904,87 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(gpi_conv_desc d, gpi_code
                     ci[u] = min(j / K, d.cin - 1);
                     ky[u] = j - (j / K) * K;
                 }
-                f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-                for (int ty = wv; ty < G.th; ty += 4) {
-                    const float* grow = gl + (co * G.gh + (T.oy0 + ty - gy0)) * G.PG + HALO - kx;
-                    const float* brow[2];
+                // the second column block is a compile-time branch around the whole row loop, so the
+                // accumulators stay in the MFMA registers (a runtime branch inside the loop made the
+                // compiler copy them in and out of AGPRs around every MFMA)
+                f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+                auto rows = [&](auto two_c) {
+                    constexpr bool TWO = decltype(two_c)::value;
+                    for (int ty = wv; ty < G.th; ty += 4) {
+                        const float* grow = gl + (co * G.gh + (T.oy0 + ty - gy0)) * G.PG + HALO - kx;
+                        const float* brow[2];
 #pragma unroll
-                    for (int u = 0; u < 2; ++u) {
-                        const int ry = UP ? fdiv2(T.oy0 + ty - d.pad + ky[u]) - iy0 : ty * S + ky[u];
-                        brow[u] = al + (ci[u] * G.rh + ry) * G.P + HALO;
-                    }
-                    // operands of four steps are read before their MFMAs (the loop is
-                    // latency-bound otherwise: LDS read -> dependent MFMA each step)
-                    if (UP) {
-                        // nearest x2 upsampling: virtual columns 2p + pad and 2p + pad + 1 both read
-                        // input column p, so their gradient columns are summed first and the
-                        // reduction runs over the (half as many) input columns p
-                        const int plo = fdiv2(-d.pad), nps = (fdiv2(XW - 1 - d.pad) - plo + 4) >> 2;
-                        int ps = 0;
-                        for (; ps + 4 <= nps; ps += 4) {
-                            float a[4], b0[4], b1[4];
+                        for (int u = 0; u < 2; ++u) {
+                            const int ry = UP ? fdiv2(T.oy0 + ty - d.pad + ky[u]) - iy0 : ty * S + ky[u];
+                            brow[u] = al + (ci[u] * G.rh + ry) * G.P + HALO;
+                        }
+                        // operands of four steps are read before their MFMAs (LDS read -> dependent
+                        // MFMA would serialise every step)
+                        if constexpr (UP != 0) {
+                            // nearest x2 upsampling: virtual columns 2p + pad and 2p + pad + 1 both read
+                            // input column p, so their gradient columns are summed first and the
+                            // reduction runs over the (half as many) input columns p
+                            const int plo = fdiv2(-d.pad), nps = (fdiv2(XW - 1 - d.pad) - plo + 4) >> 2;
+                            int ps = 0;
+                            for (; ps + 4 <= nps; ps += 4) {
+                                float a[4], b0[4], b1[4];
 #pragma unroll
-                            for (int u = 0; u < 4; ++u) {
-                                const int pc = plo + 4 * (ps + u) + kq;
+                                for (int u = 0; u < 4; ++u) {
+                                    const int pc = plo + 4 * (ps + u) + kq;
+                                    const int xv = 2 * pc + d.pad;
+                                    a[u] = grow[xv] + grow[xv + 1];
+                                    b0[u] = brow[0][pc];
+                                    if (TWO) b1[u] = brow[1][pc];
+                                }
+#pragma unroll
+                                for (int u = 0; u < 4; ++u) {
+                                    acc0 = mfma4(a[u], b0[u], acc0);
+                                    if (TWO) acc1 = mfma4(a[u], b1[u], acc1);
+                                }
+                            }
+                            for (; ps < nps; ++ps) {
+                                const int pc = plo + 4 * ps + kq;
                                 const int xv = 2 * pc + d.pad;
-                                a[u] = grow[xv] + grow[xv + 1];
-                                b0[u] = brow[0][pc];
-                                b1[u] = two ? brow[1][pc] : 0.f;
+                                const float a = grow[xv] + grow[xv + 1];
+                                acc0 = mfma4(a, brow[0][pc], acc0);
+                                if (TWO) acc1 = mfma4(a, brow[1][pc], acc1);
                             }
-#pragma unroll
-                            for (int u = 0; u < 4; ++u) {
-                                acc[0] = mfma4(a[u], b0[u], acc[0]);
-                                if (two) acc[1] = mfma4(a[u], b1[u], acc[1]);
-                            }
-                        }
-                        for (; ps < nps; ++ps) {
-                            const int pc = plo + 4 * ps + kq;
-                            const int xv = 2 * pc + d.pad;
-                            const float a = grow[xv] + grow[xv + 1];
-                            acc[0] = mfma4(a, brow[0][pc], acc[0]);
-                            if (two) acc[1] = mfma4(a, brow[1][pc], acc[1]);
-                        }
-                        continue;
-                    }
-                    int xs = 0;                    for (; xs < nxs; ++xs) {
-                        const int xv = 4 * xs + kq;
-                        float a;
-                        if (S == 2) {
-                            const int t2 = xv - kx;
-                            a = (t2 & 1) ? 0.f : grow[kx + (t2 >> 1)];
                         } else {
-                            a = grow[xv];
+                            auto a_at = [&](int xv) -> float {
+                                if (S == 2) {
+                                    const int t2 = xv - kx;
+                                    return (t2 & 1) ? 0.f : grow[kx + (t2 >> 1)];
+                                }
+                                return grow[xv];
+                            };
+                            int xs = 0;
+                            for (; xs + 4 <= nxs; xs += 4) {
+                                float a[4], b0[4], b1[4];
+#pragma unroll
+                                for (int u = 0; u < 4; ++u) {
+                                    const int xv = 4 * (xs + u) + kq;
+                                    a[u] = a_at(xv);
+                                    b0[u] = brow[0][xv - d.pad];
+                                    if (TWO) b1[u] = brow[1][xv - d.pad];
+                                }
+#pragma unroll
+                                for (int u = 0; u < 4; ++u) {
+                                    acc0 = mfma4(a[u], b0[u], acc0);
+                                    if (TWO) acc1 = mfma4(a[u], b1[u], acc1);
+                                }
+                            }
+                            for (; xs < nxs; ++xs) {
+                                const int xv = 4 * xs + kq;
+                                const float a = a_at(xv);
+                                acc0 = mfma4(a, brow[0][xv - d.pad], acc0);
+                                if (TWO) acc1 = mfma4(a, brow[1][xv - d.pad], acc1);
+                            }
                         }
-                        const int ix = UP ? fdiv2(xv - d.pad) : xv - d.pad;
-                        acc[0] = mfma4(a, brow[0][ix], acc[0]);
-                        if (two) acc[1] = mfma4(a, brow[1][ix], acc[1]);
                     }
-                }
+                };
+                if (two) rows(BoolC<true>{});
+                else rows(BoolC<false>{});
+                const f32x4 acc[2] = {acc0, acc1};
                 // fixed-order sum of the four waves' partial tiles
 #pragma unroll
                 for (int u = 0; u < 2; ++u)
