@@ -447,7 +447,7 @@ __device__ __forceinline__ void activate_img(float* img, const ConvGeom& G, cons
 constexpr int FWD_HDR = 8 * GPI_MAX_CIN + 2 * GPI_MAX_CIN + 64 + 16;
 
 template <int K, int S, int UP, int CP>
-__global__ __launch_bounds__(256) void conv_fwd_kernel(gpi_conv_desc d, gpi_codec_ctx c, ConvGeom G) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void conv_fwd_kernel(gpi_conv_desc d, gpi_codec_ctx c, ConvGeom G) {
     constexpr int KK = K * K;
     extern __shared__ __attribute__((aligned(16))) float smem[];
     double* gst = (double*)smem;
@@ -624,7 +624,7 @@ struct BoolC {
 constexpr int BWD_RED = 2048;   // [4 waves][2 column blocks][4][64] partial dW / per-wave channel sums
 
 template <int K, int S, int UP>
-__global__ __launch_bounds__(256) void conv_bwd_kernel(gpi_conv_desc d, gpi_codec_ctx c, ConvGeom G) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 : 6))) void conv_bwd_kernel(gpi_conv_desc d, gpi_codec_ctx c, ConvGeom G) {
     constexpr int KK = K * K;
     extern __shared__ __attribute__((aligned(16))) float smem[];
     double* gst = (double*)smem;
