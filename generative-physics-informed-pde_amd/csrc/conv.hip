@@ -155,7 +155,8 @@ bool conv_geom(const gpi_conv_desc& d, const gpi_groups& g, ConvGeom& G, bool fw
                      t_bwdup = env_int("GPI_TILE_BWDUP", 1024), t_bwdrows = env_int("GPI_TILE_BWDROWS", 8);
     const int target = d.stride == 2 ? (d.cin == 1 ? t_s2c1 : (fwd ? t_s2 : t_s2brows * d.w_out))
                                      : (fwd ? (d.w_out >= 64 ? t_fwd64 : t_fwd)
-                                            : (d.w_out >= 64 ? (d.upsample ? t_bwdup : t_bwd) : t_bwdrows * d.w_out));
+                                            : (d.upsample && d.w_out >= 32 ? t_bwdup / 64 * min(d.w_out, 64)
+                                                                            : (d.w_out >= 64 ? t_bwd : t_bwdrows * d.w_out)));
     G.th = target / d.w_out;
     if (G.th < 1) G.th = 1;
     if (G.th > d.h_out) G.th = d.h_out;
