@@ -147,8 +147,8 @@ bool conv_geom(const gpi_conv_desc& d, const gpi_groups& g, ConvGeom& G, bool fw
     // the transition convs 4 output rows (more workgroups for the parity-class input gradient).
     // Forward: 1024-pixel tiles on planes >= 64 wide, 512 below, halved while the input row image
     // exceeds 28 KB of LDS (keeps >= 5 workgroups per CU on the wide-channel 32x32 convs).
-    // Backward: 8 output rows below 64 wide; 512 px on 64-wide planes, 1024 for the upsampling conv
-    // (per-operator sweeps, tools/tile_sweep.sh).
+    // Backward: 8 output rows below 64 wide, 512 px on 64-wide planes; the upsampling convs 16 rows on
+    // 32- and 64-wide planes, 1024 px on wider ones (per-operator sweeps with bench.py --kprof).
     static const int t_fwd = env_int("GPI_TILE_FWD", 512), t_fwd64 = env_int("GPI_TILE_FWD64", 1024),
                      t_bwd = env_int("GPI_TILE_BWD", 512), t_s2 = env_int("GPI_TILE_S2", 128),
                      t_s2brows = env_int("GPI_TILE_S2BROWS", 4), t_s2c1 = env_int("GPI_TILE_S2C1", 256),
