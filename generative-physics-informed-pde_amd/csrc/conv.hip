@@ -622,7 +622,7 @@ struct BoolC {
     static constexpr bool value = B;
 };
 
-constexpr int BWD_RED = 2048;   // [4 waves][2 column blocks][4][64] partial dW / per-wave channel sums
+constexpr int BWD_RED = 1024;   // [4 waves][4][64] partial dW of one column block / per-wave channel sums
 
 template <int K, int S, int UP>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 : 6))) void conv_bwd_kernel(gpi_conv_desc d, gpi_codec_ctx c, ConvGeom G) {
@@ -986,24 +986,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 
                 if (two) rows(BoolC<true>{});
                 else rows(BoolC<false>{});
                 const f32x4 acc[2] = {acc0, acc1};
-                // fixed-order sum of the four waves' partial tiles
+                // fixed-order sum of the four waves' partial tiles, one column block at a time
+                // (1024 floats of scratch)
 #pragma unroll
-                for (int u = 0; u < 2; ++u)
+                for (int u = 0; u < 2; ++u) {
+                    if (u == 1 && !two) break;
+                    if (u == 1) __syncthreads();
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) red[((wv * 2 + u) * 4 + r) * 64 + lane] = acc[u][r];
-                __syncthreads();
-                {
+                    for (int r = 0; r < 4; ++r) red[(wv * 4 + r) * 64 + lane] = acc[u][r];
+                    __syncthreads();
                     const int r = tid >> 6, ln = tid & 63;
                     const int i2 = 16 * mb + (ln >> 4) * 4 + r;
-#pragma unroll
-                    for (int u = 0; u < 2; ++u) {
-                        const int j2 = 16 * (nb0 + u) + (ln & 15);
-                        if ((u == 0 || two) && i2 < MI && j2 < NJ) {
-                            const float v = red[((0 * 2 + u) * 4 + r) * 64 + ln] + red[((1 * 2 + u) * 4 + r) * 64 + ln] +
-                                            red[((2 * 2 + u) * 4 + r) * 64 + ln] + red[((3 * 2 + u) * 4 + r) * 64 + ln];
-                            const int co2 = i2 / K, kx2 = i2 - co2 * K, ci2 = j2 / K, ky2 = j2 - ci2 * K;
-                            slab[co2 * J + ci2 * KK + ky2 * K + kx2] = v;
-                        }
+                    const int j2 = 16 * (nb0 + u) + (ln & 15);
+                    if (i2 < MI && j2 < NJ) {
+                        const float v = red[(0 * 4 + r) * 64 + ln] + red[(1 * 4 + r) * 64 + ln] +
+                                        red[(2 * 4 + r) * 64 + ln] + red[(3 * 4 + r) * 64 + ln];
+                        const int co2 = i2 / K, kx2 = i2 - co2 * K, ci2 = j2 / K, ky2 = j2 - ci2 * K;
+                        slab[co2 * J + ci2 * KK + ky2 * K + kx2] = v;
                     }
                 }
                 __syncthreads();
