@@ -145,16 +145,17 @@ bool conv_geom(const gpi_conv_desc& d, const gpi_groups& g, ConvGeom& G, bool fw
     // GPI_TILE_FWD / GPI_TILE_BWD / GPI_TILE_S2 override the targets (tuning runs only)
     // Stride 2: the single-channel input conv (no input gradient) takes larger tiles, the backward of
     // the transition convs 4 output rows (more workgroups for the parity-class input gradient).
-    // Forward: 1024-pixel tiles on planes >= 64 wide, 512 below, halved while the input row image
-    // exceeds 28 KB of LDS (keeps >= 5 workgroups per CU on the wide-channel 32x32 convs).
+    // Forward: 1024-pixel tiles on planes >= 64 wide, 8 rows on 32-wide planes, 512 px below, halved
+    // while the input row image exceeds 28 KB of LDS.
     // Backward: 8 output rows below 64 wide, 512 px on 64-wide planes; the upsampling convs 16 rows on
     // 32- and 64-wide planes, 1024 px on wider ones (per-operator sweeps with bench.py --kprof).
     static const int t_fwd = env_int("GPI_TILE_FWD", 512), t_fwd64 = env_int("GPI_TILE_FWD64", 1024),
                      t_bwd = env_int("GPI_TILE_BWD", 512), t_s2 = env_int("GPI_TILE_S2", 128),
                      t_s2brows = env_int("GPI_TILE_S2BROWS", 4), t_s2c1 = env_int("GPI_TILE_S2C1", 256),
-                     t_bwdup = env_int("GPI_TILE_BWDUP", 1024), t_bwdrows = env_int("GPI_TILE_BWDROWS", 8);
+                     t_bwdup = env_int("GPI_TILE_BWDUP", 1024), t_bwdrows = env_int("GPI_TILE_BWDROWS", 8),
+                     t_fwdrows = env_int("GPI_TILE_FWDROWS", 8);
     const int target = d.stride == 2 ? (d.cin == 1 ? t_s2c1 : (fwd ? t_s2 : t_s2brows * d.w_out))
-                                     : (fwd ? (d.w_out >= 64 ? t_fwd64 : t_fwd)
+                                     : (fwd ? (d.w_out >= 64 ? t_fwd64 : (d.w_out >= 32 ? t_fwdrows * d.w_out : t_fwd))
                                             : (d.upsample && d.w_out >= 32 ? t_bwdup / 64 * min(d.w_out, 64)
                                                                             : (d.w_out >= 64 ? t_bwd : t_bwdrows * d.w_out)));
     G.th = target / d.w_out;
