@@ -8,7 +8,7 @@
 // halo chunks and rows outside the plane read a zero page.  A workgroup runs
 // in four phases so that it pays ONE global round trip before it computes:
 //   1. issue every global read at once: the LDS images (input, output
-//      gradient, BN-backward operand), the weights, the 32 replicas of the BN
+//      gradient, BN-backward operand), the weights, the 16 replicas of the BN
 //      batch sums and the input-gradient operands (registers);
 //   2. BN coefficients from the fp64 sums (train mode, biased variance);
 //   3. activation transforms in LDS, in place (BN + ReLU of the input image,

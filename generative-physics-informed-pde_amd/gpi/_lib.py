@@ -19,7 +19,7 @@ GPI_MAX_CIN = 32
 GPI_MAX_COUT = 8
 GPI_MAX_REDUCE_ITEMS = 48
 GPI_MAX_GEMM_ITEMS = 12
-GPI_REPLICAS = 32
+GPI_REPLICAS = 16
 FINALIZE_ACCUMULATE = 1
 FINALIZE_ZERO = 2
 

@@ -43,7 +43,7 @@ extern "C" {
  * over GPI_REPLICAS copies indexed by workgroup % GPI_REPLICAS so that
  * thousands of workgroups never serialise on one fp64 atomic address; the
  * reader sums the replicas. */
-#define GPI_REPLICAS 32
+#define GPI_REPLICAS 16
 
 /* Conv epilogues */
 #define GPI_EPI_STORE 0        /* store raw output */
