@@ -1325,7 +1325,10 @@ int launch(const gpi_conv_desc& d, const gpi_codec_ctx& c, hipStream_t st, bool 
 // Thread (w, p) sums rows p, p + P, ... of its row chunk for weight w
 // (coalesced: consecutive w read consecutive floats of a slab row), the P
 // partials meet in LDS, one fp64 atomic per weight per workgroup.
-constexpr int RROWS = 64;
+#ifndef GPI_RROWS
+#define GPI_RROWS 64
+#endif
+constexpr int RROWS = GPI_RROWS;
 
 struct ReduceArgs {
     gpi_reduce_item it[GPI_MAX_REDUCE_ITEMS];

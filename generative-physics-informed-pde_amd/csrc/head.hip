@@ -15,7 +15,10 @@ using namespace gpi;
 
 namespace {
 
-constexpr int HT = 128;     // threads per sample
+#ifndef GPI_HEAD_HT
+#define GPI_HEAD_HT 128
+#endif
+constexpr int HT = GPI_HEAD_HT;   // threads per sample
 constexpr int VMAX = 512;   // max vector length
 
 __device__ __forceinline__ float block_sum128(float v, float* scratch) {
@@ -24,7 +27,10 @@ __device__ __forceinline__ float block_sum128(float v, float* scratch) {
     __syncthreads();
     if (lane == 0) scratch[wid] = v;
     __syncthreads();
-    return scratch[0] + scratch[1];
+    float t = scratch[0];
+#pragma unroll
+    for (int w = 1; w < HT / 64; ++w) t += scratch[w];
+    return t;
 }
 
 // The weight reads are the latency chain of these kernels (one sample per workgroup, weights
