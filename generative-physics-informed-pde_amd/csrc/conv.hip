@@ -1257,6 +1257,7 @@ conv_kernel_t pick(int cp, bool fwd) {
     if (!fwd) return conv_bwd_kernel<K, S, UP>;
     if (cp == 2) return conv_fwd_kernel<K, S, UP, 2>;
     if (cp == 4) return conv_fwd_kernel<K, S, UP, 4>;
+    if (cp == 6) return conv_fwd_kernel<K, S, UP, 6>;
     return conv_fwd_kernel<K, S, UP, 8>;
 }
 
@@ -1273,7 +1274,16 @@ conv_kernel_t select_kernel(const gpi_conv_desc& d, int cp, bool fwd) {
     }
 }
 
-int cp_of(int cout) { return cout <= 2 ? 2 : (cout <= 4 ? 4 : 8); }
+// output channels per thread in the forward (accumulators; weights stored with this stride): the
+// 5- and 6-channel 1x1, stride-2 and upsampling convs take 6 (float2 weight reads) instead of padding
+// to 8; the 3x3 stride-1 and 7x7 ones measured faster with 8 (float4 reads)
+int cp_of(const gpi_conv_desc& d) {
+    const int cout = d.cout;
+    if (cout <= 2) return 2;
+    if (cout <= 4) return 4;
+    const bool wide8 = d.k == 7 || (d.k == 3 && d.stride == 1 && !d.upsample);
+    return (cout <= 6 && !wide8) ? 6 : 8;
+}
 
 // Alignment preconditions of the 16-byte operand paths (row images, float4 epilogue).
 bool aligned_ok(const gpi_conv_desc& d, const gpi_codec_ctx& c, bool fwd) {
@@ -1295,7 +1305,7 @@ int launch(const gpi_conv_desc& d, const gpi_codec_ctx& c, hipStream_t st, bool 
     if (!aligned_ok(d, c, fwd)) return GPI_ERR_UNSUPPORTED;
     if (!fwd && d.gin_off >= 0 && ((G.ph * d.w_in) & 15)) return GPI_ERR_UNSUPPORTED;
     if (!fwd && d.gin_off >= 0 && d.stride == 2 && ((d.w_in & 7) || (G.ph & 1))) return GPI_ERR_UNSUPPORTED;
-    const int cp = cp_of(d.cout);
+    const int cp = cp_of(d);
     conv_kernel_t k = select_kernel(d, cp, fwd);
     if (!k) return GPI_ERR_UNSUPPORTED;
     static const float* zero = nullptr;
