@@ -9,8 +9,9 @@
 // (edge conductance c = (kappa_a + kappa_b) / 2 of the two triangles having the edge as a leg), SPD.
 // One workgroup of 1024 threads per sample runs Jacobi-preconditioned CG in the Chronopoulos-Gear
 // form, so that every iteration has ONE fused block reduction ((r,u), (Au,u), (r,r)) and one more
-// barrier (the preconditioned residual u is read by the neighbours' stencil).  The per-sample
-// vectors live in the caller's workspace (L2 / MALL resident at 64^2: 10 doubles per node).
+// barrier (the preconditioned residual u is read by the neighbours' stencil).  Up to 64^2 every
+// vector lives in registers and u in LDS (fom_pcg_reg_kernel); larger grids keep the vectors in the
+// caller's workspace (fom_pcg_kernel).
 //
 // gpi_random_field: separable restatement x = mean + sigma L_y (S o G) L_x^T of the KL sampler (the SE
 // kernel on a tensor grid is C_y (x) C_x), two batched fp64 products with 16-row panels in LDS.
@@ -191,6 +192,142 @@ __global__ __launch_bounds__(FT) void fom_pcg_kernel(gpi_fom_desc d, FomGeom G) 
     }
 }
 
+// Register-resident variant for grids whose free nodes fit NPT per thread (n <= 64 at NPT = 4): the
+// iteration vectors x, r, p, s, w live in registers; the stencil operand u, the conductances and the
+// Jacobi scaling in LDS -- no global traffic inside the iteration.  Same algorithm, same per-thread
+// node order and reduction order as fom_pcg_kernel.
+template <int NPT>
+__global__ __launch_bounds__(FT) void fom_pcg_reg_kernel(gpi_fom_desc d, FomGeom G) {
+    extern __shared__ __attribute__((aligned(16))) double sm[];
+    __shared__ double red[FW * 4];
+    const int f = blockIdx.x, tid = threadIdx.x;
+    const int n = G.n, nm = n - 1, dy = G.dy;
+    double* us = sm;                    // [dy] preconditioned residual (stencil operand)
+    double* dinv = us + dy;             // [dy]
+    double* ch = dinv + dy;             // [(n+1) n]
+    double* cv = ch + G.ne_h;           // [n (n+1)]
+    const double* lk = d.logkappa + (int64_t)f * 2 * n * n;
+    const double* ub = d.bc + 4 * f;
+    double* x = d.y + (int64_t)f * dy;
+    for (int e = tid; e < G.ne_h; e += FT) {
+        const int j = e / n, i = e - j * n;
+        double c = 0.0;
+        if (j < n) c += kc(lk, n, i, j, 0);
+        if (j > 0) c += kc(lk, n, i, j - 1, 1);
+        ch[e] = 0.5 * c;
+    }
+    for (int e = tid; e < G.ne_v; e += FT) {
+        const int j = e / (n + 1), i = e - j * (n + 1);
+        double c = 0.0;
+        if (i < n) c += kc(lk, n, i, j, 1);
+        if (i > 0) c += kc(lk, n, i - 1, j, 0);
+        cv[e] = 0.5 * c;
+    }
+    __syncthreads();
+    double X[NPT], R[NPT], Pd[NPT], Sv[NPT], Wv[NPT];
+    int IJ[NPT];                        // i | j << 16
+    const bool warm = d.flags & GPI_FOM_WARM;
+    auto valid = [&](int k) { return tid + k * FT < dy; };
+    auto node = [&](int k) { return tid + k * FT; };
+    // (K_ff v)_p with v from LDS (Dirichlet columns zero); vp = v at p itself
+    auto apply = [&](int k, double vp) {
+        const int p = node(k), i = IJ[k] & 0xffff, j = IJ[k] >> 16;
+        const double cl = ch[j * n + i - 1], cr = ch[j * n + i];
+        const double cd = j > 0 ? cv[(j - 1) * (n + 1) + i] : 0.0, cu = j < n ? cv[j * (n + 1) + i] : 0.0;
+        double a = (cl + cr + cd + cu) * vp;
+        if (i > 1) a -= cl * us[p - 1];
+        if (i < nm) a -= cr * us[p + 1];
+        if (j > 0) a -= cd * us[p - nm];
+        if (j < n) a -= cu * us[p + nm];
+        return a;
+    };
+    double bb = 0.0;
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+        const int p = valid(k) ? node(k) : 0;
+        const int j = p / nm, i = p - j * nm + 1;
+        IJ[k] = i | (j << 16);
+        Pd[k] = Sv[k] = Wv[k] = R[k] = 0.0;
+        X[k] = 0.0;
+        if (!valid(k)) continue;
+        const double cl = ch[j * n + i - 1], cr = ch[j * n + i];
+        const double cd = j > 0 ? cv[(j - 1) * (n + 1) + i] : 0.0, cu = j < n ? cv[j * (n + 1) + i] : 0.0;
+        dinv[p] = 1.0 / (cl + cr + cd + cu);
+        const double gl = bcv(ub, 0, j, n), gr = bcv(ub, 1, j, n);
+        X[k] = warm ? x[p] : gl + (gr - gl) * ((double)i / (double)n);
+        const double b = (i == 1 ? cl * gl : 0.0) + (i == nm ? cr * gr : 0.0);
+        R[k] = b;                       // b; A x0 subtracted below
+        bb += b * b;
+        us[p] = X[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NPT; ++k)
+        if (valid(k)) R[k] -= apply(k, X[k]);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NPT; ++k)
+        if (valid(k)) us[node(k)] = dinv[node(k)] * R[k];
+    __syncthreads();
+    double v4[4] = {0.0, 0.0, 0.0, bb};
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+        if (!valid(k)) continue;
+        const double u = us[node(k)];
+        Wv[k] = apply(k, u);
+        v4[0] += R[k] * u;
+        v4[1] += Wv[k] * u;
+        v4[2] += R[k] * R[k];
+    }
+    block_sum4(v4, red);
+    const double tol2 = d.rtol * d.rtol * v4[3];
+    double gam = v4[0], alpha = v4[0] / v4[1], beta = 0.0;
+    bool conv = v4[2] <= tol2;
+    int it = 0;
+    while (!conv && it < d.max_iter) {
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+            if (!valid(k)) continue;
+            const int p = node(k);
+            const double u = us[p];
+            Pd[k] = it == 0 ? u : u + beta * Pd[k];
+            Sv[k] = it == 0 ? Wv[k] : Wv[k] + beta * Sv[k];
+            X[k] += alpha * Pd[k];
+            R[k] -= alpha * Sv[k];
+        }
+        __syncthreads();                // every u read before it is overwritten
+#pragma unroll
+        for (int k = 0; k < NPT; ++k)
+            if (valid(k)) us[node(k)] = dinv[node(k)] * R[k];
+        __syncthreads();
+        double q[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+            if (!valid(k)) continue;
+            const double u = us[node(k)];
+            Wv[k] = apply(k, u);
+            q[0] += R[k] * u;
+            q[1] += Wv[k] * u;
+            q[2] += R[k] * R[k];
+        }
+        block_sum4(q, red);
+        ++it;
+        conv = q[2] <= tol2;
+        if (!conv) {
+            beta = q[0] / gam;
+            alpha = q[0] / (q[1] - beta * q[0] / alpha);
+            gam = q[0];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < NPT; ++k)
+        if (valid(k)) x[node(k)] = X[k];
+    if (tid == 0) {
+        if (d.iters) d.iters[f] = it;
+        if (!conv && d.flag) atomicAdd(d.flag, 1);
+    }
+}
+
 // ---------------------------------------------------------------- random field
 constexpr int RB = 16;   // output rows per workgroup
 
@@ -278,7 +415,23 @@ extern "C" int gpi_fom_solve(const gpi_fom_desc* d, void* stream) {
     G.ne_h = (d->n_fine + 1) * d->n_fine;
     G.ne_v = d->n_fine * (d->n_fine + 1);
     G.ws = gpi_fom_workspace(d->n_fine);
-    hipLaunchKernelGGL(fom_pcg_kernel, dim3(d->n), dim3(FT), 0, (hipStream_t)stream, *d, G);
+    const size_t lds = sizeof(double) * (2 * (size_t)G.dy + G.ne_h + G.ne_v);
+    static bool attr = false;
+    if (!attr) {
+        attr = true;
+        if (hipFuncSetAttribute((const void*)fom_pcg_reg_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                150 * 1024) != hipSuccess ||
+            hipFuncSetAttribute((const void*)fom_pcg_reg_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                150 * 1024) != hipSuccess)
+            return GPI_ERR_LAUNCH;
+    }
+    if (G.dy <= FT && lds <= 150 * 1024) {
+        hipLaunchKernelGGL(fom_pcg_reg_kernel<1>, dim3(d->n), dim3(FT), lds, (hipStream_t)stream, *d, G);
+    } else if (G.dy <= 4 * FT && lds <= 150 * 1024) {
+        hipLaunchKernelGGL(fom_pcg_reg_kernel<4>, dim3(d->n), dim3(FT), lds, (hipStream_t)stream, *d, G);
+    } else {
+        hipLaunchKernelGGL(fom_pcg_kernel, dim3(d->n), dim3(FT), 0, (hipStream_t)stream, *d, G);
+    }
     GPI_CHECK_LAUNCH();
     return GPI_OK;
 }
