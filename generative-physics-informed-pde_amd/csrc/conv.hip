@@ -623,6 +623,11 @@ struct BoolC {
     static constexpr bool value = B;
 };
 
+template <int V>
+struct IntC {
+    static constexpr int value = V;
+};
+
 constexpr int BWD_RED = 1024;   // [4 waves][4][64] partial dW of one column block / per-wave channel sums
 
 template <int K, int S, int UP>
@@ -1133,63 +1138,78 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 
             lb[ci] = d.in_bn ? i_sh[cc] + i_mean[cc] * i_sc[cc] : 0.f;
             lr[ci] = d.in_bn ? 1.f / lg[ci] : 0.f;
         }
-        for (int gq = tid; gq < np2; gq += 256) {
-            const int qy = dq(2 * gq, G.d_win), px0 = 2 * gq - qy * d.w_in;
-            const int64_t pix = (int64_t)(py0 + qy) * d.w_in + px0;
-            const int64_t gbase_in = ((int64_t)T.b * d.in_ctot + d.in_c0) * HWi + pix;
-            float acc[4][2];
-#pragma unroll
-            for (int ci = 0; ci < 4; ++ci) acc[ci][0] = acc[ci][1] = 0.f;
-            for (int co = 0; co < d.cout; ++co) {
-#pragma unroll 1
-                for (int ky = 0; ky < K; ++ky) {
-                    const float* grow = gl + co * gplane + (qy + py0 + d.pad - ky - gy0) * G.PG + HALO + px0 +
-                                        d.pad - (K - 1);
-                    float gw[K + 1];
-#pragma unroll
-                    for (int t = 0; t < K + 1; ++t) gw[t] = grow[t];
-#pragma unroll
-                    for (int kx = 0; kx < K; ++kx) {
-                        const f32x4 w4 = *(const f32x4*)(wD + (co * KK + ky * K + kx) * 16);
-#pragma unroll
-                        for (int q = 0; q < 2; ++q) {
-                            const float gv = gw[q + K - 1 - kx];
-                            acc[0][q] = fmaf(w4[0], gv, acc[0][q]);
-                            acc[1][q] = fmaf(w4[1], gv, acc[1][q]);
-                            acc[2][q] = fmaf(w4[2], gv, acc[2][q]);
-                            acc[3][q] = fmaf(w4[3], gv, acc[3][q]);
+        // two channels' accumulators when cin <= 2 (the 5x5 output conv), four otherwise
+        auto vdg_rows = [&](auto ci_c) {
+            constexpr int CI = decltype(ci_c)::value;
+            for (int gq = tid; gq < np2; gq += 256) {
+                const int qy = dq(2 * gq, G.d_win), px0 = 2 * gq - qy * d.w_in;
+                const int64_t pix = (int64_t)(py0 + qy) * d.w_in + px0;
+                const int64_t gbase_in = ((int64_t)T.b * d.in_ctot + d.in_c0) * HWi + pix;
+                float acc[CI][2];
+    #pragma unroll
+                for (int ci = 0; ci < CI; ++ci) acc[ci][0] = acc[ci][1] = 0.f;
+                for (int co = 0; co < d.cout; ++co) {
+    #pragma unroll 1
+                    for (int ky = 0; ky < K; ++ky) {
+                        const float* grow = gl + co * gplane + (qy + py0 + d.pad - ky - gy0) * G.PG + HALO + px0 +
+                                            d.pad - (K - 1);
+                        float gw[K + 1];
+    #pragma unroll
+                        for (int t = 0; t < K + 1; ++t) gw[t] = grow[t];
+    #pragma unroll
+                        for (int kx = 0; kx < K; ++kx) {
+                            float wv[CI];
+                            if constexpr (CI == 4) {
+                                const f32x4 w4 = *(const f32x4*)(wD + (co * KK + ky * K + kx) * 16);
+                                wv[0] = w4[0];
+                                wv[1] = w4[1];
+                                wv[2] = w4[2];
+                                wv[3] = w4[3];
+                            } else {
+                                const float2 w2 = *(const float2*)(wD + (co * KK + ky * K + kx) * 16);
+                                wv[0] = w2.x;
+                                wv[1] = w2.y;
+                            }
+    #pragma unroll
+                            for (int q = 0; q < 2; ++q) {
+                                const float gv = gw[q + K - 1 - kx];
+    #pragma unroll
+                                for (int ci = 0; ci < CI; ++ci) acc[ci][q] = fmaf(wv[ci], gv, acc[ci][q]);
+                            }
                         }
                     }
                 }
-            }
-#pragma unroll
-            for (int ci = 0; ci < 4; ++ci) {
-                if (ci >= d.cin) break;
-                const float* ap = al + (ci * G.rh + (py0 - iy0 + qy)) * G.P + HALO + px0;
-                const float av[2] = {ap[0], ap[1]};
-                float pv[2] = {0.f, 0.f};
-                if (d.gin_accumulate) {
-                    auto pp = as_gld(ws + gin_off + gbase_in + (int64_t)ci * HWi);
-                    pv[0] = pp[0];
-                    pv[1] = pp[1];
-                }
-                float o[2];
-#pragma unroll
-                for (int q = 0; q < 2; ++q) {
-                    if (d.in_bn) {
-                        const float dbn = av[q] > 0.f ? acc[ci][q] : 0.f;
-                        o[q] = pv[q] + lg[ci] * dbn;
-                        vsd[ci] += dbn;
-                        vsdx[ci] += dbn * ((av[q] - lb[ci]) * lr[ci]);
-                    } else {
-                        o[q] = pv[q] + acc[ci][q];
+    #pragma unroll
+                for (int ci = 0; ci < CI; ++ci) {
+                    if (ci >= d.cin) break;
+                    const float* ap = al + (ci * G.rh + (py0 - iy0 + qy)) * G.P + HALO + px0;
+                    const float av[2] = {ap[0], ap[1]};
+                    float pv[2] = {0.f, 0.f};
+                    if (d.gin_accumulate) {
+                        auto pp = as_gld(ws + gin_off + gbase_in + (int64_t)ci * HWi);
+                        pv[0] = pp[0];
+                        pv[1] = pp[1];
                     }
+                    float o[2];
+    #pragma unroll
+                    for (int q = 0; q < 2; ++q) {
+                        if (d.in_bn) {
+                            const float dbn = av[q] > 0.f ? acc[ci][q] : 0.f;
+                            o[q] = pv[q] + lg[ci] * dbn;
+                            vsd[ci] += dbn;
+                            vsdx[ci] += dbn * ((av[q] - lb[ci]) * lr[ci]);
+                        } else {
+                            o[q] = pv[q] + acc[ci][q];
+                        }
+                    }
+                    auto op = as_gst(ws + gin_off + gbase_in + (int64_t)ci * HWi);
+                    op[0] = o[0];
+                    op[1] = o[1];
                 }
-                auto op = as_gst(ws + gin_off + gbase_in + (int64_t)ci * HWi);
-                op[0] = o[0];
-                op[1] = o[1];
             }
-        }
+        };
+        if (d.cin <= 2) vdg_rows(IntC<2>{});
+        else vdg_rows(IntC<4>{});
     }
     PHASE(6);
     if (d.in_bn) {
