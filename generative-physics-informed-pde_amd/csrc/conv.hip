@@ -844,54 +844,52 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 
     const int J = d.cin * KK;
     const int rowlen = d.cout * J + (d.in_bn ? 2 * d.cin : 0);
     float* slab = c.wpart + d.wpart_off + (int64_t)blockIdx.x * rowlen;
-    // single-channel 7x7 / stride-2 input conv: VALU weight gradient (the MFMA form below would
-    // compute ~6x the useful products: zero-interleaved stride-2 columns, 42 x 7 padded to 48 x 16)
-    const bool vwg = K == 7 && S == 2 && !UP && d.cin == 1 && !has_gin;
+    // single-channel 7x7 / stride-2 input conv: weight gradient with the reduction over the tile's
+    // output pixels (M = cout, N = the 49 taps in 4 column blocks, K = pixels), no zero-interleaved
+    // stride-2 columns (the column-shift form below would compute ~6x the useful products here)
+    const bool vwg = K == 7 && S == 2 && !UP && d.cin == 1 && !has_gin && d.cout <= 16;
     if constexpr (K == 7 && S == 2 && !UP) {
         if (vwg && !(G.dbg & 1)) {
-            // lane: 4 consecutive output pixels of the tile; wave: kernel row ky; 4 output channels
-            // per pass (acc 4 x 7); one register window of 16 input columns per lane and row
-            constexpr int PADC = K / 2, CH = 4;
+            constexpr int PADC = K / 2, NB = (KK + 15) / 16;
             const int tp = G.th * d.w_out;
-            for (int ky = wv; ky < K; ky += 4) {
-                for (int c0 = 0; c0 < d.cout; c0 += CH) {
-                    float acc[CH * K];
+            const int co_a = min(l16, d.cout - 1);                  // A row (rows >= cout never stored)
+            int tap_off[NB];                                        // B column: tap (ky, kx) of this lane
 #pragma unroll
-                    for (int a = 0; a < CH * K; ++a) acc[a] = 0.f;
-                    for (int q = lane; 4 * q < tp; q += 64) {
-                        const int p0 = 4 * q;
-                        const int ty = dq(p0, G.d_wout), ox0 = p0 - ty * d.w_out;
-                        // input columns 2 ox0 - 4 .. 2 ox0 + 11 of row 2 ty + ky (16-B aligned)
-                        const float* xr = al + (ty * S + ky) * G.P + HALO + S * ox0 - 4;
-                        float xv[16];
+            for (int nb = 0; nb < NB; ++nb) {
+                const int j = min(16 * nb + l16, KK - 1), ky = j / K, kx = j - ky * K;
+                tap_off[nb] = ky * G.P + kx - PADC;
+            }
+            f32x4 acc[NB];
 #pragma unroll
-                        for (int v = 0; v < 4; ++v) {
-                            const float4 t = *reinterpret_cast<const float4*>(xr + 4 * v);
-                            xv[4 * v] = t.x; xv[4 * v + 1] = t.y; xv[4 * v + 2] = t.z; xv[4 * v + 3] = t.w;
-                        }
-                        const float* gr = gl + (T.oy0 + ty - gy0) * G.PG + HALO + ox0;
+            for (int nb = 0; nb < NB; ++nb) acc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+            const float* gco = gl + co_a * gplane + (T.oy0 - gy0) * G.PG + HALO;
+            for (int ps = wv; 4 * ps < tp; ps += 4) {               // 4 output pixels per step, wave-strided
+                const int px = 4 * ps + kq;
+                const int ty = dq(px, G.d_wout), ox = px - ty * d.w_out;
+                const float a = gco[ty * G.PG + ox];
+                const float* xb = al + (ty * S) * G.P + HALO + S * ox;
+                float bv[NB];
 #pragma unroll
-                        for (int a = 0; a < CH; ++a) {
-                            if (c0 + a < d.cout) {
-                                const float4 g4 = *reinterpret_cast<const float4*>(gr + (c0 + a) * gplane);
-                                const float g[4] = {g4.x, g4.y, g4.z, g4.w};
+                for (int nb = 0; nb < NB; ++nb) bv[nb] = xb[tap_off[nb]];
 #pragma unroll
-                                for (int j = 0; j < 4; ++j)
+                for (int nb = 0; nb < NB; ++nb) acc[nb] = mfma4(a, bv[nb], acc[nb]);
+            }
+            // fixed-order sum of the four waves' tiles, one column block at a time
 #pragma unroll
-                                    for (int b = 0; b < K; ++b)
-                                        acc[a * K + b] = fmaf(g[j], xv[2 * j + b + 4 - PADC], acc[a * K + b]);
-                            }
-                        }
-                    }
+            for (int nb = 0; nb < NB; ++nb) {
+                if (nb > 0) __syncthreads();
 #pragma unroll
-                    for (int a = 0; a < CH; ++a)
-#pragma unroll
-                        for (int b = 0; b < K; ++b) {
-                            const float v = wave_sum(acc[a * K + b]);
-                            if (lane == 0 && c0 + a < d.cout) slab[(c0 + a) * J + ky * K + b] = v;
-                        }
+                for (int r = 0; r < 4; ++r) red[(wv * 4 + r) * 64 + lane] = acc[nb][r];
+                __syncthreads();
+                const int r = tid >> 6, ln = tid & 63;
+                const int co2 = (ln >> 4) * 4 + r, j2 = 16 * nb + (ln & 15);
+                if (co2 < d.cout && j2 < KK) {
+                    const float v = red[(0 * 4 + r) * 64 + ln] + red[(1 * 4 + r) * 64 + ln] +
+                                    red[(2 * 4 + r) * 64 + ln] + red[(3 * 4 + r) * 64 + ln];
+                    slab[co2 * J + j2] = v;
                 }
             }
+            __syncthreads();
         }
     }
     {
