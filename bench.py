@@ -44,6 +44,10 @@ CONFIGS = {
 }
 
 
+# BASELINE.json configs each bench configuration corresponds to (c64: 2 at N = 1, 3 at N = 8)
+CONFIG_TAG = {'c32': '1', 'c64': '2/3', 'c128': '4', 'c256': '5'}
+
+
 def make_data(fac, n, pool, N_s, field, seed, device):
     from physics.RandomField import NormalRandomFieldSampler
     from physics.grid import pixel_to_cells
@@ -266,8 +270,8 @@ def main():
             'value': round(value, 1), 'unit': 'samples/s', 'n_gpus': world, 'steps': args.steps,
             'warmup': args.warmup, 'ms_per_step': round(1e3 * dt / args.steps, 4), 'higher_is_better': True,
             'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32', 'data': 'synthetic',
-            'config': {'workload': 'BASELINE config 2/3: %s grid, B_u=%d unlabeled + N_s=%d labeled per GPU, '
-                                   'ROM %dx%d, fused native step' % (args.config, B_u, N_s,
+            'config': {'workload': 'BASELINE config %s: %s grid, B_u=%d unlabeled + N_s=%d labeled per GPU, '
+                                   'ROM %dx%d, fused native step' % (CONFIG_TAG[args.config], args.config, B_u, N_s,
                                                                      physics['rom'].grid.n, physics['rom'].grid.n),
                        'global_batch': world * per_step, 'grid': physics['fom'].grid.n,
                        'parallelism': 'dp%d' % world, 'graph': not args.no_graph},
