@@ -21,6 +21,7 @@ from gpi.native import anchor, set_flat, engine_for
 from gpi import _lib as L
 from gpi import vo as gvo
 from gpi.engine import rom_call, ROM_NN
+from gpi.predictive import predictive_y
 
 SHARED_PREFIXES = ('f.', 'g.', 'gp.', 'encoder.')
 
@@ -188,14 +189,15 @@ class GenerativeModel(lamp.modules.BaseModule):
         return int(torch.randint(0, 2 ** 62, (1,)).item())
 
     def _run_engine(self, engine, X_u=None, X_s=None, Y=None, F=None, eps=None, X_vo=None, F_vo=None):
-        """eps (optional, injected noise): (eps_z [B, d_z], eps_X [N_s + N_vo, n_T][, eps_y [N_vo, d_y]])."""
+        """eps (optional, injected noise): (eps_z [B, d_z], eps_X [N_s + N_vo, n_T] (None in lockX)
+        [, eps_y [N_vo, d_y]])."""
         if eps is None:
             engine.eps_z().normal_()
-            if engine.N_x > 0:
+            if engine.N_ex > 0:
                 engine.eps_x().normal_()
         else:
             engine.eps_z().copy_(eps[0])
-            if engine.N_x > 0:
+            if engine.N_ex > 0:
                 engine.eps_x().copy_(eps[1])
         if engine.N_vo > 0 and not engine.vo_holdoff:
             # y ~ reparametrize(VO.mean, VO.logsigma) (generative.py:356)
@@ -225,9 +227,18 @@ class GenerativeModel(lamp.modules.BaseModule):
         eps_y [N_vo * N_mc, d_y])."""
         if step is None:
             raise ValueError('We now require a step parameter to be passed to update VOs')
-        if Y_mean is None or Y_std is None:
-            if not self._independent_X:
-                raise NotImplementedError('the lockX VO predictive is not on the native path')
+        if (Y_mean is None or Y_std is None) and not self._independent_X:
+            # lockX (generative.py:202-204): y = g(gp(z)) with z ~ q_z['vo'] -- gpi_gp_sample without
+            # the logsigma_X noise, coarse solves, moments.  eps = (eps_Z [N_vo * N_mc, d_z], eps_y)
+            ds = self._datasets['vo']
+            if int(N_monte_carlo) > 2048:
+                raise RuntimeError('Batchsize will lead to memory issues')
+            qz = self.q_z['vo']
+            Y_mean, Y_std, PREC = predictive_y(self, qz.mean.detach(), qz.logsigma.detach(),
+                                               ds.get('F_ROM_BC').detach(), int(N_monte_carlo),
+                                               eps=(eps[0], None, eps[1]) if eps is not None else None,
+                                               seed=self._host_seed(), return_prec=True)
+        elif Y_mean is None or Y_std is None:
             ds = self._datasets['vo']
             N, N_mc = ds.N, int(N_monte_carlo)
             if N_mc > 2048:
@@ -274,8 +285,6 @@ class GenerativeModel(lamp.modules.BaseModule):
         N_vo = 0
         X_vo = F_vo = None
         if self._datasets.get('vo') and not disable_vo and not self.disable_elbo_vo:
-            if not self._independent_X:
-                raise NotImplementedError('the lockX virtual-observable variant is not on the native path')
             dsv = self._datasets['vo']
             X_vo = dsv.get('X').detach().contiguous()
             F_vo = dsv.get('F_ROM_BC').detach().contiguous()
@@ -292,8 +301,6 @@ class GenerativeModel(lamp.modules.BaseModule):
         N_s = 0
         X_s = Y = F = None
         if self._datasets.get('supervised') and not self.disable_elbo_supervised:
-            if not self._independent_X:
-                raise NotImplementedError('the lockX supervised variant is not on the native path')
             ds = self._datasets['supervised']
             X_s, Y, F = ds.get('X').detach(), ds.get('Y').detach(), ds.get('F_ROM_BC').detach()
             if self.preprocess_y_fct is not None:
@@ -329,8 +336,6 @@ class GenerativeModel(lamp.modules.BaseModule):
     def elbo_supervised(self, X, Y, step, normalize=False):
         if self.disable_elbo_supervised:
             return 0
-        if not self._independent_X:
-            raise NotImplementedError('the lockX supervised variant is not on the native path')
         F = self._datasets['supervised'].get('F_ROM_BC').detach()
         engine = self._elbo_engine(0, X.shape[0], normalize)
         return self._run_engine(engine, X_s=X.detach(), Y=Y.detach(), F=F)

@@ -6,6 +6,7 @@
 //   or z from q_z, KL                               (components.py:167-172,192-193)
 //   decoder latent map                              (Decoder.py:213,293)
 //   gp(z), X~ = q_X sample, log-lik, entropy        (generative.py:464-478, components.py:195-197,224-229)
+//   or X~ = gp(z) (lockX)                           (generative.py:429-459,300-339)
 // The backward writes per-sample deltas; the shared-weight gradients
 // (sum over samples of delta (x) input) are formed by gpi_outer_gemm, the
 // per-sample variational parameters' gradients are written directly.
@@ -180,12 +181,18 @@ __global__ __launch_bounds__(HT) void head_fwd_kernel(gpi_head_desc d, const flo
         }
     }
     if (!enc && (g.flags & GPI_HEAD_GP)) {
+        const bool lockx = g.flags & GPI_HEAD_LOCKX;             // uniform per workgroup
         float lx = 0.f, ent = 0.f;
         for (int t = tid; t < d.d_x; t += HT) {
             float a = P[d.gp_b + t];
             const float* w = P + d.gp_w + (int64_t)t * dz;
             for (int k = 0; k < dz; ++k) a = fmaf(w[k], z[k], a);
             const int64_t qi = (int64_t)q * d.d_x + t;              // workspace row
+            if (lockx) {                                           // X~ = gp(z) (generative.py:432)
+                ws[d.mux + qi] = a;
+                ws[d.xs + qi] = a;
+                continue;
+            }
             const int64_t pi = (int64_t)g.row * d.d_x + t;          // q_X parameter row
             const float lsq = P[g.qx_ls + pi];
             const float xs = fmaf(expf(lsq), ws[d.eps_x + qi], P[g.qx_mu + pi]);
@@ -196,6 +203,7 @@ __global__ __launch_bounds__(HT) void head_fwd_kernel(gpi_head_desc d, const flo
             lx += -0.5f * (2.f * gls + r * r * expf(-2.f * gls) + GPI_LOG2PI);
             ent += lsq;
         }
+        if (lockx) return;
         lx = block_sum128(lx, scratch);
         ent = block_sum128(ent, scratch);
         if (tid == 0) {
@@ -228,8 +236,15 @@ __global__ __launch_bounds__(HT) void head_bwd_kernel(gpi_head_desc d, const flo
     __syncthreads();
 
     if (!enc && (g.flags & GPI_HEAD_GP)) {
+        const bool lockx = g.flags & GPI_HEAD_LOCKX;
         for (int t = tid; t < d.d_x; t += HT) {
             const int64_t qi = (int64_t)q * d.d_x + t;
+            if (lockx) {                                    // dJ/dmu_X = dJ/dX~ (the ROM adjoint)
+                const float gm = ws[d.gxs + qi];
+                v2[t] = gm;
+                ws[d.gmux + qi] = gm;
+                continue;
+            }
             const int64_t pi = (int64_t)g.row * d.d_x + t;
             const float gls = P[d.gp_ls + t];
             const float e2 = expf(-2.f * gls);

@@ -24,7 +24,7 @@ FINALIZE_ACCUMULATE = 1
 FINALIZE_ZERO = 2
 
 EPI_STORE, EPI_STORE_STATS, EPI_GAUSS_LOSS = 0, 1, 2
-HEAD_ENC, HEAD_REPARAM, HEAD_QZ, HEAD_LATENT, HEAD_GP = 0x01, 0x02, 0x04, 0x08, 0x10
+HEAD_ENC, HEAD_REPARAM, HEAD_QZ, HEAD_LATENT, HEAD_GP, HEAD_LOCKX = 0x01, 0x02, 0x04, 0x08, 0x10, 0x20
 HEAD_PART_ENC, HEAD_PART_Q = 0x100, 0x200
 ROM_FORWARD, ROM_LOGLIK, ROM_BACKWARD = 0, 1, 2
 VO_CGR, VO_FLUX = 0x1, 0x2

@@ -5,7 +5,8 @@ pre-planned workspaces.  No host synchronisation anywhere on the path.
 ElboEngine = GenerativeModel.elbo (generative.py:247-287) for the armortized
 unsupervised term (generative.py:546-585) + the supervised freeX term
 (generative.py:461-500) + the virtual-observable freeX term
-(generative.py:341-392, hold-off variant included), and its backward:
+(generative.py:341-392, hold-off variant included), or their lockX variants
+(independent_X = False: X~ = gp(z), generative.py:300-339,429-459), and its backward:
 
   forward   encoder program (B_u)            conv.hip  (11 launches at C64)
             dense head (all samples)          head.hip  (1)
@@ -144,6 +145,9 @@ class ElboEngine(object):
         # q samples whose X~ enters the ROM / gp likelihood (hold-off VO samples do not)
         self.N_x = self.N_s + (self.N_vo if not self.vo_holdoff else 0)
         enc, dec, gp, g = model.encoder, model.f, model.gp, model.g
+        # lockX (independent_X = False): X~ = gp(z), no q_X rows, no q_X noise, no logL_X / entropy
+        self.lockx = not gp.independent_X
+        self.N_ex = 0 if self.lockx else self.N_x
         self.enc, self.dec = enc, dec
         ws = Workspace()
         self.ws = ws
@@ -187,11 +191,12 @@ class ElboEngine(object):
         h.flags = L.HEAD_LATENT
         if self.B_u > 0:
             h.flags |= L.HEAD_ENC | L.HEAD_REPARAM
+        gpf = L.HEAD_GP | (L.HEAD_LOCKX if self.lockx else 0)
         if self.N_s > 0:
-            h.flags |= L.HEAD_QZ | L.HEAD_GP
+            h.flags |= L.HEAD_QZ | gpf
         h.n_enc, h.n_q, h.n_q2 = self.B_u, self.N_s, self.N_vo
         if self.N_vo > 0:
-            h.flags2 = L.HEAD_QZ | (0 if self.vo_holdoff else L.HEAD_GP)
+            h.flags2 = L.HEAD_QZ | (0 if self.vo_holdoff else gpf)
         h.d_feat, h.d_z, h.d_lat, h.d_x = d_feat, dz, d_lat, d_x
         if self.B_u > 0:
             h.fc_w, h.fc_b = P(enc, 'features.FC.weight'), P(enc, 'features.FC.bias')
@@ -205,15 +210,20 @@ class ElboEngine(object):
         h.gp_w = h.gp_b = h.gp_ls = h.qz_mu = h.qz_ls = h.qx_mu = h.qx_ls = -1
         h.qz_mu2 = h.qz_ls2 = h.qx_mu2 = h.qx_ls2 = -1
         if self.N_x > 0:
-            h.gp_w, h.gp_b, h.gp_ls = P(gp, 'fc.weight'), P(gp, 'fc.bias'), P(gp, 'logsigmas_X')
+            h.gp_w, h.gp_b = P(gp, 'fc.weight'), P(gp, 'fc.bias')
+            if not self.lockx:
+                h.gp_ls = P(gp, 'logsigmas_X')
         if self.N_s > 0:
-            qz, qx = model.q_z['supervised'], model.q_X['supervised']
+            qz = model.q_z['supervised']
             h.qz_mu, h.qz_ls = flat.offset(qz._mean), flat.offset(qz._logsigma)
-            h.qx_mu, h.qx_ls = flat.offset(qx._mean), flat.offset(qx._logsigma)
+            if not self.lockx:
+                qx = model.q_X['supervised']
+                h.qx_mu, h.qx_ls = flat.offset(qx._mean), flat.offset(qx._logsigma)
         if self.N_vo > 0:
-            qz, qx = model.q_z['vo'], model.q_X['vo']
+            qz = model.q_z['vo']
             h.qz_mu2, h.qz_ls2 = flat.offset(qz._mean), flat.offset(qz._logsigma)
-            if not self.vo_holdoff:
+            if not self.vo_holdoff and not self.lockx:
+                qx = model.q_X['vo']
                 h.qx_mu2, h.qx_ls2 = flat.offset(qx._mean), flat.offset(qx._logsigma)
         for k, v in hb.items():
             setattr(h, k, v)
@@ -293,8 +303,8 @@ class ElboEngine(object):
         return self.ws.view(self.hb['eps_z'], self.B, self.dz)
 
     def eps_x(self):
-        """[N_x, d_x] q_X noise (supervised rows, then VO rows unless held off)."""
-        return self.ws.view(self.hb['eps_x'], self.N_x, self.d_x)
+        """[N_ex, d_x] q_X noise (supervised rows, then VO rows unless held off; none in lockX)."""
+        return self.ws.view(self.hb['eps_x'], self.N_ex, self.d_x)
 
     def y_vo(self):
         """[N_vo, d_y] VO targets y ~ N(VO.mean, VO.var) of this step (generative.py:356)."""
@@ -385,12 +395,16 @@ class ElboEngine(object):
         if self.B_u > 0:
             val = val + su * (t[T_LX0] - t[T_KL_ENC])
         if self.N_s > 0:
-            val = val + ss * (t[T_LX0 + self.g_sup] + t[T_LOGL_Y] + t[T_LOGL_X] + t[T_ENT] + self.N_s * ENT_CONST
-                              - t[T_KL_Q])
+            v = t[T_LX0 + self.g_sup] + t[T_LOGL_Y] - t[T_KL_Q]
+            if not self.lockx:
+                v = v + t[T_LOGL_X] + t[T_ENT] + self.N_s * ENT_CONST
+            val = val + ss * v
         if self.N_vo > 0:
             v = t[T_LX0 + self.g_vo] - t[T_KL_Q2]
             if not self.vo_holdoff:
-                v = v + t[T_LOGL_Y2] + t[T_LOGL_X2] + t[T_ENT2] + self.N_vo * ENT_CONST
+                v = v + t[T_LOGL_Y2]
+                if not self.lockx:
+                    v = v + t[T_LOGL_X2] + t[T_ENT2] + self.N_vo * ENT_CONST
             val = val + sv * v
         return val.to(torch.float32)
 
@@ -405,17 +419,19 @@ class ElboEngine(object):
             gi = 1
         if self.N_s > 0:
             out['supervised_logL_x'] = float(t[T_LX0 + gi])
-            out['supervised_logL_X'] = float(t[T_LOGL_X])
             out['supervised_logL_y'] = float(t[T_LOGL_Y])
             out['supervised_DKL_z'] = float(t[T_KL_Q])
-            out['supervised_entropy_X'] = float(t[T_ENT]) + self.N_s * ENT_CONST
+            if not self.lockx:
+                out['supervised_logL_X'] = float(t[T_LOGL_X])
+                out['supervised_entropy_X'] = float(t[T_ENT]) + self.N_s * ENT_CONST
         if self.N_vo > 0:
             out['vo_logL_x'] = float(t[T_LX0 + self.g_vo])
             out['vo_DKL'] = float(t[T_KL_Q2])
             if not self.vo_holdoff:
-                out['vo_logL_X'] = float(t[T_LOGL_X2])
                 out['vo_logL_y'] = float(t[T_LOGL_Y2])
-                out['vo_entropy'] = float(t[T_ENT2]) + self.N_vo * ENT_CONST
+                if not self.lockx:
+                    out['vo_logL_X'] = float(t[T_LOGL_X2])
+                    out['vo_entropy'] = float(t[T_ENT2]) + self.N_vo * ENT_CONST
         return out
 
     def backward(self, stream=None, side_extra=None):

@@ -35,7 +35,7 @@ def host_seed():
 
 
 # ---------------------------------------------------------------- predictive y
-def predictive_y(model, q_mean, q_logsigma, F, N_mc, eps=None, seed=None):
+def predictive_y(model, q_mean, q_logsigma, F, N_mc, eps=None, seed=None, return_prec=False):
     """(mean, std) [N, d_y] of the MC predictive y of every row of q (Analysis.eval_all_y).
     eps (optional, injected): (eps_z [N*N_mc, d_z], eps_x [N*N_mc, d_x], eps_y [N*N_mc, d_y])."""
     for t in (q_mean, q_logsigma, F):
@@ -60,10 +60,10 @@ def predictive_y(model, q_mean, q_logsigma, F, N_mc, eps=None, seed=None):
     F_mc = F.float().repeat_interleave(int(N_mc), 0).contiguous()
     uc = torch.empty(rows, ROM_NN(rom.nc), dtype=torch.float32, device=dev)
     rom_call(rom.nc, rom.refine, x, F_mc, False, L.ROM_FORWARD, uc=uc)
-    mean, std, _ = V.vo_moments(uc, rom.nc, rom.refine, N, int(N_mc), logsig_y=g.logsigmas_y.detach().contiguous(),
-                                eps=eps[2] if eps is not None else None, seed=seed, sub=23)
+    mean, std, prec = V.vo_moments(uc, rom.nc, rom.refine, N, int(N_mc), logsig_y=g.logsigmas_y.detach().contiguous(),
+                                   eps=eps[2] if eps is not None else None, seed=seed, sub=23)
     del keep
-    return mean, std
+    return (mean, std, prec) if return_prec else (mean, std)
 
 
 def predictive_scores(Y, mean, std):

@@ -84,7 +84,7 @@ class FusedElboStep(object):
                                           sub0 + 1, st), 'random subset')
         ez = self.engine.eps_z()
         L.check(lib.gpi_randn(L.ptr(ez), ez.numel(), self.seed, L.ptr(self.rng_off), sub0 + 2, st), 'randn z')
-        if self.N_s:
+        if self.engine.N_ex:
             ex = self.engine.eps_x()
             L.check(lib.gpi_randn(L.ptr(ex), ex.numel(), self.seed, L.ptr(self.rng_off), sub0 + 3, st), 'randn x')
 

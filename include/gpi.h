@@ -137,6 +137,9 @@ typedef struct gpi_reduce_item {
 #define GPI_HEAD_QZ       0x04  /* z from q_z params, KL (q samples) */
 #define GPI_HEAD_LATENT   0x08  /* lat = latent_map(z) for all samples */
 #define GPI_HEAD_GP       0x10  /* gp(z), X-sample from q_X, log-lik + entropy (q samples) */
+#define GPI_HEAD_LOCKX    0x20  /* with GPI_HEAD_GP: X~ = gp(z) itself, no q_X / log-lik / entropy
+                                 * (independent_X = False: _elbo_supervised_lockX generative.py:429-459,
+                                 * _elbo_virtual_observables_lockX :300-339) */
 /* launch subsets (gpi_head_backward): only the encoder samples / only the variational ones, so the
  * two halves can run on different streams (the variational half needs the ROM adjoint) */
 #define GPI_HEAD_PART_ENC 0x100

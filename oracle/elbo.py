@@ -86,6 +86,20 @@ def elbo_supervised_freeX(decoder, gp_linear, logsigmas_X_gp, rom, qz, qX, X, Y,
     return logL_x + logL_y + logL_X + ent - DKL, terms
 
 
+
+def elbo_supervised_lockX(decoder, gp_linear, rom, qz, X, Y, F, eps_z):
+    """generative.py:429-459 with independent_X=False: X~ = gp(z) (EffectivePropertyMap.forward
+    components.py:224-229 returns fc(z) only), no q_X, no logL_X / entropy.  The VO term
+    _elbo_virtual_observables_lockX (generative.py:300-339) is the same algebra with Y drawn
+    from the VO posterior."""
+    Z = reparam(qz[0], qz[1], eps_z)
+    mx, lsx = decoder(Z)
+    logL_x = dgll(X, mx, 2 * lsx)
+    mu_y, ls_y = rom(gp_linear(Z), F)
+    logL_y = dgll(Y, mu_y, 2 * ls_y)
+    DKL = kl_unit(qz[0], 2 * qz[1])
+    return logL_x + logL_y - DKL, dict(logL_x=logL_x, logL_y=logL_y, DKL=DKL)
+
 # --------------------------------------------------------------------------
 # virtual observables (VirtualObservables.py:642-669, 960-998)
 # --------------------------------------------------------------------------
@@ -122,14 +136,17 @@ def vo_mean_variances(prec_beta, N, infinite_mask, alpha0=1e-6):
     return v
 
 
-def vo_predictive(W, M, bc_dofs, qx_mean, qx_logsigma, F, logsigmas_y, eps_X, eps_y):
+def vo_predictive(W, M, bc_dofs, qx_mean, qx_logsigma, F, logsigmas_y, eps_X, eps_y, gp_linear=None):
     """update_virtual_observables' MC predictive (generative.py:191-207): per VO sample n,
     X_s = q_X mean + exp(logsigma) eps_X (components.py:174-180), y_s = rom mean(X_s) +
     exp(logsigmas_y) eps_y (components.py:304-311); returns torch.mean / torch.std (unbiased).
-    eps_X [N, N_mc, dx], eps_y [N, N_mc, d_y]."""
+    eps_X [N, N_mc, dx], eps_y [N, N_mc, d_y].  lockX (generative.py:202-204): pass q_z's
+    mean / logsigma, eps_Z and gp_linear; X_s = gp(z_s) (components.py:238-249)."""
     means, stds = [], []
     for n in range(qx_mean.shape[0]):
         X = qx_mean[n] + torch.exp(qx_logsigma[n]) * eps_X[n]
+        if gp_linear is not None:
+            X = gp_linear(X)
         mu, ls = rom_operator(W, M, bc_dofs, X, F[n].expand(X.shape[0], -1), logsigmas_y)
         y = mu + torch.exp(ls) * eps_y[n]
         means.append(torch.mean(y, 0))

@@ -20,6 +20,7 @@ Outputs (small .npz, float32 unless noted) -- inputs, outputs and gradients:
   vo_elbo_c32.npz                 GenerativeModel.update_virtual_observables (x2, CGR + flux
                                   queries through the reference's own sampler / LinearQuerry /
                                   VirtualObservablesEnsemble classes) + elbo with the VO term + bwd
+  vo_elbo_lockx_c32.npz           the same with independent_X=False (lockX: X~ = gp(z))
   pe_analysis_c32.npz             PredictionEnsemble.update (3 iterations, own Adam) and
                                   Analysis.eval_all_y (relerr / logscore / R^2)
   terms.npz                       DGLL / KL known values
@@ -314,7 +315,10 @@ class _FakeFlux(object):
         return G[:, self.free], a
 
 
-def make_vo_elbo():
+def make_vo_elbo(lockx=False):
+    """lockx: the reference's independent_X=False variants (_elbo_supervised_lockX
+    generative.py:429-459, _elbo_virtual_observables_lockX :300-339, the lockX branch of
+    update_virtual_observables :202-204) -> vo_elbo_lockx_c32.npz."""
     nc, r, mc, mf, M, W, cdofs, fdofs = c32_physics()
     n = nc * r
     rng = np.random.default_rng(8)
@@ -330,7 +334,7 @@ def make_vo_elbo():
     rom = R_ROM.ROM(_Phys(cdofs, fdofs), torch.tensor(M, dtype=torch.float32), torch.float32, 'cpu')
     g = R_comp.ReducedOrderModelOperator(rom, torch.tensor(W, dtype=torch.float32), dtype=torch.float32,
                                          device='cpu')
-    gp = R_comp.EffectivePropertyMap(dz, M.shape[2], num_hidden_layers=0, independent_X=True,
+    gp = R_comp.EffectivePropertyMap(dz, M.shape[2], num_hidden_layers=0, independent_X=not lockx,
                                      dtype=torch.float32, device='cpu')
     model = R_gen.GenerativeModel(f=dec, g=g, gp=gp, dtype=torch.float32, device='cpu')
     model.encoder = enc
@@ -367,7 +371,7 @@ def make_vo_elbo():
                             create_unsupervised_variational_approximation=False)
     with torch.no_grad():
         for key in ('supervised', 'vo'):
-            for q in (model.q_z[key], model.q_X[key]):
+            for q in (model.q_z[key],) + (() if lockx else (model.q_X[key],)):
                 q._mean.copy_(torch.tensor(rng.normal(0, 0.5, q._mean.shape)))
                 q._logsigma.copy_(torch.tensor(rng.normal(-1.0, 0.3, q._logsigma.shape)))
         g.logsigmas_y.copy_(torch.tensor(rng.normal(-2.0, 0.2, g.logsigmas_y.shape)))
@@ -378,7 +382,7 @@ def make_vo_elbo():
     # two VO updates (the second one exercises the learnable flux-row precisions)
     upd = []
     for it in range(2):
-        ex = rng.normal(size=(Nvo, Nmc, dx))
+        ex = rng.normal(size=(Nvo, Nmc, dz if lockx else dx))     # q_z draws (lockX) / q_X draws
         ey = rng.normal(size=(Nvo, Nmc, dy))
         q_randn = [torch.tensor(e, dtype=torch.float32) for e in ex]
         q_like = [torch.tensor(e, dtype=torch.float32) for e in ey]
@@ -397,12 +401,14 @@ def make_vo_elbo():
                 mock.patch('torch.cholesky', torch.linalg.cholesky):
             Ym, Ysd = model.update_virtual_observables(Nmc, return_mean_stddev=True, step=it)
         assert not q_randn and not q_like
-        upd.append(dict(eps_X=ex.reshape(Nvo * Nmc, dx), eps_y=ey.reshape(Nvo * Nmc, dy), Y_mean=Ym.numpy(),
+        upd.append(dict(eps_X=ex.reshape(Nvo * Nmc, ex.shape[2]), eps_y=ey.reshape(Nvo * Nmc, dy), Y_mean=Ym.numpy(),
                         Y_std=Ysd.numpy(), mean=VO.mean.numpy(), vars=VO.vars.numpy(),
                         vo_var=VO._mean_vo_variances.numpy(), prec_beta=VO._prec_beta.numpy()))
 
     perm = torch.tensor(rng.permutation(Nu), dtype=torch.long)
     shapes = [(bs, dz), (Ns, dz), (Ns, dx), (Nvo, dz), (Nvo, dx), (Nvo, dy)]
+    if lockx:
+        shapes = [(bs, dz), (Ns, dz), (Nvo, dz), (Nvo, dy)]
     eps = [torch.tensor(rng.normal(size=sh), dtype=torch.float32) for sh in shapes]
     queue = list(eps)
 
@@ -429,7 +435,7 @@ def make_vo_elbo():
                   if p.grad is not None}
     # hold-off variant (generative.py:361-364): only q_z['vo'] is sampled for the VO term
     model.zero_grad()
-    eps_h = [torch.tensor(rng.normal(size=sh), dtype=torch.float32) for sh in shapes[:4]]
+    eps_h = [torch.tensor(rng.normal(size=sh), dtype=torch.float32) for sh in shapes[:3 if lockx else 4]]
     queue = list(eps_h)
     with mock.patch('torch.randperm', lambda N, **k: perm.clone()), mock.patch('torch.randn_like', fake_randn_like):
         elbo_h = model.elbo(step=0, armortized_bs=bs, vo_holdoff=True)
@@ -459,8 +465,8 @@ def make_vo_elbo():
     (-elbo_h).backward()
     out.update({'gradh.' + k: p.grad.detach().numpy().copy() for k, p in model.named_parameters()
                 if p.grad is not None})
-    np.savez_compressed(os.path.join(HERE, 'vo_elbo_c32.npz'), **out)
-    print('vo elbo ok', elbo.item(), elbo_h.item())
+    np.savez_compressed(os.path.join(HERE, 'vo_elbo_lockx_c32.npz' if lockx else 'vo_elbo_c32.npz'), **out)
+    print('vo elbo ok', 'lockX' if lockx else 'freeX', elbo.item(), elbo_h.item())
     return elbo
 
 
@@ -573,4 +579,5 @@ if __name__ == '__main__':
     make_elbo()
     make_vo()
     make_vo_elbo()
+    make_vo_elbo(lockx=True)
     make_pe_analysis()

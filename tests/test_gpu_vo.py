@@ -202,7 +202,7 @@ class _DS(object):
         return self.t[key][self.perm[:random_subset]]
 
 
-def build_vo_model(d):
+def build_vo_model(d, independent_X=True):
     from bottleneck.Encoder import CNNEncoder
     from bottleneck.Decoder import CNNDecoder
     from bottleneck.components import EffectivePropertyMap, ReducedOrderModelOperator
@@ -217,7 +217,7 @@ def build_vo_model(d):
     dec = CNNDecoder(n, dz, (8, 8), 1, 4, [1, 1], False, 4, drop_rate=0.)
     rom = ROM(StructuredGrid(nc), n // nc)
     g = ReducedOrderModelOperator(rom, torch.tensor(d['W']), dtype=torch.float32, device='cuda')
-    gp = EffectivePropertyMap(dz, 2 * nc * nc, dtype=torch.float32, device='cuda')
+    gp = EffectivePropertyMap(dz, 2 * nc * nc, independent_X=independent_X, dtype=torch.float32, device='cuda')
     model = GenerativeModel(f=dec.cuda(), g=g, gp=gp, dtype=torch.float32, device=torch.device('cuda'))
     model.encoder = enc.cuda()
     perm = torch.tensor(d['perm'], device='cuda')
@@ -274,6 +274,54 @@ def test_vo_update_and_vo_elbo_match_reference(device):
     model.zero_grad()
     h = [cuda(d['epsh%d' % i]) for i in range(4)]
     elbo_h = model.elbo(step=0, armortized_bs=bs, vo_holdoff=True, eps=(torch.cat([h[0], h[1], h[3]]), h[2]))
+    assert abs(elbo_h.item() - float(d['elbo_holdoff'])) / abs(float(d['elbo_holdoff'])) < 2e-5
+    (-elbo_h).backward()
+    for k, p in model.named_parameters():
+        ref = d.get('gradh.' + k)
+        got = p.grad.cpu().numpy() if p.grad is not None else np.zeros(p.shape, np.float32)
+        if ref is None:
+            assert np.abs(got).max() == 0, k
+            continue
+        err = np.abs(got - ref).max() / max(np.abs(ref).max(), 1.0)
+        assert err < 2e-3, (k, err)
+
+
+def test_vo_update_and_vo_elbo_lockx_match_reference(device):
+    """independent_X = False (lockX): X~ = gp(z) in the supervised and VO terms
+    (generative.py:300-339,429-459) and the VO predictive y = g(gp(z)), z ~ q_z['vo']
+    (generative.py:202-204), vs the reference run recorded in vo_elbo_lockx_c32.npz.
+    Same tolerances as the freeX test."""
+    d = load('vo_elbo_lockx_c32.npz')
+    model, ens, bs = build_vo_model(d, independent_X=False)
+    assert 'supervised' not in model.q_X and 'vo' not in model.q_X
+    for it in range(2):
+        Ym, Ys = model.update_virtual_observables(int(d['cfg'][7]), return_mean_stddev=True, step=it,
+                                                  eps=(cuda(d['upd%d.eps_X' % it]), cuda(d['upd%d.eps_y' % it])))
+        assert rel(Ym.cpu(), d['upd%d.Y_mean' % it]) < 1e-5
+        assert rel(Ys.cpu(), d['upd%d.Y_std' % it]) < 1e-4
+        assert rel(ens.mean.cpu(), d['upd%d.mean' % it]) < 1e-5
+        assert rel(ens.vars.cpu(), d['upd%d.vars' % it]) < 1e-4
+    assert rel(ens._prec_beta.cpu(), d['upd1.prec_beta']) < 1e-4
+
+    e = [cuda(d['eps%d' % i]) for i in range(4)]
+    elbo = model.elbo(step=0, armortized_bs=bs, eps=(torch.cat([e[0], e[1], e[2]]), None, e[3]))
+    engine = [v for k, v in model._gpi_engines.items() if k[0] == 'elbo'][0]
+    assert engine.lockx
+    terms = engine.terms()
+    for k in ('vo_logL_y', 'vo_DKL', 'supervised_logL_y'):
+        ref = float(d['term.objective/' + k])
+        tol = 1e-4 if k == 'vo_logL_y' else 2e-5
+        assert abs(terms[k] - ref) <= tol * max(abs(ref), 1.0), (k, terms[k], ref)
+    assert abs(elbo.item() - float(d['elbo'])) / abs(float(d['elbo'])) < 2e-5
+    (-elbo).backward()
+    for k, p in model.named_parameters():
+        ref = d['grad.' + k]
+        err = np.abs(p.grad.cpu().numpy() - ref).max() / max(np.abs(ref).max(), 1.0)
+        assert err < 2e-3, (k, err)
+
+    model.zero_grad()
+    h = [cuda(d['epsh%d' % i]) for i in range(3)]
+    elbo_h = model.elbo(step=0, armortized_bs=bs, vo_holdoff=True, eps=(torch.cat(h), None))
     assert abs(elbo_h.item() - float(d['elbo_holdoff'])) / abs(float(d['elbo_holdoff'])) < 2e-5
     (-elbo_h).backward()
     for k, p in model.named_parameters():

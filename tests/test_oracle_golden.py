@@ -198,3 +198,68 @@ def test_vo_pipeline_and_vo_elbo():
             continue
         scale = max(np.abs(ref).max(), 1.0)
         np.testing.assert_allclose(p.grad.numpy() / scale, ref / scale, atol=2e-4, err_msg=k)
+
+
+def test_vo_pipeline_and_vo_elbo_lockx():
+    """independent_X = False: the VO predictive y = g(gp(z)) (generative.py:202-204), conditioning,
+    and the lockX supervised / VO ELBO terms (generative.py:300-339,429-459) + gradients, oracle vs the
+    reference's own classes (vo_elbo_lockx_c32.npz)."""
+    d = load('vo_elbo_lockx_c32.npz')
+    n, nc, dz, Nu, bs, Ns, Nvo, Nmc = [int(v) for v in d['cfg']]
+    st = _vo_fixture_state(d)
+    assert not any(k.startswith('q_X.') or k == 'gp.logsigmas_X' for k in st)
+    M = torch.tensor(d['M'], dtype=torch.float64)
+    W = torch.tensor(d['W'], dtype=torch.float64)
+    bc = torch.tensor(d['bc_dofs'])
+    t64 = lambda k: torch.tensor(d[k], dtype=torch.float64)
+    G, A = t64('Gamma'), t64('alpha')
+    m = G.shape[1]
+    infinite = torch.zeros(m, dtype=torch.bool)
+    infinite[:(nc + 1) ** 2] = True
+    vo_var = oelbo.vo_mean_variances(torch.ones(m, dtype=torch.float64), Nvo, infinite)
+    gp = lambda z: torch.nn.functional.linear(z, st['gp.fc.weight'], st['gp.fc.bias'])
+    with torch.no_grad():
+        for it in range(2):
+            ez = t64('upd%d.eps_X' % it).view(Nvo, Nmc, -1)
+            assert ez.shape[2] == dz
+            ey = t64('upd%d.eps_y' % it).view(Nvo, Nmc, -1)
+            Ym, Ysd = oelbo.vo_predictive(W, M, bc, st['q_z.vo._mean'], st['q_z.vo._logsigma'], t64('Fv'),
+                                          st['g.logsigmas_y'], ez, ey, gp_linear=gp)
+            np.testing.assert_allclose(Ym.numpy(), d['upd%d.Y_mean' % it], rtol=1e-5, atol=1e-5)
+            np.testing.assert_allclose(Ysd.numpy(), d['upd%d.Y_std' % it], rtol=1e-4, atol=1e-6)
+            g32 = torch.tensor(d['upd%d.Y_mean' % it]).double()
+            p32 = (1 / torch.tensor(d['upd%d.Y_std' % it]) ** 2).double()
+            if it == 1:
+                beta = oelbo.vo_precision_beta(list(G), list(A), list(mean_prev), list(vars_prev))
+                np.testing.assert_allclose(beta.numpy(), d['upd1.prec_beta'], rtol=1e-9)
+                vo_var = oelbo.vo_mean_variances(beta, Nvo, infinite)
+            res = [oelbo.vo_condition(G[i], A[i], g32[i], p32[i], vo_var) for i in range(Nvo)]
+            mean_prev = torch.stack([r[0] for r in res])
+            vars_prev = torch.stack([r[1] for r in res])
+            np.testing.assert_allclose(mean_prev.numpy(), d['upd%d.mean' % it], rtol=1e-6, atol=1e-6)
+            np.testing.assert_allclose(vars_prev.numpy(), d['upd%d.vars' % it], rtol=1e-5, atol=1e-9)
+
+    enc_p = {k[len('encoder.'):]: v for k, v in st.items() if k.startswith('encoder.')}
+    dec_p = {k[len('f.'):]: v for k, v in st.items() if k.startswith('f.')}
+    enc = lambda x: ocodec.encoder_forward(enc_p, x, n, [1, 1], 4, 4)
+    dec = lambda z: ocodec.decoder_forward(dec_p, z, 8, [1, 1], 4, 4)
+    rom = lambda x, F: oelbo.rom_operator(W, M, bc, x, F, st['g.logsigmas_y'])
+    qz = lambda key: (st['q_z.%s._mean' % key], st['q_z.%s._logsigma' % key])
+    e = [t64('eps%d' % i) for i in range(4)]
+    e1, _ = oelbo.elbo_unsupervised_armortized(enc, dec, t64('Xu')[torch.tensor(d['perm'][:bs])], e[0])
+    e2, t2 = oelbo.elbo_supervised_lockX(dec, gp, rom, qz('supervised'), t64('Xs'), t64('Ys'), t64('Fs'), e[1])
+    np.testing.assert_allclose(t2['logL_y'].item(), d['term.objective/supervised_logL_y'], rtol=2e-5)
+    y = (torch.tensor(d['upd1.mean']) + torch.sqrt(torch.tensor(d['upd1.vars'])) * torch.tensor(d['eps3'])).double()
+    e3, t3 = oelbo.elbo_supervised_lockX(dec, gp, rom, qz('vo'), t64('Xv'), y, t64('Fv'), e[2])
+    np.testing.assert_allclose(t3['logL_y'].item(), d['term.objective/vo_logL_y'], rtol=1e-4)
+    np.testing.assert_allclose(t3['DKL'].item(), d['term.objective/vo_DKL'], rtol=2e-5)
+    elbo = e1 + e2 + e3
+    np.testing.assert_allclose(elbo.item(), float(d['elbo']), rtol=2e-5)
+    (-elbo).backward()
+    for k, p in st.items():
+        ref = d.get('grad.' + k)
+        if ref is None:
+            assert p.grad is None or not p.grad.abs().any(), k
+            continue
+        scale = max(np.abs(ref).max(), 1.0)
+        np.testing.assert_allclose(p.grad.numpy() / scale, ref / scale, atol=2e-4, err_msg=k)
