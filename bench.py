@@ -204,9 +204,17 @@ def main():
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
     distributed = world > 1
+    # GPI_BENCH_BACKEND=gloo: rehearsal of the N > 1 path with every rank on the visible GPU(s)
+    # (ranks share a device; RCCL refuses that).  The driver's multi-GPU runs use RCCL ('nccl').
+    backend = os.environ.get('GPI_BENCH_BACKEND', 'nccl')
+    if backend != 'nccl':
+        local = local % torch.cuda.device_count()
     if distributed:
         torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        else:
+            dist.init_process_group(backend)
     device = torch.device('cuda', local)
     torch.cuda.set_device(device)
 

@@ -89,6 +89,81 @@ __device__ void solve_band(const float* L, float* b, const RomDims& D) {
     }
 }
 
+// Single-thread banded Cholesky / solves for the common coarse grids (nc = 4, 8): the band
+// is only bw + 1 = nc wide, so the factorisation is a chain of nI dependent sqrt / scale /
+// rank-1-update steps.  Run by one lane with the active (bw+1) x (bw+1) window in registers
+// and the loop fully unrolled (every window index static: the window shift is register
+// renaming), it costs ~40 VALU instructions per step instead of three LDS round trips and
+// three workgroup barriers (78 -> ~10 us for the 63-unknown system at nc = 8).
+// dinv[k] = 1 / L(k,k) is kept for the solves, which run as partially unrolled loops (a full
+// unroll lets the scheduler hoist every band load and spill).
+template <int NC>
+__device__ __forceinline__ void chol_band_seq(float* __restrict__ L, float* __restrict__ dinv) {
+    constexpr int W = NC, NI = (NC - 1) * (NC + 1);
+    float win[W][W];   // win[a][t] = L(k + a, k + a - t)
+#pragma unroll
+    for (int a = 0; a < W; ++a)
+#pragma unroll
+        for (int t = 0; t < W; ++t) win[a][t] = a < NI ? L[a * W + t] : 0.f;
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+        const float dk = sqrtf(win[0][0]);
+        const float inv = 1.f / dk;
+        win[0][0] = dk;
+        dinv[k] = inv;
+#pragma unroll
+        for (int a = 1; a < W; ++a) win[a][a] *= inv;                       // L(k+a, k)
+#pragma unroll
+        for (int a = 1; a < W; ++a)
+#pragma unroll
+            for (int b = 1; b <= a; ++b) win[a][a - b] = fmaf(-win[a][a], win[b][b], win[a][a - b]);
+#pragma unroll
+        for (int t = 0; t < W; ++t) L[k * W + t] = win[0][t];
+#pragma unroll
+        for (int a = 0; a + 1 < W; ++a)
+#pragma unroll
+            for (int t = 0; t < W; ++t) win[a][t] = win[a + 1][t];
+#pragma unroll
+        for (int t = 0; t < W; ++t) win[W - 1][t] = (k + W < NI) ? L[(k + W) * W + t] : 0.f;
+    }
+}
+
+// L L^T x = b in place, single lane (see chol_band_seq)
+template <int NC>
+__device__ __forceinline__ void solve_band_seq(const float* __restrict__ L, const float* __restrict__ dinv,
+                                               float* __restrict__ b) {
+    constexpr int BW = NC - 1, W = NC, NI = (NC - 1) * (NC + 1);
+    float h[BW];   // sliding window of the last BW solution values (h[t-1] = y[k - t])
+#pragma unroll
+    for (int t = 0; t < BW; ++t) h[t] = 0.f;
+#pragma unroll 8
+    for (int k = 0; k < NI; ++k) {
+        float a = b[k];
+#pragma unroll
+        for (int t = 1; t <= BW; ++t)
+            if (k - t >= 0) a = fmaf(-L[k * W + t], h[t - 1], a);
+        a *= dinv[k];
+        b[k] = a;
+#pragma unroll
+        for (int t = BW - 1; t > 0; --t) h[t] = h[t - 1];
+        h[0] = a;
+    }
+#pragma unroll
+    for (int t = 0; t < BW; ++t) h[t] = 0.f;        // h[t-1] = x[k + t]
+#pragma unroll 8
+    for (int k = NI - 1; k >= 0; --k) {
+        float a = b[k];
+#pragma unroll
+        for (int t = 1; t <= BW; ++t)
+            if (k + t < NI) a = fmaf(-L[(k + t) * W + t], h[t - 1], a);
+        a *= dinv[k];
+        b[k] = a;
+#pragma unroll
+        for (int t = BW - 1; t > 0; --t) h[t] = h[t - 1];
+        h[0] = a;
+    }
+}
+
 __device__ __forceinline__ void interp(int i, int j, int r, int nc, int& n00, int& n10, int& n11, float& w0,
                                        float& w1, float& w2) {
     int I = i / r, J = j / r;
@@ -101,7 +176,10 @@ __device__ __forceinline__ void interp(int i, int j, int r, int nc, int& n00, in
     else { n10 = n00 + (nc + 1); w0 = 1.f - eta; w1 = eta - xi; w2 = xi; }
 }
 
-constexpr int ROM_NT = 256;      // threads per sample
+#ifndef GPI_ROM_NT
+#define GPI_ROM_NT 256
+#endif
+constexpr int ROM_NT = GPI_ROM_NT;   // threads per sample
 constexpr int ROM_U = 8;         // fine nodes per batch of global loads
 
 __global__ __launch_bounds__(ROM_NT) void rom_kernel(gpi_rom_desc d, RomDims D) {
@@ -113,7 +191,8 @@ __global__ __launch_bounds__(ROM_NT) void rom_kernel(gpi_rom_desc d, RomDims D) 
     float* b = u + D.nn;              // [nI]
     float* lam = b + D.nI;            // [nn]
     double* du = (double*)(sm + ((D.nT + D.nI * w + 2 * D.nn + D.nI + 1) & ~1));   // [nn] fp64 W^T dmu
-    double* lred = du + D.nn;         // [4] per-wave log-likelihood sums
+    double* lred = du + D.nn;         // [ROM_NT / 64] per-wave log-likelihood sums
+    float* dinv = (float*)(lred + ROM_NT / 64);   // [nI] 1 / L(k,k) (nc = 4, 8 path)
     const int s = blockIdx.x;
     const int tid = threadIdx.x, NT = ROM_NT;
     const int nc = D.nc;
@@ -151,8 +230,16 @@ __global__ __launch_bounds__(ROM_NT) void rom_kernel(gpi_rom_desc d, RomDims D) 
         b[ii] = rhs;
     }
     __syncthreads();
-    chol_band(L, D);
-    solve_band(L, b, D);
+    if (nc == 8 || nc == 4) {
+        if (tid == 0) {
+            if (nc == 8) { chol_band_seq<8>(L, dinv); solve_band_seq<8>(L, dinv, b); }
+            else { chol_band_seq<4>(L, dinv); solve_band_seq<4>(L, dinv, b); }
+        }
+        __syncthreads();
+    } else {
+        chol_band(L, D);
+        solve_band(L, b, D);
+    }
     for (int e = tid; e < D.nn; e += NT) {
         const int I = e % (nc + 1), J = e / (nc + 1);
         u[e] = (I == 0 || I == nc) ? F[e] : b[J * (nc - 1) + (I - 1)];
@@ -247,8 +334,12 @@ __global__ __launch_bounds__(ROM_NT) void rom_kernel(gpi_rom_desc d, RomDims D) 
         Lsum = wave_sum(Lsum);
         if ((tid & 63) == 0) lred[tid >> 6] = (double)Lsum;
         __syncthreads();
-        if (tid == 0 && d.loss_acc)
-            atomicAdd(d.loss_acc + blockIdx.x % GPI_REPLICAS, (lred[0] + lred[1]) + (lred[2] + lred[3]));
+        if (tid == 0 && d.loss_acc) {
+            double t = lred[0];
+#pragma unroll
+            for (int w = 1; w < ROM_NT / 64; ++w) t += lred[w];
+            atomicAdd(d.loss_acc + blockIdx.x % GPI_REPLICAS, t);
+        }
     }
     if (d.mode == GPI_ROM_FORWARD) return;
     __syncthreads();
@@ -259,7 +350,15 @@ __global__ __launch_bounds__(ROM_NT) void rom_kernel(gpi_rom_desc d, RomDims D) 
         b[ii] = (float)du[I + (nc + 1) * J];
     }
     __syncthreads();
-    solve_band(L, b, D);
+    if (nc == 8 || nc == 4) {
+        if (tid == 0) {
+            if (nc == 8) solve_band_seq<8>(L, dinv, b);
+            else solve_band_seq<4>(L, dinv, b);
+        }
+        __syncthreads();
+    } else {
+        solve_band(L, b, D);
+    }
     for (int ii = tid; ii < D.nI; ii += NT) {
         const int J = ii / (nc - 1), I = ii - J * (nc - 1) + 1;
         lam[I + (nc + 1) * J] = b[ii];
@@ -298,7 +397,7 @@ extern "C" int gpi_rom(const gpi_rom_desc* d, void* stream) {
     D.r = d->refine;
     D.n = d->nc * d->refine;
     D.dy = (D.n + 1) * (D.n - 1);
-    const size_t lds = sizeof(float) * (D.nT + D.nI * (D.bw + 1) + 4 * D.nn + D.nI + 16);
+    const size_t lds = sizeof(float) * (D.nT + D.nI * (D.bw + 1) + 4 * D.nn + 2 * D.nI + 2 * (ROM_NT / 64) + 4);
     hipLaunchKernelGGL(rom_kernel, dim3(d->n), dim3(ROM_NT), lds, (hipStream_t)stream, *d, D);
     GPI_CHECK_LAUNCH();
     return GPI_OK;

@@ -11,6 +11,8 @@ import torch  # noqa: F401  (must be imported before the HIP library is loaded)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, 'libgpi_hip.so')
+if os.environ.get('GPI_LIB_VARIANT'):               # tools: A/B builds of the same sources (libgpi_hip_<v>.so)
+    LIB_PATH = os.path.join(HERE, 'libgpi_hip_%s.so' % os.environ['GPI_LIB_VARIANT'])
 if os.environ.get('GPI_PHASE_TIMING') == '1':      # tools/phase_probe.py: the stamped build of the same kernels
     LIB_PATH = os.path.join(HERE, 'libgpi_hip_timing.so')
 
