@@ -8,7 +8,7 @@
 // yhat = y on free nodes and the Dirichlet data g on x=0 / x=1; K is the
 // 5-point stencil with edge conductances c = (kappa_a + kappa_b)/2 of the two
 // pixels sharing the edge (kappa/2 on boundary edges).  One workgroup per
-// field; exp(logkappa) staged in LDS; coarse sums accumulated in fp64 LDS.
+// field (layout in cgr_kernel); coarse sums accumulated in fp64 LDS.
 //
 // Flux residual (FluxConstrainSampler, VirtualObservables.py:323-349 +
 // FluxConstraintReducedOrderModel, bottleneck/flux.py:81-158): r_fc = Gamma_fc y with
@@ -27,67 +27,108 @@ __device__ __forceinline__ float bcval(const float* u, int i, int j, int n) {
     return i == 0 ? (u[0] * (1.f - y) + u[1] * y) : (u[2] * (1.f - y) + u[3] * y);
 }
 
-__global__ __launch_bounds__(256) void cgr_kernel(gpi_residual_desc d) {
+// One workgroup per field, one wave per coarse row band J (fine rows J r .. J r + r - 1, plus the
+// top row j = n in the last band); lanes run over the fine columns in chunks of 64 (coalesced y /
+// log kappa loads, re-reads of neighbours served by L1/L2), each lane keeps the W^T-restricted
+// contributions of its nodes to the four corners of its coarse square in registers over the
+// band's rows, then groups of G = min(r, 64) lanes (one coarse square per group when r is a power
+// of two; G = 1 otherwise) reduce by shuffles and one lane adds 4 fp64 values per square into
+// LDS.  No field-sized LDS staging: every grid size runs (256^2 included).
+constexpr int CGR_MAXW = 8;      // waves per workgroup (bands beyond loop)
+constexpr int CGR_MAXM = 8;      // 64-column chunks per row (n <= 512)
+
+template <int MM>   // 64-column chunks per row: ceil(n / 64)
+__global__ __launch_bounds__(64 * CGR_MAXW) void cgr_kernel(gpi_residual_desc d, int G) {
     extern __shared__ __attribute__((aligned(16))) double smd[];
     const int n = d.n_fine, nc = d.nc, nn = (nc + 1) * (nc + 1);
     const int r = n / nc;
+    const float rinv = 1.f / (float)r;
     double* acc = smd;                                  // [nn]
-    float* kp = (float*)(smd + nn + 2 * nc * nc);       // [n*n] kappa by square (i + n j)
+    double* racc = smd + nn;                            // [2 nc^2]
     const int f = blockIdx.x;
     const float* lk = d.logkappa + (int64_t)f * n * n;
     const float* y = d.y + (int64_t)f * (n + 1) * (n - 1);
     const float* u = d.bc + 4 * f;
-    for (int e = threadIdx.x; e < n * n; e += 256) {
-        const int row = e / n, col = e - row * n;      // image pixel (row 0 = top)
-        kp[col + n * (n - 1 - row)] = expf(lk[e]);
-    }
-    for (int e = threadIdx.x; e < nn; e += 256) acc[e] = 0.0;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (int e = threadIdx.x; e < nn + 2 * nc * nc; e += blockDim.x) smd[e] = 0.0;
     __syncthreads();
-    const int dy = (n + 1) * (n - 1);
-    for (int p = threadIdx.x; p < dy; p += 256) {
-        const int j = p / (n - 1), i = p - j * (n - 1) + 1;
-        const float yc = y[p];
-        auto yhat = [&](int ii, int jj) -> float {
-            if (ii == 0 || ii == n) return bcval(u, ii, jj, n);
-            return y[jj * (n - 1) + ii - 1];
-        };
-        auto K = [&](int ii, int jj) -> float { return kp[ii + n * jj]; };
-        // horizontal neighbours (i-1, j), (i+1, j)
-        float ch_l = 0.f, ch_r = 0.f, cv_d = 0.f, cv_u = 0.f;
-        if (j < n) { ch_l += K(i - 1, j); ch_r += K(i, j); }
-        if (j > 0) { ch_l += K(i - 1, j - 1); ch_r += K(i, j - 1); }
-        if (j > 0) { cv_d = K(i - 1, j - 1) + K(i, j - 1); }
-        if (j < n) { cv_u = K(i - 1, j) + K(i, j); }
-        float Ky = 0.5f * (ch_l * (yc - yhat(i - 1, j)) + ch_r * (yc - yhat(i + 1, j)));
-        if (j > 0) Ky += 0.5f * cv_d * (yc - yhat(i, j - 1));
-        if (j < n) Ky += 0.5f * cv_u * (yc - yhat(i, j + 1));
-        // restriction W^T: closed-form P1 weights
-        int I = i / r, J = j / r;
-        if (I > nc - 1) I = nc - 1;
-        if (J > nc - 1) J = nc - 1;
-        const float xi = (float)(i - I * r) / (float)r, eta = (float)(j - J * r) / (float)r;
-        const int n00 = I + (nc + 1) * J, n11 = n00 + (nc + 1) + 1;
-        int n10;
-        float w0, w1, w2;
-        if (xi >= eta) { n10 = n00 + 1; w0 = 1.f - xi; w1 = xi - eta; w2 = eta; }
-        else { n10 = n00 + (nc + 1); w0 = 1.f - eta; w1 = eta - xi; w2 = xi; }
-        if (w0 != 0.f) atomicAdd(&acc[n00], (double)(w0 * Ky));
-        if (w1 != 0.f) atomicAdd(&acc[n10], (double)(w1 * Ky));
-        if (w2 != 0.f) atomicAdd(&acc[n11], (double)(w2 * Ky));
+    // kappa of square (a, b) (b counted from the bottom; image row 0 = top)
+    auto K = [&](int a, int b) -> float { return expf(lk[(n - 1 - b) * n + a]); };
+    auto yhat = [&](int ii, int jj) -> float {
+        if (ii == 0 || ii == n) return bcval(u, ii, jj, n);
+        return y[jj * (n - 1) + ii - 1];
+    };
+    for (int J = wave; J < nc; J += nw) {
+        float c[MM][4];
+        // carried across the band's rows: kappa of the squares below the row (kd*), y of the rows
+        // below (yd), at (yc) and above (yu): per node 2 kappa loads (+ exp) and 3 y loads
+        float kdl[MM], kdr[MM], yd[MM], yc[MM], yu[MM];
+        const int j0 = J * r, j1 = J == nc - 1 ? n : (J + 1) * r - 1;
+#pragma unroll
+        for (int m = 0; m < MM; ++m) {
+            c[m][0] = c[m][1] = c[m][2] = c[m][3] = 0.f;
+            const int i = 64 * m + lane;
+            const bool act = i >= 1 && i <= n - 1;
+            kdl[m] = (act && j0 > 0) ? K(i - 1, j0 - 1) : 0.f;
+            kdr[m] = (act && j0 > 0) ? K(i, j0 - 1) : 0.f;
+            yc[m] = act ? y[j0 * (n - 1) + i - 1] : 0.f;
+            yd[m] = (act && j0 > 0) ? y[(j0 - 1) * (n - 1) + i - 1] : 0.f;
+        }
+#pragma unroll 2
+        for (int j = j0; j <= j1; ++j) {
+            const float eta = (float)(j - j0) * rinv;
+#pragma unroll
+            for (int m = 0; m < MM; ++m) {
+                const int i = 64 * m + lane;
+                const bool act = i >= 1 && i <= n - 1;
+                const float kul = (act && j < n) ? K(i - 1, j) : 0.f, kur = (act && j < n) ? K(i, j) : 0.f;
+                yu[m] = (act && j < n) ? y[(j + 1) * (n - 1) + i - 1] : 0.f;
+                const float yl = act ? yhat(i - 1, j) : 0.f, yr = act ? yhat(i + 1, j) : 0.f;
+                const float ycm = yc[m], ydm = yd[m];
+                float Ky = (kul + kdl[m]) * (ycm - yl) + (kur + kdr[m]) * (ycm - yr);
+                if (j > 0) Ky += (kdl[m] + kdr[m]) * (ycm - ydm);
+                if (j < n) Ky += (kul + kur) * (ycm - yu[m]);
+                Ky = act ? 0.5f * Ky : 0.f;
+                int I = i / r;
+                if (I > nc - 1) I = nc - 1;
+                const float xi = (float)(i - I * r) * rinv;
+                if (xi >= eta) {
+                    c[m][0] += (1.f - xi) * Ky; c[m][1] += (xi - eta) * Ky; c[m][3] += eta * Ky;
+                } else {
+                    c[m][0] += (1.f - eta) * Ky; c[m][2] += (eta - xi) * Ky; c[m][3] += xi * Ky;
+                }
+                kdl[m] = kul; kdr[m] = kur;
+                yd[m] = ycm; yc[m] = yu[m];
+            }
+        }
+#pragma unroll
+        for (int m = 0; m < MM; ++m) {
+            for (int o = 1; o < G; o <<= 1)
+#pragma unroll
+                for (int k = 0; k < 4; ++k) c[m][k] += __shfl_xor(c[m][k], o, 64);
+            const int i = 64 * m + lane;
+            if ((lane % G) == 0 && i < n) {
+                int I = i / r;
+                if (I > nc - 1) I = nc - 1;
+                const int v0 = I + (nc + 1) * J;
+                atomicAdd(&acc[v0], (double)c[m][0]);
+                atomicAdd(&acc[v0 + 1], (double)c[m][1]);
+                atomicAdd(&acc[v0 + nc + 1], (double)c[m][2]);
+                atomicAdd(&acc[v0 + nc + 2], (double)c[m][3]);
+            }
+        }
     }
     __syncthreads();
     if (d.r)
-        for (int e = threadIdx.x; e < nn; e += 256) d.r[(int64_t)f * nn + e] = (float)acc[e];
+        for (int e = threadIdx.x; e < nn; e += blockDim.x) d.r[(int64_t)f * nn + e] = (float)acc[e];
     if (!d.r_flux) return;
-    // ---- flux rows: one task per (coarse triangle, edge), r facets each
+    // ---- flux rows: one task per (coarse triangle, edge), r facets each (fp32 facet sums per
+    // task, fp64 across tasks; a lane-parallel facet split with shuffle sums measured slower)
     const int nT = 2 * nc * nc;
-    double* racc = acc + nn;                            // [nT]
-    for (int e = threadIdx.x; e < nT; e += 256) racc[e] = 0.0;
-    __syncthreads();
     auto uf = [&](int ii, int jj) -> float {            // free value, 0 on Dirichlet nodes
         return (ii < 1 || ii > n - 1) ? 0.f : y[jj * (n - 1) + ii - 1];
     };
-    for (int task = threadIdx.x; task < 3 * nT; task += 256) {
+    for (int task = threadIdx.x; task < 3 * nT; task += blockDim.x) {
         const int k = task / 3, e = task - 3 * k;
         const int Q = k >> 1, ul = k & 1;
         const int I = Q % nc, J = Q / nc;
@@ -109,12 +150,12 @@ __global__ __launch_bounds__(256) void cgr_kernel(gpi_residual_desc d) {
             float v;
             if (ul == 0) v = e == 0 ? u1 - u3 : (e == 1 ? u1 - u0 : u0 - 2.f * u1 + u3);
             else v = e == 0 ? u2 - u3 : (e == 1 ? u2 - u0 : u0 - 2.f * u2 + u3);
-            s = fmaf(kp[i + n * j], v, s);
+            s = fmaf(K(i, j), v, s);
         }
         atomicAdd(&racc[k], (double)s);
     }
     __syncthreads();
-    for (int e = threadIdx.x; e < nT; e += 256) d.r_flux[(int64_t)f * nT + e] = (float)racc[e];
+    for (int e = threadIdx.x; e < nT; e += blockDim.x) d.r_flux[(int64_t)f * nT + e] = (float)racc[e];
 }
 
 }  // namespace
@@ -123,11 +164,21 @@ extern "C" int gpi_cgr_residual(const gpi_residual_desc* d, void* stream) {
     if (!d || !d->logkappa || !d->y || !d->bc || (!d->r && !d->r_flux) || d->nc < 1 || d->n_fine < 2 || d->n < 0)
         return GPI_ERR_ARG;
     if (d->n_fine % d->nc) return GPI_ERR_ARG;
+    if (d->n_fine > 64 * CGR_MAXM) return GPI_ERR_UNSUPPORTED;
     if (d->n == 0) return GPI_OK;
     const int nn = (d->nc + 1) * (d->nc + 1);
-    const size_t lds = sizeof(double) * (nn + 2 * d->nc * d->nc) + sizeof(float) * d->n_fine * d->n_fine;
+    const size_t lds = sizeof(double) * (nn + 2 * d->nc * d->nc);
     if (lds > 160 * 1024) return GPI_ERR_UNSUPPORTED;
-    hipLaunchKernelGGL(cgr_kernel, dim3(d->n), dim3(256), lds, (hipStream_t)stream, *d);
+    const int r = d->n_fine / d->nc;
+    const int G = (r & (r - 1)) == 0 ? (r < 64 ? r : 64) : 1;   // lanes per coarse square (see cgr_kernel)
+    const int waves = d->nc < CGR_MAXW ? d->nc : CGR_MAXW;
+    const int M = (d->n_fine + 63) / 64;
+    const dim3 grid(d->n), block(64 * waves);
+    const hipStream_t st = (hipStream_t)stream;
+    if (M == 1) hipLaunchKernelGGL(cgr_kernel<1>, grid, block, lds, st, *d, G);
+    else if (M == 2) hipLaunchKernelGGL(cgr_kernel<2>, grid, block, lds, st, *d, G);
+    else if (M <= 4) hipLaunchKernelGGL(cgr_kernel<4>, grid, block, lds, st, *d, G);
+    else hipLaunchKernelGGL(cgr_kernel<8>, grid, block, lds, st, *d, G);
     GPI_CHECK_LAUNCH();
     return GPI_OK;
 }

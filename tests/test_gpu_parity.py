@@ -106,6 +106,25 @@ def test_cgr_residual_random_fields(device, nc, r, N):
         assert np.abs(out[i] - ref).max() / scale < 1e-5
 
 
+@pytest.mark.parametrize('n,N', [(128, 2), (256, 1)])
+def test_cgr_residual_large_grids(device, n, N):
+    """BASELINE configs 4 / 5 grids (ROM 8x8, r = 16 / 32): W^T [K yhat]_free vs the oracle's
+    matrix-free fp64 FE residual (oracle.fem.fom_residual); max error <= 1e-5 of the largest
+    residual entry (no Gamma is formed at these sizes to normalise by)."""
+    from gpi.engine import cgr_residual
+    rng = np.random.default_rng(n)
+    nc = 8
+    mc, mf = fem.unit_square_mesh(nc), fem.unit_square_mesh(n)
+    W = fem.prolongation_free(mc, mf)
+    imgs = rng.normal(0.4, 0.8, (N, n, n))
+    U = rng.uniform(-0.5, 0.5, (N, 4))
+    y = rng.normal(0, 0.3, (N, W.shape[0]))
+    out = cgr_residual(cuda(imgs), cuda(y), cuda(U), nc=nc).cpu().numpy()
+    for i in range(N):
+        ref = W.T @ fem.fom_residual(mf, np.exp(fem.image_to_cells(imgs[i])), U[i], y[i])
+        assert np.abs(out[i] - ref).max() / np.abs(ref).max() < 1e-5
+
+
 def test_cgr_residual_vanishes_at_fom_solution(device):
     from gpi.engine import cgr_residual
     rng = np.random.default_rng(0)
