@@ -173,20 +173,18 @@ __global__ __launch_bounds__(HT) void head_fwd_kernel(gpi_head_desc d, const flo
     __syncthreads();
     if (d.flags & GPI_HEAD_LATENT) {
         float* lat = ws + d.lat + (int64_t)s * d.d_lat;
-        for (int j = tid; j < d.d_lat; j += HT) {
-            float a = P[d.lat_b + j];
-            const float* w = P + d.lat_w + (int64_t)j * dz;
-            for (int k = 0; k < dz; ++k) a = fmaf(w[k], z[k], a);
-            lat[j] = a;
-        }
+        matvec(P + d.lat_w, P + d.lat_b, z, d.d_lat, dz, v1);       // UL weight loads in flight
+        __syncthreads();
+        for (int j = tid; j < d.d_lat; j += HT) lat[j] = v1[j];
     }
     if (!enc && (g.flags & GPI_HEAD_GP)) {
         const bool lockx = g.flags & GPI_HEAD_LOCKX;             // uniform per workgroup
         float lx = 0.f, ent = 0.f;
+        __syncthreads();
+        matvec(P + d.gp_w, P + d.gp_b, z, d.d_x, dz, v3);           // gp(z), UL weight loads in flight
+        __syncthreads();
         for (int t = tid; t < d.d_x; t += HT) {
-            float a = P[d.gp_b + t];
-            const float* w = P + d.gp_w + (int64_t)t * dz;
-            for (int k = 0; k < dz; ++k) a = fmaf(w[k], z[k], a);
+            const float a = v3[t];
             const int64_t qi = (int64_t)q * d.d_x + t;              // workspace row
             if (lockx) {                                           // X~ = gp(z) (generative.py:432)
                 ws[d.mux + qi] = a;
