@@ -37,7 +37,10 @@ __device__ __forceinline__ float bcval(const float* u, int i, int j, int n) {
 constexpr int CGR_MAXW = 8;      // waves per workgroup (bands beyond loop)
 constexpr int CGR_MAXM = 8;      // 64-column chunks per row (n <= 512)
 
-template <int MM>   // 64-column chunks per row: ceil(n / 64)
+// FLUX: the flux rows in the same pass -- pixel (i, j) of the band adds kappa_ij * (u-differences
+// of its corners) to the rows of its coarse square's two triangles when it lies on one of their
+// edges (the per-task sums of the reference's facet loops, flux.py:99-158), so the field is read once.
+template <int MM, bool FLUX>   // MM: 64-column chunks per row, ceil(n / 64)
 __global__ __launch_bounds__(64 * CGR_MAXW) void cgr_kernel(gpi_residual_desc d, int G) {
     extern __shared__ __attribute__((aligned(16))) double smd[];
     const int n = d.n_fine, nc = d.nc, nn = (nc + 1) * (nc + 1);
@@ -63,14 +66,16 @@ __global__ __launch_bounds__(64 * CGR_MAXW) void cgr_kernel(gpi_residual_desc d,
         // carried across the band's rows: kappa of the squares below the row (kd*), y of the rows
         // below (yd), at (yc) and above (yu): per node 2 kappa loads (+ exp) and 3 y loads
         float kdl[MM], kdr[MM], yd[MM], yc[MM], yu[MM];
+        float flr[MM], ful[MM];        // flux rows of the square's lower-right / upper-left triangle
         const int j0 = J * r, j1 = J == nc - 1 ? n : (J + 1) * r - 1;
 #pragma unroll
         for (int m = 0; m < MM; ++m) {
             c[m][0] = c[m][1] = c[m][2] = c[m][3] = 0.f;
+            flr[m] = ful[m] = 0.f;
             const int i = 64 * m + lane;
             const bool act = i >= 1 && i <= n - 1;
             kdl[m] = (act && j0 > 0) ? K(i - 1, j0 - 1) : 0.f;
-            kdr[m] = (act && j0 > 0) ? K(i, j0 - 1) : 0.f;
+            kdr[m] = (i < n && j0 > 0) ? K(i, j0 - 1) : 0.f;
             yc[m] = act ? y[j0 * (n - 1) + i - 1] : 0.f;
             yd[m] = (act && j0 > 0) ? y[(j0 - 1) * (n - 1) + i - 1] : 0.f;
         }
@@ -81,9 +86,14 @@ __global__ __launch_bounds__(64 * CGR_MAXW) void cgr_kernel(gpi_residual_desc d,
             for (int m = 0; m < MM; ++m) {
                 const int i = 64 * m + lane;
                 const bool act = i >= 1 && i <= n - 1;
-                const float kul = (act && j < n) ? K(i - 1, j) : 0.f, kur = (act && j < n) ? K(i, j) : 0.f;
+                const bool pix = i < n && j < n;              // pixel (i, j) (FLUX; i = 0 included)
+                const float kul = (act && j < n) ? K(i - 1, j) : 0.f;
+                const float kur = ((FLUX ? pix : act) && j < n) ? K(i, j) : 0.f;
                 yu[m] = (act && j < n) ? y[(j + 1) * (n - 1) + i - 1] : 0.f;
-                const float yl = act ? yhat(i - 1, j) : 0.f, yr = act ? yhat(i + 1, j) : 0.f;
+                const bool rf = i + 1 <= n - 1;                // right neighbour is a free node
+                const float yR = (FLUX ? (i < n && rf) : (act && rf)) ? y[j * (n - 1) + i] : 0.f;
+                const float yl = act ? yhat(i - 1, j) : 0.f;
+                const float yr = act ? (rf ? yR : bcval(u, n, j, n)) : 0.f;
                 const float ycm = yc[m], ydm = yd[m];
                 float Ky = (kul + kdl[m]) * (ycm - yl) + (kur + kdr[m]) * (ycm - yr);
                 if (j > 0) Ky += (kdl[m] + kdr[m]) * (ycm - ydm);
@@ -97,6 +107,19 @@ __global__ __launch_bounds__(64 * CGR_MAXW) void cgr_kernel(gpi_residual_desc d,
                 } else {
                     c[m][0] += (1.f - eta) * Ky; c[m][2] += (eta - xi) * Ky; c[m][3] += xi * Ky;
                 }
+                if (FLUX && pix) {
+                    const float u0 = act ? ycm : 0.f, u1 = yR, u2 = act ? yu[m] : 0.f;
+                    const float u3 = rf ? y[(j + 1) * (n - 1) + i] : 0.f;
+                    const int tr = i - (i / r) * r, tj = j - j0;
+                    float vl = 0.f, vu = 0.f;
+                    if (tj == 0 && J > 0) vl += u1 - u3;             // bottom edge (not on y = 0)
+                    if (tr == r - 1) vl += u1 - u0;                  // right edge
+                    if (tr == 0) vu += u2 - u3;                      // left edge
+                    if (tj == r - 1 && J < nc - 1) vu += u2 - u0;    // top edge (not on y = 1)
+                    if (tr == tj) { vl += u0 - 2.f * u1 + u3; vu += u0 - 2.f * u2 + u3; }   // diagonal
+                    flr[m] = fmaf(kur, vl, flr[m]);
+                    ful[m] = fmaf(kur, vu, ful[m]);
+                }
                 kdl[m] = kul; kdr[m] = kur;
                 yd[m] = ycm; yc[m] = yu[m];
             }
@@ -106,6 +129,11 @@ __global__ __launch_bounds__(64 * CGR_MAXW) void cgr_kernel(gpi_residual_desc d,
             for (int o = 1; o < G; o <<= 1)
 #pragma unroll
                 for (int k = 0; k < 4; ++k) c[m][k] += __shfl_xor(c[m][k], o, 64);
+            if (FLUX)
+                for (int o = 1; o < G; o <<= 1) {
+                    flr[m] += __shfl_xor(flr[m], o, 64);
+                    ful[m] += __shfl_xor(ful[m], o, 64);
+                }
             const int i = 64 * m + lane;
             if ((lane % G) == 0 && i < n) {
                 int I = i / r;
@@ -115,47 +143,26 @@ __global__ __launch_bounds__(64 * CGR_MAXW) void cgr_kernel(gpi_residual_desc d,
                 atomicAdd(&acc[v0 + 1], (double)c[m][1]);
                 atomicAdd(&acc[v0 + nc + 1], (double)c[m][2]);
                 atomicAdd(&acc[v0 + nc + 2], (double)c[m][3]);
+                if (FLUX) {
+                    const int q = I + nc * J;
+                    atomicAdd(&racc[2 * q], (double)flr[m]);
+                    atomicAdd(&racc[2 * q + 1], (double)ful[m]);
+                }
             }
         }
     }
     __syncthreads();
     if (d.r)
         for (int e = threadIdx.x; e < nn; e += blockDim.x) d.r[(int64_t)f * nn + e] = (float)acc[e];
-    if (!d.r_flux) return;
-    // ---- flux rows: one task per (coarse triangle, edge), r facets each (fp32 facet sums per
-    // task, fp64 across tasks; a lane-parallel facet split with shuffle sums measured slower)
+    if (!FLUX) return;
     const int nT = 2 * nc * nc;
-    auto uf = [&](int ii, int jj) -> float {            // free value, 0 on Dirichlet nodes
-        return (ii < 1 || ii > n - 1) ? 0.f : y[jj * (n - 1) + ii - 1];
-    };
-    for (int task = threadIdx.x; task < 3 * nT; task += blockDim.x) {
-        const int k = task / 3, e = task - 3 * k;
-        const int Q = k >> 1, ul = k & 1;
-        const int I = Q % nc, J = Q / nc;
-        if (ul == 0 && e == 0 && J == 0) continue;          // bottom edge on y = 0
-        if (ul == 1 && e == 1 && J == nc - 1) continue;     // top edge on y = 1
-        float s = 0.f;
-        for (int t = 0; t < r; ++t) {
-            int i, j;
-            if (ul == 0) {
-                if (e == 0) { i = I * r + t; j = J * r; }
-                else if (e == 1) { i = (I + 1) * r - 1; j = J * r + t; }
-                else { i = I * r + t; j = J * r + t; }
-            } else {
-                if (e == 0) { i = I * r; j = J * r + t; }
-                else if (e == 1) { i = I * r + t; j = (J + 1) * r - 1; }
-                else { i = I * r + t; j = J * r + t; }
-            }
-            const float u0 = uf(i, j), u1 = uf(i + 1, j), u2 = uf(i, j + 1), u3 = uf(i + 1, j + 1);
-            float v;
-            if (ul == 0) v = e == 0 ? u1 - u3 : (e == 1 ? u1 - u0 : u0 - 2.f * u1 + u3);
-            else v = e == 0 ? u2 - u3 : (e == 1 ? u2 - u0 : u0 - 2.f * u2 + u3);
-            s = fmaf(K(i, j), v, s);
-        }
-        atomicAdd(&racc[k], (double)s);
-    }
-    __syncthreads();
     for (int e = threadIdx.x; e < nT; e += blockDim.x) d.r_flux[(int64_t)f * nT + e] = (float)racc[e];
+}
+
+template <int MM>
+void launch_cgr(const gpi_residual_desc& d, int G, dim3 grid, dim3 block, size_t lds, hipStream_t st) {
+    if (d.r_flux) hipLaunchKernelGGL((cgr_kernel<MM, true>), grid, block, lds, st, d, G);
+    else hipLaunchKernelGGL((cgr_kernel<MM, false>), grid, block, lds, st, d, G);
 }
 
 }  // namespace
@@ -175,10 +182,10 @@ extern "C" int gpi_cgr_residual(const gpi_residual_desc* d, void* stream) {
     const int M = (d->n_fine + 63) / 64;
     const dim3 grid(d->n), block(64 * waves);
     const hipStream_t st = (hipStream_t)stream;
-    if (M == 1) hipLaunchKernelGGL(cgr_kernel<1>, grid, block, lds, st, *d, G);
-    else if (M == 2) hipLaunchKernelGGL(cgr_kernel<2>, grid, block, lds, st, *d, G);
-    else if (M <= 4) hipLaunchKernelGGL(cgr_kernel<4>, grid, block, lds, st, *d, G);
-    else hipLaunchKernelGGL(cgr_kernel<8>, grid, block, lds, st, *d, G);
+    if (M == 1) launch_cgr<1>(*d, G, grid, block, lds, st);
+    else if (M == 2) launch_cgr<2>(*d, G, grid, block, lds, st);
+    else if (M <= 4) launch_cgr<4>(*d, G, grid, block, lds, st);
+    else launch_cgr<8>(*d, G, grid, block, lds, st);
     GPI_CHECK_LAUNCH();
     return GPI_OK;
 }
