@@ -178,10 +178,12 @@ class GenerativeModel(lamp.modules.BaseModule):
             set_flat(self, self._flat)
         return self._flat
 
-    def _elbo_engine(self, B_u, N_s, normalize, N_vo=0, vo_holdoff=False):
+    def _elbo_engine(self, B_u, N_s, normalize, N_vo=0, vo_holdoff=False, q_unsup=None):
         flat = self.native_flat()
-        return engine_for(self, ('elbo', B_u, N_s, N_vo, bool(vo_holdoff), bool(normalize), id(flat)),
-                          lambda: ElboEngine(self, B_u, N_s, normalize=normalize, N_vo=N_vo, vo_holdoff=vo_holdoff))
+        return engine_for(self, ('elbo', B_u, N_s, N_vo, bool(vo_holdoff), bool(normalize), id(flat),
+                                 q_unsup is not None),
+                          lambda: ElboEngine(self, B_u, N_s, normalize=normalize, N_vo=N_vo, vo_holdoff=vo_holdoff,
+                                             q_unsup=q_unsup))
 
     @staticmethod
     def _host_seed():
@@ -291,9 +293,13 @@ class GenerativeModel(lamp.modules.BaseModule):
             N_vo = X_vo.shape[0]
         X_u = None
         B_u = 0
-        if self._datasets.get('unsupervised') and not self.disable_elbo_unsupervised:
-            if self.encoder is None:
-                raise NotImplementedError('non-armortized unsupervised q_z is not on the native path')
+        q_unsup = None
+        if self._datasets.get('unsupervised') and not self.disable_elbo_unsupervised and self.encoder is None:
+            # elbo_unsupervised (generative.py:515-544): per-sample q_z['unsupervised'] over the whole set
+            q_unsup = self.q_z['unsupervised']
+            X_u = self._datasets['unsupervised'].get('X').detach().contiguous()
+            B_u = X_u.shape[0]
+        elif self._datasets.get('unsupervised') and not self.disable_elbo_unsupervised:
             if armortized_bs is None:
                 raise ValueError('If armortized learning is used, we need to provide a batch size')
             X_u = self._datasets['unsupervised'].get('X', random_subset=armortized_bs).detach().contiguous()
@@ -308,7 +314,7 @@ class GenerativeModel(lamp.modules.BaseModule):
             N_s = X_s.shape[0]
         if B_u == 0 and N_s == 0 and N_vo == 0:
             return 0
-        engine = self._elbo_engine(B_u, N_s, normalize, N_vo=N_vo, vo_holdoff=vo_holdoff)
+        engine = self._elbo_engine(B_u, N_s, normalize, N_vo=N_vo, vo_holdoff=vo_holdoff, q_unsup=q_unsup)
         elbo = self._run_engine(engine, X_u, X_s, Y, F, eps, X_vo=X_vo, F_vo=F_vo)
         if l2_penalty is not None:
             pen = sum(torch.norm(p) for p in self.f.parameters())

@@ -134,8 +134,13 @@ class ElboEngine(object):
     rows as the head's second variational segment, a second ROM launch against targets sampled
     from the VO posterior); vo_holdoff keeps only its logL_x - KL part (generative.py:349-364)."""
 
-    def __init__(self, model, B_u, N_s, normalize=False, N_vo=0, vo_holdoff=False):
+    def __init__(self, model, B_u, N_s, normalize=False, N_vo=0, vo_holdoff=False, q_unsup=None):
+        """q_unsup: q_z['unsupervised'] for the non-armortized unsupervised term (no encoder,
+        GenerativeModel.elbo_unsupervised generative.py:515-544): its rows replace the encoder
+        heads; the term's KL is the reference's KLD of q_z['supervised'] (sic, :525)."""
         self.model = model
+        self.q_unsup = q_unsup
+        self.armortized = q_unsup is None
         flat = model._flat
         self.flat = flat
         dev = flat.P.device
@@ -158,7 +163,7 @@ class ElboEngine(object):
         dz = dec.dim_latent
         self.dz = dz
         # ---- encoder program
-        if self.B_u > 0:
+        if self.B_u > 0 and self.armortized:
             ec = enc.native_config()
             self.ep = encoder_program(**ec)
             self.enc_descs = self.ep.layout(self.B_u, ws.ws, ws.stats, ws.parts, groups_struct([self.B_u]), offE)
@@ -192,7 +197,7 @@ class ElboEngine(object):
         h = L.HeadDesc()
         h.flags = L.HEAD_LATENT
         if self.B_u > 0:
-            h.flags |= L.HEAD_ENC | L.HEAD_REPARAM
+            h.flags |= (L.HEAD_ENC if self.armortized else 0) | L.HEAD_REPARAM
         gpf = L.HEAD_GP | (L.HEAD_LOCKX if self.lockx else 0)
         if self.N_s > 0:
             h.flags |= L.HEAD_QZ | gpf
@@ -200,7 +205,7 @@ class ElboEngine(object):
         if self.N_vo > 0:
             h.flags2 = L.HEAD_QZ | (0 if self.vo_holdoff else gpf)
         h.d_feat, h.d_z, h.d_lat, h.d_x = d_feat, dz, d_lat, d_x
-        if self.B_u > 0:
+        if self.B_u > 0 and self.armortized:
             h.fc_w, h.fc_b = P(enc, 'features.FC.weight'), P(enc, 'features.FC.bias')
             h.mu_w, h.mu_b = P(enc, 'features.SplitDense.fc_mean.weight'), P(enc, 'features.SplitDense.fc_mean.bias')
             h.ls_w, h.ls_b = P(enc, 'features.SplitDense.fc_logvar.weight'), P(enc, 'features.SplitDense.fc_logvar.bias')
@@ -235,6 +240,13 @@ class ElboEngine(object):
         sv = 1.0 / self.N_vo if (self.normalize and self.N_vo) else 1.0
         self.su, self.ss, self.sv = su, ss, sv
         h.kl_scale_enc, h.kl_scale_q, h.lx_scale = su, ss, ss
+        if not self.armortized and self.B_u > 0:
+            if self.N_s == 0:
+                raise KeyError("elbo_unsupervised takes the KL of q_z['supervised'] (generative.py:525)")
+            # the unsupervised term's KL is q_z['supervised']'s: no KL gradient on q_z['unsupervised'],
+            # a second one (scale su) on the supervised rows
+            h.kl_scale_enc = 0.0
+            h.kl_scale_q = ss + su
         h.kl_scale_q2, h.lx_scale2 = sv, sv
         h.terms = ws.term_ptr(T_KL_ENC).value
         h.terms2 = ws.term_ptr(T_KL_Q2).value
@@ -262,7 +274,7 @@ class ElboEngine(object):
         gemm(self.dp.input.s_off, hb['z'], B, d_lat, dz, d_lat, dz, h.lat_w, h.lat_b)
         if self.N_x > 0:
             gemm(hb['gmux'], hb['z'] + self.B_u * dz, self.N_x, d_x, dz, d_x, dz, h.gp_w, h.gp_b)
-        if self.B_u > 0:
+        if self.B_u > 0 and self.armortized:
             gemm(hb['dzmu'], hb['hpre'], self.B_u, dz, d_feat, dz, d_feat, h.mu_w, h.mu_b, 1)
             gemm(hb['dzls'], hb['hpre'], self.B_u, dz, d_feat, dz, d_feat, h.ls_w, h.ls_b, 1)
             gemm(hb['dhpre'], h.feat, self.B_u, d_feat, d_feat, d_feat, d_feat, h.fc_w, h.fc_b)
@@ -317,8 +329,11 @@ class ElboEngine(object):
         if self.B_u > 0:
             L.require_device(X_u)
             assert X_u.dtype == torch.float32 and X_u.is_contiguous()
-            self.ectx.ext_in = X_u.data_ptr()
-            self.ectx.ext_idx = u_index.data_ptr() if u_index is not None else None
+            if self.armortized:
+                self.ectx.ext_in = X_u.data_ptr()
+                self.ectx.ext_idx = u_index.data_ptr() if u_index is not None else None
+            else:
+                assert X_u.shape[0] == self.B_u and u_index is None
             self.dctx.tgt[0] = X_u.data_ptr()
             self.dctx.tgt_idx[0] = u_index.data_ptr() if u_index is not None else None
         if self.N_s > 0:
@@ -354,6 +369,11 @@ class ElboEngine(object):
         if self.ep is not None:
             _run(lib.gpi_codec_forward, self.enc_descs, len(self.enc_descs), C.byref(self.ectx), st,
                  what='encoder forward')
+        if not self.armortized and self.B_u > 0:
+            # q_z['unsupervised'] rows as the "encoder" outputs of the head's first segment
+            # (torch copies on the current stream, which the launches use)
+            self.ws.view(self.hb['zmu'], self.B_u, self.dz).copy_(self.q_unsup._mean.detach())
+            self.ws.view(self.hb['zls'], self.B_u, self.dz).copy_(self.q_unsup._logsigma.detach())
         _run(lib.gpi_head_forward, C.byref(self.head), C.c_void_p(self.flat.P.data_ptr()),
              C.c_void_p(self.ws.t_ws.data_ptr()), st, what='head forward')
         if self.roms:
@@ -397,7 +417,7 @@ class ElboEngine(object):
         su, ss, sv = self.su, self.ss, self.sv
         val = t.new_zeros(())
         if self.B_u > 0:
-            val = val + su * (t[T_LX0] - t[T_KL_ENC])
+            val = val + su * (t[T_LX0] - (t[T_KL_ENC] if self.armortized else t[T_KL_Q]))
         if self.N_s > 0:
             v = t[T_LX0 + self.g_sup] + t[T_LOGL_Y] - t[T_KL_Q]
             if not self.lockx:
@@ -418,8 +438,12 @@ class ElboEngine(object):
         out = {}
         gi = 0
         if self.B_u > 0:
-            out['ARM_unsupervised_logL_x'] = float(t[T_LX0])
-            out['ARM_unsupervised_DKL_z'] = float(t[T_KL_ENC])
+            if self.armortized:
+                out['ARM_unsupervised_logL_x'] = float(t[T_LX0])
+                out['ARM_unsupervised_DKL_z'] = float(t[T_KL_ENC])
+            else:
+                out['unsupervised_logL_x'] = float(t[T_LX0])
+                out['unsupervised_DKL_z'] = float(t[T_KL_Q])
             gi = 1
         if self.N_s > 0:
             out['supervised_logL_x'] = float(t[T_LX0 + gi])
@@ -460,6 +484,12 @@ class ElboEngine(object):
             _run(lib.gpi_head_backward, C.byref(hd), P_, W_, G_, st, what='head backward (encoder samples)')
         else:
             _run(lib.gpi_head_backward, C.byref(self.head), P_, W_, G_, st, what='head backward')
+        if not self.armortized and self.B_u > 0:
+            # d/dmu, d/dlogsigma of q_z['unsupervised'] (written by the head for its first segment)
+            n = self.B_u * self.dz
+            for src, q in (('dzmu', self.q_unsup._mean), ('dzls', self.q_unsup._logsigma)):
+                o = self.flat.offset(q)
+                self.flat.gacc[o:o + n].add_(self.ws.view(self.hb[src], n).double())
         # the decoder's slab reduction and the dense weight gradients depend only on what is
         # done by now: run them on the side stream, concurrently with the encoder backward
         # (enqueued after it, so the encoder stays on the main chain's queue in a graph)

@@ -16,6 +16,7 @@ Outputs (small .npz, float32 unless noted) -- inputs, outputs and gradients:
   codec_c32.npz / codec_c64.npz   CNNEncoder / CNNDecoder fwd + bwd
   rom_c32.npz                     ROM solve + ReducedOrderModelOperator bwd
   elbo_c32.npz                    GenerativeModel.elbo (armortized + freeX) + bwd
+  elbo_nonarm_c32.npz             GenerativeModel.elbo without an encoder (elbo_unsupervised + freeX) + bwd
   vo_c32.npz                      VirtualObservable.update / precision (fp64)
   vo_elbo_c32.npz                 GenerativeModel.update_virtual_observables (x2, CGR + flux
                                   queries through the reference's own sampler / LinearQuerry /
@@ -237,6 +238,62 @@ def make_elbo():
 
 
 # --------------------------------------------------------------------------
+def make_elbo_nonarmortized():
+    """GenerativeModel.elbo without an encoder: elbo_unsupervised (generative.py:515-544, per-sample
+    q_z['unsupervised'] over the whole set, KL of q_z['supervised'] sic :525) + the supervised freeX
+    term -> elbo_nonarm_c32.npz."""
+    nc, r, mc, mf, M, W, cdofs, fdofs = c32_physics()
+    n = nc * r
+    rng = np.random.default_rng(14)
+    Nu, Ns = 6, 4
+    dz = 16
+    torch.manual_seed(0)
+    gen = torch.Generator().manual_seed(15)
+    dec = CNNDecoder(n, dz, (8, 8), 1, 4, [1, 1], False, 4, drop_rate=0., upsample='nearest',
+                     force_single_output=False, homoscedastic=False)
+    randomize_bn(dec, gen)
+    rom = R_ROM.ROM(_Phys(cdofs, fdofs), torch.tensor(M, dtype=torch.float32), torch.float32, 'cpu')
+    g = R_comp.ReducedOrderModelOperator(rom, torch.tensor(W, dtype=torch.float32),
+                                         dtype=torch.float32, device='cpu')
+    gp = R_comp.EffectivePropertyMap(dz, M.shape[2], num_hidden_layers=0, independent_X=True,
+                                     dtype=torch.float32, device='cpu')
+    model = R_gen.GenerativeModel(f=dec, g=g, gp=gp, dtype=torch.float32, device='cpu')
+    Xu = torch.tensor(random_fields(rng, Nu, n), dtype=torch.float32)
+    Xs_img = random_fields(rng, Ns, n)
+    Xs = torch.tensor(Xs_img, dtype=torch.float32)
+    U = rng.uniform(-0.5, 0.5, (Ns, 4))
+    Y = np.stack([fem.solve_fom(mf, np.exp(fem.image_to_cells(x)), u) for x, u in zip(Xs_img, U)])
+    F = np.stack([fem.f_rom_bc(mc, u) for u in U])
+    ds_sup = _DS(X=Xs, Y=torch.tensor(Y, dtype=torch.float32), F_ROM_BC=torch.tensor(F, dtype=torch.float32))
+    model.register_datasets({'supervised': ds_sup, 'unsupervised': _DS(X=Xu)}, None,
+                            create_unsupervised_variational_approximation=True)
+    with torch.no_grad():
+        for q in (model.q_z['unsupervised'], model.q_z['supervised'], model.q_X['supervised']):
+            q._mean.copy_(torch.tensor(rng.normal(0, 0.5, q._mean.shape)))
+            q._logsigma.copy_(torch.tensor(rng.normal(-1.0, 0.3, q._logsigma.shape)))
+        g.logsigmas_y.copy_(torch.tensor(rng.normal(-2.0, 0.2, g.logsigmas_y.shape)))
+    eps = [torch.tensor(rng.normal(size=s_), dtype=torch.float32) for s_ in [(Nu, dz), (Ns, dz), (Ns, M.shape[2])]]
+    queue = list(eps)
+
+    def fake_randn_like(t, *a, **k):
+        e = queue.pop(0)
+        assert e.shape == t.shape, (e.shape, t.shape)
+        return e.to(dtype=t.dtype)
+
+    state0 = {k: v.detach().cpu().numpy().copy() for k, v in model.state_dict().items()}
+    with mock.patch('torch.randn_like', fake_randn_like):
+        elbo = model.elbo(step=0)
+    assert not queue
+    (-elbo).backward()
+    out = {'state.' + k: v for k, v in state0.items()}
+    out.update({'grad.' + k: p.grad.detach().numpy() for k, p in model.named_parameters() if p.grad is not None})
+    out.update(Xu=Xu.numpy(), Xs=Xs.numpy(), Y=Y.astype(np.float32), F=F.astype(np.float32), U=U,
+               eps_u=eps[0].numpy(), eps_qz=eps[1].numpy(), eps_qX=eps[2].numpy(), elbo=np.float64(elbo.item()),
+               M=M.astype(np.float32), W=W.astype(np.float32), bc_dofs=cdofs, cfg=np.array([n, nc, dz, Nu, Ns]))
+    np.savez_compressed(os.path.join(HERE, 'elbo_nonarm_c32.npz'), **out)
+    print('elbo non-armortized ok', elbo.item())
+
+
 def make_vo():
     nc, r, mc, mf, M, W, cdofs, fdofs = c32_physics()
     n = nc * r
@@ -577,6 +634,7 @@ if __name__ == '__main__':
     make_codec('c64', 64, 64, 8, [1, 2, 1], 4, 6, 6, B=4)
     make_rom()
     make_elbo()
+    make_elbo_nonarmortized()
     make_vo()
     make_vo_elbo()
     make_vo_elbo(lockx=True)

@@ -234,6 +234,37 @@ def test_elbo_step_matches_reference(device):
         assert err < 2e-3, (k, err)
 
 
+def test_elbo_nonarmortized_matches_reference(device):
+    """GenerativeModel.elbo without an encoder (elbo_unsupervised generative.py:515-544: per-sample
+    q_z['unsupervised'] rows over the whole set, the KL of q_z['supervised'] sic) + the supervised
+    term, + backward, vs the reference run in elbo_nonarm_c32.npz; same tolerances as the armortized test."""
+    from bottleneck.Decoder import CNNDecoder
+    from bottleneck.components import EffectivePropertyMap, ReducedOrderModelOperator
+    from bottleneck.ROM import ROM
+    from bottleneck.generative import GenerativeModel
+    from physics.grid import StructuredGrid
+    d = load('elbo_nonarm_c32.npz')
+    n, nc, dz, Nu, Ns = [int(v) for v in d['cfg']]
+    dec = CNNDecoder(n, dz, (8, 8), 1, 4, [1, 1], False, 4, drop_rate=0.)
+    g = ReducedOrderModelOperator(ROM(StructuredGrid(nc), n // nc), torch.tensor(d['W']), dtype=torch.float32,
+                                  device='cuda')
+    gp = EffectivePropertyMap(dz, 2 * nc * nc, dtype=torch.float32, device='cuda')
+    model = GenerativeModel(f=dec.cuda(), g=g, gp=gp, dtype=torch.float32, device=torch.device('cuda'))
+    model.register_datasets({'supervised': _DS(X=cuda(d['Xs']), Y=cuda(d['Y']), F_ROM_BC=cuda(d['F'])),
+                             'unsupervised': _DS(X=cuda(d['Xu']))}, None,
+                            create_unsupervised_variational_approximation=True)
+    model.load_state_dict({k[6:]: torch.tensor(v) for k, v in d.items() if k.startswith('state.')})
+    model.cuda()
+    eps = (torch.cat([cuda(d['eps_u']), cuda(d['eps_qz'])]), cuda(d['eps_qX']))
+    elbo = model.elbo(step=0, eps=eps)
+    assert abs(elbo.item() - float(d['elbo'])) / abs(float(d['elbo'])) < 2e-5
+    (-elbo).backward()
+    for k, p in model.named_parameters():
+        ref = d['grad.' + k]
+        err = np.abs(p.grad.cpu().numpy() - ref).max() / max(np.abs(ref).max(), 1.0)
+        assert err < 2e-3, (k, err)
+
+
 def test_elbo_grad_accumulation_semantics(device):
     """zero_grad(set_to_none=False) + two backward passes accumulate like torch.
     Atomic accumulation order is not fixed, so the two passes agree to fp32 rounding only."""

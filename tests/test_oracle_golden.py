@@ -263,3 +263,33 @@ def test_vo_pipeline_and_vo_elbo_lockx():
             continue
         scale = max(np.abs(ref).max(), 1.0)
         np.testing.assert_allclose(p.grad.numpy() / scale, ref / scale, atol=2e-4, err_msg=k)
+
+
+def test_elbo_nonarmortized():
+    """elbo_unsupervised (generative.py:515-544) + supervised freeX, oracle vs the reference run."""
+    d = load('elbo_nonarm_c32.npz')
+    n, nc, dz, Nu, Ns = [int(v) for v in d['cfg']]
+    st = _vo_fixture_state(d)
+    t64 = lambda k: torch.tensor(d[k], dtype=torch.float64)
+    dec_p = {k[len('f.'):]: v for k, v in st.items() if k.startswith('f.')}
+    dec = lambda z: ocodec.decoder_forward(dec_p, z, 8, [1, 1], 4, 4)
+    M, W = t64('M'), t64('W')
+    qzs = (st['q_z.supervised._mean'], st['q_z.supervised._logsigma'])
+    Zu = oelbo.reparam(st['q_z.unsupervised._mean'], st['q_z.unsupervised._logsigma'], t64('eps_u'))
+    mx, lsx = dec(Zu)
+    e1 = oelbo.dgll(t64('Xu'), mx, 2 * lsx) - oelbo.kl_unit(qzs[0], 2 * qzs[1])      # KL of q_z['supervised'] (sic)
+    e2, _ = oelbo.elbo_supervised_freeX(
+        dec, lambda z: torch.nn.functional.linear(z, st['gp.fc.weight'], st['gp.fc.bias']), st['gp.logsigmas_X'],
+        lambda x, F: oelbo.rom_operator(W, M, torch.tensor(d['bc_dofs']), x, F, st['g.logsigmas_y']), qzs,
+        (st['q_X.supervised._mean'], st['q_X.supervised._logsigma']), t64('Xs'), t64('Y'), t64('F'), t64('eps_qz'),
+        t64('eps_qX'))
+    elbo = e1 + e2
+    np.testing.assert_allclose(elbo.item(), float(d['elbo']), rtol=2e-5)
+    (-elbo).backward()
+    for k, p in st.items():
+        ref = d.get('grad.' + k)
+        if ref is None:
+            assert p.grad is None or not p.grad.abs().any(), k
+            continue
+        scale = max(np.abs(ref).max(), 1.0)
+        np.testing.assert_allclose(p.grad.numpy() / scale, ref / scale, atol=2e-4, err_msg=k)
