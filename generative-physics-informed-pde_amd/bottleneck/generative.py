@@ -284,6 +284,9 @@ class GenerativeModel(lamp.modules.BaseModule):
         assert not (armortized_bs is not None and self.encoder is None)
         if l1_penalty is not None:
             raise NotImplementedError
+        if not self.config['reconstruct_log_eff_property']:
+            # the native decoder loss is the log-property Gaussian (generative.py:236-237, the default)
+            raise NotImplementedError('reconstruct_log_eff_property=False is not on the native path')
         N_vo = 0
         X_vo = F_vo = None
         if self._datasets.get('vo') and not disable_vo and not self.disable_elbo_vo:
