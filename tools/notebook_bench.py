@@ -1,0 +1,105 @@
+"""Notebook-semantics training iteration vs the reference's only published number.
+
+The reference publishes 35.57 it/s for its full training loop (example.ipynb:112, unnamed CUDA GPU,
+PyTorch 1.1): highres32 (32x32), armortized unlabeled batch 64 from a pool of 1024, N_s = 128
+labeled, N_val = 128, N_vo = 0, and per iteration (training.py:403-455)
+    zero_grad -> elbo -> backward -> Adam -> PredictionEnsemble.update x N_PE_updates (3)
+    -> [every N_monitor_interval = 1000 iterations: Analysis.eval_all_y(64 MC) on the validation set]
+    -> scheduler step.
+Here: the fused native ELBO step (one HIP graph), the three PredictionEnsemble iterations (decoder-only
+hold-off ELBO + backward + Adam on the validation q_z rows, one more HIP graph), and the monitoring
+evaluation timed separately and amortised over its 1000-iteration interval.  Tensorboard writes are
+not reproduced.  Synthetic fields / FOM labels as in bench.py (random-init weights).
+
+usage: python tools/notebook_bench.py [iterations] [out.json]
+"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+import torch  # noqa: E402
+
+PUBLISHED_IT_S = 35.57      # example.ipynb:112
+N_PE = 3
+N_MONITOR = 1000
+N_MC_ANALYSIS = 64
+
+
+def main():
+    iters = int(sys.argv[1]) if len(sys.argv) > 1 else 200
+    out = sys.argv[2] if len(sys.argv) > 2 else None
+    dev = torch.device('cuda', 0)
+    bench.CONFIGS['nb32'] = ('highres32', 64, 128, 1024, (0.4, 0.8, 0.15))
+    model, (Xu, Xs, Y, F), (B_u, N_s), physics = bench.build('nb32', dev, seed=11)
+    # validation set: 128 labeled fields (X for the PE, X / Y / F for the monitoring analysis)
+    from factories.model import ModelFactory
+    _, Xv, Yv, Fv, _ = bench.make_data(ModelFactory.FromIdentifier('highres32'), 32, 1, 128, (0.4, 0.8, 0.15), 12,
+                                       dev)
+    from gpi.train import FusedElboStep
+    from gpi.predictive import PredictionEnsembleEngine, predictive_y, predictive_scores
+    from bottleneck.components import VariationalApproximation
+
+    step = FusedElboStep(model, Xu, B_u, Xs, Y, F, lr=1e-2, seed=4321)
+    step.capture()
+    q_val = VariationalApproximation(model.dim_latent, Xv.shape[0], Xv).to(dev)
+    pe = PredictionEnsembleEngine(model, q_val, Xv, lambda: 1e-2)
+    for _ in range(2):
+        pe.update()
+    torch.cuda.synchronize()
+    g_pe = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        pe.update()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    with torch.cuda.graph(g_pe):
+        for _ in range(N_PE):
+            pe.update()
+
+    def iteration():
+        step.step()
+        g_pe.replay()
+
+    for _ in range(20):
+        iteration()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        iteration()
+    torch.cuda.synchronize()
+    t_it = (time.perf_counter() - t0) / iters
+
+    # monitoring: Analysis.eval_all_y on the PE's q_z (components.py:494-524), every 1000 iterations
+    def monitor():
+        mean, std = predictive_y(model, q_val.mean, q_val.logsigma, Fv, N_MC_ANALYSIS)
+        return predictive_scores(Yv, mean, std)
+
+    monitor()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(5):
+        monitor()
+    t_mon = (time.perf_counter() - t0) / 5
+
+    t_total = t_it + t_mon / N_MONITOR
+    res = {'metric': 'notebook training iterations/sec (highres32, B_u=64 of 1024, N_s=128, N_val=128, 3 PE updates)',
+           'value': round(1.0 / t_total, 1), 'unit': 'it/s', 'published': PUBLISHED_IT_S,
+           'published_source': 'example.ipynb:112 (unnamed CUDA GPU, PyTorch 1.1)',
+           'vs_published': round(1.0 / t_total / PUBLISHED_IT_S, 2),
+           'ms_per_iteration': round(t_total * 1e3, 4), 'ms_step_plus_pe': round(t_it * 1e3, 4),
+           'ms_monitoring_eval': round(t_mon * 1e3, 3), 'iterations': iters, 'n_gpus': 1, 'dtype': 'f32',
+           'data': 'synthetic', 'elbo_samples_per_s': round((B_u + N_s) / t_total, 1),
+           'excluded': 'tensorboard writes, host-side monitoring prints'}
+    print(json.dumps(res))
+    if out:
+        with open(out, 'w') as fh:
+            json.dump(res, fh, indent=1)
+
+
+if __name__ == '__main__':
+    main()
