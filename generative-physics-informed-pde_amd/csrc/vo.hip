@@ -14,7 +14,8 @@
 //                                     coarse ROM solutions (no [n_mc, d_y] sample matrix)
 //   vo_lambda_kernel                  Lambda = Gamma C Gamma^T + diag(v), 32x32 fp64 tiles
 //   vo_chol_kernel                    Cholesky + (Gamma g - alpha) + solve, one workgroup per sample
-//   vo_columns_kernel                 posterior mean / variance per column (|L^-1 Gamma_i|^2)
+//   vo_linv_kernel                    L^-1 (into lam's upper triangle)
+//   vo_columns_kernel                 posterior mean / variance per column (|L^-1 Gamma_i|^2, blocked GEMM)
 //   vo_precision_kernel               beta / mean VO variances (deterministic row reductions)
 #include "common.h"
 
@@ -449,41 +450,143 @@ __global__ __launch_bounds__(256) void vo_chol_kernel(gpi_vo_condition_desc d) {
         for (int e = tid; e < m * m; e += 256) lam[e] = A[e];
 }
 
-// One lane per column i of Gamma: q = L^{-1} Gamma_i (forward substitution, q in LDS),
-// mean_i = g_i - cov_i Gamma_i . solvec, vars_i = cov_i - cov_i^2 |q|^2.
-__global__ __launch_bounds__(64) void vo_columns_kernel(gpi_vo_condition_desc d) {
-    extern __shared__ __attribute__((aligned(16))) double sq[];   // [m][64]
+// L^{-1} per sample, stored transposed in the strict upper triangle of lam (lam[c*m + a] =
+// (L^{-1})_{ac}, a > c; the diagonal is 1 / L_aa, the lower triangle keeps L).  One thread per
+// column c (forward substitution over the rows below it).
+__global__ __launch_bounds__(256) void vo_linv_kernel(gpi_vo_condition_desc d) {
+    const int j = blockIdx.x, m = d.m;
+    double* lam = d.lam + (int64_t)j * m * m;
+    for (int c = threadIdx.x; c < m; c += blockDim.x) {
+        double* x = lam + (int64_t)c * m;            // x[a] = (L^{-1})_{ac} for a > c
+        const double xc = 1.0 / lam[(int64_t)c * m + c];
+        for (int a = c + 1; a < m; ++a) {
+            const double* La = lam + (int64_t)a * m;
+            double s = La[c] * xc;
+            for (int b = c + 1; b < a; ++b) s = fma(La[b], x[b], s);
+            x[a] = -s / La[a];
+        }
+    }
+}
+
+// The same, one wave per column c (m <= 256): column-oriented forward substitution of L x = e_c
+// with x in registers (lane holds x[lane + 64k]); per row b one broadcast of x[b] and an axpy of
+// L's column b over the rows below.  Reciprocal diagonal in LDS.
+__global__ __launch_bounds__(256) void vo_linv_wave_kernel(gpi_vo_condition_desc d) {
+    __shared__ double dinv[256];
+    const int j = blockIdx.y, m = d.m;
+    double* lam = d.lam + (int64_t)j * m * m;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int a = threadIdx.x; a < m; a += blockDim.x) dinv[a] = 1.0 / lam[(int64_t)a * m + a];
+    __syncthreads();
+    const int c = blockIdx.x * 4 + w;
+    if (c >= m) return;
+    double x[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) x[k] = (lane + 64 * k == c) ? 1.0 : 0.0;
+    for (int b = c; b < m; ++b) {
+        const int kb = b >> 6;
+        const double own = kb == 0 ? x[0] : kb == 1 ? x[1] : kb == 2 ? x[2] : x[3];
+        const double xb = __shfl(own, b & 63, 64) * dinv[b];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int a = lane + 64 * k;
+            if (a == b) x[k] = xb;
+            else if (a > b && a < m) x[k] = fma(-lam[(int64_t)a * m + b], xb, x[k]);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int a = lane + 64 * k;
+        if (a > c && a < m) lam[(int64_t)c * m + a] = x[k];
+    }
+}
+
+// Posterior per column i of Gamma (fp64): q = L^{-1} Gamma_i as a blocked lower-triangular GEMM
+// Q = L^{-1} Gamma over a 64-column tile (64 x 32 L^{-1} blocks and 32 x 64 Gamma blocks in LDS,
+// 4 x 4 fp64 accumulators per thread), only |q|^2 kept;  mean_i = g_i - cov_i Gamma_i . solvec,
+// vars_i = cov_i - cov_i^2 |q|^2.
+constexpr int VC_BA = 64, VC_BK = 32, VC_BN = 64;
+__global__ __launch_bounds__(256) void vo_columns_kernel(gpi_vo_condition_desc d) {
+    __shared__ double Ls[VC_BA][VC_BK + 1];
+    __shared__ double Gs[VC_BK][VC_BN];
+    __shared__ double red[16][VC_BN];
     const int j = blockIdx.y;
     const int m = d.m, dy = d.d_y;
-    const int lane = threadIdx.x;
-    const int i = blockIdx.x * 64 + lane;
-    const bool act = i < dy;
-    const int ic = act ? i : dy - 1;
+    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+    const int i0 = blockIdx.x * VC_BN;
     const double* gam = d.gamma + (int64_t)j * m * dy;
-    const double* L = d.lam + (int64_t)j * m * m;
+    const double* lam = d.lam + (int64_t)j * m * m;
     const double* sv = d.solvec + (int64_t)j * m;
-    double qn = 0.0, sm = 0.0;
-    for (int a = 0; a < m; ++a) {
-        const double ga = gam[(int64_t)a * dy + ic];
-        const double* La = L + (int64_t)a * m;
-        double acc = ga;
-        int bb = 0;
-        for (; bb + 4 <= a; bb += 4) {
-            acc -= La[bb] * sq[bb * 64 + lane];
-            acc -= La[bb + 1] * sq[(bb + 1) * 64 + lane];
-            acc -= La[bb + 2] * sq[(bb + 2) * 64 + lane];
-            acc -= La[bb + 3] * sq[(bb + 3) * 64 + lane];
-        }
-        for (; bb < a; ++bb) acc -= La[bb] * sq[bb * 64 + lane];
-        const double qa = acc / La[a];
-        sq[a * 64 + lane] = qa;
-        qn = fma(qa, qa, qn);
-        sm = fma(ga, sv[a], sm);
+    // Gamma_i . solvec: 4 partial sums per column
+    {
+        const int col = tid & 63, part = tid >> 6;
+        const int i = i0 + col;
+        double s = 0.0;
+        if (i < dy)
+            for (int a = part; a < m; a += 4) s = fma(gam[(int64_t)a * dy + i], sv[a], s);
+        red[part][col] = s;
     }
-    if (!act) return;
+    __syncthreads();
+    double smv = 0.0;
+    if (tid < VC_BN) smv = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
+    __syncthreads();
+    double qp[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int A0 = 0; A0 < m; A0 += VC_BA) {
+        double acc[4][4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) acc[r][c] = 0.0;
+        const int bend = min(A0 + VC_BA, m);
+        for (int B0 = 0; B0 < bend; B0 += VC_BK) {
+            // L^{-1}[A0 + ra][B0 + rb]
+            for (int e = tid; e < VC_BA * VC_BK; e += 256) {
+                const int ra = e & (VC_BA - 1), rb = e / VC_BA;
+                const int a = A0 + ra, b = B0 + rb;
+                double v = 0.0;
+                if (a < m && b < m) {
+                    if (a > b) v = lam[(int64_t)b * m + a];
+                    else if (a == b) v = 1.0 / lam[(int64_t)a * m + a];
+                }
+                Ls[ra][rb] = v;
+            }
+            for (int e = tid; e < VC_BK * VC_BN; e += 256) {
+                const int rb = e / VC_BN, col = e & (VC_BN - 1);
+                const int b = B0 + rb, i = i0 + col;
+                Gs[rb][col] = (b < m && i < dy) ? gam[(int64_t)b * dy + i] : 0.0;
+            }
+            __syncthreads();
+#pragma unroll 4
+            for (int kk = 0; kk < VC_BK; ++kk) {
+                double lv[4], gv[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) lv[r] = Ls[ty * 4 + r][kk];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) gv[c] = Gs[kk][tx * 4 + c];
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) acc[r][c] = fma(lv[r], gv[c], acc[r][c]);
+            }
+            __syncthreads();
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) qp[c] = fma(acc[r][c], acc[r][c], qp[c]);
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) red[ty][tx * 4 + c] = qp[c];
+    __syncthreads();
+    if (tid >= VC_BN) return;
+    const int i = i0 + tid;
+    if (i >= dy) return;
+    double qn = 0.0;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) qn += red[t][tid];
     const int64_t o = (int64_t)j * dy + i;
     const double cov = 1.0 / (double)d.prec[o];
-    const double mean = (double)d.g[o] - cov * sm;
+    const double mean = (double)d.g[o] - cov * smv;
     const double var = cov - cov * cov * qn;
     d.mean[o] = mean;
     d.vars[o] = var;
@@ -677,8 +780,6 @@ extern "C" int gpi_vo_condition(const gpi_vo_condition_desc* d, void* stream) {
         !d->vars || d->n < 0 || d->m < 1 || d->d_y < 1)
         return GPI_ERR_ARG;
     if (d->n == 0) return GPI_OK;
-    const size_t col_lds = sizeof(double) * 64 * d->m;
-    if (col_lds > 160 * 1024) return GPI_ERR_UNSUPPORTED;
     const hipStream_t st = (hipStream_t)stream;
     const int T = (d->m + LT - 1) / LT;
     hipLaunchKernelGGL(vo_lambda_kernel, dim3(T * (T + 1) / 2, d->n), dim3(256), 0, st, *d);
@@ -690,11 +791,10 @@ extern "C" int gpi_vo_condition(const gpi_vo_condition_desc* d, void* stream) {
         hipLaunchKernelGGL(vo_chol_kernel<false>, dim3(d->n), dim3(256), sizeof(double) * d->m, st, *d);
     }
     GPI_CHECK_LAUNCH();
-    if (col_lds > 64 * 1024 &&
-        hipFuncSetAttribute((const void*)vo_columns_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)col_lds) != hipSuccess)
-        return GPI_ERR_LAUNCH;
-    hipLaunchKernelGGL(vo_columns_kernel, dim3((d->d_y + 63) / 64, d->n), dim3(64), col_lds, st, *d);
+    if (d->m <= 256) hipLaunchKernelGGL(vo_linv_wave_kernel, dim3((d->m + 3) / 4, d->n), dim3(256), 0, st, *d);
+    else hipLaunchKernelGGL(vo_linv_kernel, dim3(d->n), dim3(256), 0, st, *d);
+    GPI_CHECK_LAUNCH();
+    hipLaunchKernelGGL(vo_columns_kernel, dim3((d->d_y + VC_BN - 1) / VC_BN, d->n), dim3(256), 0, st, *d);
     GPI_CHECK_LAUNCH();
     return GPI_OK;
 }

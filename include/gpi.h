@@ -316,7 +316,7 @@ typedef struct gpi_vo_condition_desc {
     const float* g;            /* [n, d_y] prior mean */
     const float* prec;         /* [n, d_y] prior precision */
     const double* vo_var;      /* [m] */
-    double* lam;               /* workspace [n, m, m] (holds L on return) */
+    double* lam;               /* workspace [n, m, m] (L in the lower triangle, L^-T above it on return) */
     double* solvec;            /* workspace [n, m] */
     double* mean;              /* [n, d_y] out */
     double* vars;              /* [n, d_y] out */
