@@ -404,6 +404,68 @@ __device__ void chol_block(double* A, int m, bool& bad) {
     }
 }
 
+// Blocked right-looking Cholesky of the global-memory Lambda (m <= 256): per 16-column panel the
+// diagonal block is factored in LDS, the rows below solve against it (one thread per row, panel in
+// LDS) and the trailing lower triangle takes ONE rank-16 update (instead of 16 rank-1 sweeps over
+// global memory).
+constexpr int CP_W = 16, CP_R = 256;
+__device__ void chol_panel(double* A, int m, bool& bad) {
+    __shared__ double D[CP_W][CP_W + 1];
+    __shared__ double P[CP_R][CP_W + 1];
+    const int tid = threadIdx.x;
+    for (int K0 = 0; K0 < m; K0 += CP_W) {
+        const int w = min(CP_W, m - K0), R0 = K0 + w, R = m - R0;
+        for (int e = tid; e < CP_W * CP_W; e += 256) {
+            const int r = e / CP_W, c = e - r * CP_W;
+            D[r][c] = (r < w && c <= r) ? A[(int64_t)(K0 + r) * m + K0 + c] : 0.0;
+        }
+        for (int e = tid; e < R * CP_W; e += 256) {
+            const int r = e / CP_W, c = e - r * CP_W;
+            P[r][c] = c < w ? A[(int64_t)(R0 + r) * m + K0 + c] : 0.0;
+        }
+        __syncthreads();
+        for (int k = 0; k < w; ++k) {               // diagonal block
+            const double akk = D[k][k];
+            if (!(akk > 0.0)) bad = true;
+            const double dk = sqrt(akk);
+            __syncthreads();
+            if (tid > k && tid < w) D[tid][k] /= dk;
+            if (tid == 0) D[k][k] = dk;
+            __syncthreads();
+            if (tid < CP_W * CP_W) {
+                const int r = tid / CP_W, c = tid - r * CP_W;
+                if (r > k && c > k && c <= r && r < w) D[r][c] -= D[r][k] * D[c][k];
+            }
+            __syncthreads();
+        }
+        if (tid < R) {                              // panel rows: x L11^T = a
+            for (int c = 0; c < w; ++c) {
+                double a = P[tid][c];
+                for (int k = 0; k < c; ++k) a -= P[tid][k] * D[c][k];
+                P[tid][c] = a / D[c][c];
+            }
+        }
+        __syncthreads();
+        for (int e = tid; e < CP_W * CP_W; e += 256) {
+            const int r = e / CP_W, c = e - r * CP_W;
+            if (r < w && c <= r) A[(int64_t)(K0 + r) * m + K0 + c] = D[r][c];
+        }
+        for (int e = tid; e < R * CP_W; e += 256) {
+            const int r = e / CP_W, c = e - r * CP_W;
+            if (c < w) A[(int64_t)(R0 + r) * m + K0 + c] = P[r][c];
+        }
+        for (int i = 0; i < R; ++i) {               // trailing update, lower triangle
+            for (int jj = tid; jj <= i; jj += 256) {
+                double s = 0.0;
+#pragma unroll
+                for (int c = 0; c < CP_W; ++c) s = fma(P[i][c], P[jj][c], s);
+                A[(int64_t)(R0 + i) * m + R0 + jj] -= s;
+            }
+        }
+        __syncthreads();
+    }
+}
+
 template <bool LDS>
 __global__ __launch_bounds__(256) void vo_chol_kernel(gpi_vo_condition_desc d) {
     extern __shared__ __attribute__((aligned(16))) double sm[];   // [m] rhs (+ [m*m] matrix if LDS)
@@ -418,7 +480,9 @@ __global__ __launch_bounds__(256) void vo_chol_kernel(gpi_vo_condition_desc d) {
         __syncthreads();
     }
     bool bad = false;
-    chol_block(A, m, bad);
+    if constexpr (LDS) chol_block(A, m, bad);
+    else if (m <= CP_R) chol_panel(A, m, bad);
+    else chol_block(A, m, bad);
     if (bad && d.flag && tid == 0) atomicOr(d.flag, 1);
     // b = Gamma g - alpha
     const double* gam = d.gamma + (int64_t)j * m * dy;
