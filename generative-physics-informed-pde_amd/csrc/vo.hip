@@ -494,6 +494,12 @@ __global__ __launch_bounds__(256) void vo_chol_kernel(gpi_vo_condition_desc d) {
         if (lane == 0) b[a] = s - d.alpha[(int64_t)j * m + a];
     }
     __syncthreads();
+    if (!LDS) {
+        // large m: the two triangular sweeps would be 2 m barrier-separated steps over global memory;
+        // b is handed to vo_solvec_kernel, which applies L^-T L^-1 once L^-1 exists
+        for (int e = tid; e < m; e += 256) d.solvec[(int64_t)j * m + e] = b[e];
+        return;
+    }
     // L z = b, L^T x = z
     for (int k = 0; k < m; ++k) {
         const double zk = b[k] / A[k * m + k];
@@ -562,6 +568,28 @@ __global__ __launch_bounds__(256) void vo_linv_wave_kernel(gpi_vo_condition_desc
     for (int k = 0; k < 4; ++k) {
         const int a = lane + 64 * k;
         if (a > c && a < m) lam[(int64_t)c * m + a] = x[k];
+    }
+}
+
+// solvec = Lambda^{-1} b = L^-T (L^-1 b) from the L^-1 in lam's upper triangle (large-m path).
+constexpr int VS_MAXM = 1024;
+__global__ __launch_bounds__(256) void vo_solvec_kernel(gpi_vo_condition_desc d) {
+    __shared__ double bs[VS_MAXM], ts[VS_MAXM];
+    const int j = blockIdx.x, m = d.m;
+    const double* lam = d.lam + (int64_t)j * m * m;
+    double* sv = d.solvec + (int64_t)j * m;
+    for (int a = threadIdx.x; a < m; a += blockDim.x) bs[a] = sv[a];
+    __syncthreads();
+    for (int a = threadIdx.x; a < m; a += blockDim.x) {          // t = L^-1 b
+        double s = bs[a] / lam[(int64_t)a * m + a];
+        for (int c = 0; c < a; ++c) s = fma(lam[(int64_t)c * m + a], bs[c], s);
+        ts[a] = s;
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < m; c += blockDim.x) {          // solvec = L^-T t
+        double s = ts[c] / lam[(int64_t)c * m + c];
+        for (int a = c + 1; a < m; ++a) s = fma(lam[(int64_t)c * m + a], ts[a], s);
+        sv[c] = s;
     }
 }
 
@@ -843,6 +871,7 @@ extern "C" int gpi_vo_condition(const gpi_vo_condition_desc* d, void* stream) {
     if (!d || !d->gamma || !d->alpha || !d->g || !d->prec || !d->vo_var || !d->lam || !d->solvec || !d->mean ||
         !d->vars || d->n < 0 || d->m < 1 || d->d_y < 1)
         return GPI_ERR_ARG;
+    if (d->m > VS_MAXM) return GPI_ERR_UNSUPPORTED;
     if (d->n == 0) return GPI_OK;
     const hipStream_t st = (hipStream_t)stream;
     const int T = (d->m + LT - 1) / LT;
@@ -857,6 +886,8 @@ extern "C" int gpi_vo_condition(const gpi_vo_condition_desc* d, void* stream) {
     GPI_CHECK_LAUNCH();
     if (d->m <= 256) hipLaunchKernelGGL(vo_linv_wave_kernel, dim3((d->m + 3) / 4, d->n), dim3(256), 0, st, *d);
     else hipLaunchKernelGGL(vo_linv_kernel, dim3(d->n), dim3(256), 0, st, *d);
+    GPI_CHECK_LAUNCH();
+    if (lds_small > 64 * 1024) hipLaunchKernelGGL(vo_solvec_kernel, dim3(d->n), dim3(256), 0, st, *d);
     GPI_CHECK_LAUNCH();
     hipLaunchKernelGGL(vo_columns_kernel, dim3((d->d_y + VC_BN - 1) / VC_BN, d->n), dim3(256), 0, st, *d);
     GPI_CHECK_LAUNCH();
