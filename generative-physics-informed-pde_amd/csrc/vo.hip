@@ -454,13 +454,16 @@ __device__ void chol_panel(double* A, int m, bool& bad) {
             const int r = e / CP_W, c = e - r * CP_W;
             if (c < w) A[(int64_t)(R0 + r) * m + K0 + c] = P[r][c];
         }
-        for (int i = 0; i < R; ++i) {               // trailing update, lower triangle
-            for (int jj = tid; jj <= i; jj += 256) {
-                double s = 0.0;
+        const int ntri = R * (R + 1) / 2;           // trailing update over the lower triangle, flattened
+        for (int e = tid; e < ntri; e += 256) {
+            int i = (int)((sqrtf(8.f * (float)e + 1.f) - 1.f) * 0.5f);
+            while (i * (i + 1) / 2 > e) --i;
+            while ((i + 1) * (i + 2) / 2 <= e) ++i;
+            const int jj = e - i * (i + 1) / 2;
+            double s = 0.0;
 #pragma unroll
-                for (int c = 0; c < CP_W; ++c) s = fma(P[i][c], P[jj][c], s);
-                A[(int64_t)(R0 + i) * m + R0 + jj] -= s;
-            }
+            for (int c = 0; c < CP_W; ++c) s = fma(P[i][c], P[jj][c], s);
+            A[(int64_t)(R0 + i) * m + R0 + jj] -= s;
         }
         __syncthreads();
     }
