@@ -221,7 +221,8 @@ typedef struct gpi_rom_desc {
  * VirtualObservables.py:57-69,297-321 + physics/LinearElliptic.py:137-159):
  *   r = W^T [K_f(kappa) yhat]_free  (= Gamma y - alpha),
  * kappa = exp(logkappa image) per pixel, yhat = y on free nodes and the NDP
- * Dirichlet data u0..u3 on x=0 / x=1.  Matrix-free 5-point stencil. */
+ * Dirichlet data u0..u3 on x=0 / x=1.  Matrix-free 5-point stencil, flux rows (r_flux) in the
+ * same pass; any n_fine <= 512 with n_fine % nc == 0 (GPI_ERR_UNSUPPORTED above). */
 typedef struct gpi_residual_desc {
     int32_t n_fine, nc, n, _pad;
     const float* logkappa;     /* [n, n_fine, n_fine] image (row 0 = top) */
