@@ -193,7 +193,7 @@ class _DS(object):
         return self.t[key][self.perm[:random_subset]]
 
 
-def build_golden_model(d):
+def build_golden_model(d, independent_X=True):
     from bottleneck.Encoder import CNNEncoder
     from bottleneck.Decoder import CNNDecoder
     from bottleneck.components import EffectivePropertyMap, ReducedOrderModelOperator
@@ -205,7 +205,7 @@ def build_golden_model(d):
     dec = CNNDecoder(n, dz, (8, 8), 1, 4, [1, 1], False, 4, drop_rate=0.)
     rom = ROM(StructuredGrid(nc), n // nc)
     g = ReducedOrderModelOperator(rom, torch.tensor(d['W']), dtype=torch.float32, device='cuda')
-    gp = EffectivePropertyMap(dz, 2 * nc * nc, dtype=torch.float32, device='cuda')
+    gp = EffectivePropertyMap(dz, 2 * nc * nc, independent_X=independent_X, dtype=torch.float32, device='cuda')
     model = GenerativeModel(f=dec.cuda(), g=g, gp=gp, dtype=torch.float32, device=torch.device('cuda'))
     model.encoder = enc.cuda()
     perm = torch.tensor(d['perm'], device='cuda')
@@ -214,6 +214,8 @@ def build_golden_model(d):
     model.register_datasets({'supervised': ds_s, 'unsupervised': ds_u}, None,
                             create_unsupervised_variational_approximation=False)
     state = {k[6:]: torch.tensor(v) for k, v in d.items() if k.startswith('state.')}
+    if not independent_X:     # lockX: no q_X rows, no gp.logsigmas_X
+        state = {k: v for k, v in state.items() if not k.startswith('q_X.') and k != 'gp.logsigmas_X'}
     model.load_state_dict(state)
     model.cuda()
     return model, bs
@@ -382,7 +384,8 @@ def test_codec_large_grids_vs_oracle(device, imsize, blocks, B):
 
 
 # ---------------------------------------------------------------- fused training step
-def test_fused_step_matches_module_path(device):
+@pytest.mark.parametrize('independent_X', [True, False])
+def test_fused_step_matches_module_path(device, independent_X):
     """FusedElboStep (graph-capturable step: noise and subset drawn one step ahead, fused epilogue)
     against GenerativeModel.elbo + backward with the same noise / subset and parameters, over two
     steps with the native Adam update in between (training.py:405-417; Adam itself is checked by
@@ -390,7 +393,7 @@ def test_fused_step_matches_module_path(device):
     import copy
     from gpi.train import FusedElboStep
     d = load('elbo_c32.npz')
-    model, bs = build_golden_model(d)
+    model, bs = build_golden_model(d, independent_X)
     ref_model = copy.deepcopy(model)
     Xu, Xs, Y, F = cuda(d['Xu']), cuda(d['Xs']), cuda(d['Y']), cuda(d['F'])
     step = FusedElboStep(model, Xu, bs, Xs, Y, F, lr=1e-3, seed=7)
@@ -400,7 +403,7 @@ def test_fused_step_matches_module_path(device):
                 assert k == k2
                 q.copy_(p)
         e = step.engine
-        eps = (e.eps_z().clone(), e.eps_x().clone())
+        eps = (e.eps_z().clone(), e.eps_x().clone() if independent_X else None)
         idx = step.idx.clone().long()
         ref_model._datasets['unsupervised'].perm = idx
         ref_model.zero_grad()
