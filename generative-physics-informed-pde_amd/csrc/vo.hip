@@ -690,39 +690,39 @@ __global__ __launch_bounds__(256) void vo_columns_kernel(gpi_vo_condition_desc d
 }
 
 // ---------------------------------------------------------------- precision
+// One workgroup per (row a, VO sample j): its term (Gamma_j mean_j - alpha_j)_a^2 + (Gamma_j^2 vars_j)_a
+// added in fp64 into beta[a] (zeroed by the launcher); vo_precision_final turns the sums into beta / vo_var.
 __global__ __launch_bounds__(256) void vo_precision_kernel(gpi_vo_precision_desc d) {
-    __shared__ double red[4];
-    const int a = blockIdx.x;
+    __shared__ double red[2][4];
+    const int a = blockIdx.x, j = blockIdx.y;
     const int m = d.m, dy = d.d_y;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    double tot = 0.0;
-    for (int j = 0; j < d.n; ++j) {
-        const double* row = d.gamma + ((int64_t)j * m + a) * dy;
-        const double* mu = d.mean + (int64_t)j * dy;
-        const double* va = d.vars + (int64_t)j * dy;
-        double s1 = 0.0, s2 = 0.0;
-        for (int i = tid; i < dy; i += 256) {
-            const double gv = row[i];
-            s1 = fma(gv, mu[i], s1);
-            s2 = fma(gv * gv, va[i], s2);
-        }
-        s1 = wave_sum_d(s1);
-        s2 = wave_sum_d(s2);
-        __syncthreads();
-        if (lane == 0) { red[wid] = s1; }
-        __syncthreads();
-        const double r1 = (red[0] + red[1]) + (red[2] + red[3]) - d.alpha[(int64_t)j * m + a];
-        __syncthreads();
-        if (lane == 0) red[wid] = s2;
-        __syncthreads();
-        const double r2 = (red[0] + red[1]) + (red[2] + red[3]);
-        tot += r1 * r1 + r2;
+    const double* row = d.gamma + ((int64_t)j * m + a) * dy;
+    const double* mu = d.mean + (int64_t)j * dy;
+    const double* va = d.vars + (int64_t)j * dy;
+    double s1 = 0.0, s2 = 0.0;
+    for (int i = tid; i < dy; i += 256) {
+        const double gv = row[i];
+        s1 = fma(gv, mu[i], s1);
+        s2 = fma(gv * gv, va[i], s2);
     }
+    s1 = wave_sum_d(s1);
+    s2 = wave_sum_d(s2);
+    if (lane == 0) { red[0][wid] = s1; red[1][wid] = s2; }
+    __syncthreads();
     if (tid == 0) {
-        const double beta = 0.5 * tot + d.beta0;
-        d.beta[a] = beta;
-        d.vo_var[a] = (d.infinite && d.infinite[a]) ? 0.0 : beta / (0.5 * (double)d.n + d.alpha0 + 1.0);
+        const double r1 = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]) - d.alpha[(int64_t)j * m + a];
+        const double r2 = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+        atomicAdd(&d.beta[a], r1 * r1 + r2);
     }
+}
+
+__global__ __launch_bounds__(256) void vo_precision_final(gpi_vo_precision_desc d) {
+    const int a = blockIdx.x * 256 + threadIdx.x;
+    if (a >= d.m) return;
+    const double beta = 0.5 * d.beta[a] + d.beta0;
+    d.beta[a] = beta;
+    d.vo_var[a] = (d.infinite && d.infinite[a]) ? 0.0 : beta / (0.5 * (double)d.n + d.alpha0 + 1.0);
 }
 
 // ---------------------------------------------------------------- reparametrised rows
@@ -901,7 +901,13 @@ extern "C" int gpi_vo_precision(const gpi_vo_precision_desc* d, void* stream) {
     if (!d || !d->gamma || !d->alpha || !d->mean || !d->vars || !d->beta || !d->vo_var || d->n < 0 || d->m < 1 ||
         d->d_y < 1)
         return GPI_ERR_ARG;
-    hipLaunchKernelGGL(vo_precision_kernel, dim3(d->m), dim3(256), 0, (hipStream_t)stream, *d);
+    const hipStream_t st = (hipStream_t)stream;
+    if (hipMemsetAsync(d->beta, 0, sizeof(double) * d->m, st) != hipSuccess) return GPI_ERR_LAUNCH;
+    if (d->n > 0) {
+        hipLaunchKernelGGL(vo_precision_kernel, dim3(d->m, d->n), dim3(256), 0, st, *d);
+        GPI_CHECK_LAUNCH();
+    }
+    hipLaunchKernelGGL(vo_precision_final, dim3((d->m + 255) / 256), dim3(256), 0, st, *d);
     GPI_CHECK_LAUNCH();
     return GPI_OK;
 }
