@@ -487,6 +487,7 @@ __global__ __launch_bounds__(256) void vo_chol_kernel(gpi_vo_condition_desc d) {
     else if (m <= CP_R) chol_panel(A, m, bad);
     else chol_block(A, m, bad);
     if (bad && d.flag && tid == 0) atomicOr(d.flag, 1);
+    if (!LDS) return;       // large m: b by vo_rhs_kernel, solves by vo_solvec_kernel
     // b = Gamma g - alpha
     const double* gam = d.gamma + (int64_t)j * m * dy;
     const float* g = d.g + (int64_t)j * dy;
@@ -497,12 +498,6 @@ __global__ __launch_bounds__(256) void vo_chol_kernel(gpi_vo_condition_desc d) {
         if (lane == 0) b[a] = s - d.alpha[(int64_t)j * m + a];
     }
     __syncthreads();
-    if (!LDS) {
-        // large m: the two triangular sweeps would be 2 m barrier-separated steps over global memory;
-        // b is handed to vo_solvec_kernel, which applies L^-T L^-1 once L^-1 exists
-        for (int e = tid; e < m; e += 256) d.solvec[(int64_t)j * m + e] = b[e];
-        return;
-    }
     // L z = b, L^T x = z
     for (int k = 0; k < m; ++k) {
         const double zk = b[k] / A[k * m + k];
@@ -572,6 +567,23 @@ __global__ __launch_bounds__(256) void vo_linv_wave_kernel(gpi_vo_condition_desc
         const int a = lane + 64 * k;
         if (a > c && a < m) lam[(int64_t)c * m + a] = x[k];
     }
+}
+
+// b = Gamma g - alpha into solvec (large-m path; one workgroup per (row a, VO sample j)): the two
+// triangular sweeps would be 2 m barrier-separated steps over global memory, so vo_solvec_kernel
+// applies L^-T L^-1 to it once L^-1 exists.
+__global__ __launch_bounds__(256) void vo_rhs_kernel(gpi_vo_condition_desc d) {
+    __shared__ double red[4];
+    const int a = blockIdx.x, j = blockIdx.y, m = d.m, dy = d.d_y;
+    const double* row = d.gamma + ((int64_t)j * m + a) * dy;
+    const float* g = d.g + (int64_t)j * dy;
+    double s = 0.0;
+    for (int i = threadIdx.x; i < dy; i += 256) s = fma(row[i], (double)g[i], s);
+    s = wave_sum_d(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0)
+        d.solvec[(int64_t)j * m + a] = (red[0] + red[1]) + (red[2] + red[3]) - d.alpha[(int64_t)j * m + a];
 }
 
 // solvec = Lambda^{-1} b = L^-T (L^-1 b) from the L^-1 in lam's upper triangle (large-m path).
@@ -884,6 +896,8 @@ extern "C" int gpi_vo_condition(const gpi_vo_condition_desc* d, void* stream) {
     if (lds_small <= 64 * 1024) {
         hipLaunchKernelGGL(vo_chol_kernel<true>, dim3(d->n), dim3(256), lds_small, st, *d);
     } else {
+        hipLaunchKernelGGL(vo_rhs_kernel, dim3(d->m, d->n), dim3(256), 0, st, *d);
+        GPI_CHECK_LAUNCH();
         hipLaunchKernelGGL(vo_chol_kernel<false>, dim3(d->n), dim3(256), sizeof(double) * d->m, st, *d);
     }
     GPI_CHECK_LAUNCH();
