@@ -610,7 +610,7 @@ __global__ __launch_bounds__(256) void vo_solvec_kernel(gpi_vo_condition_desc d)
 
 // Posterior per column i of Gamma (fp64): q = L^{-1} Gamma_i as a blocked lower-triangular GEMM
 // Q = L^{-1} Gamma over a 64-column tile (64 x 32 L^{-1} blocks and 32 x 64 Gamma blocks in LDS,
-// 4 x 4 fp64 accumulators per thread), only |q|^2 kept;  mean_i = g_i - cov_i Gamma_i . solvec,
+// fp64 MFMA 16x16x4 per wave), only |q|^2 kept;  mean_i = g_i - cov_i Gamma_i . solvec,
 // vars_i = cov_i - cov_i^2 |q|^2.
 constexpr int VC_BA = 64, VC_BK = 32, VC_BN = 64;
 __global__ __launch_bounds__(256) void vo_columns_kernel(gpi_vo_condition_desc d) {
@@ -619,7 +619,7 @@ __global__ __launch_bounds__(256) void vo_columns_kernel(gpi_vo_condition_desc d
     __shared__ double red[16][VC_BN];
     const int j = blockIdx.y;
     const int m = d.m, dy = d.d_y;
-    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+    const int tid = threadIdx.x;
     const int i0 = blockIdx.x * VC_BN;
     const double* gam = d.gamma + (int64_t)j * m * dy;
     const double* lam = d.lam + (int64_t)j * m * m;
@@ -637,16 +637,17 @@ __global__ __launch_bounds__(256) void vo_columns_kernel(gpi_vo_condition_desc d
     double smv = 0.0;
     if (tid < VC_BN) smv = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
     __syncthreads();
-    double qp[4] = {0.0, 0.0, 0.0, 0.0};
+    // v_mfma_f64_16x16x4_f64: wave w owns rows [16w, 16w + 16) of the 64-row block and the four 16-column
+    // sub-blocks; A[l&15][k=l>>4], B[k=l>>4][l&15], D col = l&15, row = (l>>4) + 4 reg.
+    typedef double f64x4 __attribute__((ext_vector_type(4)));
+    const int lane = tid & 63, w = tid >> 6;
+    double qp[4] = {0.0, 0.0, 0.0, 0.0};          // per 16-column sub-block, this lane's column
     for (int A0 = 0; A0 < m; A0 += VC_BA) {
-        double acc[4][4];
+        f64x4 acc[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int c = 0; c < 4; ++c) acc[r][c] = 0.0;
+        for (int cb = 0; cb < 4; ++cb) acc[cb] = f64x4{0.0, 0.0, 0.0, 0.0};
         const int bend = min(A0 + VC_BA, m);
         for (int B0 = 0; B0 < bend; B0 += VC_BK) {
-            // L^{-1}[A0 + ra][B0 + rb]
             for (int e = tid; e < VC_BA * VC_BK; e += 256) {
                 const int ra = e & (VC_BA - 1), rb = e / VC_BA;
                 const int a = A0 + ra, b = B0 + rb;
@@ -663,34 +664,36 @@ __global__ __launch_bounds__(256) void vo_columns_kernel(gpi_vo_condition_desc d
                 Gs[rb][col] = (b < m && i < dy) ? gam[(int64_t)b * dy + i] : 0.0;
             }
             __syncthreads();
-#pragma unroll 4
-            for (int kk = 0; kk < VC_BK; ++kk) {
-                double lv[4], gv[4];
 #pragma unroll
-                for (int r = 0; r < 4; ++r) lv[r] = Ls[ty * 4 + r][kk];
+            for (int k0 = 0; k0 < VC_BK; k0 += 4) {
+                const double av = Ls[16 * w + (lane & 15)][k0 + (lane >> 4)];
 #pragma unroll
-                for (int c = 0; c < 4; ++c) gv[c] = Gs[kk][tx * 4 + c];
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-#pragma unroll
-                    for (int c = 0; c < 4; ++c) acc[r][c] = fma(lv[r], gv[c], acc[r][c]);
+                for (int cb = 0; cb < 4; ++cb) {
+                    const double bv = Gs[k0 + (lane >> 4)][16 * cb + (lane & 15)];
+                    acc[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[cb], 0, 0, 0);
+                }
             }
             __syncthreads();
         }
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
+        for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
-            for (int c = 0; c < 4; ++c) qp[c] = fma(acc[r][c], acc[r][c], qp[c]);
+            for (int r = 0; r < 4; ++r) qp[cb] = fma(acc[cb][r], acc[cb][r], qp[cb]);
     }
+    // sum the four row groups of the wave (lanes l, l^16, l^32, l^48), then the four waves
 #pragma unroll
-    for (int c = 0; c < 4; ++c) red[ty][tx * 4 + c] = qp[c];
+    for (int cb = 0; cb < 4; ++cb) {
+        qp[cb] += __shfl_xor(qp[cb], 16, 64);
+        qp[cb] += __shfl_xor(qp[cb], 32, 64);
+    }
+    if (lane < 16)
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) red[w][16 * cb + lane] = qp[cb];
     __syncthreads();
     if (tid >= VC_BN) return;
     const int i = i0 + tid;
     if (i >= dy) return;
-    double qn = 0.0;
-#pragma unroll
-    for (int t = 0; t < 16; ++t) qn += red[t][tid];
+    const double qn = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
     const int64_t o = (int64_t)j * dy + i;
     const double cov = 1.0 / (double)d.prec[o];
     const double mean = (double)d.g[o] - cov * smv;
