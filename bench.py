@@ -52,12 +52,14 @@ CONFIGS = {
 CONFIG_TAG = {'c32': '1', 'c64': '2/3', 'c128': '4', 'c256': '5'}
 
 
-def make_data(fac, n, pool, N_s, field, seed, device):
+def make_data(fac, n, pool, N_s, field, seed, device, rank=0):
+    """Unlabeled pool: the SAME on every rank (seed), each rank slices a shared global permutation
+    of it; labeled samples (fields, FOM labels, ROM boundary forces): rank-owned (seed + 1 + rank)."""
     from physics.RandomField import NormalRandomFieldSampler
     from physics.grid import pixel_to_cells
-    rng = np.random.default_rng(seed)
     rfs = NormalRandomFieldSampler.FromImage(n, n, *field)
-    Xu = rfs.sample(batch_size=pool, rng=rng)
+    Xu = rfs.sample(batch_size=pool, rng=np.random.default_rng(seed))
+    rng = np.random.default_rng(seed + 1 + rank)
     Xs = rfs.sample(batch_size=N_s, rng=rng)
     U = rng.uniform(-0.5, 0.5, (N_s, 4))
     physics = fac._physics()
@@ -68,10 +70,10 @@ def make_data(fac, n, pool, N_s, field, seed, device):
     return t(Xu), t(Xs), t(Y), t(F), U
 
 
-def build(cfg_name, device, seed):
+def build(cfg_name, device, seed, rank=0, world=1):
     from factories.model import ModelFactory
-    from utils.data import DataSet, DataLoader
     fname, B_u, N_s, pool, field = CONFIGS[cfg_name]
+    pool *= world                              # global pool; per-GPU work fixed (weak scaling)
     fac = ModelFactory.FromIdentifier(fname)
     fac.set('device', 'cuda')
     torch.manual_seed(0)                       # identical shared parameters on every rank
@@ -79,7 +81,7 @@ def build(cfg_name, device, seed):
     model = model.to(device)
     encoder = encoder.to(device)
     n = physics['fom'].grid.n
-    Xu, Xs, Y, F, U = make_data(fac, n, pool, N_s, field, seed, device)
+    Xu, Xs, Y, F, U = make_data(fac, n, pool, N_s, field, seed, device, rank)
 
     class _T(object):       # device-resident dataset views
         def __init__(self, **t):
@@ -143,19 +145,39 @@ def profile_kernels(step, reps=20):
     return out
 
 
-def cpu_baseline(model, data, B_u, N_s, physics, budget_s=12.0, max_steps=20):
-    """The oracle (CPU port of the reference step, torch fp32) timed on the host cores."""
+def host_cpu():
+    """(cores this process may run on, all host cores, CPU model string)."""
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count() or 1
+    model = 'unknown'
+    try:
+        with open('/proc/cpuinfo') as fh:
+            for line in fh:
+                if line.startswith('model name'):
+                    model = line.split(':', 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return usable, os.cpu_count() or usable, model
+
+
+def cpu_baseline(model, data, B_u, N_s, physics, warmup=10, steps=50, budget_s=45.0):
+    """The oracle (CPU port of the reference step, torch fp32) timed on the host cores
+    (BASELINE.md section 3): torch threads = every core this process may run on, 10 warm-up + 50
+    timed steps of the same step shape; if the warm-up shows 50 steps would exceed budget_s, fewer
+    timed steps (>= 5) and the sample says so."""
     from oracle import codec as ocodec
     from oracle import elbo as oelbo
     from oracle import fem
-    threads = min(16, os.cpu_count() or 1)
+    threads, host_cores, cpu_model = host_cpu()
     torch.set_num_threads(threads)
     Xu, Xs, Y, F = [t.detach().cpu() for t in data]
     enc, dec = model.encoder, model.f
     ec, dc = enc.native_config(), dec.native_config()
     params = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in model.named_parameters()}
     nc = physics['rom'].grid.n
-    n = physics['fom'].grid.n
     M = torch.tensor(fem.rom_stiffness_tensor(fem.unit_square_mesh(nc)), dtype=torch.float32)
     W = torch.tensor(physics['W'], dtype=torch.float32)
     bc = torch.tensor(physics['rom'].grid.constrained_dofs)
@@ -180,16 +202,45 @@ def cpu_baseline(model, data, B_u, N_s, physics, budget_s=12.0, max_steps=20):
         (-(e1 + e2)).backward()
         opt.step()
 
-    one_step()                      # warm-up
     t0 = time.perf_counter()
-    k = 0
-    while k < max_steps and (time.perf_counter() - t0) < budget_s:
+    for _ in range(warmup):
         one_step()
-        k += 1
+    t_step = (time.perf_counter() - t0) / warmup
+    k = steps if t_step * steps <= budget_s else max(5, int(budget_s / t_step))
+    t0 = time.perf_counter()
+    for _ in range(k):
+        one_step()
     dt = time.perf_counter() - t0
-    return dict(value=(B_u + N_s) * k / dt, unit='samples/s', cores=threads, kind='port',
-                sample='%d steps of the same C64 step (B_u=%d, N_s=%d) on CPU torch fp32 (oracle port)' % (
-                    k, B_u, N_s))
+    note = '' if k == steps else ' (budget-capped from %d)' % steps
+    return dict(value=round((B_u + N_s) * k / dt, 1), unit='samples/s', cores=threads, host_cores=host_cores,
+                cpu_model=cpu_model, kind='port', ms_per_step=round(1e3 * dt / k, 2),
+                sample='%d warm-up + %d timed steps%s of the same step (B_u=%d, N_s=%d) on CPU torch fp32 '
+                       '(oracle port), torch threads = %d' % (warmup, k, note, B_u, N_s, threads))
+
+
+def step_bytes(model, B_u, N_s, physics):
+    """Algorithmic HBM bytes of one step: per unlabeled sample
+    4 [6 (S_enc + S_dec) + 6 H W], per labeled sample 4 [6 S_dec + 6 H W] + 4 (d_y + n_c + 2 n_T),
+    S = sum over BatchNorm layers of their input elements per sample."""
+    from gpi.plan import encoder_program, decoder_program
+
+    def S(prog):
+        return sum(op.cin * op.src.H * op.src.W for op in prog.ops if op.bn is not None)
+    s_enc = S(encoder_program(**model.encoder.native_config()))
+    s_dec = S(decoder_program(**model.f.native_config()))
+    n = physics['fom'].grid.n
+    nc = physics['rom'].grid.n
+    d_y, n_c, n_T = (n + 1) * (n - 1), (nc + 1) ** 2, 2 * nc * nc
+    per_u = 4 * (6 * (s_enc + s_dec) + 6 * n * n)
+    per_s = 4 * (6 * s_dec + 6 * n * n) + 4 * (d_y + n_c + 2 * n_T)
+    return B_u * per_u + N_s * per_s, dict(S_enc=s_enc, S_dec=s_dec, per_unlabeled=per_u, per_labeled=per_s)
+
+
+def conv_source_sha():
+    """sha1 of csrc/conv.hip: PMC traffic figures are only used for the code they were measured on."""
+    import hashlib
+    with open(os.path.join(PKG, 'csrc', 'conv.hip'), 'rb') as fh:
+        return hashlib.sha1(fh.read()).hexdigest()
 
 
 def main():
@@ -203,6 +254,10 @@ def main():
     ap.add_argument('--no-roofline', action='store_true')
     ap.add_argument('--kprof', default=None, help='write the per-operator HIP-event profile (JSON) here')
     args = ap.parse_args()
+    dbg = sorted(k for k in os.environ if k.startswith('GPI_DBG_'))
+    if dbg:
+        raise SystemExit('bench.py refuses to report with %s set (timing-build switches that skip work)' % dbg)
+    tuning = {k: os.environ[k] for k in sorted(os.environ) if k.startswith('GPI_TILE_')}
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
@@ -223,9 +278,11 @@ def main():
     torch.cuda.set_device(device)
 
     from gpi.train import FusedElboStep
-    model, data, (B_u, N_s), physics = build(args.config, device, seed=1000 + rank)
+    model, data, (B_u, N_s), physics = build(args.config, device, seed=1000, rank=rank, world=world)
     Xu, Xs, Y, F = data
-    step = FusedElboStep(model, Xu, B_u, Xs, Y, F, lr=1e-2, seed=4321 + rank, distributed=distributed)
+    # shared subset seed: every rank draws the same global permutation and takes its slice
+    step = FusedElboStep(model, Xu, B_u, Xs, Y, F, lr=1e-2, seed=4321 + rank, subset_seed=777,
+                         distributed=distributed, rank=rank, world=world)
     if not args.no_graph:
         step.capture()
     for _ in range(args.warmup):
@@ -247,13 +304,15 @@ def main():
         dist.all_reduce(dt, op=dist.ReduceOp.MAX)
     dt = float(dt.item())
     elbo = float(step.elbo().item())
-    if not math.isfinite(elbo) and not os.environ.get('GPI_DBG_SKIP'):   # timing experiments skip work
+    if not math.isfinite(elbo):
         raise RuntimeError('non-finite ELBO %r' % elbo)
-    if not os.environ.get('GPI_DBG_SKIP'):
-        step.engine.check_flag()
+    step.engine.check_flag()
 
     roof = None
     cpu = None
+    per_step = B_u + N_s
+    ms_step = 1e3 * dt / args.steps
+    sbytes, sparts = step_bytes(model, B_u, N_s, physics)
     if rank == 0 and not args.no_roofline:
         prof = profile_kernels(step)
         if args.kprof:
@@ -262,25 +321,33 @@ def main():
         name, ms, byts = max(prof, key=lambda t: t[1])
         ach = byts / (ms * 1e-3) / 1e9
         traffic = None
+        traffic_note = 'no PMC traffic file'
         if os.path.exists(TRAFFIC_JSON):
             with open(TRAFFIC_JSON) as fh:
-                t = json.load(fh)['ops'].get(name)
-            traffic = round(t['traffic_bytes']) if t else None
+                tj = json.load(fh)
+            if tj.get('conv_hip_sha1') != conv_source_sha():
+                traffic_note = 'PMC traffic file measured on other conv.hip code: dropped'
+            else:
+                t = tj['ops'].get(name)
+                traffic = round(t['traffic_bytes']) if t else None
+                traffic_note = '%s (PMC FETCH_SIZE / WRITE_SIZE passes)' % os.path.basename(TRAFFIC_JSON)
+        step_ach = sbytes / (ms_step * 1e-3) / 1e9
         roof = dict(bound='hbm', achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit='GB/s',
-                    frac=round(ach / HBM_PEAK_GBS, 4), traffic=traffic, kernel=name,
+                    frac=round(ach / HBM_PEAK_GBS, 4), traffic=traffic, traffic_source=traffic_note, kernel=name,
                     kernel_ms=round(ms, 5), bytes_per_launch=byts,
-                    codec_ms_sum=round(sum(t[1] for t in prof), 4))
+                    codec_ms_sum=round(sum(t[1] for t in prof), 4),
+                    step=dict(bytes=sbytes, achieved=round(step_ach, 1), frac=round(step_ach / HBM_PEAK_GBS, 4),
+                              **sparts))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(model, data, B_u, N_s, physics)
 
     if rank == 0:
-        per_step = B_u + N_s
         value = world * per_step * args.steps / dt
         line = {
             'metric': 'ELBO training-step samples/sec (64x64 grids)' if args.config == 'c64' else
             'ELBO training-step samples/sec (%s)' % args.config,
             'value': round(value, 1), 'unit': 'samples/s', 'n_gpus': world, 'steps': args.steps,
-            'warmup': args.warmup, 'ms_per_step': round(1e3 * dt / args.steps, 4), 'higher_is_better': True,
+            'warmup': args.warmup, 'ms_per_step': round(ms_step, 4), 'higher_is_better': True,
             'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32', 'data': 'synthetic',
             'config': {'workload': 'BASELINE config %s: %s grid, B_u=%d unlabeled + N_s=%d labeled per GPU, '
                                    'ROM %dx%d, fused native step' % (CONFIG_TAG[args.config], args.config, B_u, N_s,
@@ -292,6 +359,8 @@ def main():
             'roofline': roof,
             'cpu_baseline': cpu,
         }
+        if tuning:
+            line['tuning_env'] = tuning
         print(json.dumps(line))
     if distributed:
         dist.destroy_process_group()

@@ -86,8 +86,18 @@ struct ConvGeom {
     int in_sq, in_sr, in_sc;   // 256 chunks of the input image = (planes, rows, chunks)
     int g_sq, g_sr, g_sc;      // ... of the output-gradient image
     Div d_in4, d_P4, d_g4, d_PG4, d_cin, d_cout, d_win, d_tp, d_wout, d_w2;
-    int dbg;   // GPI_DBG_SKIP (timing experiments only, results invalid): 1 skip wgrad, 2 skip dgrad
+#ifdef GPI_PHASE_TIMING
+    int dbg;   // GPI_DBG_SKIP of the timing build (never the product): 1 skip wgrad, 2 dgrad, 4 loss atomics
+#endif
 };
+
+// Work-skip switches exist only in the timing build (make timing); the product library always
+// does all of the work.
+#ifdef GPI_PHASE_TIMING
+#define SKIP(G, bit) (((G).dbg & (bit)) != 0)
+#else
+#define SKIP(G, bit) false
+#endif
 
 // first input row and row count of the input image of output rows [o0, o0 + t)
 __host__ __device__ inline void in_rows(int k, int s, int up, int pad, int o0, int t, int& i0, int& len) {
@@ -190,8 +200,10 @@ bool conv_geom(const gpi_conv_desc& d, const gpi_groups& g, ConvGeom& G, bool fw
         eo * d.w_in >= lim || 256ull * G.th * d.w_out >= lim)
         return false;
     G.zero = nullptr;   // set by launch()
+#ifdef GPI_PHASE_TIMING
     static const int dbg = env_int("GPI_DBG_SKIP", 0);
     G.dbg = dbg;
+#endif
     {
         const int P4 = G.P / 4, pl = G.rh * P4, Q4 = G.PG / 4, gl = G.gh * Q4;
         G.in_sq = 256 / pl;
@@ -586,7 +598,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void c
         float v[1] = {Lv};
         block_sum<1>(v, scratch, red);
         __syncthreads();
-        if (tid == 0 && !(G.dbg & 4)) atomicAdd(c.loss_acc + T.grp * GPI_REPLICAS + blockIdx.x % GPI_REPLICAS, (double)red[0]);
+        if (tid == 0 && !SKIP(G, 4)) atomicAdd(c.loss_acc + T.grp * GPI_REPLICAS + blockIdx.x % GPI_REPLICAS, (double)red[0]);
         PHASE(7);
         RTSTAMP(1);
         return;
@@ -594,7 +606,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void c
     if (d.epilogue == GPI_EPI_STORE_STATS) {
         block_sum<2 * CP>(vst, scratch, red);
         __syncthreads();
-        if (tid < 2 * d.cout && !(G.dbg & 4)) {
+        if (tid < 2 * d.cout && !SKIP(G, 4)) {
             gpi_stat* st = stat_slot(c, d.out_stat + (tid >> 1), T.grp);
             atomicAdd((tid & 1) ? &st->sumsq : &st->sum, (double)red[tid]);
         }
@@ -704,7 +716,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 
     // cin <= 4 at stride 1: the input gradient runs on the VALU (phase 4b'), the MFMA form would
     // leave >= 3/4 of its N = 16 columns empty
     const bool vdg = K == 5 && S == 1 && !UP && has_gin && d.cin <= 4;
-    const int nmblk = (has_gin && !vdg && !(G.dbg & 2)) ? (G.ph * d.w_in) >> 4 : 0;
+    const int nmblk = (has_gin && !vdg && !SKIP(G, 2)) ? (G.ph * d.w_in) >> 4 : 0;
     const int ci_l = min(l16, d.cin - 1);
     const bool cok = l16 < d.cin;
     const int64_t ibase = ((int64_t)T.b * d.in_ctot + d.in_c0 + ci_l) * HWi + (int64_t)py0 * d.w_in;
@@ -849,7 +861,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 
     // stride-2 columns (the column-shift form below would compute ~6x the useful products here)
     const bool vwg = K == 7 && S == 2 && !UP && d.cin == 1 && !has_gin && d.cout <= 16;
     if constexpr (K == 7 && S == 2 && !UP) {
-        if (vwg && !(G.dbg & 1)) {
+        if (vwg && !SKIP(G, 1)) {
             constexpr int PADC = K / 2, NB = (KK + 15) / 16;
             const int tp = G.th * d.w_out;
             const int co_a = min(l16, d.cout - 1);                  // A row (rows >= cout never stored)
@@ -894,7 +906,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 
     }
     {
         const int MI = d.cout * K, NJ = d.cin * K;
-        const int nmb = ((G.dbg & 1) || vwg) ? 0 : (MI + 15) >> 4, nnb = (NJ + 15) >> 4;
+        const int nmb = (SKIP(G, 1) || vwg) ? 0 : (MI + 15) >> 4, nnb = (NJ + 15) >> 4;
         const int XW = UP ? d.w_out + K - 1 : S * (d.w_out - 1) + K;   // virtual input columns
         const int nxs = (XW + 3) >> 2;
         for (int mb = 0; mb < nmb; ++mb) {
@@ -1126,7 +1138,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 
     // an owned row per thread, all (<= 4) input channels at once; weights are LDS broadcasts of
     // the same zero-padded [co * KK + tap][16] table the MFMA path uses.
     float vsd[4] = {0.f, 0.f, 0.f, 0.f}, vsdx[4] = {0.f, 0.f, 0.f, 0.f};
-    if (vdg && !(G.dbg & 2)) {
+    if (vdg && !SKIP(G, 2)) {
         const int np2 = (G.ph * d.w_in) >> 1;
         float lg[4], lb[4], lr[4];
 #pragma unroll
@@ -1244,7 +1256,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 
             slab[d.cout * J + d.cin + tid] = (float)s_d;     // dbeta
             gpi_stat* st = stat_slot(c, d.in_stat + tid, T.grp);
             const double gm = i_gam[tid];
-            if (!(G.dbg & 4)) {
+            if (!SKIP(G, 4)) {
                 atomicAdd(&st->ssum, gm * s_d);
                 atomicAdd(&st->sxsum, gm * s_dx);
             }
@@ -1335,11 +1347,13 @@ int launch(const gpi_conv_desc& d, const gpi_codec_ctx& c, hipStream_t st, bool 
     G.zero = zero;
     const size_t lds = fwd ? fwd_lds(d, G, cp) : bwd_lds(d, G);
     if (lds > 160 * 1024) return GPI_ERR_UNSUPPORTED;
+#ifdef GPI_PHASE_TIMING
     static const int dbg_print = env_int("GPI_DBG_PRINT", 0);
     if (dbg_print)
         fprintf(stderr, "conv %s k%d s%d up%d cin%d cout%d in%dx%d out%dx%d th%d blocks %d lds %zu\n",
                 fwd ? "fwd" : "bwd", d.k, d.stride, d.upsample, d.cin, d.cout, d.h_in, d.w_in, d.h_out, d.w_out, G.th,
                 G.nblocks, lds);
+#endif
     if (lds > 64 * 1024) {
         if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
             return GPI_ERR_LAUNCH;

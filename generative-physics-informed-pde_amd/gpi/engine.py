@@ -17,7 +17,6 @@ unsupervised term (generative.py:546-585) + the supervised freeX term
 """
 import ctypes as C
 import math
-import os
 
 import torch
 
@@ -25,7 +24,6 @@ from . import _lib as L
 from .plan import Arena, encoder_program, decoder_program
 
 ENT_CONST = 0.5 * (math.log(2 * math.pi) + 1)
-_DBG_NO_ROM = os.environ.get('GPI_DBG_NO_ROM') == '1'
 N_TERMS = 16
 R = L.GPI_REPLICAS
 # term slots in the fp64 scratch
@@ -389,8 +387,6 @@ class ElboEngine(object):
         if self.roms:
             self._side.wait_event(self._ev_fork)
             for r in self.roms:
-                if _DBG_NO_ROM:       # timing experiments only (results invalid)
-                    continue
                 _run(lib.gpi_rom, C.byref(r), C.c_void_p(self._side.cuda_stream), what='rom')
             self._ev_join.record(self._side)
             self._pending_join = True
@@ -681,8 +677,9 @@ def rom_call(nc, refine, x, F, input_kappa, mode, mu_y=None, uc=None, dmu=None, 
     _run(_lib().gpi_rom, C.byref(r), L.stream_handle(), what='rom')
 
 
-def cgr_residual(logkappa_img, y, bc, nc):
-    """W^T [K(kappa) yhat]_free for a batch of fields -> [N, (nc+1)^2]."""
+def cgr_residual(logkappa_img, y, bc, nc, flux=False):
+    """W^T [K(kappa) yhat]_free for a batch of fields -> [N, (nc+1)^2]; flux=True also returns the
+    flux-constraint residual Gamma_fc y [N, 2 nc^2] of the same pass (flux.py:81-158, alpha = 0)."""
     for t in (logkappa_img, y, bc):
         L.require_device(t)
     N, n = logkappa_img.shape[0], logkappa_img.shape[-1]
@@ -690,6 +687,8 @@ def cgr_residual(logkappa_img, y, bc, nc):
     d = L.ResidualDesc()
     lk, yy, bb = logkappa_img.contiguous().float(), y.contiguous().float(), bc.contiguous().float()
     d.n_fine, d.nc, d.n = n, nc, N
-    d.logkappa, d.y, d.bc, d.r, d.r_flux = lk.data_ptr(), yy.data_ptr(), bb.data_ptr(), r.data_ptr(), None
+    rf = torch.empty(N, 2 * nc * nc, dtype=torch.float32, device=y.device) if flux else None
+    d.logkappa, d.y, d.bc, d.r = lk.data_ptr(), yy.data_ptr(), bb.data_ptr(), r.data_ptr()
+    d.r_flux = rf.data_ptr() if flux else None
     _run(_lib().gpi_cgr_residual, C.byref(d), L.stream_handle(), what='cgr residual')
-    return r
+    return (r, rf) if flux else r

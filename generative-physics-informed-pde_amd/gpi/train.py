@@ -28,33 +28,61 @@ def allreduce_shared(flat, group=None):
         dist.all_reduce(flat.G[:n], op=dist.ReduceOp.SUM, group=group)
 
 
+class FusedAdamSchedule(torch.optim.Optimizer):
+    """The learning-rate handle of a FusedElboStep as a torch Optimizer, so that torch LR schedulers
+    (and lamp.optimization.LearningScheduleWrapper, lamp/optimization.py:71-93, training.py:452,615)
+    drive the fused step's device-resident Adam exactly as they drive torch.optim.Adam: the
+    scheduler edits ``param_groups[0]['lr']``; FusedElboStep copies a changed value into the
+    device learning rate before its next step (an async fill, no host synchronisation)."""
+
+    def __init__(self, lr, betas, eps):
+        super().__init__([torch.zeros(1)], dict(lr=lr, betas=betas, eps=eps))
+
+    def step(self, closure=None):     # the update itself runs inside the fused step
+        return None
+
+
 class FusedElboStep(object):
+    """rank / world: data-parallel position.  Every rank holds the same global unlabeled pool and
+    draws the same global permutation (``subset_seed``, shared) of which it takes its B_u-slice
+    (SURVEY.md section 8e); labeled samples and their q rows are rank-owned; the
+    reparametrisation noise uses ``seed`` (per rank)."""
 
     def __init__(self, model, X_pool, B_u, X_s=None, Y=None, F=None, lr=1e-2, betas=(0.9, 0.999), eps=1e-8,
-                 seed=0, normalize=False, process_group=None, distributed=False):
+                 seed=0, normalize=False, process_group=None, distributed=False, rank=0, world=1, subset_seed=None):
         self.model = model
         self.flat = model.native_flat()
         self.N_s = 0 if X_s is None else int(X_s.shape[0])
         self.B_u = int(B_u)
+        self.rank, self.world = int(rank), int(world)
+        assert 0 <= self.rank < self.world
         self.engine = ElboEngine(model, self.B_u, self.N_s, normalize=normalize)
         dev = self.flat.P.device
         self.X_pool = X_pool.contiguous().float() if X_pool is not None else None
         self.X_s, self.Y, self.F = X_s, Y, F
-        self.idx = torch.zeros(max(self.B_u, 1), dtype=torch.int32, device=dev)
+        # global subset of world * B_u pool indices; this rank's slice [rank * B_u, (rank + 1) * B_u)
+        self.n_sub = self.world * self.B_u
+        self.idx = torch.zeros(max(self.n_sub, 1), dtype=torch.int32, device=dev)
         self.rng_off = torch.zeros(1, dtype=torch.int64, device=dev)
         self.step_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
         self.lr = torch.tensor([lr], dtype=torch.float32, device=dev)
+        self.optimizer = FusedAdamSchedule(lr, betas, eps)
+        self._lr_host = float(lr)
         self.m = torch.zeros_like(self.flat.P)
         self.v = torch.zeros_like(self.flat.P)
         self.seed = int(seed)
+        self.subset_seed = int(seed if subset_seed is None else subset_seed)
         self.distributed = distributed
         self.pg = process_group
         self.adam = L.AdamDesc(p=self.flat.P.data_ptr(), g=self.flat.G.data_ptr(), m=self.m.data_ptr(),
                                v=self.v.data_ptr(), n=self.flat.numel, lr=self.lr.data_ptr(),
                                step=self.step_ctr.data_ptr(), beta1=betas[0], beta2=betas[1], eps=eps)
         self.idx_next = torch.zeros_like(self.idx)
-        self.engine.bind(X_u=self.X_pool, u_index=self.idx if self.B_u else None, X_s=X_s, Y=Y, F=F)
+        my_idx = self.idx[self.rank * self.B_u:(self.rank + 1) * self.B_u] if self.B_u else None
+        self.engine.bind(X_u=self.X_pool, u_index=my_idx, X_s=X_s, Y=Y, F=F)
         n_pool = self.X_pool.shape[0] if self.X_pool is not None else 0
+        if self.B_u and self.n_sub > n_pool:
+            raise ValueError('the pool (%d) is smaller than the global armortized batch (%d)' % (n_pool, self.n_sub))
         self.n_pool = n_pool
         self.rng_span = max(n_pool, (self.engine.B * self.engine.dz + 3) // 4 + 1,
                             (self.N_s * self.engine.d_x + 3) // 4 + 1)
@@ -67,7 +95,7 @@ class FusedElboStep(object):
                                       step=self.step_ctr.data_ptr(), scratch=ws.t_scr.data_ptr(),
                                       n_scratch=ws.t_scr.numel(), terms_dst=self.last_terms.data_ptr(),
                                       idx_src=self.idx_next.data_ptr(), idx_dst=self.idx.data_ptr(),
-                                      n_idx=self.B_u)
+                                      n_idx=self.n_sub if self.B_u else 0)
         self.graph = None
         # the first step's noise; every step then draws the next step's during its backward
         self._launch_noise(L.stream_handle(), self.idx, sub0=100)
@@ -80,7 +108,7 @@ class FusedElboStep(object):
         differs from step k's own, which was drawn during step k-1 or by the prologue (sub0 = 100)."""
         lib = L.lib()
         if self.B_u:
-            L.check(lib.gpi_random_subset(L.ptr(idx), self.n_pool, self.B_u, self.seed, L.ptr(self.rng_off),
+            L.check(lib.gpi_random_subset(L.ptr(idx), self.n_pool, self.n_sub, self.subset_seed, L.ptr(self.rng_off),
                                           sub0 + 1, st), 'random subset')
         ez = self.engine.eps_z()
         L.check(lib.gpi_randn(L.ptr(ez), ez.numel(), self.seed, L.ptr(self.rng_off), sub0 + 2, st), 'randn z')
@@ -102,6 +130,13 @@ class FusedElboStep(object):
         if self.distributed:
             allreduce_shared(self.flat, self.pg)
 
+    def sync_lr(self):
+        """Copy a scheduler-changed learning rate (optimizer.param_groups[0]['lr']) to the device."""
+        lr = float(self.optimizer.param_groups[0]['lr'])
+        if lr != self._lr_host:
+            self.lr.fill_(lr)
+            self._lr_host = lr
+
     def update(self, stream=None):
         st = stream if stream is not None else L.stream_handle()
         L.check(L.lib().gpi_adam(C.byref(self.adam), st), 'adam (+ rng offset advance)')
@@ -112,14 +147,31 @@ class FusedElboStep(object):
         self.update()
 
     # ------------------------------------------------------------------
+    def _mutable_state(self):
+        """Every device buffer a step writes: parameters, Adam moments and counter, Philox offset,
+        subsets, accumulators, gradient, the workspace (incl. the pre-drawn noise) and the term /
+        statistics scratch."""
+        ws = self.engine.ws
+        return [self.flat.P, self.m, self.v, self.step_ctr, self.rng_off, self.idx, self.idx_next,
+                self.flat.gacc, self.flat.G, ws.t_ws, ws.t_scr, ws.t_parts, ws.t_flag, self.last_terms]
+
     def capture(self):
-        """Capture the step into HIP graph(s); the all-reduce stays outside the graph."""
+        """Capture the step into HIP graph(s); the all-reduce stays outside the graph.
+        The two warm-up steps run on snapshots: capture() leaves parameters, optimizer state,
+        step counter, random stream and the pre-drawn subset / noise exactly as it found them, so
+        the first replayed step is the step an eager loop would take next."""
+        torch.cuda.synchronize()
+        saved = [t.clone() for t in self._mutable_state()]
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(2):          # warm up allocator / kernels on the side stream
                 self.step_eager()
         torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        for t, v in zip(self._mutable_state(), saved):
+            t.copy_(v)
+        del saved
         torch.cuda.synchronize()
         self.g_fb = torch.cuda.CUDAGraph()
         self.g_up = None
@@ -136,6 +188,7 @@ class FusedElboStep(object):
         self.graph = True
 
     def step(self):
+        self.sync_lr()
         if self.graph is None:
             return self.step_eager()
         self.g_fb.replay()

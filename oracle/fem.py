@@ -361,3 +361,47 @@ def _bary(p, pt):
     l1 = g[1] @ (pt - p[0])
     l2 = g[2] @ (pt - p[0])
     return None, np.array([1 - l1 - l2, l1, l2])
+
+
+def flux_residual_structured(nc, r, kappa_lr, kappa_ul, y_free):
+    """r_fc = Gamma_fc[:, free] y for every coarse triangle (bottleneck/flux.py:81-158, the rows of
+    ``flux_rows`` above, alpha = 0), in closed form on the structured mesh and vectorised so that it
+    runs at 128^2 / 256^2 where the generic facet search of ``flux_rows`` does not finish.  Pinned
+    against ``flux_rows`` on small meshes (tests/test_physics_stencil.py).
+
+    kappa_lr / kappa_ul: [n, n] conductivities of the fine T_lr / T_ul of square (i, j) at [j, i];
+    y_free: fine free-node values (Dirichlet columns x = 0 / 1 enter as 0, the free-column
+    restriction).  Per fine triangle with corner values u0 (i,j), u1 (i+1,j), u2 (i,j+1), u3
+    (i+1,j+1), |e| kappa grad(u).n on its facets:
+      T_lr: bottom kappa (u1 - u3), right kappa (u1 - u0), diagonal kappa (u0 - 2 u1 + u3);
+      T_ul: left kappa (u2 - u3), top kappa (u2 - u0), diagonal kappa (u0 - 2 u2 + u3).
+    Coarse T_lr rows take the bottom facets (not on y = 0: dS without a neighbour), right facets and
+    diagonal of their coarse square; T_ul rows the left facets, top facets (not on y = 1) and
+    diagonal."""
+    n = nc * r
+    u = np.zeros((n + 1, n + 1))
+    u[:, 1:n] = np.asarray(y_free, dtype=np.float64).reshape(n + 1, n - 1)
+    kl = np.asarray(kappa_lr, dtype=np.float64)
+    ku = np.asarray(kappa_ul, dtype=np.float64)
+    u0, u1, u2, u3 = u[:-1, :-1], u[:-1, 1:], u[1:, :-1], u[1:, 1:]          # [j, i] of square (i, j)
+    rows = np.zeros((nc, nc, 2))                                            # [J, I, lr / ul]
+    # T_lr bottom facets: fine row j = J r, summed over the r squares of each coarse column
+    bot = (kl * (u1 - u3))[::r, :].reshape(nc, nc, r).sum(2)
+    bot[0, :] = 0.0
+    right = (kl * (u1 - u0))[:, r - 1::r].reshape(nc, r, nc).sum(1)
+    a = np.arange(n)
+    diag_sq = (a % r)[None, :] == (a % r)[:, None]                           # squares on the coarse diagonals
+    dl = np.where(diag_sq, kl * (u0 - 2 * u1 + u3), 0.0).reshape(nc, r, nc, r).sum((1, 3))
+    rows[:, :, 0] = bot + right + dl
+    left = (ku * (u2 - u3))[:, ::r].reshape(nc, r, nc).sum(1)
+    top = (ku * (u2 - u0))[r - 1::r, :].reshape(nc, nc, r).sum(2)
+    top[-1, :] = 0.0
+    du = np.where(diag_sq, ku * (u0 - 2 * u2 + u3), 0.0).reshape(nc, r, nc, r).sum((1, 3))
+    rows[:, :, 1] = left + top + du
+    return rows.reshape(-1)            # coarse cell 2 (I + nc J) + {0: T_lr, 1: T_ul}
+
+
+def image_to_square_kappa(img):
+    """Pixel image (row 0 = top) -> [n, n] per-square values at [j, i] (both triangles)."""
+    img = np.asarray(img, dtype=np.float64)
+    return img[..., ::-1, :]

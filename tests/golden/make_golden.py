@@ -133,10 +133,23 @@ class _Phys(object):
         self.free_dofs = f
 
 
-def make_rom():
-    nc, r, mc, mf, M, W, cdofs, fdofs = c32_physics()
-    rng = np.random.default_rng(3)
-    N = 6
+def c64_physics():
+    """highres (factories/model.py:172-213): ROM 8x8, 3 refinements -> 64x64."""
+    nc, r = 8, 8
+    mc = fem.unit_square_mesh(nc)
+    mf = fem.unit_square_mesh(nc * r)
+    M = fem.rom_stiffness_tensor(mc)
+    W = fem.prolongation_free(mc, mf)
+    cdofs, fdofs = fem.dirichlet_split(mc)
+    return nc, r, mc, mf, M, W, cdofs, fdofs
+
+
+def make_rom(tag='c32'):
+    """ROM solve + ReducedOrderModelOperator forward / adjoint (ROM.py:59-100, components.py:296-298).
+    c64: nc = 8 (81 coarse nodes), N = 32 = the benchmarked labeled batch."""
+    nc, r, mc, mf, M, W, cdofs, fdofs = c32_physics() if tag == 'c32' else c64_physics()
+    rng = np.random.default_rng(3 if tag == 'c32' else 33)
+    N = 6 if tag == 'c32' else 32
     rom = R_ROM.ROM(_Phys(cdofs, fdofs), torch.tensor(M, dtype=torch.float32), torch.float32, 'cpu')
     g = R_comp.ReducedOrderModelOperator(rom, torch.tensor(W, dtype=torch.float32),
                                          dtype=torch.float32, device='cpu')
@@ -149,12 +162,17 @@ def make_rom():
     Y = torch.tensor(rng.normal(0, 0.3, mu.shape), dtype=torch.float32)
     L = R_utils.DiagonalGaussianLogLikelihood(Y, mu, 2 * ls)
     (-L).backward()
-    np.savez_compressed(os.path.join(HERE, 'rom_c32.npz'), M=M.astype(np.float32), W=W.astype(np.float32),
-                        bc_dofs=cdofs, U=U, F=F.numpy(), effprop=effprop.detach().numpy(),
+    extra = {}
+    if tag != 'c32':
+        extra = dict(nc=np.int64(nc), r=np.int64(r))       # M / W are rebuilt from the oracle at test time
+    else:
+        extra = dict(M=M.astype(np.float32), W=W.astype(np.float32))
+    np.savez_compressed(os.path.join(HERE, 'rom_%s.npz' % tag), bc_dofs=cdofs, U=U, F=F.numpy(),
+                        effprop=effprop.detach().numpy(),
                         logsigmas_y=g.logsigmas_y.detach().numpy(), mu_y=mu.detach().numpy(),
                         Y=Y.numpy(), logL=L.detach().numpy(), grad_effprop=effprop.grad.numpy(),
-                        grad_logsigmas_y=g.logsigmas_y.grad.numpy())
-    print('rom ok', float(L))
+                        grad_logsigmas_y=g.logsigmas_y.grad.numpy(), **extra)
+    print('rom ok', tag, float(L))
 
 
 # --------------------------------------------------------------------------
@@ -235,6 +253,126 @@ def make_elbo():
     np.savez_compressed(os.path.join(HERE, 'elbo_c32.npz'), **out)
     print('elbo ok', elbo.item(), 'n params', sum(p.numel() for p in model.parameters()))
     del real_randn_like
+
+
+def _elbo_model(phys, n, dz, blocks, growth, f0, gen, independent_X=True):
+    nc, r, mc, mf, M, W, cdofs, fdofs = phys
+    torch.manual_seed(0)
+    enc = CNNEncoder(n, dz, blocks, growth, f0, drop_rate=0)
+    dec = CNNDecoder(n, dz, (8, 8), 1, f0, blocks, False, growth, drop_rate=0., upsample='nearest',
+                     force_single_output=False, homoscedastic=False)
+    randomize_bn(enc, gen)
+    randomize_bn(dec, gen)
+    rom = R_ROM.ROM(_Phys(cdofs, fdofs), torch.tensor(M, dtype=torch.float32), torch.float32, 'cpu')
+    g = R_comp.ReducedOrderModelOperator(rom, torch.tensor(W, dtype=torch.float32), dtype=torch.float32, device='cpu')
+    gp = R_comp.EffectivePropertyMap(dz, M.shape[2], num_hidden_layers=0, independent_X=independent_X,
+                                     dtype=torch.float32, device='cpu')
+    model = R_gen.GenerativeModel(f=dec, g=g, gp=gp, dtype=torch.float32, device='cpu')
+    model.encoder = enc
+    return model, g
+
+
+def _elbo_run(model, perm, eps, **kw):
+    """One reference model.elbo(...) + backward with injected permutation / noise; returns
+    (elbo, grads)."""
+    queue = list(eps)
+
+    def fake_randn_like(t, *a, **k):
+        e = queue.pop(0)
+        assert e.shape == t.shape, (e.shape, t.shape)
+        return e.to(dtype=t.dtype)
+
+    model.zero_grad()
+    with mock.patch('torch.randperm', lambda N, **k: perm.clone()), mock.patch('torch.randn_like', fake_randn_like):
+        elbo = model.elbo(step=0, **kw)
+    assert not queue
+    (-elbo).backward()
+    return elbo, {k: p.grad.detach().numpy().copy() for k, p in model.named_parameters() if p.grad is not None}
+
+
+def make_elbo_c64():
+    """GenerativeModel.elbo (armortized + supervised freeX) + backward at the BENCHMARKED shape:
+    highres codec (d_z 64, blocks [1, 2, 1], growth 4, init features 6), ROM 8x8 on 64x64,
+    B_u = 256 armortized samples out of a pool of 256 (random order), N_s = 32 labeled
+    -> elbo_c64.npz.  ~5 MB: inputs stored in fp32, M / W rebuilt from the oracle by the tests."""
+    phys = c64_physics()
+    nc, r, mc, mf, M, W, cdofs, fdofs = phys
+    n = nc * r
+    rng = np.random.default_rng(64)
+    Nu, bs, Ns, dz = 256, 256, 32, 64
+    gen = torch.Generator().manual_seed(65)
+    model, g = _elbo_model(phys, n, dz, [1, 2, 1], 4, 6, gen)
+    Xu = torch.tensor(random_fields(rng, Nu, n), dtype=torch.float32)
+    Xs_img = random_fields(rng, Ns, n).astype(np.float32)
+    U = rng.uniform(-0.5, 0.5, (Ns, 4))
+    Y = np.stack([fem.solve_fom(mf, np.exp(fem.image_to_cells(x.astype(np.float64))), u) for x, u in zip(Xs_img, U)])
+    F = np.stack([fem.f_rom_bc(mc, u) for u in U])
+    model.register_datasets({'supervised': _DS(X=torch.tensor(Xs_img), Y=torch.tensor(Y, dtype=torch.float32),
+                                               F_ROM_BC=torch.tensor(F, dtype=torch.float32)),
+                             'unsupervised': _DS(X=Xu)}, None, create_unsupervised_variational_approximation=False)
+    with torch.no_grad():
+        for q in (model.q_z['supervised'], model.q_X['supervised']):
+            q._mean.copy_(torch.tensor(rng.normal(0, 0.5, q._mean.shape)))
+            q._logsigma.copy_(torch.tensor(rng.normal(-1.0, 0.3, q._logsigma.shape)))
+        g.logsigmas_y.copy_(torch.tensor(rng.normal(-2.0, 0.2, g.logsigmas_y.shape)))
+    perm = torch.tensor(rng.permutation(Nu), dtype=torch.long)
+    eps = [torch.tensor(rng.normal(size=s), dtype=torch.float32) for s in [(bs, dz), (Ns, dz), (Ns, M.shape[2])]]
+    state0 = {k: v.detach().cpu().numpy().copy() for k, v in model.state_dict().items()}
+    elbo, gr = _elbo_run(model, perm, eps, armortized_bs=bs)
+    out = {'state.' + k: v for k, v in state0.items()}
+    out.update({'grad.' + k: v for k, v in gr.items()})
+    out.update(Xu=Xu.numpy(), Xs=Xs_img, Y=Y.astype(np.float32), F=F.astype(np.float32), U=U,
+               perm=perm.numpy(), eps_enc=eps[0].numpy(), eps_qz=eps[1].numpy(), eps_qX=eps[2].numpy(),
+               elbo=np.float64(elbo.item()), bc_dofs=cdofs, cfg=np.array([n, nc, dz, Nu, bs, Ns]))
+    np.savez_compressed(os.path.join(HERE, 'elbo_c64.npz'), **out)
+    print('elbo c64 ok', elbo.item(), 'n params', sum(p.numel() for p in model.parameters()))
+
+
+def make_elbo_options_c32():
+    """model.elbo(normalize=True) and model.elbo(l2_penalty=...) (generative.py:247-287: every term
+    divided by its batch size; minus l2_penalty * sum of the parameter norms of f and the encoder)
+    at the C32 shape of elbo_c32 -> elbo_opts_c32.npz."""
+    phys = c32_physics()
+    nc, r, mc, mf, M, W, cdofs, fdofs = phys
+    n = nc * r
+    rng = np.random.default_rng(44)
+    Nu, bs, Ns, dz = 16, 8, 4, 16
+    gen = torch.Generator().manual_seed(45)
+    model, g = _elbo_model(phys, n, dz, [1, 1], 4, 4, gen)
+    Xu = torch.tensor(random_fields(rng, Nu, n), dtype=torch.float32)
+    Xs_img = random_fields(rng, Ns, n)
+    U = rng.uniform(-0.5, 0.5, (Ns, 4))
+    Y = np.stack([fem.solve_fom(mf, np.exp(fem.image_to_cells(x)), u) for x, u in zip(Xs_img, U)])
+    F = np.stack([fem.f_rom_bc(mc, u) for u in U])
+    model.register_datasets({'supervised': _DS(X=torch.tensor(Xs_img, dtype=torch.float32),
+                                               Y=torch.tensor(Y, dtype=torch.float32),
+                                               F_ROM_BC=torch.tensor(F, dtype=torch.float32)),
+                             'unsupervised': _DS(X=Xu)}, None, create_unsupervised_variational_approximation=False)
+    with torch.no_grad():
+        for q in (model.q_z['supervised'], model.q_X['supervised']):
+            q._mean.copy_(torch.tensor(rng.normal(0, 0.5, q._mean.shape)))
+            q._logsigma.copy_(torch.tensor(rng.normal(-1.0, 0.3, q._logsigma.shape)))
+        g.logsigmas_y.copy_(torch.tensor(rng.normal(-2.0, 0.2, g.logsigmas_y.shape)))
+    perm = torch.tensor(rng.permutation(Nu), dtype=torch.long)
+    shapes = [(bs, dz), (Ns, dz), (Ns, M.shape[2])]
+    eps = [torch.tensor(rng.normal(size=s), dtype=torch.float32) for s in shapes]
+    state0 = {k: v.detach().cpu().numpy().copy() for k, v in model.state_dict().items()}
+    out = {'state.' + k: v for k, v in state0.items()}
+    class _Writer(object):           # the reference's l2 branch logs unconditionally (generative.py:278)
+        def add_scalar(self, k, v, global_step=None):
+            pass
+
+    for tag, kw in (('norm', dict(normalize=True)), ('l2', dict(l2_penalty=0.05))):
+        model.writer = _Writer() if tag == 'l2' else None
+        elbo, gr = _elbo_run(model, perm, eps, armortized_bs=bs, **kw)
+        out.update({'%s.grad.%s' % (tag, k): v for k, v in gr.items()})
+        out['%s.elbo' % tag] = np.float64(elbo.item())
+        print('elbo option', tag, elbo.item())
+    out.update(Xu=Xu.numpy(), Xs=Xs_img.astype(np.float32), Y=Y.astype(np.float32), F=F.astype(np.float32), U=U,
+               perm=perm.numpy(), eps_enc=eps[0].numpy(), eps_qz=eps[1].numpy(), eps_qX=eps[2].numpy(),
+               M=M.astype(np.float32), W=W.astype(np.float32), bc_dofs=cdofs, cfg=np.array([n, nc, dz, Nu, bs, Ns]),
+               l2_penalty=np.float64(0.05))
+    np.savez_compressed(os.path.join(HERE, 'elbo_opts_c32.npz'), **out)
 
 
 # --------------------------------------------------------------------------
@@ -628,14 +766,23 @@ def make_terms():
                         kl=R_utils.UnitGaussianKullbackLeiblerDivergence(m, lv).numpy())
 
 
+ALL = {
+    'terms': make_terms,
+    'codec_c32': lambda: make_codec('c32', 32, 16, 8, [1, 1], 4, 4, 4, B=8),
+    'codec_c64': lambda: make_codec('c64', 64, 64, 8, [1, 2, 1], 4, 6, 6, B=4),
+    'rom_c32': make_rom,
+    'rom_c64': lambda: make_rom('c64'),
+    'elbo_c32': make_elbo,
+    'elbo_c64': make_elbo_c64,
+    'elbo_opts_c32': make_elbo_options_c32,
+    'elbo_nonarm_c32': make_elbo_nonarmortized,
+    'vo_c32': make_vo,
+    'vo_elbo_c32': make_vo_elbo,
+    'vo_elbo_lockx_c32': lambda: make_vo_elbo(lockx=True),
+    'pe_analysis_c32': make_pe_analysis,
+}
+
 if __name__ == '__main__':
-    make_terms()
-    make_codec('c32', 32, 16, 8, [1, 1], 4, 4, 4, B=8)
-    make_codec('c64', 64, 64, 8, [1, 2, 1], 4, 6, 6, B=4)
-    make_rom()
-    make_elbo()
-    make_elbo_nonarmortized()
-    make_vo()
-    make_vo_elbo()
-    make_vo_elbo(lockx=True)
-    make_pe_analysis()
+    # python tests/golden/make_golden.py [fixture ...]   (default: all)
+    for name in (sys.argv[1:] or list(ALL)):
+        ALL[name]()

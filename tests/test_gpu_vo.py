@@ -426,3 +426,29 @@ def test_vo_ensemble_with_random_test_functions(device):
         mo, vo = oelbo.vo_condition(QE.gamma[i].cpu(), QE.alpha[i].cpu(), G[i].cpu().double(), P[i].cpu().double(),
                                     ens._mean_vo_variances.cpu())
         assert rel(ens._mean64[i].cpu(), mo) < 1e-7
+
+
+@pytest.mark.parametrize('n,N', [(64, 4), (128, 2), (256, 2)])
+def test_flux_residual_fused_large_grids(device, n, N):
+    """The flux-constraint residual fused into the CGR pass (r_flux of gpi_cgr_residual) at the
+    64^2 / 128^2 / 256^2 grids (ROM 8x8, r = 8 / 16 / 32) vs the fp64 oracle's closed-form flux rows
+    (oracle.fem.flux_residual_structured, pinned to the generic flux_rows): max error <= 1e-5 of the
+    largest entry (random y, no cancellation); the CGR output of the same launch vs the matrix-free
+    fp64 FE residual, same bound."""
+    from gpi.engine import cgr_residual
+    rng = np.random.default_rng(n + 1)
+    nc = 8
+    r = n // nc
+    mc, mf = fem.unit_square_mesh(nc), fem.unit_square_mesh(n)
+    W = fem.prolongation_free(mc, mf)
+    imgs = rng.normal(0.4, 0.8, (N, n, n))
+    U = rng.uniform(-0.5, 0.5, (N, 4))
+    y = rng.normal(0, 0.3, (N, (n + 1) * (n - 1)))
+    rc, rf = cgr_residual(cuda(imgs), cuda(y), cuda(U), nc=nc, flux=True)
+    rc, rf = rc.cpu().numpy(), rf.cpu().numpy()
+    for i in range(N):
+        kap = np.exp(fem.image_to_square_kappa(imgs[i].astype(np.float32).astype(np.float64)))
+        ref_f = fem.flux_residual_structured(nc, r, kap, kap, y[i].astype(np.float32).astype(np.float64))
+        assert np.abs(rf[i] - ref_f).max() / np.abs(ref_f).max() < 1e-5
+        ref_c = W.T @ fem.fom_residual(mf, np.exp(fem.image_to_cells(imgs[i])), U[i], y[i])
+        assert np.abs(rc[i] - ref_c).max() / np.abs(ref_c).max() < 1e-5

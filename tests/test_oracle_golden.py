@@ -293,3 +293,48 @@ def test_elbo_nonarmortized():
             continue
         scale = max(np.abs(ref).max(), 1.0)
         np.testing.assert_allclose(p.grad.numpy() / scale, ref / scale, atol=2e-4, err_msg=k)
+
+
+# ---------------------------------------------------------------- benchmarked shape (C64) and elbo options
+def test_rom_c64():
+    """nc = 8 ROM solve + adjoint (the benchmarked labeled path) vs the reference run (rom_c64.npz)."""
+    from elbo_ref import physics
+    d = load('rom_c64.npz')
+    M, W, bc = physics(int(d['nc']), int(d['r']))
+    assert np.array_equal(bc, d['bc_dofs'])
+    e = torch.tensor(d['effprop'], dtype=torch.float64, requires_grad=True)
+    ls = torch.tensor(d['logsigmas_y'], dtype=torch.float64, requires_grad=True)
+    mu, lsr = oelbo.rom_operator(torch.tensor(W), torch.tensor(M), torch.tensor(bc), e,
+                                 torch.tensor(d['F'], dtype=torch.float64), ls)
+    np.testing.assert_allclose(mu.detach().numpy(), d['mu_y'], rtol=1e-4, atol=1e-5)
+    L = oelbo.dgll(torch.tensor(d['Y'], dtype=torch.float64), mu, 2 * lsr)
+    np.testing.assert_allclose(L.item(), d['logL'], rtol=1e-5)
+    (-L).backward()
+    from elbo_ref import tensor_rel
+    assert tensor_rel(e.grad.numpy(), d['grad_effprop']) < 1e-3
+    assert tensor_rel(ls.grad.numpy(), d['grad_logsigmas_y']) < 1e-4
+
+
+def test_elbo_c64():
+    """fp64 oracle of the benchmarked step (highres codec, ROM 8x8, B_u = 256, N_s = 32) vs the
+    reference's fp32 CPU run (elbo_c64.npz): value 1e-5; gradients by elbo_ref.check_grads (the reference's
+    own fp32 run flips a few near-tie ReLUs of the encoder: ~3e-3 on the tensors upstream of them, ~3e-6
+    elsewhere)."""
+    from elbo_ref import oracle_fixture_elbo, tensor_rel, check_grads
+    d = load('elbo_c64.npz')
+    val, gr = oracle_fixture_elbo(d)
+    assert abs(val - float(d['elbo'])) <= 1e-5 * abs(float(d['elbo']))
+    assert set(gr) == {k[5:] for k in d if k.startswith('grad.')}
+    print(check_grads({k: tensor_rel(g, d['grad.' + k]) for k, g in gr.items()}))
+
+
+@pytest.mark.parametrize('opt', ['norm', 'l2'])
+def test_elbo_options(opt):
+    """elbo(normalize=True) and elbo(l2_penalty=0.05) (generative.py:247-287) vs the reference run."""
+    from elbo_ref import oracle_fixture_elbo, tensor_rel
+    d = load('elbo_opts_c32.npz')
+    kw = dict(normalize=True) if opt == 'norm' else dict(l2_penalty=float(d['l2_penalty']))
+    val, gr = oracle_fixture_elbo(d, **kw)
+    assert abs(val - float(d[opt + '.elbo'])) <= 1e-5 * abs(float(d[opt + '.elbo']))
+    bad = {k: e for k, e in ((k, tensor_rel(g, d[opt + '.grad.' + k])) for k, g in gr.items()) if e >= 2e-3}
+    assert not bad, bad

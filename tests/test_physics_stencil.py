@@ -67,3 +67,25 @@ def test_rom_tensor_and_sum_rule():
 def test_pixel_mapping():
     img = np.arange(16.0).reshape(4, 4)
     np.testing.assert_array_equal(pixel_to_cells(img), fem.image_to_cells(img))
+
+
+def test_flux_residual_structured_matches_generic_rows():
+    """The vectorised closed-form flux residual (oracle.fem.flux_residual_structured, used by the
+    GPU flux tests at 64^2..256^2) equals the generic facet-search rows of oracle.fem.flux_rows
+    (flux.py:81-158 restated) on small meshes, per-triangle conductivities that differ inside a
+    square included."""
+    import numpy as np
+    from oracle import fem
+    rng = np.random.default_rng(7)
+    for nc, r in ((2, 2), (2, 4), (3, 3), (4, 2)):
+        n = nc * r
+        mc, mf = fem.unit_square_mesh(nc), fem.unit_square_mesh(n)
+        kap = np.exp(rng.normal(0.3, 0.8, 2 * n * n))
+        G, a = fem.flux_rows(mc, mf, kap)
+        free = fem.dirichlet_split(mf)[1]
+        y = rng.normal(0, 0.5, free.size)
+        ref = G[:, free] @ y - a
+        kl = kap[0::2].reshape(n, n)
+        ku = kap[1::2].reshape(n, n)
+        got = fem.flux_residual_structured(nc, r, kl, ku, y)
+        assert np.abs(got - ref).max() <= 1e-12 * max(np.abs(ref).max(), 1.0), (nc, r)

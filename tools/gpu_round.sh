@@ -11,7 +11,7 @@ OUT=$R/gpurun_out
 mkdir -p "$OUT"
 cd "$R"
 
-timeout -k 10 400 python -m pytest tests -m gpu -q -p no:cacheprovider > "$OUT/gpu_tests_$TAG.log" 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread > "$OUT/gpu_tests_$TAG.log" 2>&1
 rc=$?
 echo "pytest rc=$rc" >> "$OUT/gpu_tests_$TAG.log"
 tail -5 "$OUT/gpu_tests_$TAG.log"
