@@ -145,12 +145,50 @@ def profile_kernels(step, reps=20):
     return out
 
 
+def log(msg):
+    """Progress on stderr (the JSON line is the only stdout output)."""
+    sys.stderr.write('[bench %.1fs] %s\n' % (time.perf_counter() - T_START, msg))
+    sys.stderr.flush()
+
+
+T_START = time.perf_counter()
+
+
+def cgroup_cpus():
+    """CPU quota of this process's cgroup (cpu.max / cfs quota), None when unlimited."""
+    try:
+        with open('/sys/fs/cgroup/cpu.max') as fh:
+            q, p = fh.read().split()[:2]
+            if q != 'max':
+                return max(1, int(int(q) / int(p)))
+    except (OSError, ValueError):
+        pass
+    try:
+        with open('/sys/fs/cgroup/cpu/cpu.cfs_quota_us') as fh:
+            q = int(fh.read())
+        with open('/sys/fs/cgroup/cpu/cpu.cfs_period_us') as fh:
+            p = int(fh.read())
+        if q > 0:
+            return max(1, q // p)
+    except (OSError, ValueError):
+        pass
+    return None
+
+
 def host_cpu():
-    """(cores this process may run on, all host cores, CPU model string)."""
+    """(cores this process may run on, all host cores, CPU model string).  The usable cores are the
+    affinity set capped by the cgroup CPU quota (a GPU box shows every CPU of the machine but grants
+    one GPU's share: 256 torch threads there ran the step at 100 s instead of ~0.2 s, r02b)."""
     try:
         usable = len(os.sched_getaffinity(0))
     except AttributeError:
         usable = os.cpu_count() or 1
+    quota = cgroup_cpus()
+    if quota is not None:
+        usable = min(usable, quota)
+    env = os.environ.get('OMP_NUM_THREADS')
+    if env and env.isdigit() and quota is None:
+        usable = min(usable, int(env))
     model = 'unknown'
     try:
         with open('/proc/cpuinfo') as fh:
@@ -203,9 +241,15 @@ def cpu_baseline(model, data, B_u, N_s, physics, warmup=10, steps=50, budget_s=4
         opt.step()
 
     t0 = time.perf_counter()
-    for _ in range(warmup):
+    w = 0
+    while w < warmup:
         one_step()
-    t_step = (time.perf_counter() - t0) / warmup
+        w += 1
+        if time.perf_counter() - t0 > budget_s / 3:       # a slow host: fewer warm-up steps
+            break
+    t_step = (time.perf_counter() - t0) / w
+    log('cpu baseline: %d threads, %d warm-up steps, %.3f s/step' % (threads, w, t_step))
+    warmup = w
     k = steps if t_step * steps <= budget_s else max(5, int(budget_s / t_step))
     t0 = time.perf_counter()
     for _ in range(k):
@@ -278,13 +322,16 @@ def main():
     torch.cuda.set_device(device)
 
     from gpi.train import FusedElboStep
+    log('building %s (rank %d of %d)' % (args.config, rank, world))
     model, data, (B_u, N_s), physics = build(args.config, device, seed=1000, rank=rank, world=world)
+    log('data ready')
     Xu, Xs, Y, F = data
     # shared subset seed: every rank draws the same global permutation and takes its slice
     step = FusedElboStep(model, Xu, B_u, Xs, Y, F, lr=1e-2, seed=4321 + rank, subset_seed=777,
                          distributed=distributed, rank=rank, world=world)
     if not args.no_graph:
         step.capture()
+    log('captured; warm-up')
     for _ in range(args.warmup):
         step.step()
     torch.cuda.synchronize()
@@ -313,8 +360,10 @@ def main():
     per_step = B_u + N_s
     ms_step = 1e3 * dt / args.steps
     sbytes, sparts = step_bytes(model, B_u, N_s, physics)
+    log('timed %d steps: %.4f ms/step' % (args.steps, ms_step))
     if rank == 0 and not args.no_roofline:
         prof = profile_kernels(step)
+        log('per-operator profile done')
         if args.kprof:
             with open(args.kprof, 'w') as fh:
                 json.dump([dict(op=n, ms=m, bytes=b, gbs=b / (m * 1e-3) / 1e9) for n, m, b in prof], fh, indent=1)
@@ -339,6 +388,7 @@ def main():
                     step=dict(bytes=sbytes, achieved=round(step_ach, 1), frac=round(step_ach / HBM_PEAK_GBS, 4),
                               **sparts))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log('cpu baseline')
         cpu = cpu_baseline(model, data, B_u, N_s, physics)
 
     if rank == 0:

@@ -323,7 +323,11 @@ class ElboEngine(object):
         return self.ws.view(self.hb['y_vo'], self.N_vo if not self.vo_holdoff else 0, self.d_y)
 
     def bind(self, X_u=None, u_index=None, X_s=None, Y=None, F=None, X_vo=None, F_vo=None):
-        """Point the launch descriptors at this step's data tensors."""
+        """Point the launch descriptors at this step's data tensors.  The engine keeps them alive
+        until the next bind: the backward reads X_u again (the input conv's weight gradient), so a
+        caller's temporary (e.g. a random-subset gather) must not return to the allocator between
+        the forward and the backward."""
+        self._bound = (X_u, u_index, X_s, Y, F, X_vo, F_vo)
         if self.B_u > 0:
             L.require_device(X_u)
             assert X_u.dtype == torch.float32 and X_u.is_contiguous()

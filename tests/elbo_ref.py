@@ -36,10 +36,12 @@ def state_of(d, dtype=torch.float64):
             if k.startswith('state.') and not k.endswith(('running_mean', 'running_var', 'num_batches_tracked'))}
 
 
-def oracle_elbo(st, Xu, Xs, Y, F, eps_enc, eps_qz, eps_qX, nc, r, normalize=False, l2_penalty=None):
+def oracle_elbo(st, Xu, Xs, Y, F, eps_enc, eps_qz, eps_qX, nc, r, normalize=False, l2_penalty=None, masks=None):
     """ELBO of the armortized + supervised-freeX model in fp64 from the parameter dict ``st``
     (reference state_dict names) and fully injected inputs / noise; returns the 0-d ELBO (backward
-    fills st[*].grad)."""
+    fills st[*].grad).  masks: optional {'enc', 'dec_u', 'dec_s'} ReLU decisions of the kernels
+    under test (oracle/codec.py, tests/gpu_masks.py)."""
+    mk = masks or {}
     t = lambda a: torch.as_tensor(np.asarray(a), dtype=torch.float64)
     n = nc * r
     cfg = CODEC[n] if n in CODEC else CODEC[64]
@@ -47,9 +49,10 @@ def oracle_elbo(st, Xu, Xs, Y, F, eps_enc, eps_qz, eps_qX, nc, r, normalize=Fals
     M, W, bc = t(M), t(W), torch.as_tensor(bc)
     enc_p = {k[8:]: v for k, v in st.items() if k.startswith('encoder.')}
     dec_p = {k[2:]: v for k, v in st.items() if k.startswith('f.')}
-    enc = lambda x: ocodec.encoder_forward(enc_p, x, n, cfg['blocks'], cfg['growth'], cfg['f0'])
-    dec = lambda z: ocodec.decoder_forward(dec_p, z, 8, cfg['blocks'], cfg['growth'], cfg['f0'])
-    e1, _ = oelbo.elbo_unsupervised_armortized(enc, dec, t(Xu), t(eps_enc))
+    enc = lambda x: ocodec.encoder_forward(enc_p, x, n, cfg['blocks'], cfg['growth'], cfg['f0'], mk.get('enc'))
+    dec_u = lambda z: ocodec.decoder_forward(dec_p, z, 8, cfg['blocks'], cfg['growth'], cfg['f0'], mk.get('dec_u'))
+    dec = lambda z: ocodec.decoder_forward(dec_p, z, 8, cfg['blocks'], cfg['growth'], cfg['f0'], mk.get('dec_s'))
+    e1, _ = oelbo.elbo_unsupervised_armortized(enc, dec_u, t(Xu), t(eps_enc))
     gp = lambda z: torch.nn.functional.linear(z, st['gp.fc.weight'], st['gp.fc.bias'])
     rom = lambda x, Fm: oelbo.rom_operator(W, M, bc, x, Fm, st['g.logsigmas_y'])
     e2, _ = oelbo.elbo_supervised_freeX(

@@ -3,14 +3,18 @@
 
 Checked against (1) the reference's own fp32 CPU run of the same step (elbo_c64.npz, rom_c64.npz,
 tests/golden/make_golden.py) and (2) the fp64 oracle on identical inputs (tests/elbo_ref.py).
-Tolerances: ELBO value 1e-5 relative to the fp64 oracle (north_star); gradients per tensor
-relative (max|g - ref| / max|ref|, no floor) by elbo_ref.check_grads: mask-free tensors 1e-4,
-median 2e-5, >= 70 % of tensors 1e-4, all 5e-3 (isolated ReLU near-tie flips, see check_grads)."""
+Tolerances: ELBO value 1e-5 relative to the fp64 oracle (north_star); every gradient tensor
+5e-5 relative (r02c: worst 1.4e-5) (max|g - ref| / max|ref|, no floor), median 2e-5.  The oracle takes the kernels'
+ReLU decisions (tests/gpu_masks.py): among the ~10^7 activations of a C64 batch a few tens lie
+within fp32 rounding of 0, and a different branch there moves every gradient upstream of that
+pixel by up to 1e-2 (measured r02b without this); the audit below checks that every decision
+the oracle adopts is such a tie (|fp64 input| < 1e-4) and that there are few of them."""
 import numpy as np
 import pytest
 import torch
 
 from elbo_ref import load, physics, state_of, oracle_elbo, oracle_fixture_elbo, tensor_rel, check_grads
+from oracle import codec as ocodec
 from oracle import elbo as oelbo
 
 pytestmark = pytest.mark.gpu
@@ -21,10 +25,17 @@ def cuda(a, dtype=torch.float32):
     return torch.tensor(np.asarray(a), dtype=dtype, device='cuda')
 
 
-def fixture_oracle(name):
-    if name not in _ORACLE:
-        _ORACLE[name] = oracle_fixture_elbo(load(name))
-    return _ORACLE[name]
+def check_mask_audit(max_abs=1e-4, max_frac=1e-5):
+    """The decisions taken from the kernels differ from the oracle's own sign tests only at ties."""
+    n_dis = sum(a[1] for a in ocodec.MASK_AUDIT)
+    n_all = sum(a[3] for a in ocodec.MASK_AUDIT)
+    worst = max((a[2] for a in ocodec.MASK_AUDIT), default=0.0)
+    rep = [a for a in ocodec.MASK_AUDIT if a[1]]
+    print('relu ties adopted from the kernels: %d of %d activations, largest |x| %.2e %s' % (n_dis, n_all, worst, rep))
+    assert n_all > 0
+    assert worst < max_abs, rep
+    assert n_dis <= max_frac * n_all, rep
+    ocodec.MASK_AUDIT.clear()
 
 
 class _DS(object):
@@ -118,53 +129,80 @@ def test_rom_c64_fused_loglik(device):
 def test_elbo_c64_module_path(device):
     """GenerativeModel.elbo + backward (the drop-in module path) at B_u = 256, N_s = 32 with the
     fixture's injected permutation / noise, vs the fp64 oracle and the reference's fp32 run."""
+    from gpu_masks import engine_relu_masks
     d = load('elbo_c64.npz')
     model, bs = highres_model(d)
     eps = (torch.cat([cuda(d['eps_enc']), cuda(d['eps_qz'])]), cuda(d['eps_qX']))
     elbo = model.elbo(step=0, armortized_bs=bs, eps=eps)
     (-elbo).backward()
-    val_o, gr_o = fixture_oracle('elbo_c64.npz')
+    masks = engine_relu_masks(model._elbo_engine(bs, int(d['cfg'][5]), False))
+    ocodec.MASK_AUDIT.clear()
+    val_o, gr_o = oracle_fixture_elbo(d, masks=masks)
+    check_mask_audit()
     assert abs(elbo.item() - val_o) <= 1e-5 * abs(val_o), (elbo.item(), val_o)
     assert abs(elbo.item() - float(d['elbo'])) <= 1e-5 * abs(val_o)
     errs = {k: tensor_rel(p.grad.cpu(), gr_o[k]) for k, p in model.named_parameters()}
-    print(check_grads(errs))
+    print(check_grads(errs, tol_all=5e-5, frac_tight=1.0))
 
 
 def test_fused_step_c64(device):
-    """FusedElboStep -- the graph-captured step bench.py times -- at the benchmarked shape over
-    two steps with the native Adam between them: each step's ELBO and gradient vs the fp64 oracle
-    evaluated on that step's parameters, subset and device-drawn noise."""
+    """FusedElboStep -- the graph-captured step bench.py times -- at the benchmarked shape over three
+    steps with the native Adam between them.  Every step: the ELBO vs the fp64 oracle on that step's
+    parameters, subset and device-drawn noise (1e-5); the gradient vs the module path
+    (GenerativeModel.elbo, itself checked against the oracle above) on the same inputs, 1e-5 per
+    tensor (same kernels); and vs the fp64 oracle with the kernels' ReLU tie decisions: every
+    tensor 5e-5, median 2e-5."""
+    from gpu_masks import engine_relu_masks
+    import copy
     from gpi.train import FusedElboStep
     d = load('elbo_c64.npz')
     model, bs = highres_model(d)
+    ref_model = copy.deepcopy(model)
     Xu, Xs, Y, F = cuda(d['Xu']), cuda(d['Xs']), cuda(d['Y']), cuda(d['F'])
     step = FusedElboStep(model, Xu, bs, Xs, Y, F, lr=1e-3, seed=11)
     n, nc = int(d['cfg'][0]), int(d['cfg'][1])
     names = [k for k, _ in model.named_parameters()]
-    for it in range(2):
+    off = step.flat.name_offsets
+    for it in range(3):
         e = step.engine
-        eps_z = e.eps_z().cpu().numpy().astype(np.float64)
-        eps_x = e.eps_x().cpu().numpy().astype(np.float64)
-        idx = step.idx.cpu().numpy().astype(np.int64)
-        P = step.flat.P
-        st = {k: torch.tensor(P[step.flat.name_offsets[k]:step.flat.name_offsets[k] + p.numel()].view(p.shape)
-                              .cpu().numpy(), dtype=torch.float64, requires_grad=True)
-              for k, p in model.named_parameters()}
+        eps_z_t, eps_x_t = e.eps_z().clone(), e.eps_x().clone()
+        eps_z = eps_z_t.cpu().numpy().astype(np.float64)
+        eps_x = eps_x_t.cpu().numpy().astype(np.float64)
+        idx_t = step.idx.clone().long()
+        idx = idx_t.cpu().numpy()
+        with torch.no_grad():
+            for (k, p), (k2, q) in zip(model.named_parameters(), ref_model.named_parameters()):
+                assert k == k2
+                q.copy_(p)
+        ref_model._datasets['unsupervised'].perm = idx_t
+        ref_model.zero_grad()
+        ref = ref_model.elbo(step=it, armortized_bs=bs, eps=(eps_z_t, eps_x_t))
+        (-ref).backward()
+        st = {k: torch.tensor(p.detach().cpu().numpy(), dtype=torch.float64, requires_grad=True)
+              for k, p in ref_model.named_parameters()}
+        masks = engine_relu_masks(ref_model._elbo_engine(bs, int(d['cfg'][5]), False))
         step.forward_backward()
         torch.cuda.synchronize()
-        val = oracle_elbo(st, d['Xu'][idx], d['Xs'], d['Y'], d['F'], eps_z[:bs], eps_z[bs:], eps_x, nc, n // nc)
+        ocodec.MASK_AUDIT.clear()
+        val = oracle_elbo(st, d['Xu'][idx], d['Xs'], d['Y'], d['F'], eps_z[:bs], eps_z[bs:], eps_x, nc, n // nc,
+                          masks=masks)
+        check_mask_audit()
         (-val).backward()
         got = step.elbo().item()
         assert abs(got - val.item()) <= 1e-5 * abs(val.item()), (it, got, val.item())
+        assert abs(got - ref.item()) <= 1e-6 * abs(val.item()), (it, got, ref.item())
         G = step.flat.G
-        # FusedElboStep's G and the oracle's .grad both hold d(-ELBO)/dtheta
-        errs = {k: tensor_rel(G[step.flat.name_offsets[k]:step.flat.name_offsets[k] + st[k].numel()].cpu().numpy()
-                              .reshape(st[k].shape), st[k].grad.numpy()) for k in names}
+        # FusedElboStep's G, the module path's .grad and the oracle's .grad all hold d(-ELBO)/dtheta
+        g_of = lambda k: G[off[k]:off[k] + st[k].numel()].cpu().numpy().reshape(st[k].shape)
+        errs_mod = {k: tensor_rel(g_of(k), p.grad.cpu().numpy()) for k, p in ref_model.named_parameters()}
+        bad = {k: v for k, v in errs_mod.items() if v >= 1e-5}
+        assert not bad, (it, bad)
+        errs = {k: tensor_rel(g_of(k), st[k].grad.numpy()) for k in names}
         print('step', it)
-        print(check_grads(errs))
+        print(check_grads(errs, tol_all=5e-5, frac_tight=1.0))
         step.update()
         torch.cuda.synchronize()
-    assert step.step_ctr.item() == 2
+    assert step.step_ctr.item() == 3
 
 
 # ---------------------------------------------------------------- elbo(normalize=True), elbo(l2_penalty=...)
