@@ -1441,6 +1441,18 @@ extern "C" int gpi_conv_blocks(const gpi_conv_desc* op, const gpi_groups* groups
     return GPI_OK;
 }
 
+extern "C" int gpi_conv_launch_info(const gpi_conv_desc* op, const gpi_groups* groups, int fwd, int32_t* info) {
+    if (!op || !groups || !info) return GPI_ERR_ARG;
+    ConvGeom G;
+    if (!conv_geom(*op, *groups, G, fwd != 0)) return GPI_ERR_UNSUPPORTED;
+    const int cp = cp_of(*op);
+    info[0] = G.th;
+    info[1] = G.nblocks;
+    info[2] = (int32_t)(fwd ? fwd_lds(*op, G, cp) : bwd_lds(*op, G));
+    info[3] = cp;
+    return GPI_OK;
+}
+
 extern "C" int gpi_conv_forward(const gpi_conv_desc* op, const gpi_codec_ctx* ctx, void* stream) {
     if (!op || !ctx) return GPI_ERR_ARG;
     return launch(*op, *ctx, (hipStream_t)stream, true);

@@ -163,6 +163,7 @@ SIGNATURES = {
     'gpi_struct_sizes': (C.c_int, [C.POINTER(i64), C.c_int]),
     'gpi_error_string': (C.c_char_p, [C.c_int]),
     'gpi_conv_blocks': (C.c_int, [C.POINTER(ConvDesc), C.POINTER(Groups), C.POINTER(i32)]),
+    'gpi_conv_launch_info': (C.c_int, [C.POINTER(ConvDesc), C.POINTER(Groups), C.c_int, C.POINTER(i32)]),
     'gpi_conv_forward': (C.c_int, [C.POINTER(ConvDesc), C.POINTER(CodecCtx), vp]),
     'gpi_conv_backward': (C.c_int, [C.POINTER(ConvDesc), C.POINTER(CodecCtx), vp]),
     'gpi_codec_forward': (C.c_int, [C.POINTER(ConvDesc), C.c_int, C.POINTER(CodecCtx), vp]),

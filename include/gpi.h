@@ -393,6 +393,10 @@ const char* gpi_error_string(int code);
 
 /* Number of workgroups (= partial-slab rows) a conv backward launch uses. */
 int gpi_conv_blocks(const gpi_conv_desc* op, const gpi_groups* groups, int32_t* blocks);
+/* Launch geometry of one conv pass (fwd != 0: forward) for tuning / profiling tools:
+ * info[0] output rows per tile, info[1] workgroups, info[2] LDS bytes per workgroup,
+ * info[3] output channels per forward thread.  No device work. */
+int gpi_conv_launch_info(const gpi_conv_desc* op, const gpi_groups* groups, int fwd, int32_t* info);
 int gpi_conv_forward(const gpi_conv_desc* op, const gpi_codec_ctx* ctx, void* stream);
 int gpi_conv_backward(const gpi_conv_desc* op, const gpi_codec_ctx* ctx, void* stream);
 /* Run a codec program: ops in order (forward) / reverse order (backward). */
