@@ -222,14 +222,23 @@ def cpu_baseline(model, data, B_u, N_s, physics, warmup=10, steps=50, budget_s=4
     pe = {k[8:]: v for k, v in params.items() if k.startswith('encoder.')}
     pd = {k[2:]: v for k, v in params.items() if k.startswith('f.')}
     opt = torch.optim.Adam(params.values(), lr=1e-2)
+    from gpi.plan import encoder_program, decoder_program
+    drop_e = encoder_program(**ec).ops if ec['drop_rate'] else []
+    drop_d = decoder_program(**dc).ops if dc['drop_rate'] else []
+    drop_e = [(op.name, op.cout) for op in drop_e if op.drop]
+    drop_d = [(op.name, op.cout) for op in drop_d if op.drop]
+
+    def masks(layers, B, p):       # Dropout2d in train mode, as every reference forward draws it
+        return {n: torch.bernoulli(torch.full((B, c), 1 - p)) / (1 - p) for n, c in layers} if layers else None
 
     def one_step():
         opt.zero_grad()
         idx = torch.randperm(Xu.shape[0])[:B_u]
         X = Xu[idx]
-        encf = lambda x: ocodec.encoder_forward(pe, x, ec['imsize'], ec['blocks'], ec['growth'], ec['init_features'])
+        encf = lambda x: ocodec.encoder_forward(pe, x, ec['imsize'], ec['blocks'], ec['growth'], ec['init_features'],
+                                                drops=masks(drop_e, x.shape[0], ec['drop_rate']))
         decf = lambda z: ocodec.decoder_forward(pd, z, dc['latent_img_size'], dc['blocks'], dc['growth'],
-                                                dc['init_features'])
+                                                dc['init_features'], drops=masks(drop_d, z.shape[0], dc['drop_rate']))
         e1, _ = oelbo.elbo_unsupervised_armortized(encf, decf, X, torch.randn(B_u, dec.dim_latent))
         gp = lambda z: torch.nn.functional.linear(z, params['gp.fc.weight'], params['gp.fc.bias'])
         rom = lambda x, Fm: oelbo.rom_operator(W, M, bc, x, Fm, params['g.logsigmas_y'])

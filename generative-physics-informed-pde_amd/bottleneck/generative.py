@@ -190,9 +190,17 @@ class GenerativeModel(lamp.modules.BaseModule):
         # Philox seed from torch's CPU generator: torch.manual_seed reproducibility, no device sync
         return int(torch.randint(0, 2 ** 62, (1,)).item())
 
-    def _run_engine(self, engine, X_u=None, X_s=None, Y=None, F=None, eps=None, X_vo=None, F_vo=None):
+    def _run_engine(self, engine, X_u=None, X_s=None, Y=None, F=None, eps=None, X_vo=None, F_vo=None, dropout=None):
         """eps (optional, injected noise): (eps_z [B, d_z], eps_X [N_s + N_vo, n_T] (None in lockX)
-        [, eps_y [N_vo, d_y]])."""
+        [, eps_y [N_vo, d_y]]).  dropout (optional, injected Dropout2d channel scales):
+        {'enc': {conv name: [B_u, cout]}, 'dec': {conv name: [B, cout]}} -- otherwise drawn on the
+        device for every call, as nn.Dropout2d does in train mode."""
+        if engine.has_dropout:
+            if dropout is not None:
+                from gpi.engine import inject_dropout
+                inject_dropout(engine.dropout_views(), dropout)
+            else:
+                engine.draw_dropout(L.stream_handle(), self._host_seed())
         if eps is None:
             engine.eps_z().normal_()
             if engine.N_ex > 0:
@@ -278,9 +286,10 @@ class GenerativeModel(lamp.modules.BaseModule):
 
     # ------------------------------------------------------------ ELBO
     def elbo(self, step, vo_holdoff=False, disable_vo=False, armortized_bs=None, normalize=False, l1_penalty=None,
-             l2_penalty=None, eps=None):
+             l2_penalty=None, eps=None, dropout=None):
         """Reference generative.py:247-287.  ``eps`` optionally injects the reparametrisation
-        noise as (eps_z [B_u + N_s + N_vo, d_z], eps_X [N_s + N_vo, n_T][, eps_y [N_vo, d_y]])."""
+        noise as (eps_z [B_u + N_s + N_vo, d_z], eps_X [N_s + N_vo, n_T][, eps_y [N_vo, d_y]]);
+        ``dropout`` the Dropout2d channel scales (see _run_engine)."""
         assert not (armortized_bs is not None and self.encoder is None)
         if l1_penalty is not None:
             raise NotImplementedError
@@ -318,7 +327,7 @@ class GenerativeModel(lamp.modules.BaseModule):
         if B_u == 0 and N_s == 0 and N_vo == 0:
             return 0
         engine = self._elbo_engine(B_u, N_s, normalize, N_vo=N_vo, vo_holdoff=vo_holdoff, q_unsup=q_unsup)
-        elbo = self._run_engine(engine, X_u, X_s, Y, F, eps, X_vo=X_vo, F_vo=F_vo)
+        elbo = self._run_engine(engine, X_u, X_s, Y, F, eps, X_vo=X_vo, F_vo=F_vo, dropout=dropout)
         if l2_penalty is not None:
             pen = sum(torch.norm(p) for p in self.f.parameters())
             if self.encoder is not None:

@@ -483,6 +483,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void c
     const TileIdx T = tile_of(G, c.groups);
     const int HWi = d.h_in * d.w_in, HWo = d.h_out * d.w_out;
     const float* ib = input_base(d, c, T.b);
+    // Dropout2d after this conv: the sample's output-channel scales (0 or 1/(1-p))
+    const bool drop = d.drop_off >= 0;
+    float dsc[CP];
+#pragma unroll
+    for (int co = 0; co < CP; ++co)
+        dsc[co] = (drop && co < d.cout) ? *as_gld(ws + d.drop_off + (int64_t)T.b * d.cout + co) : 1.f;
     PHASE(1);
 
     // ---- phase 1: every global read of the tile in flight together
@@ -559,6 +565,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void c
             }
         }
         PHASE(6);
+        if (drop) {
+#pragma unroll
+            for (int co = 0; co < CP; ++co) acc[co] *= dsc[co];
+        }
         if (d.epilogue == GPI_EPI_GAUSS_LOSS) {
             if (active) {
                 const float mu = acc[0], ls = acc[1];
@@ -629,7 +639,8 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
 }
 
 // header floats: gst fp64 [4*(MAX_CIN+MAX_COUT)] | i_sc i_sh i_mean i_inv i_gam [MAX_CIN] | o_coef [4*MAX_COUT]
-constexpr int BWD_HDR = 8 * (GPI_MAX_CIN + GPI_MAX_COUT) + 5 * GPI_MAX_CIN + 4 * GPI_MAX_COUT;
+// | o_drop [MAX_COUT]
+constexpr int BWD_HDR = 8 * (GPI_MAX_CIN + GPI_MAX_COUT) + 5 * GPI_MAX_CIN + 5 * GPI_MAX_COUT;
 template <bool B>
 struct BoolC {
     static constexpr bool value = B;
@@ -653,6 +664,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 
     float* i_inv = i_mean + GPI_MAX_CIN;
     float* i_gam = i_inv + GPI_MAX_CIN;
     float* o_coef = i_gam + GPI_MAX_CIN;              // [MAX_COUT][4]: mean, inv, mS, mSx
+    float* o_drop = o_coef + 4 * GPI_MAX_COUT;        // [MAX_COUT] Dropout2d scales of the output channels
     const bool has_gin = d.gin_off >= 0;
     const bool obn = d.gout_mode == 0;
     const int KD = d.cout * KK;                       // input-gradient reduction length
@@ -738,6 +750,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 
         gam = *as_gld(params + d.gamma_off + tid);
         bet = *as_gld(params + d.beta_off + tid);
     }
+    const bool drop = d.drop_off >= 0;
+    if (tid >= 128 && tid < 128 + d.cout)
+        o_drop[tid - 128] = drop ? *as_gld(ws + d.drop_off + (int64_t)T.b * d.cout + (tid - 128)) : 1.f;
     {
         StatLoad L;
         stat_issue(c.stats, c.n_stats, T.grp, d.in_stat, d.in_bn ? d.cin : 0, gst, d.out_stat, obn ? d.cout : 0,
@@ -836,14 +851,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 
                 if (ok[u]) {
                     const float* oc = o_coef + 4 * co[u];
                     const float m = oc[0], inv = oc[1], mS = oc[2], mSx = oc[3];
+                    const float ds = o_drop[co[u]];     // d(dropped output)/d(conv output)
                     float4 o;
-                    o.x = (sv[u].x - mS - ((zv[u].x - m) * inv) * mSx) * inv;
-                    o.y = (sv[u].y - mS - ((zv[u].y - m) * inv) * mSx) * inv;
-                    o.z = (sv[u].z - mS - ((zv[u].z - m) * inv) * mSx) * inv;
-                    o.w = (sv[u].w - mS - ((zv[u].w - m) * inv) * mSx) * inv;
+                    o.x = ds * ((sv[u].x - mS - ((zv[u].x - m) * inv) * mSx) * inv);
+                    o.y = ds * ((sv[u].y - mS - ((zv[u].y - m) * inv) * mSx) * inv);
+                    o.z = ds * ((sv[u].z - mS - ((zv[u].z - m) * inv) * mSx) * inv);
+                    o.w = ds * ((sv[u].w - mS - ((zv[u].w - m) * inv) * mSx) * inv);
                     g4[e0 + 256 * u] = o;
                 }
             }
+        }
+    }
+    if (!obn && drop) {
+        // direct output gradient: scale by the dropout mask (halo / margin zeros stay zero)
+        const int plane4 = G.gh * (G.PG >> 2), total = d.cout * plane4;
+        float4* g4 = reinterpret_cast<float4*>(gl);
+        for (int e = tid; e < total; e += 256) {
+            const float ds = o_drop[dq(e, G.d_g4)];
+            float4 v = g4[e];
+            v.x *= ds;
+            v.y *= ds;
+            v.z *= ds;
+            v.w *= ds;
+            g4[e] = v;
         }
     }
     __syncthreads();

@@ -68,6 +68,18 @@ __global__ __launch_bounds__(256) void randn_kernel(float* out, int64_t n, uint6
         if (q * 4 + k < n) out[q * 4 + k] = v[k];
 }
 
+__global__ __launch_bounds__(256) void dropout_mask_kernel(float* out, int64_t n, float p, float scale, uint64_t seed,
+                                                          const uint64_t* offset, uint64_t sub) {
+    const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;   // one Philox block -> 4 channels
+    if (q * 4 >= n) return;
+    const uint64_t base = offset ? *offset : 0;
+    const uint4_ r = philox(base + (uint64_t)q, sub, seed);
+    const float u[4] = {u01(r.x), u01(r.y), u01(r.z), u01(r.w)};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (q * 4 + k < n) out[q * 4 + k] = u[k] < p ? 0.f : scale;
+}
+
 __global__ void rng_advance_kernel(uint64_t* offset, uint64_t by) { *offset += by; }
 
 // random subset: sort (random key, index) pairs with a bitonic network in LDS
@@ -169,6 +181,17 @@ extern "C" int gpi_randn(float* out, int64_t n, uint64_t seed, const uint64_t* o
     const int64_t nq = (n + 3) / 4;
     hipLaunchKernelGGL(randn_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, (hipStream_t)stream, out, n,
                        seed, offset, sub);
+    GPI_CHECK_LAUNCH();
+    return GPI_OK;
+}
+
+extern "C" int gpi_dropout_masks(float* out, int64_t n, float p, uint64_t seed, const uint64_t* offset, uint64_t sub,
+                                 void* stream) {
+    if (!out || n < 0 || !(p >= 0.f && p < 1.f)) return GPI_ERR_ARG;
+    if (n == 0) return GPI_OK;
+    const int64_t nq = (n + 3) / 4;
+    hipLaunchKernelGGL(dropout_mask_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, (hipStream_t)stream, out,
+                       n, p, 1.f / (1.f - p), seed, offset, sub);
     GPI_CHECK_LAUNCH();
     return GPI_OK;
 }

@@ -109,14 +109,15 @@ class ModelFactory(object):
 
 
 class highres(ModelFactory):
-    """64 x 64 (factories/model.py:172-213).  The reference sets ptype 'ND' (unreachable, App. C #2) and
-    droprate 0.2; the native codec runs drop_rate 0 and ptype 'NDP' (SURVEY.md section 8d, config 2)."""
+    """64 x 64 (factories/model.py:172-213), droprate 0.2 as the reference (:187): Dropout2d in train
+    mode on the native codec.  The reference sets ptype 'ND', which is unreachable;
+    'NDP' here."""
     CODEC = dict(latent=8, latent_features=1, f_dec=6, f_enc=6, blocks=[1, 2, 1], growth=4)
 
     def __init__(self, **kwargs):
         super().__init__()
         self.params.update(ptype='NDP', dim_latent=64, dtype='float32', device='best', nx_rom=8, ny_rom=8,
-                           eff_property_map_hidden_layers=0, num_refines=3, droprate=0.0)
+                           eff_property_map_hidden_layers=0, num_refines=3, droprate=0.2)
         self._identifier = 'highres'
         self.set(kwargs)
 
@@ -134,24 +135,26 @@ class highres32(ModelFactory):
 
 
 class highres128(ModelFactory):
-    """128 x 128 scale-up (BASELINE config 4): deeper codec, ROM 8x8 with 4 refinements."""
+    """128 x 128 scale-up (BASELINE config 4): deeper codec, ROM 8x8 with 4 refinements, droprate 0.2
+    as the 64 x 64 factory it extends."""
     CODEC = dict(latent=8, latent_features=1, f_dec=6, f_enc=6, blocks=[1, 2, 2, 1], growth=4)
 
     def __init__(self, **kwargs):
         super().__init__()
         self.params.update(ptype='NDP', dim_latent=64, dtype='float32', device='best', nx_rom=8, ny_rom=8,
-                           eff_property_map_hidden_layers=0, num_refines=4, droprate=0.0)
+                           eff_property_map_hidden_layers=0, num_refines=4, droprate=0.2)
         self._identifier = 'highres128'
         self.set(kwargs)
 
 
 class highres256(ModelFactory):
-    """256 x 256 scale-up (BASELINE config 5): blocks [1, 2, 2, 2, 1], ROM 8x8 with 5 refinements."""
+    """256 x 256 scale-up (BASELINE config 5): blocks [1, 2, 2, 2, 1], ROM 8x8 with 5 refinements,
+    droprate 0.2."""
     CODEC = dict(latent=8, latent_features=1, f_dec=6, f_enc=6, blocks=[1, 2, 2, 2, 1], growth=4)
 
     def __init__(self, **kwargs):
         super().__init__()
         self.params.update(ptype='NDP', dim_latent=64, dtype='float32', device='best', nx_rom=8, ny_rom=8,
-                           eff_property_map_hidden_layers=0, num_refines=5, droprate=0.0)
+                           eff_property_map_hidden_layers=0, num_refines=5, droprate=0.2)
         self._identifier = 'highres256'
         self.set(kwargs)

@@ -51,7 +51,13 @@ class ConvDesc(C.Structure):
                 ('in_off', i64), ('in_ctot', i32), ('in_c0', i32), ('in_bn', i32), ('gin_accumulate', i32),
                 ('gamma_off', i64), ('beta_off', i64), ('in_stat', i64), ('w_off', i64),
                 ('out_off', i64), ('out_ctot', i32), ('out_c0', i32), ('out_stat', i64),
-                ('epilogue', i32), ('gout_mode', i32), ('gout_off', i64), ('gin_off', i64), ('wpart_off', i64)]
+                ('epilogue', i32), ('gout_mode', i32), ('gout_off', i64), ('gin_off', i64), ('wpart_off', i64),
+                ('drop_off', i64)]
+
+    def __init__(self, *a, **k):
+        super().__init__(*a, **k)
+        if 'drop_off' not in k:
+            self.drop_off = -1
 
 
 class CodecCtx(C.Structure):
@@ -181,6 +187,7 @@ SIGNATURES = {
     'gpi_fom_solve': (C.c_int, [C.POINTER(FomDesc), vp]),
     'gpi_random_field': (C.c_int, [C.POINTER(RandomFieldDesc), vp]),
     'gpi_randn': (C.c_int, [vp, i64, u64, vp, u64, vp]),
+    'gpi_dropout_masks': (C.c_int, [vp, i64, f32, u64, vp, u64, vp]),
     'gpi_rng_advance': (C.c_int, [vp, u64, vp]),
     'gpi_random_subset': (C.c_int, [vp, i32, i32, u64, vp, u64, vp]),
     'gpi_vo_rows': (C.c_int, [i32, i32, i32]),

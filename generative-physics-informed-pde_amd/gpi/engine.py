@@ -126,6 +126,30 @@ def _run(fn, *args, what=None):
     L.check(fn(*args), what or fn.__name__)
 
 
+def dropout_views(ws, progs):
+    out = {}
+    for key, prog, B in progs:
+        if prog is None or prog.drop_numel == 0:
+            continue
+        out[key] = {name: ws.view(off, B, cout) for name, off, cout in prog.drop_ops()}
+    return out
+
+
+def draw_dropout(ws, progs, stream, seed, offset_ptr=None, sub=20):
+    for k, prog in enumerate(progs):
+        if prog is None or prog.drop_numel == 0:
+            continue
+        _run(_lib().gpi_dropout_masks, ws.fptr(prog.drop_off), prog.drop_numel, prog.drop_rate, seed,
+             offset_ptr, sub + k, stream, what='dropout masks')
+
+
+def inject_dropout(views, masks):
+    """Copy given channel scales {'enc' / 'dec': {conv name: [B, cout]}} into the engine's views."""
+    for key, d in masks.items():
+        for name, m in d.items():
+            views[key][name].copy_(m)
+
+
 class ElboEngine(object):
     """Fused armortized-unsupervised + supervised-freeX (+ virtual-observable freeX) ELBO of a
     GenerativeModel.  N_vo > 0 adds the VO term (its own decoder BN group, q_z['vo'] / q_X['vo']
@@ -313,6 +337,19 @@ class ElboEngine(object):
     # ------------------------------------------------------------------
     def eps_z(self):
         return self.ws.view(self.hb['eps_z'], self.B, self.dz)
+
+    @property
+    def has_dropout(self):
+        return any(p is not None and p.drop_numel > 0 for p in (self.ep, self.dp))
+
+    def dropout_views(self):
+        """{'enc': {conv name: [B_u, cout]}, 'dec': {conv name: [B, cout]}}: the Dropout2d channel
+        scales (0 or 1/(1-p)) the next forward uses."""
+        return dropout_views(self.ws, (('enc', self.ep, self.B_u), ('dec', self.dp, self.B)))
+
+    def draw_dropout(self, stream, seed, offset_ptr=None, sub=20):
+        """Fresh Dropout2d scales for every dropout conv of both codecs (device Philox)."""
+        draw_dropout(self.ws, (self.ep, self.dp), stream, seed, offset_ptr, sub)
 
     def eps_x(self):
         """[N_ex, d_x] q_X noise (supervised rows, then VO rows unless held off; none in lockX)."""
@@ -573,13 +610,19 @@ class EncoderEngine(object):
                              N=d_feat, lda=d_feat, ldb=d_feat, flags=0))
         self.gemm_items = (L.GemmItem * len(gi))(*gi)
 
-    def forward(self, x):
+    def forward(self, x, dropout=None, seed=0):
+        """dropout: optional injected channel scales {conv name: [B, cout]} (else drawn, seed)."""
         L.require_device(x)
         x = x.contiguous().float()
         self._x = x
         self.ctx.ext_in = x.data_ptr()
         self.ctx.ext_idx = None
         lib, st = _lib(), L.stream_handle()
+        if self.p.drop_numel:
+            if dropout is not None:
+                inject_dropout(dropout_views(self.ws, (('enc', self.p, self.B),)), {'enc': dropout})
+            else:
+                draw_dropout(self.ws, (self.p,), st, seed)
         self.ws.zero_scratch()
         _run(lib.gpi_codec_forward, self.descs, len(self.descs), C.byref(self.ctx), st, what='encoder forward')
         _run(lib.gpi_head_forward, C.byref(self.head), C.c_void_p(self.flat.P.data_ptr()),
@@ -637,10 +680,16 @@ class DecoderEngine(object):
         o = self.p.output
         self.out_shape = (self.B, o.C, o.H, o.W)
 
-    def forward(self, z):
+    def forward(self, z, dropout=None, seed=0):
+        """dropout: optional injected channel scales {conv name: [B, cout]} (else drawn, seed)."""
         L.require_device(z)
         lib, st = _lib(), L.stream_handle()
         self.ws.view(self.hb['z'], self.B, self.dz).copy_(z)
+        if self.p.drop_numel:
+            if dropout is not None:
+                inject_dropout(dropout_views(self.ws, (('dec', self.p, self.B),)), {'dec': dropout})
+            else:
+                draw_dropout(self.ws, (self.p,), st, seed)
         self.ws.zero_scratch()
         _run(lib.gpi_head_forward, C.byref(self.head), C.c_void_p(self.flat.P.data_ptr()),
              C.c_void_p(self.ws.t_ws.data_ptr()), st, what='latent map')

@@ -59,9 +59,9 @@ def _deliver(flat, scale=None):
 class EncoderFunction(torch.autograd.Function):
 
     @staticmethod
-    def forward(ctx, a, x, engine):
+    def forward(ctx, a, x, engine, dropout=None, seed=0):
         ctx.engine = engine
-        return engine.forward(x)
+        return engine.forward(x, dropout, seed)
 
     @staticmethod
     def backward(ctx, dmu, dls):
@@ -70,7 +70,19 @@ class EncoderFunction(torch.autograd.Function):
         dls = torch.zeros(e.B, e.dz, device=e.flat.P.device) if dls is None else dls.contiguous()
         e.backward(dmu, dls)
         _deliver(e.flat)
-        return None, None, None
+        return None, None, None, None, None
+
+
+def _seed():
+    return int(torch.randint(0, 2 ** 62, (1,)).item())
+
+
+def _take_injected(module):
+    """Dropout2d channel scales a test injected for the next call (module._gpi_inject_dropout)."""
+    d = getattr(module, '_gpi_inject_dropout', None)
+    if d is not None:
+        object.__setattr__(module, '_gpi_inject_dropout', None)
+    return d
 
 
 def encoder_forward(enc, x):
@@ -81,22 +93,23 @@ def encoder_forward(enc, x):
     flat = module_flat(enc, dev)
     B = x.shape[0]
     e = engine_for(enc, ('enc', B, id(flat)), lambda: EncoderEngine(enc, flat, B))
-    return EncoderFunction.apply(anchor(enc, dev), x, e)
+    drop = _take_injected(enc)
+    return EncoderFunction.apply(anchor(enc, dev), x, e, drop, _seed() if (e.p.drop_numel and drop is None) else 0)
 
 
 class DecoderFunction(torch.autograd.Function):
 
     @staticmethod
-    def forward(ctx, a, z, engine):
+    def forward(ctx, a, z, engine, dropout=None, seed=0):
         ctx.engine = engine
-        return engine.forward(z.contiguous().float())
+        return engine.forward(z.contiguous().float(), dropout, seed)
 
     @staticmethod
     def backward(ctx, dout):
         e = ctx.engine
         dz = e.backward(dout.contiguous())
         _deliver(e.flat)
-        return None, dz, None
+        return None, dz, None, None, None
 
 
 def decoder_forward(dec, z):
@@ -105,7 +118,8 @@ def decoder_forward(dec, z):
     flat = module_flat(dec, dev)
     B = z.shape[0]
     e = engine_for(dec, ('dec', B, id(flat)), lambda: DecoderEngine(dec, flat, B))
-    return DecoderFunction.apply(anchor(dec, dev), z, e)
+    drop = _take_injected(dec)
+    return DecoderFunction.apply(anchor(dec, dev), z, e, drop, _seed() if (e.p.drop_numel and drop is None) else 0)
 
 
 class RomOperatorFunction(torch.autograd.Function):

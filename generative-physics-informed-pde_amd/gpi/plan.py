@@ -53,8 +53,11 @@ class Buffer(object):
 class Op(object):
     """Python-side mirror of gpi_conv_desc before offsets are resolved."""
 
-    def __init__(self, name, src, c0, cin, dst, d0, cout, k, stride, pad, upsample, w, bn=None, epilogue=None):
+    def __init__(self, name, src, c0, cin, dst, d0, cout, k, stride, pad, upsample, w, bn=None, epilogue=None,
+                 drop=False):
         self.name = name
+        self.drop = bool(drop)   # nn.Dropout2d on this conv's output (codec.py:177-178,218-282)
+        self.drop_off = None
         self.src, self.c0, self.cin = src, c0, cin
         self.dst, self.d0, self.cout = dst, d0, cout
         self.k, self.stride, self.pad, self.upsample = k, stride, pad, upsample
@@ -68,8 +71,11 @@ class Op(object):
 class CodecProgram(object):
     """Ordered conv ops + buffers of one encoder or decoder."""
 
-    def __init__(self, kind):
+    def __init__(self, kind, drop_rate=0.0):
         self.kind = kind
+        self.drop_rate = float(drop_rate)
+        if not 0.0 <= self.drop_rate < 1.0:
+            raise ValueError('drop_rate must be in [0, 1)')
         self.ops = []
         self.buffers = []
         self.input = None       # Buffer fed from outside (image / latent map)
@@ -81,6 +87,8 @@ class CodecProgram(object):
         return b
 
     def conv(self, *a, **k):
+        if k.pop('dropout', False) and self.drop_rate > 0:
+            k['drop'] = True
         op = Op(*a, **k)
         if op.bn is not None:
             op.src.bn_consumed = True
@@ -96,6 +104,12 @@ class CodecProgram(object):
             b.off = ws.alloc(B * b.per_sample)
             if b.bn_consumed:
                 b.stat = stats.alloc(b.C) if isinstance(stats, Arena) else None
+        # Dropout2d channel scales [B][cout] of every dropout op, one contiguous region
+        self.drop_off = ws.size
+        for op in self.ops:
+            if op.drop:
+                op.drop_off = ws.alloc(B * op.cout)
+        self.drop_numel = ws.size - self.drop_off
         # backward buffers
         if grad:
             for b in self.buffers:
@@ -147,10 +161,15 @@ class CodecProgram(object):
             op.numel = op.cout * op.cin * op.k * op.k
             op.rowlen = op.numel + (2 * op.cin if op.bn is not None else 0)
             d.wpart_off = parts.alloc(op.blocks * op.rowlen) if grad else -1
+            d.drop_off = op.drop_off if op.drop else -1
             op.desc = d
             descs.append(d)
         arr = (L.ConvDesc * len(descs))(*descs)
         return arr
+
+    def drop_ops(self):
+        """[(op name, workspace offset, cout)] of the Dropout2d ops (batch-major [B][cout] each)."""
+        return [(op.name, op.drop_off, op.cout) for op in self.ops if op.drop]
 
     def reduce_items(self, param_offset):
         """Slab reductions: the conv weight, then the input BN's (dgamma, dbeta) that
@@ -177,10 +196,10 @@ class CodecProgram(object):
 
 # --------------------------------------------------------------------------
 def encoder_program(imsize, blocks, growth, init_features, bn_size=8, bottleneck=True, drop_rate=0.0):
-    """CNNEncoder (Encoder.py:133-196) -> program; output buffer = flattened features."""
-    if drop_rate:
-        raise NotImplementedError('Dropout2d is not implemented on the native codec (drop_rate must be 0)')
-    P = CodecProgram('encoder')
+    """CNNEncoder (Encoder.py:133-196) -> program; output buffer = flattened features.
+    drop_rate > 0: Dropout2d after every dense-layer conv and both transition convs
+    (codec.py:177-178,218-219,226-227), as the reference's _DenseLayer / _Transition(down) place it."""
+    P = CodecProgram('encoder', drop_rate)
     x = P.buf('input', 1, imsize, imsize)
     x.external = True
     P.input = x
@@ -197,7 +216,7 @@ def encoder_program(imsize, blocks, growth, init_features, bn_size=8, bottleneck
         nf += nl * growth
         t = 'features.TransDown%d' % (i + 1)
         T = P.buf(t, nf // 2, h, h)
-        P.conv(t + '.conv1', D, 0, nf, T, 0, nf // 2, 1, 1, 0, 0, t + '.conv1.weight', bn=t + '.norm1')
+        P.conv(t + '.conv1', D, 0, nf, T, 0, nf // 2, 1, 1, 0, 0, t + '.conv1.weight', bn=t + '.norm1', dropout=True)
         nf //= 2
         h //= 2
         if i < len(blocks) - 1:
@@ -205,7 +224,7 @@ def encoder_program(imsize, blocks, growth, init_features, bn_size=8, bottleneck
         else:
             Dn = P.buf('features', nf, h, h)
             P.output = Dn
-        P.conv(t + '.conv2', T, 0, nf, Dn, 0, nf, 3, 2, 1, 0, t + '.conv2.weight', bn=t + '.norm2')
+        P.conv(t + '.conv2', T, 0, nf, Dn, 0, nf, 3, 2, 1, 0, t + '.conv2.weight', bn=t + '.norm2', dropout=True)
         D = Dn
     P.d_feat = nf * h * h
     return P
@@ -218,17 +237,18 @@ def _dense_layer(P, name, D, cin, growth, bn_size, bottleneck, h):
         P.conv(name + '.conv1', D, 0, cin, Bt, 0, bn_size * growth, 1, 1, 0, 0, name + '.conv1.weight',
                bn=name + '.norm1')
         P.conv(name + '.conv2', Bt, 0, bn_size * growth, D, cin, growth, 3, 1, 1, 0, name + '.conv2.weight',
-               bn=name + '.norm2')
+               bn=name + '.norm2', dropout=True)
     else:
-        P.conv(name + '.conv1', D, 0, cin, D, cin, growth, 3, 1, 1, 0, name + '.conv1.weight', bn=name + '.norm1')
+        P.conv(name + '.conv1', D, 0, cin, D, cin, growth, 3, 1, 1, 0, name + '.conv1.weight', bn=name + '.norm1',
+               dropout=True)
 
 
 def decoder_program(latent_img_size, latent_img_features, init_features, blocks, growth, out_channels=2,
                     drop_rate=0.0, final_epilogue=None):
-    """CNNDecoder (Decoder.py:163-305) -> program; input buffer = latent map image."""
-    if drop_rate:
-        raise NotImplementedError('Dropout2d is not implemented on the native codec (drop_rate must be 0)')
-    P = CodecProgram('decoder')
+    """CNNDecoder (Decoder.py:163-305) -> program; input buffer = latent map image.
+    drop_rate > 0: Dropout2d after every dense-layer conv, both transition-up convs and the first
+    conv of last_decoding (codec.py:177-178,231-232,239-240,259-260), not after conv0 / conv2 / conv3."""
+    P = CodecProgram('decoder', drop_rate)
     h = latent_img_size
     z = P.buf('latent', latent_img_features, h, h)
     P.input = z
@@ -243,15 +263,17 @@ def decoder_program(latent_img_size, latent_img_features, init_features, blocks,
         if i < len(blocks) - 1:
             t = 'features.TransUp%d' % (i + 1)
             U = P.buf(t, nf // 2, h, h)
-            P.conv(t + '.conv1', D, 0, nf, U, 0, nf // 2, 1, 1, 0, 0, t + '.conv1.weight', bn=t + '.norm1')
+            P.conv(t + '.conv1', D, 0, nf, U, 0, nf // 2, 1, 1, 0, 0, t + '.conv1.weight', bn=t + '.norm1',
+                   dropout=True)
             nf //= 2
             h *= 2
             D2 = P.buf('DecBlock%d' % (i + 2), nf + blocks[i + 1] * growth, h, h)
-            P.conv(t + '.conv2', U, 0, nf, D2, 0, nf, 3, 1, 1, 1, t + '.conv2.weight', bn=t + '.norm2')
+            P.conv(t + '.conv2', U, 0, nf, D2, 0, nf, 3, 1, 1, 1, t + '.conv2.weight', bn=t + '.norm2',
+                   dropout=True)
             D = D2
     t = 'features.LastTransUp'
     L1 = P.buf(t + '.1', nf // 2, h, h)
-    P.conv(t + '.conv1', D, 0, nf, L1, 0, nf // 2, 3, 1, 1, 0, t + '.conv1.weight', bn=t + '.norm1')
+    P.conv(t + '.conv1', D, 0, nf, L1, 0, nf // 2, 3, 1, 1, 0, t + '.conv1.weight', bn=t + '.norm1', dropout=True)
     L2 = P.buf(t + '.2', nf // 4, 2 * h, 2 * h)
     P.conv(t + '.conv2', L1, 0, nf // 2, L2, 0, nf // 4, 3, 1, 1, 1, t + '.conv2.weight', bn=t + '.norm2')
     out = P.buf('output', out_channels, 2 * h, 2 * h)

@@ -125,7 +125,8 @@ class PredictionEnsembleEngine(object):
         self.seed = host_seed()
         self.rng_off = torch.zeros(1, dtype=torch.int64, device=dev)
         self.adam.rng_offset = self.rng_off.data_ptr()
-        self.adam.rng_advance = (self.N * self.engine.dz + 3) // 4 + 1
+        dp = self.engine.dp
+        self.adam.rng_advance = max((self.N * self.engine.dz + 3) // 4 + 1, (dp.drop_numel + 3) // 4 + 1)
 
     def _sync_decoder(self):
         src_flat = getattr(self.model.f, '_gpi_flat', None)
@@ -161,6 +162,8 @@ class PredictionEnsembleEngine(object):
             ez.copy_(eps)
         else:
             L.check(lib.gpi_randn(L.ptr(ez), ez.numel(), self.seed, L.ptr(self.rng_off), 5, st), 'randn pe')
+        if self.engine.has_dropout:     # the reference calls the decoder in train mode (components.py:371)
+            self.engine.draw_dropout(st, self.seed, L.ptr(self.rng_off), 6)
         self.engine.forward(st, compute_value=False)
         t = self.engine.ws.terms
         from .engine import T_LX0, T_KL_Q2

@@ -84,8 +84,10 @@ class FusedElboStep(object):
         if self.B_u and self.n_sub > n_pool:
             raise ValueError('the pool (%d) is smaller than the global armortized batch (%d)' % (n_pool, self.n_sub))
         self.n_pool = n_pool
+        drop_span = max([(p.drop_numel + 3) // 4 + 1 for p in (self.engine.ep, self.engine.dp)
+                         if p is not None and p.drop_numel] or [0])
         self.rng_span = max(n_pool, (self.engine.B * self.engine.dz + 3) // 4 + 1,
-                            (self.N_s * self.engine.d_x + 3) // 4 + 1)
+                            (self.N_s * self.engine.d_x + 3) // 4 + 1, drop_span)
         self.adam.rng_offset = self.rng_off.data_ptr()
         self.adam.rng_advance = self.rng_span
         ws = self.engine.ws
@@ -115,6 +117,8 @@ class FusedElboStep(object):
         if self.engine.N_ex:
             ex = self.engine.eps_x()
             L.check(lib.gpi_randn(L.ptr(ex), ex.numel(), self.seed, L.ptr(self.rng_off), sub0 + 3, st), 'randn x')
+        if self.engine.has_dropout:      # Dropout2d channel scales of both codecs (sub ids sub0 + 4, + 5)
+            self.engine.draw_dropout(st, self.seed, L.ptr(self.rng_off), sub0 + 4)
 
     def forward_backward(self, stream=None):
         """One step without the parameter update.  The step's noise and subset were drawn by the

@@ -95,6 +95,10 @@ typedef struct gpi_conv_desc {
     int64_t gin_off;               /* S buffer / gradient of the input (input layout), or -1 */
     int64_t wpart_off;             /* partial slab, one row per workgroup:
                                       [cout*cin*k*k dW][cin dgamma][cin dbeta] (BN part only if in_bn) */
+    int64_t drop_off;              /* Dropout2d after this conv (codec.py:177-178,218-282): workspace
+                                      floats [B][cout], the per-(sample, channel) scale 0 or 1/(1-p)
+                                      applied to the output (forward) and to its gradient
+                                      (backward); -1: no dropout */
 } gpi_conv_desc;
 
 /* Per-call pointers shared by all codec operators. */
@@ -457,6 +461,10 @@ int gpi_adam(const gpi_adam_desc* d, void* stream);
  * offset is a device uint64 advanced by gpi_rng_advance (graph-replay safe). */
 int gpi_randn(float* out, int64_t n, uint64_t seed, const uint64_t* offset, uint64_t sub, void* stream);
 int gpi_rng_advance(uint64_t* offset, uint64_t by, void* stream);
+/* Dropout2d channel scales (nn.Dropout2d train mode, codec.py:177-178): out[i] = 0 with
+ * probability p, else 1/(1-p), for Philox counter (*offset + i/4); 0 <= p < 1. */
+int gpi_dropout_masks(float* out, int64_t n, float p, uint64_t seed, const uint64_t* offset, uint64_t sub,
+                      void* stream);
 /* Uniform random subset (randperm(n)[:k] semantics, utils/data.py:444). */
 int gpi_random_subset(int32_t* out, int32_t n, int32_t k, uint64_t seed, const uint64_t* offset, uint64_t sub, void* stream);
 

@@ -45,34 +45,39 @@ def _bn_relu(x, p, name, masks=None):
     return _relu(x, masks, name)
 
 
-def _conv(x, p, name, stride=1, padding=0):
+def _conv(x, p, name, stride=1, padding=0, drops=None):
+    """Conv; ``drops`` {conv name: [B, C] channel scales} applies the Dropout2d that follows it
+    (codec.py:177-178,218-219,226-227,231-232,239-240,259-260) with an injected mask."""
     w = p[name + '.weight']
     b = p.get(name + '.bias')
-    return F.conv2d(x, w, b, stride=stride, padding=padding)
+    y = F.conv2d(x, w, b, stride=stride, padding=padding)
+    if drops is not None and name in drops:
+        y = y * drops[name].to(y.dtype)[:, :, None, None]
+    return y
 
 
 def _up(x):
     return F.interpolate(x, scale_factor=2.0, mode='nearest')
 
 
-def _dense_layer(x, p, name, in_features, growth, bn_size, bottleneck, masks=None):
+def _dense_layer(x, p, name, in_features, growth, bn_size, bottleneck, masks=None, drops=None):
     """codec.py:150-182 (cat [x, y] on channels)."""
     if bottleneck and in_features > bn_size * growth:
         y = _conv(_bn_relu(x, p, name + '.norm1', masks), p, name + '.conv1')
-        y = _conv(_bn_relu(y, p, name + '.norm2', masks), p, name + '.conv2', padding=1)
+        y = _conv(_bn_relu(y, p, name + '.norm2', masks), p, name + '.conv2', padding=1, drops=drops)
     else:
-        y = _conv(_bn_relu(x, p, name + '.norm1', masks), p, name + '.conv1', padding=1)
+        y = _conv(_bn_relu(x, p, name + '.norm1', masks), p, name + '.conv1', padding=1, drops=drops)
     return torch.cat([x, y], 1)
 
 
-def _dense_block(x, p, name, num_layers, in_features, growth, bn_size, bottleneck, masks=None):
+def _dense_block(x, p, name, num_layers, in_features, growth, bn_size, bottleneck, masks=None, drops=None):
     for i in range(num_layers):
         x = _dense_layer(x, p, '%s.denselayer%d' % (name, i + 1), in_features + i * growth,
-                         growth, bn_size, bottleneck, masks)
+                         growth, bn_size, bottleneck, masks, drops)
     return x
 
 
-def encoder_forward(p, x, imsize, blocks, growth, init_features, masks=None):
+def encoder_forward(p, x, imsize, blocks, growth, init_features, masks=None, drops=None):
     """CNNEncoder.forward -> (mean, logsigma)  (Encoder.py:147-196)."""
     if x.dim() < 4:
         x = x.unsqueeze(1)
@@ -80,11 +85,11 @@ def encoder_forward(p, x, imsize, blocks, growth, init_features, masks=None):
     h = _conv(x, p, 'features.In_conv', stride=2, padding=pad)
     nf = init_features
     for i, L in enumerate(blocks):
-        h = _dense_block(h, p, 'features.EncBlock%d' % (i + 1), L, nf, growth, 8, True, masks)
+        h = _dense_block(h, p, 'features.EncBlock%d' % (i + 1), L, nf, growth, 8, True, masks, drops)
         nf = nf + L * growth
         t = 'features.TransDown%d' % (i + 1)
-        h = _conv(_bn_relu(h, p, t + '.norm1', masks), p, t + '.conv1')
-        h = _conv(_bn_relu(h, p, t + '.norm2', masks), p, t + '.conv2', stride=2, padding=1)
+        h = _conv(_bn_relu(h, p, t + '.norm1', masks), p, t + '.conv1', drops=drops)
+        h = _conv(_bn_relu(h, p, t + '.norm2', masks), p, t + '.conv2', stride=2, padding=1, drops=drops)
         nf = nf // 2
     h = h.reshape(h.shape[0], -1)
     h = _relu(F.linear(h, p['features.FC.weight'], p['features.FC.bias']), masks, 'features.FC')
@@ -93,22 +98,22 @@ def encoder_forward(p, x, imsize, blocks, growth, init_features, masks=None):
     return mean, logsig
 
 
-def decoder_forward(p, z, latent_img_size, blocks, growth, init_features, masks=None):
+def decoder_forward(p, z, latent_img_size, blocks, growth, init_features, masks=None, drops=None):
     """CNNDecoder.forward -> (mean, logsigma) [B, H, W]  (Decoder.py:288-305)."""
     h = F.linear(z, p['latent_map.weight'], p['latent_map.bias'])
     h = h.reshape(h.shape[0], -1, latent_img_size, latent_img_size)
     h = _conv(h, p, 'features.conv0', padding=1)
     nf = init_features
     for i, L in enumerate(blocks):
-        h = _dense_block(h, p, 'features.DecBlock%d' % (i + 1), L, nf, growth, 4, False, masks)
+        h = _dense_block(h, p, 'features.DecBlock%d' % (i + 1), L, nf, growth, 4, False, masks, drops)
         nf += L * growth
         if i < len(blocks) - 1:
             t = 'features.TransUp%d' % (i + 1)
-            h = _conv(_bn_relu(h, p, t + '.norm1', masks), p, t + '.conv1')
-            h = _conv(_up(_bn_relu(h, p, t + '.norm2', masks)), p, t + '.conv2', padding=1)
+            h = _conv(_bn_relu(h, p, t + '.norm1', masks), p, t + '.conv1', drops=drops)
+            h = _conv(_up(_bn_relu(h, p, t + '.norm2', masks)), p, t + '.conv2', padding=1, drops=drops)
             nf = nf // 2
     t = 'features.LastTransUp'
-    h = _conv(_bn_relu(h, p, t + '.norm1', masks), p, t + '.conv1', padding=1)
+    h = _conv(_bn_relu(h, p, t + '.norm1', masks), p, t + '.conv1', padding=1, drops=drops)
     h = _conv(_up(_bn_relu(h, p, t + '.norm2', masks)), p, t + '.conv2', padding=1)
     h = _conv(_bn_relu(h, p, t + '.norm3', masks), p, t + '.conv3', padding=2)
     return h[:, 0], h[:, 1]

@@ -36,12 +36,18 @@ def state_of(d, dtype=torch.float64):
             if k.startswith('state.') and not k.endswith(('running_mean', 'running_var', 'num_batches_tracked'))}
 
 
-def oracle_elbo(st, Xu, Xs, Y, F, eps_enc, eps_qz, eps_qX, nc, r, normalize=False, l2_penalty=None, masks=None):
+def oracle_elbo(st, Xu, Xs, Y, F, eps_enc, eps_qz, eps_qX, nc, r, normalize=False, l2_penalty=None, masks=None,
+                drops=None):
     """ELBO of the armortized + supervised-freeX model in fp64 from the parameter dict ``st``
     (reference state_dict names) and fully injected inputs / noise; returns the 0-d ELBO (backward
     fills st[*].grad).  masks: optional {'enc', 'dec_u', 'dec_s'} ReLU decisions of the kernels
-    under test (oracle/codec.py, tests/gpu_masks.py)."""
+    under test (oracle/codec.py, tests/gpu_masks.py).  drops: optional Dropout2d channel scales
+    {'enc': {conv: [B_u, C]}, 'dec': {conv: [B_u + N_s, C]}} (decoder rows: unlabeled, then labeled)."""
     mk = masks or {}
+    dr = drops or {}
+    nu = len(Xu)
+    sl = lambda d, a, b: {k: torch.as_tensor(np.asarray(v))[a:b] for k, v in d.items()} if d else None
+    dr_enc, dr_u, dr_s = (sl(dr.get('enc'), 0, nu), sl(dr.get('dec'), 0, nu), sl(dr.get('dec'), nu, None))
     t = lambda a: torch.as_tensor(np.asarray(a), dtype=torch.float64)
     n = nc * r
     cfg = CODEC[n] if n in CODEC else CODEC[64]
@@ -49,9 +55,12 @@ def oracle_elbo(st, Xu, Xs, Y, F, eps_enc, eps_qz, eps_qX, nc, r, normalize=Fals
     M, W, bc = t(M), t(W), torch.as_tensor(bc)
     enc_p = {k[8:]: v for k, v in st.items() if k.startswith('encoder.')}
     dec_p = {k[2:]: v for k, v in st.items() if k.startswith('f.')}
-    enc = lambda x: ocodec.encoder_forward(enc_p, x, n, cfg['blocks'], cfg['growth'], cfg['f0'], mk.get('enc'))
-    dec_u = lambda z: ocodec.decoder_forward(dec_p, z, 8, cfg['blocks'], cfg['growth'], cfg['f0'], mk.get('dec_u'))
-    dec = lambda z: ocodec.decoder_forward(dec_p, z, 8, cfg['blocks'], cfg['growth'], cfg['f0'], mk.get('dec_s'))
+    enc = lambda x: ocodec.encoder_forward(enc_p, x, n, cfg['blocks'], cfg['growth'], cfg['f0'], mk.get('enc'),
+                                           dr_enc)
+    dec_u = lambda z: ocodec.decoder_forward(dec_p, z, 8, cfg['blocks'], cfg['growth'], cfg['f0'], mk.get('dec_u'),
+                                             dr_u)
+    dec = lambda z: ocodec.decoder_forward(dec_p, z, 8, cfg['blocks'], cfg['growth'], cfg['f0'], mk.get('dec_s'),
+                                           dr_s)
     e1, _ = oelbo.elbo_unsupervised_armortized(enc, dec_u, t(Xu), t(eps_enc))
     gp = lambda z: torch.nn.functional.linear(z, st['gp.fc.weight'], st['gp.fc.bias'])
     rom = lambda x, Fm: oelbo.rom_operator(W, M, bc, x, Fm, st['g.logsigmas_y'])

@@ -116,6 +116,73 @@ def make_codec(tag, imsize, dz, latent, blocks, growth, f_enc, f_dec, B):
           'dec params', sum(p.numel() for p in dec.parameters()))
 
 
+def dropout_conv_names(module):
+    """{id(nn.Dropout2d): name of the conv whose output it drops} for a reference codec
+    (codec.py:177-178: a dense layer's 'dropout' follows its last conv; 'dropoutK' follows 'convK')."""
+    out = {}
+    for name, m in module.named_modules():
+        if isinstance(m, torch.nn.Dropout2d):
+            parent, leaf = name.rsplit('.', 1)
+            if leaf == 'dropout':
+                sub = dict(module.named_modules())[parent]
+                conv = 'conv2' if hasattr(sub, 'conv2') else 'conv1'
+            else:
+                conv = 'conv' + leaf[len('dropout'):]
+            out[id(m)] = parent + '.' + conv
+    return out
+
+
+def make_codec_drop(tag, imsize, dz, latent, blocks, growth, f0, B, p=0.2):
+    """CNNEncoder / CNNDecoder with drop_rate p in train mode (codec.py:177-178,218-282): every
+    nn.Dropout2d is patched to multiply by an injected per-(sample, channel) scale (bernoulli(1-p)/(1-p)),
+    recorded as drop.enc.<conv> / drop.dec.<conv> -> codec_drop_<tag>.npz."""
+    torch.manual_seed(0)
+    gen = torch.Generator().manual_seed(31)
+    enc = CNNEncoder(imsize, dz, blocks, growth, f0, drop_rate=p)
+    dec = CNNDecoder(imsize, dz, (latent, latent), 1, f0, blocks, False, growth, drop_rate=p,
+                     upsample='nearest', force_single_output=False)
+    randomize_bn(enc, gen)
+    randomize_bn(dec, gen)
+    masks = {}
+    names = {}
+    for key, mod in (('enc', enc), ('dec', dec)):
+        for i, nm in dropout_conv_names(mod).items():
+            names[i] = (key, nm)
+
+    def fake_forward(self, x):
+        key, nm = names[id(self)]
+        if (key, nm) not in masks:
+            masks[(key, nm)] = torch.bernoulli(torch.full(x.shape[:2], 1 - p), generator=gen) / (1 - p)
+        return x * masks[(key, nm)][:, :, None, None]
+
+    rng = np.random.default_rng(32)
+    X = torch.tensor(random_fields(rng, B, imsize), dtype=torch.float32, requires_grad=True)
+    with mock.patch.object(torch.nn.Dropout2d, 'forward', fake_forward):
+        mu, ls = enc(X)
+        wm = torch.randn(mu.shape, generator=gen)
+        ws = torch.randn(ls.shape, generator=gen)
+        (torch.sum(mu * wm) + torch.sum(ls * ws)).backward()
+        Z = torch.randn(B, dz, generator=gen).requires_grad_(True)
+        mx, lsx = dec(Z)
+        vm = torch.randn(mx.shape, generator=gen)
+        vs = torch.randn(lsx.shape, generator=gen)
+        (torch.sum(mx * vm) + torch.sum(lsx * vs)).backward()
+    assert len(masks) == len(names), (len(masks), len(names))
+    out = dict(X=X.detach().numpy(), enc_mu=mu.detach().numpy(), enc_ls=ls.detach().numpy(),
+               enc_wm=wm.numpy(), enc_ws=ws.numpy(), grad_X=X.grad.numpy(),
+               Z=Z.detach().numpy(), dec_mu=mx.detach().numpy(), dec_ls=lsx.detach().numpy(),
+               dec_vm=vm.numpy(), dec_vs=vs.numpy(), grad_Z=Z.grad.numpy(), p=np.float64(p),
+               cfg=np.array([imsize, dz, latent, growth, f0, f0] + list(blocks)))
+    for (key, nm), m in masks.items():
+        out['drop.%s.%s' % (key, nm)] = m.numpy()
+    out.update(sd(enc, 'enc.'))
+    out.update(grads(enc, 'enc.grad.'))
+    out.update(sd(dec, 'dec.'))
+    out.update(grads(dec, 'dec.grad.'))
+    np.savez_compressed(os.path.join(HERE, 'codec_drop_%s.npz' % tag), **out)
+    print('codec dropout', tag, len(masks), 'dropout layers')
+
+
 # --------------------------------------------------------------------------
 def c32_physics():
     nc, r = 4, 8
@@ -770,6 +837,7 @@ ALL = {
     'terms': make_terms,
     'codec_c32': lambda: make_codec('c32', 32, 16, 8, [1, 1], 4, 4, 4, B=8),
     'codec_c64': lambda: make_codec('c64', 64, 64, 8, [1, 2, 1], 4, 6, 6, B=4),
+    'codec_drop_c64': lambda: make_codec_drop('c64', 64, 64, 8, [1, 2, 1], 4, 6, B=8),
     'rom_c32': make_rom,
     'rom_c64': lambda: make_rom('c64'),
     'elbo_c32': make_elbo,

@@ -53,11 +53,12 @@ class _DS(object):
         return self.t[key][self.perm[:random_subset]]
 
 
-def highres_model(d):
+def highres_model(d, droprate=0.0):
     """ModelFactory('highres') (the bench's model) with the fixture's parameters and data."""
     from factories.model import ModelFactory
     fac = ModelFactory.FromIdentifier('highres')
     fac.set('device', 'cuda')
+    fac.set('droprate', droprate)
     physics_, model, _, encoder, _, _ = fac.setup()
     model.encoder = encoder.cuda()
     n, nc, dz, Nu, bs, Ns = [int(v) for v in d['cfg']]
@@ -145,7 +146,8 @@ def test_elbo_c64_module_path(device):
     print(check_grads(errs, tol_all=5e-5, frac_tight=1.0))
 
 
-def test_fused_step_c64(device):
+@pytest.mark.parametrize('droprate', [0.0, 0.2])
+def test_fused_step_c64(device, droprate):
     """FusedElboStep -- the graph-captured step bench.py times -- at the benchmarked shape over three
     steps with the native Adam between them.  Every step: the ELBO vs the fp64 oracle on that step's
     parameters, subset and device-drawn noise (1e-5); the gradient vs the module path
@@ -156,7 +158,7 @@ def test_fused_step_c64(device):
     import copy
     from gpi.train import FusedElboStep
     d = load('elbo_c64.npz')
-    model, bs = highres_model(d)
+    model, bs = highres_model(d, droprate)
     ref_model = copy.deepcopy(model)
     Xu, Xs, Y, F = cuda(d['Xu']), cuda(d['Xs']), cuda(d['Y']), cuda(d['F'])
     step = FusedElboStep(model, Xu, bs, Xs, Y, F, lr=1e-3, seed=11)
@@ -166,6 +168,13 @@ def test_fused_step_c64(device):
     for it in range(3):
         e = step.engine
         eps_z_t, eps_x_t = e.eps_z().clone(), e.eps_x().clone()
+        # the step's device-drawn Dropout2d scales (highres: p = 0.2, factories/model.py:187)
+        drops = {k: {n: v.clone() for n, v in dd.items()} for k, dd in e.dropout_views().items()}
+        assert bool(drops) == (droprate > 0)
+        for dd in drops.values():
+            for v in dd.values():
+                u = torch.unique(v)
+                assert set(u.tolist()) <= {0.0, 1.0 / (1.0 - droprate)}
         eps_z = eps_z_t.cpu().numpy().astype(np.float64)
         eps_x = eps_x_t.cpu().numpy().astype(np.float64)
         idx_t = step.idx.clone().long()
@@ -176,7 +185,7 @@ def test_fused_step_c64(device):
                 q.copy_(p)
         ref_model._datasets['unsupervised'].perm = idx_t
         ref_model.zero_grad()
-        ref = ref_model.elbo(step=it, armortized_bs=bs, eps=(eps_z_t, eps_x_t))
+        ref = ref_model.elbo(step=it, armortized_bs=bs, eps=(eps_z_t, eps_x_t), dropout=drops or None)
         (-ref).backward()
         st = {k: torch.tensor(p.detach().cpu().numpy(), dtype=torch.float64, requires_grad=True)
               for k, p in ref_model.named_parameters()}
@@ -185,7 +194,8 @@ def test_fused_step_c64(device):
         torch.cuda.synchronize()
         ocodec.MASK_AUDIT.clear()
         val = oracle_elbo(st, d['Xu'][idx], d['Xs'], d['Y'], d['F'], eps_z[:bs], eps_z[bs:], eps_x, nc, n // nc,
-                          masks=masks)
+                          masks=masks, drops={k: {n: v.double().cpu() for n, v in dd.items()}
+                                              for k, dd in drops.items()})
         check_mask_audit()
         (-val).backward()
         got = step.elbo().item()

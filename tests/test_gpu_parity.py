@@ -476,3 +476,54 @@ def test_lr_schedule_drives_fused_step(device):
     # the lr in effect during step k (the scheduler steps after it, the fused step picks the new value
     # up when it starts): milestones 2 and 4
     np.testing.assert_allclose(seen, [1e-2, 1e-2, 1e-3, 1e-3, 1e-4, 1e-4], rtol=1e-6)
+
+
+def test_codec_dropout_matches_reference(device):
+    """CNNEncoder / CNNDecoder with drop_rate 0.2 in train mode (codec.py:177-178,218-282) on the native
+    codec, with the reference run's Dropout2d masks injected, vs codec_drop_c64.npz."""
+    from bottleneck.Encoder import CNNEncoder
+    from bottleneck.Decoder import CNNDecoder
+    d = load('codec_drop_c64.npz')
+    imsize, dz, latent, growth, f_enc, f_dec = [int(v) for v in d['cfg'][:6]]
+    blocks = [int(v) for v in d['cfg'][6:]]
+    p = float(d['p'])
+    enc = CNNEncoder(imsize, dz, blocks, growth, f_enc, drop_rate=p)
+    dec = CNNDecoder(imsize, dz, (latent, latent), 1, f_dec, blocks, False, growth, drop_rate=p)
+    enc.load_state_dict({k[4:]: torch.tensor(v) for k, v in d.items() if k.startswith('enc.') and
+                         not k.startswith('enc.grad.')})
+    dec.load_state_dict({k[4:]: torch.tensor(v) for k, v in d.items() if k.startswith('dec.') and
+                         not k.startswith('dec.grad.')})
+    enc, dec = enc.cuda(), dec.cuda()
+    drops = {key: {k[len('drop.%s.' % key):]: cuda(v) for k, v in d.items() if k.startswith('drop.%s.' % key)}
+             for key in ('enc', 'dec')}
+    object.__setattr__(enc, '_gpi_inject_dropout', drops['enc'])
+    mu, ls = enc(cuda(d['X']))
+    assert rel(mu.detach().cpu(), d['enc_mu']) < 1e-4
+    assert rel(ls.detach().cpu(), d['enc_ls']) < 1e-4
+    (torch.sum(mu * cuda(d['enc_wm'])) + torch.sum(ls * cuda(d['enc_ws']))).backward()
+    for k, q in enc.named_parameters():
+        assert rel(q.grad.cpu(), d['enc.grad.' + k]) < 2e-3, k
+    object.__setattr__(dec, '_gpi_inject_dropout', drops['dec'])
+    Z = cuda(d['Z']).requires_grad_(True)
+    mx, lsx = dec(Z)
+    assert rel(mx.detach().cpu(), d['dec_mu']) < 1e-4
+    assert rel(lsx.detach().cpu(), d['dec_ls']) < 1e-4
+    (torch.sum(mx * cuda(d['dec_vm'])) + torch.sum(lsx * cuda(d['dec_vs']))).backward()
+    assert rel(Z.grad.cpu(), d['grad_Z']) < 2e-3
+    for k, q in dec.named_parameters():
+        assert rel(q.grad.cpu(), d['dec.grad.' + k]) < 2e-3, k
+    # without injection the masks are drawn on the device: channel scales 0 or 1/(1-p), about p dropped
+    out = [dec(Z)[0] for _ in range(2)]
+    assert not torch.equal(out[0], out[1])
+
+
+def test_dropout_mask_statistics(device):
+    """gpi_dropout_masks: values in {0, 1/(1-p)}, drop fraction p."""
+    from gpi import _lib as L
+    import ctypes as C
+    x = torch.empty(1 << 20, device='cuda')
+    off = torch.zeros(1, dtype=torch.int64, device='cuda')
+    L.check(L.lib().gpi_dropout_masks(L.ptr(x), x.numel(), C.c_float(0.2), 5, L.ptr(off), 1, L.stream_handle()), 'm')
+    v = x.cpu().numpy()
+    assert set(np.unique(v).tolist()) == {0.0, np.float32(1.25)}
+    assert abs((v == 0).mean() - 0.2) < 3e-3

@@ -338,3 +338,29 @@ def test_elbo_options(opt):
     assert abs(val - float(d[opt + '.elbo'])) <= 1e-5 * abs(float(d[opt + '.elbo']))
     bad = {k: e for k, e in ((k, tensor_rel(g, d[opt + '.grad.' + k])) for k, g in gr.items()) if e >= 2e-3}
     assert not bad, bad
+
+
+def test_codec_dropout():
+    """Oracle codec with injected Dropout2d scales vs the reference's CNNEncoder / CNNDecoder in train
+    mode with drop_rate 0.2 and the same injected masks (codec_drop_c64.npz)."""
+    d = load('codec_drop_c64.npz')
+    imsize, dz, latent, growth, f_enc, f_dec = [int(v) for v in d['cfg'][:6]]
+    blocks = [int(v) for v in d['cfg'][6:]]
+    drops = {key: {k[len('drop.%s.' % key):]: torch.tensor(v, dtype=torch.float64) for k, v in d.items()
+                   if k.startswith('drop.%s.' % key)} for key in ('enc', 'dec')}
+    assert len(drops['enc']) == 10 and len(drops['dec']) == 9
+    pe = params(d, 'enc.', grad=True)
+    X = torch.tensor(d['X'], dtype=torch.float64, requires_grad=True)
+    mu, ls = ocodec.encoder_forward(pe, X, imsize, blocks, growth, f_enc, drops=drops['enc'])
+    np.testing.assert_allclose(mu.detach().numpy(), d['enc_mu'], rtol=1e-4, atol=1e-5)
+    (torch.sum(mu * torch.tensor(d['enc_wm'])) + torch.sum(ls * torch.tensor(d['enc_ws']))).backward()
+    for k, p in pe.items():
+        np.testing.assert_allclose(p.grad.numpy(), d['enc.grad.' + k], rtol=1e-3, atol=2e-3, err_msg=k)
+    pd = params(d, 'dec.', grad=True)
+    Z = torch.tensor(d['Z'], dtype=torch.float64, requires_grad=True)
+    mx, lsx = ocodec.decoder_forward(pd, Z, latent, blocks, growth, f_dec, drops=drops['dec'])
+    np.testing.assert_allclose(mx.detach().numpy(), d['dec_mu'], rtol=1e-4, atol=1e-5)
+    (torch.sum(mx * torch.tensor(d['dec_vm'])) + torch.sum(lsx * torch.tensor(d['dec_vs']))).backward()
+    np.testing.assert_allclose(Z.grad.numpy(), d['grad_Z'], rtol=1e-3, atol=1e-4)
+    for k, p in pd.items():
+        np.testing.assert_allclose(p.grad.numpy(), d['dec.grad.' + k], rtol=1e-3, atol=2e-3, err_msg=k)
