@@ -280,21 +280,27 @@ class PredictionEnsemble(object):
 
 
 class DataPair(object):
+    """A monitored scalar series (components.py:396-424's role): (iteration, value) records, optionally
+    mirrored to a tensorboard-style writer under '<label>/<name>'."""
 
     def __init__(self, writer=None, label='', name=None):
         if writer is not None and name is None:
             raise ValueError('Required to provide a name for the writer')
-        self.iteration = list()
-        self.value = list()
-        self._writer = writer
-        self._label = label
-        self._name = name
+        self._records = []
+        self._writer, self._tag = writer, '%s/%s' % (label, name)
+
+    @property
+    def iteration(self):
+        return [i for i, _ in self._records]
+
+    @property
+    def value(self):
+        return [v for _, v in self._records]
 
     def append(self, iteration, value):
-        self.iteration.append(iteration)
-        self.value.append(value)
+        self._records.append((iteration, value))
         if self._writer is not None:
-            self._writer.add_scalar(self._label + '/' + self._name, value, global_step=iteration)
+            self._writer.add_scalar(self._tag, value, global_step=iteration)
 
     def min(self):
         return min(self.value)
@@ -303,7 +309,7 @@ class DataPair(object):
         return max(self.value)
 
     def final(self):
-        return self.value[-1]
+        return self._records[-1][1]
 
 
 class Analysis(object):
@@ -330,11 +336,12 @@ class Analysis(object):
 
     @classmethod
     def FromEncoder(cls, model, dataset):
+        """q_z of every sample = the encoder's (mean, logsigma) (components.py:443-453), held fixed."""
         with torch.no_grad():
-            Z_mean, Z_logsigma = model.encoder(dataset.get('X'))
-        q = VariationalApproximation(Z_mean.shape[1], Z_mean.shape[0], dataset.get('X'), dtype=Z_mean.dtype,
-                                     device=Z_mean.device, requires_grad=False)
-        q.init(Z_mean, Z_logsigma)
+            mean, logsigma = model.encoder(dataset.get('X'))
+        q = VariationalApproximation(mean.shape[1], mean.shape[0], dataset.get('X'), dtype=mean.dtype,
+                                     device=mean.device, requires_grad=False)
+        q.init(mean, logsigma)
         return cls(q, model, dataset)
 
     @property
@@ -401,30 +408,34 @@ class Analysis(object):
             return logp
         self.data['logscore_y'].append(iteration, logp)
 
+    def _x_moments(self, N_monte_carlo):
+        """Per sample: mean and unbiased std over N_monte_carlo decoder draws of the field.  One
+        decoder call per sample, as the reference's per-index loop (components.py:472-491):
+        train-mode BatchNorm normalises over exactly those N_monte_carlo draws."""
+        for index in range(self._q.N):
+            draws = self.sample_predictive_x(N_monte_carlo, index).reshape(N_monte_carlo, -1)
+            yield index, draws.mean(0), draws.std(0)
+
+    def _record(self, key, value, iteration, ReturnValue=True):
+        if iteration is None:
+            return value
+        self.data[key].append(iteration, value)
+        return value if ReturnValue else None
+
     @torch.no_grad()
     def relative_error_x(self, N_monte_carlo, iteration=None, ReturnValue=False):
-        relerrs = np.zeros(self._q.N)
-        for index in range(self._q.N):
-            mean_x = torch.mean(self.sample_predictive_x(N_monte_carlo, index), 0)
-            relerrs[index] = (torch.norm(mean_x.flatten() - self.X[index].flatten()) /
-                              torch.norm(self.X[index].flatten())).item()
-        relerr = float(np.mean(relerrs))
-        if iteration is None:
-            return relerr
-        self.data['relerr_x'].append(iteration, relerr)
-        if ReturnValue:
-            return relerr
+        """Mean over samples of ||E[x] - x|| / ||x|| (components.py:526-546)."""
+        X = self.X.reshape(self._q.N, -1)
+        err = [float(torch.linalg.vector_norm(m - X[i]) / torch.linalg.vector_norm(X[i]))
+               for i, m, _ in self._x_moments(N_monte_carlo)]
+        return self._record('relerr_x', float(np.mean(err)), iteration, ReturnValue)
 
     @torch.no_grad()
     def predictive_log_probability_x(self, N_monte_carlo, iteration=None):
-        logp = np.zeros(self._q.N)
-        for index in range(self._q.N):
-            X_pred = self.sample_predictive_x(N_monte_carlo, index)
-            x_mean = torch.mean(X_pred, 0).flatten()
-            x_std = torch.std(X_pred, 0).flatten()
-            logp[index] = torch.mean(-torch.log(x_std) - 0.5 * ((self.X[index, :].flatten() - x_mean) ** 2 /
-                                                                x_std ** 2) - 0.5 * np.log(2 * np.pi)).item()
-        logp = float(np.mean(logp))
-        if iteration is None:
-            return logp
-        self.data['logscore_x'].append(iteration, logp)
+        """Mean over samples and pixels of the Gaussian log-density of x under the MC moments
+        (components.py:548-570)."""
+        X = self.X.reshape(self._q.N, -1)
+        half_log2pi = 0.5 * float(np.log(2 * np.pi))
+        lp = [float(torch.mean(-torch.log(sd) - 0.5 * ((X[i] - m) / sd) ** 2 - half_log2pi))
+              for i, m, sd in self._x_moments(N_monte_carlo)]
+        return self._record('logscore_x', float(np.mean(lp)), iteration, ReturnValue=False)

@@ -1447,7 +1447,46 @@ __global__ __launch_bounds__(256) void wgrad_reduce(ReduceArgs a, const float* _
     }
 }
 
+// One thread per (BN layer, channel): the layer's codec calls in order.
+__global__ __launch_bounds__(256) void bn_running_kernel(const gpi_bn_running_item* items, int n_items, int max_ch,
+                                                         const gpi_stat* stats, int64_t n_stats, float momentum) {
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    const int li = t / max_ch, c = t - li * max_ch;
+    if (li >= n_items) return;
+    const gpi_bn_running_item it = items[li];
+    if (c >= it.channels) return;
+    double rm = it.running_mean[c], rv = it.running_var[c];
+    for (int k = 0; k < it.n_calls; ++k) {
+        double s = 0.0, s2 = 0.0;
+        for (int r = 0; r < GPI_REPLICAS; ++r) {
+            const gpi_stat& st = stats[((int64_t)r * GPI_MAX_GROUPS + it.group[k]) * n_stats + it.stat + c];
+            s += st.sum;
+            s2 += st.sumsq;
+        }
+        const double n = it.count[k];
+        const double mean = s / n;
+        double var = s2 / n - mean * mean;
+        if (var < 0.0) var = 0.0;
+        rm = (1.0 - momentum) * rm + momentum * mean;
+        rv = (1.0 - momentum) * rv + momentum * (n > 1.0 ? var * n / (n - 1.0) : var);
+    }
+    it.running_mean[c] = (float)rm;
+    it.running_var[c] = (float)rv;
+    if (c == 0) *it.num_batches_tracked += it.n_calls;
+}
+
 }  // namespace
+
+extern "C" int gpi_bn_running_update(const gpi_bn_running_item* items, int n_items, int max_channels,
+                                     const gpi_stat* stats, int64_t n_stats, float momentum, void* stream) {
+    if (n_items < 0 || max_channels < 1 || (n_items > 0 && (!items || !stats))) return GPI_ERR_ARG;
+    if (n_items == 0) return GPI_OK;
+    const int threads = n_items * max_channels;
+    hipLaunchKernelGGL(bn_running_kernel, dim3((threads + 255) / 256), dim3(256), 0, (hipStream_t)stream, items, n_items,
+                       max_channels, stats, n_stats, momentum);
+    GPI_CHECK_LAUNCH();
+    return GPI_OK;
+}
 
 #ifdef GPI_PHASE_TIMING
 // timing build only (not declared in gpi.h): copy the phase / real-time stamps out and clear them.

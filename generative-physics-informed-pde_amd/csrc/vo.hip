@@ -706,7 +706,7 @@ __global__ __launch_bounds__(256) void vo_columns_kernel(gpi_vo_condition_desc d
 
 // ---------------------------------------------------------------- precision
 // One workgroup per (row a, VO sample j): its term (Gamma_j mean_j - alpha_j)_a^2 + (Gamma_j^2 vars_j)_a
-// added in fp64 into beta[a] (zeroed by the launcher); vo_precision_final turns the sums into beta / vo_var.
+// into terms[a, j]; vo_precision_final sums them over j in order (reproducible) into beta / vo_var.
 __global__ __launch_bounds__(256) void vo_precision_kernel(gpi_vo_precision_desc d) {
     __shared__ double red[2][4];
     const int a = blockIdx.x, j = blockIdx.y;
@@ -728,14 +728,16 @@ __global__ __launch_bounds__(256) void vo_precision_kernel(gpi_vo_precision_desc
     if (tid == 0) {
         const double r1 = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]) - d.alpha[(int64_t)j * m + a];
         const double r2 = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
-        atomicAdd(&d.beta[a], r1 * r1 + r2);
+        d.terms[(int64_t)a * d.n + j] = r1 * r1 + r2;
     }
 }
 
 __global__ __launch_bounds__(256) void vo_precision_final(gpi_vo_precision_desc d) {
     const int a = blockIdx.x * 256 + threadIdx.x;
     if (a >= d.m) return;
-    const double beta = 0.5 * d.beta[a] + d.beta0;
+    double sum = 0.0;
+    for (int j = 0; j < d.n; ++j) sum += d.terms[(int64_t)a * d.n + j];
+    const double beta = 0.5 * sum + d.beta0;
     d.beta[a] = beta;
     d.vo_var[a] = (d.infinite && d.infinite[a]) ? 0.0 : beta / (0.5 * (double)d.n + d.alpha0 + 1.0);
 }
@@ -916,10 +918,9 @@ extern "C" int gpi_vo_condition(const gpi_vo_condition_desc* d, void* stream) {
 
 extern "C" int gpi_vo_precision(const gpi_vo_precision_desc* d, void* stream) {
     if (!d || !d->gamma || !d->alpha || !d->mean || !d->vars || !d->beta || !d->vo_var || d->n < 0 || d->m < 1 ||
-        d->d_y < 1)
+        d->d_y < 1 || (d->n > 0 && !d->terms))
         return GPI_ERR_ARG;
     const hipStream_t st = (hipStream_t)stream;
-    if (hipMemsetAsync(d->beta, 0, sizeof(double) * d->m, st) != hipSuccess) return GPI_ERR_LAUNCH;
     if (d->n > 0) {
         hipLaunchKernelGGL(vo_precision_kernel, dim3(d->m, d->n), dim3(256), 0, st, *d);
         GPI_CHECK_LAUNCH();

@@ -60,6 +60,12 @@ class ConvDesc(C.Structure):
             self.drop_off = -1
 
 
+class BnRunningItem(C.Structure):
+    _fields_ = [('stat', i64), ('channels', i32), ('n_calls', i32), ('group', i32 * GPI_MAX_GROUPS),
+                ('count', C.c_double * GPI_MAX_GROUPS), ('running_mean', vp), ('running_var', vp),
+                ('num_batches_tracked', vp)]
+
+
 class CodecCtx(C.Structure):
     _fields_ = [('params', vp), ('ws', vp), ('stats', vp), ('gacc', vp), ('wpart', vp),
                 ('ext_in', vp), ('ext_idx', vp), ('ext_stride', i64),
@@ -128,7 +134,7 @@ class VoConditionDesc(C.Structure):
 class VoPrecisionDesc(C.Structure):
     _fields_ = [('n', i32), ('m', i32), ('d_y', i32), ('_pad', i32),
                 ('gamma', vp), ('alpha', vp), ('mean', vp), ('vars', vp), ('infinite', vp),
-                ('alpha0', C.c_double), ('beta0', C.c_double), ('beta', vp), ('vo_var', vp)]
+                ('alpha0', C.c_double), ('beta0', C.c_double), ('beta', vp), ('vo_var', vp), ('terms', vp)]
 
 
 class GpSampleDesc(C.Structure):
@@ -169,6 +175,7 @@ SIGNATURES = {
     'gpi_struct_sizes': (C.c_int, [C.POINTER(i64), C.c_int]),
     'gpi_error_string': (C.c_char_p, [C.c_int]),
     'gpi_conv_blocks': (C.c_int, [C.POINTER(ConvDesc), C.POINTER(Groups), C.POINTER(i32)]),
+    'gpi_bn_running_update': (C.c_int, [vp, C.c_int, C.c_int, vp, i64, f32, vp]),
     'gpi_conv_launch_info': (C.c_int, [C.POINTER(ConvDesc), C.POINTER(Groups), C.c_int, C.POINTER(i32)]),
     'gpi_conv_forward': (C.c_int, [C.POINTER(ConvDesc), C.POINTER(CodecCtx), vp]),
     'gpi_conv_backward': (C.c_int, [C.POINTER(ConvDesc), C.POINTER(CodecCtx), vp]),

@@ -143,6 +143,49 @@ def draw_dropout(ws, progs, stream, seed, offset_ptr=None, sub=20):
              offset_ptr, sub + k, stream, what='dropout masks')
 
 
+class BnRunning(object):
+    """BatchNorm2d running statistics of a set of codec programs (train mode, momentum 0.1):
+    the reference updates running_mean / running_var / num_batches_tracked at every codec call;
+    here one tiny launch per step folds every call's fp64 batch sums (gpi_bn_running_update)."""
+
+    def __init__(self, entries, ws, device):
+        """entries: [(program, module owning the BN layers, [(group, samples), ...] in call order)]."""
+        items = []
+        self.buffers = []
+        max_ch = 1
+        for prog, module, calls in entries:
+            if prog is None or module is None or not calls:
+                continue
+            for op in prog.ops:
+                if op.bn is None:
+                    continue
+                bn = module.get_submodule(op.bn)
+                if bn.running_mean is None or bn.running_mean.device != device:
+                    continue
+                it = L.BnRunningItem()
+                it.stat, it.channels, it.n_calls = op.desc.in_stat, op.cin, len(calls)
+                for k, (g, n) in enumerate(calls):
+                    it.group[k] = g
+                    it.count[k] = float(n * op.src.H * op.src.W)
+                it.running_mean, it.running_var = bn.running_mean.data_ptr(), bn.running_var.data_ptr()
+                it.num_batches_tracked = bn.num_batches_tracked.data_ptr()
+                items.append(it)
+                self.buffers += [bn.running_mean, bn.running_var, bn.num_batches_tracked]
+                max_ch = max(max_ch, op.cin)
+        self.n = len(items)
+        self.max_ch = max_ch
+        self.ws = ws
+        if self.n:
+            arr = (L.BnRunningItem * self.n)(*items)
+            raw = bytes(arr)
+            self.dev = torch.tensor(list(raw), dtype=torch.uint8, device=device)
+
+    def launch(self, stream, momentum=0.1):
+        if self.n:
+            _run(_lib().gpi_bn_running_update, C.c_void_p(self.dev.data_ptr()), self.n, self.max_ch,
+                 self.ws.stats_ptr, self.ws.n_stats, momentum, stream, what='bn running stats')
+
+
 def inject_dropout(views, masks):
     """Copy given channel scales {'enc' / 'dec': {conv name: [B, cout]}} into the engine's views."""
     for key, d in masks.items():
@@ -156,7 +199,8 @@ class ElboEngine(object):
     rows as the head's second variational segment, a second ROM launch against targets sampled
     from the VO posterior); vo_holdoff keeps only its logL_x - KL part (generative.py:349-364)."""
 
-    def __init__(self, model, B_u, N_s, normalize=False, N_vo=0, vo_holdoff=False, q_unsup=None):
+    def __init__(self, model, B_u, N_s, normalize=False, N_vo=0, vo_holdoff=False, q_unsup=None,
+                 running_modules=None):
         """q_unsup: q_z['unsupervised'] for the non-armortized unsupervised term (no encoder,
         GenerativeModel.elbo_unsupervised generative.py:515-544): its rows replace the encoder
         heads; the term's KL is the reference's KLD of q_z['supervised'] (sic, :525)."""
@@ -333,6 +377,12 @@ class ElboEngine(object):
         self._fixed = (self.B_u, self.N_s, self.N_vo)
         self._side = None
         self._pending_join = False
+        # BN running statistics: encoder once, decoder once per term in the reference's call order
+        # (unsupervised, supervised, vo: generative.py:247-287)
+        run_mods = running_modules or {}
+        self.running = BnRunning([(self.ep, run_mods.get('enc', enc), [(0, self.B_u)]),
+                                  (self.dp, run_mods.get('dec', dec), list(enumerate(self.dec_sizes)))], ws, dev)
+        self._running_pending = False
 
     # ------------------------------------------------------------------
     def eps_z(self):
@@ -395,10 +445,11 @@ class ElboEngine(object):
                 assert F_vo.shape[0] == self.N_vo
                 self.rom_vo.F = F_vo.data_ptr()
 
-    def forward(self, stream=None, compute_value=True, zero_gacc=True, zero_scratch=True):
+    def forward(self, stream=None, compute_value=True, zero_gacc=True, zero_scratch=True, running='now'):
         """Launch the forward; returns the 0-d ELBO tensor (no host sync).  zero_gacc / zero_scratch
         False when the previous step's epilogue already cleared the accumulator / the statistics
-        and term scratch (gpi_step_epilogue)."""
+        and term scratch (gpi_step_epilogue).  running: BN running-statistics update 'now' (end of
+        the forward), 'defer' (on the side stream during backward) or None."""
         lib = _lib()
         st = stream if stream is not None else L.stream_handle()
         if zero_scratch:
@@ -431,6 +482,9 @@ class ElboEngine(object):
                 _run(lib.gpi_rom, C.byref(r), C.c_void_p(self._side.cuda_stream), what='rom')
             self._ev_join.record(self._side)
             self._pending_join = True
+        if running == 'now':
+            self.running.launch(st)
+        self._running_pending = running == 'defer'
         if compute_value:
             self._join()
             return self.elbo_value()
@@ -543,6 +597,9 @@ class ElboEngine(object):
             _run(lib.gpi_head_backward, C.byref(hq), P_, W_, G_, sst, what='head backward (variational samples)')
             self._pending_join = False          # joined below with the rest of the side work
         run_reduce(self.reduce_dec, self.ws, self.flat, sst)
+        if self._running_pending:
+            self.running.launch(sst)
+            self._running_pending = False
         _run(lib.gpi_outer_gemm, self.gemm_items, len(self.gemm_items), C.c_void_p(self.ws.t_ws.data_ptr()),
              C.c_void_p(self.flat.gacc.data_ptr()), sst, what='outer gemm')
         if side_extra is not None:
@@ -609,6 +666,7 @@ class EncoderEngine(object):
         gi.append(L.GemmItem(a_off=hb['dhpre'], b_off=h.feat, c_off=h.fc_w, bias_off=h.fc_b, S=self.B, M=d_feat,
                              N=d_feat, lda=d_feat, ldb=d_feat, flags=0))
         self.gemm_items = (L.GemmItem * len(gi))(*gi)
+        self.running = BnRunning([(self.p, enc, [(0, self.B)])], ws, flat.P.device)
 
     def forward(self, x, dropout=None, seed=0):
         """dropout: optional injected channel scales {conv name: [B, cout]} (else drawn, seed)."""
@@ -625,6 +683,7 @@ class EncoderEngine(object):
                 draw_dropout(self.ws, (self.p,), st, seed)
         self.ws.zero_scratch()
         _run(lib.gpi_codec_forward, self.descs, len(self.descs), C.byref(self.ctx), st, what='encoder forward')
+        self.running.launch(st)
         _run(lib.gpi_head_forward, C.byref(self.head), C.c_void_p(self.flat.P.data_ptr()),
              C.c_void_p(self.ws.t_ws.data_ptr()), st, what='head forward')
         return (self.ws.view(self.hb['zmu'], self.B, self.dz).clone(),
@@ -679,6 +738,7 @@ class DecoderEngine(object):
                                                       S=self.B, M=d_lat, N=dz, lda=d_lat, ldb=dz, flags=0))
         o = self.p.output
         self.out_shape = (self.B, o.C, o.H, o.W)
+        self.running = BnRunning([(self.p, dec, [(0, self.B)])], ws, flat.P.device)
 
     def forward(self, z, dropout=None, seed=0):
         """dropout: optional injected channel scales {conv name: [B, cout]} (else drawn, seed)."""
@@ -694,6 +754,7 @@ class DecoderEngine(object):
         _run(lib.gpi_head_forward, C.byref(self.head), C.c_void_p(self.flat.P.data_ptr()),
              C.c_void_p(self.ws.t_ws.data_ptr()), st, what='latent map')
         _run(lib.gpi_codec_forward, self.descs, len(self.descs), C.byref(self.ctx), st, what='decoder forward')
+        self.running.launch(st)
         return self.ws.view(self.p.output.off, *self.out_shape).clone()
 
     def backward(self, dout):

@@ -110,7 +110,9 @@ class PredictionEnsembleEngine(object):
         self.q_n = self.flat.numel - self.q_off
         assert self.q_off == self.n_dec and self.q_n == 2 * q_z._mean.numel()
         em = _EngineModel(self.shadow, model.gp, model.g, q_z, self.flat)
-        self.engine = ElboEngine(em, 0, 0, N_vo=self.N, vo_holdoff=True)
+        # the PE's decoder calls are the model's decoder's in the reference (components.py:371): its BN
+        # running statistics are model.f's
+        self.engine = ElboEngine(em, 0, 0, N_vo=self.N, vo_holdoff=True, running_modules={'dec': model.f})
         self.engine.bind(X_vo=self.X)
         self.m = torch.zeros(self.q_n, dtype=torch.float32, device=dev)
         self.v = torch.zeros_like(self.m)
@@ -164,7 +166,7 @@ class PredictionEnsembleEngine(object):
             L.check(lib.gpi_randn(L.ptr(ez), ez.numel(), self.seed, L.ptr(self.rng_off), 5, st), 'randn pe')
         if self.engine.has_dropout:     # the reference calls the decoder in train mode (components.py:371)
             self.engine.draw_dropout(st, self.seed, L.ptr(self.rng_off), 6)
-        self.engine.forward(st, compute_value=False)
+        self.engine.forward(st, compute_value=False, running='defer')
         t = self.engine.ws.terms
         from .engine import T_LX0, T_KL_Q2
         logL, kld = t[T_LX0].float(), t[T_KL_Q2].float()

@@ -126,7 +126,7 @@ class FusedElboStep(object):
         the head backward has consumed this step's; the epilogue (gradient finalisation, scratch
         reset, subset hand-over) is one launch."""
         st = stream if stream is not None else L.stream_handle()
-        self.engine.forward(st, compute_value=False, zero_gacc=False, zero_scratch=False)
+        self.engine.forward(st, compute_value=False, zero_gacc=False, zero_scratch=False, running='defer')
         self.engine.backward(st, side_extra=lambda sst: self._launch_noise(sst, self.idx_next))
         L.check(L.lib().gpi_step_epilogue(C.byref(self.epi), st), 'step epilogue')
 
@@ -157,7 +157,8 @@ class FusedElboStep(object):
         statistics scratch."""
         ws = self.engine.ws
         return [self.flat.P, self.m, self.v, self.step_ctr, self.rng_off, self.idx, self.idx_next,
-                self.flat.gacc, self.flat.G, ws.t_ws, ws.t_scr, ws.t_parts, ws.t_flag, self.last_terms]
+                self.flat.gacc, self.flat.G, ws.t_ws, ws.t_scr, ws.t_parts, ws.t_flag, self.last_terms] + \
+            self.engine.running.buffers
 
     def capture(self):
         """Capture the step into HIP graph(s); the all-reduce stays outside the graph.

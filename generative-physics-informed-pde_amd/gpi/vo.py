@@ -124,8 +124,10 @@ def vo_precision(gamma, alpha, mean, vars_, infinite, beta, vo_var, alpha0=ALPHA
     N, m, dy = gamma.shape
     assert mean.shape == (N, dy) and vars_.shape == (N, dy) and infinite.shape == (m,)
     assert infinite.dtype == torch.int32 and beta.shape == (m,) and vo_var.shape == (m,)
+    terms = torch.empty(m, max(N, 1), dtype=torch.float64, device=beta.device)
     d = L.VoPrecisionDesc(n=N, m=m, d_y=dy, gamma=_p(gamma), alpha=_p(alpha), mean=_p(mean), vars=_p(vars_),
-                          infinite=_p(infinite), alpha0=alpha0, beta0=beta0, beta=_p(beta), vo_var=_p(vo_var))
+                          infinite=_p(infinite), alpha0=alpha0, beta0=beta0, beta=_p(beta), vo_var=_p(vo_var),
+                          terms=_p(terms))
     L.check(L.lib().gpi_vo_precision(C.byref(d), L.stream_handle()), 'vo precision')
 
 

@@ -345,6 +345,8 @@ typedef struct gpi_vo_precision_desc {
     double alpha0, beta0;
     double* beta;              /* [m] out (prec_beta) */
     double* vo_var;            /* [m] out (mean VO variances) */
+    double* terms;             /* [m, n] workspace: per-(row, VO sample) terms, summed over samples in a
+                                  fixed order (bitwise reproducible beta / vo_var) */
 } gpi_vo_precision_desc;
 
 /* Predictive effective properties (Analysis.sample_predictive_y's first two stages,
@@ -394,6 +396,25 @@ int gpi_version(void);
 /* sizeof of every struct above, in declaration order (ABI self-check); returns the count. */
 int gpi_struct_sizes(int64_t* out, int n);
 const char* gpi_error_string(int code);
+
+/* BatchNorm2d running statistics (train mode, codec.py BatchNorm2d layers, momentum 0.1): for every
+ * item (one BN layer: `channels` stat records from `stat`), and for each of its codec calls in call
+ * order (group g[k], element count count[k] = samples * H * W):
+ *   running_mean = (1 - m) running_mean + m mean,  running_var = (1 - m) running_var + m var * n / (n - 1),
+ *   num_batches_tracked += n_calls
+ * from the fp64 batch sums the forward kernels accumulated (before the step epilogue clears them). */
+typedef struct gpi_bn_running_item {
+    int64_t stat;
+    int32_t channels, n_calls;
+    int32_t group[GPI_MAX_GROUPS];
+    double count[GPI_MAX_GROUPS];
+    float* running_mean;
+    float* running_var;
+    int64_t* num_batches_tracked;
+} gpi_bn_running_item;
+/* items: device array of n_items records (persistent, graph-capture safe). */
+int gpi_bn_running_update(const gpi_bn_running_item* items, int n_items, int max_channels, const gpi_stat* stats,
+                          int64_t n_stats, float momentum, void* stream);
 
 /* Number of workgroups (= partial-slab rows) a conv backward launch uses. */
 int gpi_conv_blocks(const gpi_conv_desc* op, const gpi_groups* groups, int32_t* blocks);

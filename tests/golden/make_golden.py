@@ -395,6 +395,48 @@ def make_elbo_c64():
     print('elbo c64 ok', elbo.item(), 'n params', sum(p.numel() for p in model.parameters()))
 
 
+def make_bn_running_c32():
+    """BatchNorm2d running statistics (train mode, momentum 0.1): the reference model after two
+    model.elbo calls (encoder once, decoder twice -- unsupervised then supervised -- per call) ->
+    bn_running_c32.npz (state before, running buffers after, injected noise)."""
+    phys = c32_physics()
+    nc, r, mc, mf, M, W, cdofs, fdofs = phys
+    n = nc * r
+    rng = np.random.default_rng(54)
+    Nu, bs, Ns, dz = 16, 8, 4, 16
+    gen = torch.Generator().manual_seed(55)
+    model, g = _elbo_model(phys, n, dz, [1, 1], 4, 4, gen)
+    Xu = torch.tensor(random_fields(rng, Nu, n), dtype=torch.float32)
+    Xs_img = random_fields(rng, Ns, n)
+    U = rng.uniform(-0.5, 0.5, (Ns, 4))
+    Y = np.stack([fem.solve_fom(mf, np.exp(fem.image_to_cells(x)), u) for x, u in zip(Xs_img, U)])
+    F = np.stack([fem.f_rom_bc(mc, u) for u in U])
+    model.register_datasets({'supervised': _DS(X=torch.tensor(Xs_img, dtype=torch.float32),
+                                               Y=torch.tensor(Y, dtype=torch.float32),
+                                               F_ROM_BC=torch.tensor(F, dtype=torch.float32)),
+                             'unsupervised': _DS(X=Xu)}, None, create_unsupervised_variational_approximation=False)
+    with torch.no_grad():       # non-trivial running buffers to start from
+        for m in model.modules():
+            if isinstance(m, torch.nn.BatchNorm2d):
+                m.running_mean.copy_(torch.randn(m.running_mean.shape, generator=gen))
+                m.running_var.copy_(torch.rand(m.running_var.shape, generator=gen) + 0.5)
+    perm = torch.tensor(rng.permutation(Nu), dtype=torch.long)
+    state0 = {k: v.detach().cpu().numpy().copy() for k, v in model.state_dict().items()}
+    out = {'state.' + k: v for k, v in state0.items()}
+    for call in range(2):
+        eps = [torch.tensor(rng.normal(size=s_), dtype=torch.float32) for s_ in [(bs, dz), (Ns, dz), (Ns, M.shape[2])]]
+        _elbo_run(model, perm, eps, armortized_bs=bs)
+        for i, e in enumerate(eps):
+            out['eps%d_%d' % (call, i)] = e.numpy()
+    out.update({'after.' + k: v.detach().cpu().numpy().copy() for k, v in model.state_dict().items()
+                if k.endswith(('running_mean', 'running_var', 'num_batches_tracked'))})
+    out.update(Xu=Xu.numpy(), Xs=Xs_img.astype(np.float32), Y=Y.astype(np.float32), F=F.astype(np.float32),
+               perm=perm.numpy(), M=M.astype(np.float32), W=W.astype(np.float32), bc_dofs=cdofs,
+               cfg=np.array([n, nc, dz, Nu, bs, Ns]))
+    np.savez_compressed(os.path.join(HERE, 'bn_running_c32.npz'), **out)
+    print('bn running ok')
+
+
 def make_elbo_options_c32():
     """model.elbo(normalize=True) and model.elbo(l2_penalty=...) (generative.py:247-287: every term
     divided by its batch size; minus l2_penalty * sum of the parameter norms of f and the encoder)
@@ -843,6 +885,7 @@ ALL = {
     'elbo_c32': make_elbo,
     'elbo_c64': make_elbo_c64,
     'elbo_opts_c32': make_elbo_options_c32,
+    'bn_running_c32': make_bn_running_c32,
     'elbo_nonarm_c32': make_elbo_nonarmortized,
     'vo_c32': make_vo,
     'vo_elbo_c32': make_vo_elbo,

@@ -427,6 +427,11 @@ def test_fused_step_matches_module_path(device, independent_X):
         assert len(set(step.idx.tolist())) == bs
         step.update()
         torch.cuda.synchronize()
+        # BN running statistics: the fused step updates them as the module path does
+        sd, rsd = model.state_dict(), ref_model.state_dict()
+        for k in sd:
+            if k.endswith(('running_mean', 'running_var', 'num_batches_tracked')):
+                torch.testing.assert_close(sd[k], rsd[k], rtol=1e-5, atol=1e-6)
     assert step.step_ctr.item() == 2
 
 
@@ -527,3 +532,28 @@ def test_dropout_mask_statistics(device):
     v = x.cpu().numpy()
     assert set(np.unique(v).tolist()) == {0.0, np.float32(1.25)}
     assert abs((v == 0).mean() - 0.2) < 3e-3
+
+
+def test_bn_running_statistics_match_reference(device):
+    """BatchNorm2d running_mean / running_var / num_batches_tracked after two model.elbo calls (train
+    mode, momentum 0.1; the decoder's unsupervised and supervised calls update in that order) vs the
+    reference run (bn_running_c32.npz)."""
+    d = load('bn_running_c32.npz')
+    model, bs = build_golden_model(d)
+    for call in range(2):
+        eps = (torch.cat([cuda(d['eps%d_0' % call]), cuda(d['eps%d_1' % call])]), cuda(d['eps%d_2' % call]))
+        model.elbo(step=call, armortized_bs=bs, eps=eps)
+    torch.cuda.synchronize()
+    sd = model.state_dict()
+    n = 0
+    for k, v in d.items():
+        if not k.startswith('after.'):
+            continue
+        name = k[6:]
+        got = sd[name].cpu().numpy()
+        if name.endswith('num_batches_tracked'):
+            assert int(got) == int(v), name
+        else:
+            np.testing.assert_allclose(got, v, rtol=2e-5, atol=2e-6, err_msg=name)
+        n += 1
+    assert n > 0

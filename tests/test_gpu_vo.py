@@ -125,7 +125,7 @@ def test_vo_moments(device):
     assert rel(std0.cpu(), y0.std(1, ddof=1)) < 1e-5
 
 
-@pytest.mark.parametrize('m_kind', ['cgr', 'cgr_flux_c64'])
+@pytest.mark.parametrize('m_kind', ['cgr', 'cgr_flux_c64', 'cgr_flux_nc16'])
 def test_vo_condition_vs_oracle(device, m_kind):
     """Conditioning kernel vs the oracle restatement of VirtualObservable.update on the same
     fp32-rounded prior (the reference casts its fp32 Y_mean / PREC to double).  m = 25 keeps Lambda in
@@ -141,7 +141,7 @@ def test_vo_condition_vs_oracle(device, m_kind):
         from gpi import _lib as L
         from gpi.vo import vo_query
         rng = np.random.default_rng(11)
-        nc, r, N = 8, 8, 2
+        nc, r, N = (8, 8, 2) if m_kind == 'cgr_flux_c64' else (16, 4, 1)
         n = nc * r
         x = rng.normal(0.4, 0.8, (N, 2 * n * n))
         u = rng.uniform(-0.5, 0.5, (N, 4))
@@ -181,6 +181,9 @@ def test_vo_precision_vs_oracle(device):
     beta = torch.empty(m, dtype=torch.float64, device='cuda')
     vv = torch.empty_like(beta)
     vo_precision(G, A, mu, va, inf, beta, vv)
+    beta2, vv2 = torch.empty_like(beta), torch.empty_like(vv)
+    vo_precision(G, A, mu, va, inf, beta2, vv2)
+    assert torch.equal(beta, beta2) and torch.equal(vv, vv2)       # fixed-order sums: reproducible
     assert rel(beta.cpu(), d['prec_beta']) < 1e-12
     ref = oelbo.vo_mean_variances(torch.tensor(d['prec_beta']), G.shape[0], inf.cpu().bool())
     assert rel(vv.cpu(), ref) < 1e-12
