@@ -24,6 +24,7 @@
 #include "common.h"
 #include <stdlib.h>
 #include <stdio.h>
+#include <algorithm>
 
 using namespace gpi;
 
@@ -83,6 +84,9 @@ struct ConvGeom {
     int gh, PG;     // output-gradient image: rows [gy0, gy0 + gh), pitch PG = w_out + 2H
     int ph;         // owned input rows (backward)
     const float* zero;   // the zero page (kernel argument: no per-use address reload)
+    int zreg;       // backward: the BN-backward operand z of the output in registers (<= ZREG chunks / thread)
+    int split;      // backward: 2 workgroups per tile, input gradient (blockIdx < nblocks) and weight gradient
+                    // (the rest) in parallel on otherwise idle CUs (launches well under one round)
     int in_sq, in_sr, in_sc;   // 256 chunks of the input image = (planes, rows, chunks)
     int g_sq, g_sr, g_sc;      // ... of the output-gradient image
     Div d_in4, d_P4, d_g4, d_PG4, d_cin, d_cout, d_win, d_tp, d_wout, d_w2;
@@ -127,6 +131,9 @@ __host__ __device__ inline void owned_rows(int s, int up, int o0, int t, int& p0
     else if (s == 2) { p0 = 2 * o0; len = 2 * t; }
     else { p0 = o0; len = t; }
 }
+
+// Chunks (16 B) of the output's raw z image a backward thread holds in registers instead of LDS.
+constexpr int ZREG = 3;
 
 // Tiles: the forward computes one output pixel per thread (<= 256 per tile); the MFMA
 // backward takes taller tiles (fewer halo rows and per-tile fixed costs per pixel).
@@ -200,6 +207,10 @@ bool conv_geom(const gpi_conv_desc& d, const gpi_groups& g, ConvGeom& G, bool fw
         eo * d.w_in >= lim || 256ull * G.th * d.w_out >= lim)
         return false;
     G.zero = nullptr;   // set by launch()
+    // the BN-backward operand image in registers when it is small: LDS = gradient + input images only
+    // (one more resident workgroup per CU on the 32x32 / 64x64 decoder planes)
+    G.zreg = (!fwd && d.gout_mode == 0 && (int64_t)d.cout * G.gh * (G.PG / 4) <= (int64_t)ZREG * 256) ? 1 : 0;
+    G.split = 0;   // decided by launch() from the LDS footprint
 #ifdef GPI_PHASE_TIMING
     static const int dbg = env_int("GPI_DBG_SKIP", 0);
     G.dbg = dbg;
@@ -403,10 +414,11 @@ struct TileIdx {
     int b, oy0, grp, gsz;
 };
 
-__device__ __forceinline__ TileIdx tile_of(const ConvGeom& G, const gpi_groups& g) {
+__device__ __forceinline__ TileIdx tile_of(const ConvGeom& G, const gpi_groups& g, int tile = -1) {
+    if (tile < 0) tile = blockIdx.x;
     TileIdx t;
-    t.b = blockIdx.x / G.tiles;
-    t.oy0 = (blockIdx.x - t.b * G.tiles) * G.th;
+    t.b = tile / G.tiles;
+    t.oy0 = (tile - t.b * G.tiles) * G.th;
     t.grp = group_of(g, t.b);
     t.gsz = g.start[t.grp + 1] - g.start[t.grp];
     return t;
@@ -457,8 +469,8 @@ __device__ __forceinline__ void activate_img(float* img, const ConvGeom& G, cons
 }
 
 // ---------------------------------------------------------------------------------- forward
-// header floats: gst fp64 [4*MAX_CIN] | sc | sh [MAX_CIN] | scratch [64] | red [16]
-constexpr int FWD_HDR = 8 * GPI_MAX_CIN + 2 * GPI_MAX_CIN + 64 + 16;
+// header floats: gst fp64 [4*MAX_CIN] | sc | sh [MAX_CIN] | scratch [64] | red [16] | dropout scales [8]
+constexpr int FWD_HDR = 8 * GPI_MAX_CIN + 2 * GPI_MAX_CIN + 64 + 16 + 8;
 
 template <int K, int S, int UP, int CP>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void conv_fwd_kernel(gpi_conv_desc d, gpi_codec_ctx c, ConvGeom G) {
@@ -469,6 +481,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void c
     float* sh = sc + GPI_MAX_CIN;
     float* scratch = sh + GPI_MAX_CIN;   // 2*CP*4 <= 64
     float* red = scratch + 64;           // 2*CP <= 16
+    float* dsl = red + 16;               // [CP] Dropout2d scales of this sample's output channels
     float* wT = smem + pad256(FWD_HDR);  // [cin][KK][CP]
     const int nw = d.cin * KK * CP;
     float* img = wT + pad256(nw);        // [cin][rh][P] + zero margin
@@ -483,12 +496,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void c
     const TileIdx T = tile_of(G, c.groups);
     const int HWi = d.h_in * d.w_in, HWo = d.h_out * d.w_out;
     const float* ib = input_base(d, c, T.b);
-    // Dropout2d after this conv: the sample's output-channel scales (0 or 1/(1-p))
+    // Dropout2d after this conv: the sample's output-channel scales (0 or 1/(1-p)) into LDS (read by
+    // the epilogue after the barriers below; no registers held across the compute)
     const bool drop = d.drop_off >= 0;
-    float dsc[CP];
-#pragma unroll
-    for (int co = 0; co < CP; ++co)
-        dsc[co] = (drop && co < d.cout) ? *as_gld(ws + d.drop_off + (int64_t)T.b * d.cout + co) : 1.f;
     PHASE(1);
 
     // ---- phase 1: every global read of the tile in flight together
@@ -500,6 +510,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void c
     in_rows(K, S, UP, d.pad, T.oy0, G.th, iy0, rh_);
     stage_img(img, d.cin, G.rh, G.P, G.d_in4, G.d_P4, G.in_sq, G.in_sr, G.in_sc, iy0, d.h_in, d.w_in, zero,
               [&](int q) -> const float* { return ib + (int64_t)q * HWi; });
+    if (drop && tid >= 64 && tid < 64 + d.cout)      // (after the DMA issue: its wait overlaps the stat loads)
+        dsl[tid - 64] = *as_gld(ws + d.drop_off + (int64_t)T.b * d.cout + (tid - 64));
     if (d.in_bn) {
         float gam = 0.f, bet = 0.f;
         if (tid < d.cin) {
@@ -567,7 +579,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void c
         PHASE(6);
         if (drop) {
 #pragma unroll
-            for (int co = 0; co < CP; ++co) acc[co] *= dsc[co];
+            for (int co = 0; co < CP; ++co)
+                if (co < d.cout) acc[co] *= dsl[co];
         }
         if (d.epilogue == GPI_EPI_GAUSS_LOSS) {
             if (active) {
@@ -638,9 +651,11 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-// header floats: gst fp64 [4*(MAX_CIN+MAX_COUT)] | i_sc i_sh i_mean i_inv i_gam [MAX_CIN] | o_coef [4*MAX_COUT]
-// | o_drop [MAX_COUT]
-constexpr int BWD_HDR = 8 * (GPI_MAX_CIN + GPI_MAX_COUT) + 5 * GPI_MAX_CIN + 5 * GPI_MAX_COUT;
+// header floats, sized by the launch's channel counts: gst fp64 [4*(cin+cout)] | i_sc i_sh i_mean i_inv i_gam [cin]
+// | o_coef [4*cout] | o_drop [cout], padded to 64 floats (LDS is the residency limit of the large backward
+// launches: <= 31 KB gives 5 workgroups per CU, measured tools/bench_dispatch.hip)
+__host__ __device__ inline int pad64(int n) { return (n + 63) & ~63; }
+__host__ __device__ inline int bwd_hdr(int cin, int cout) { return pad64(8 * (cin + cout) + 5 * cin + 5 * cout); }
 template <bool B>
 struct BoolC {
     static constexpr bool value = B;
@@ -651,25 +666,26 @@ struct IntC {
     static constexpr int value = V;
 };
 
-constexpr int BWD_RED = 1024;   // [4 waves][4][64] partial dW of one column block / per-wave channel sums
+// per-wave input-channel sums [2][4 waves][32] (256 floats) alias the offset table (>= 256 floats)
+constexpr int SLAB_ROWS = 4;    // partial-slab rows per workgroup: one per wave (no cross-wave dW reduction)
 
 template <int K, int S, int UP>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 : 6))) void conv_bwd_kernel(gpi_conv_desc d, gpi_codec_ctx c, ConvGeom G) {
     constexpr int KK = K * K;
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    double* gst = (double*)smem;
-    float* i_sc = smem + 8 * (GPI_MAX_CIN + GPI_MAX_COUT);
-    float* i_sh = i_sc + GPI_MAX_CIN;
-    float* i_mean = i_sh + GPI_MAX_CIN;
-    float* i_inv = i_mean + GPI_MAX_CIN;
-    float* i_gam = i_inv + GPI_MAX_CIN;
-    float* o_coef = i_gam + GPI_MAX_CIN;              // [MAX_COUT][4]: mean, inv, mS, mSx
-    float* o_drop = o_coef + 4 * GPI_MAX_COUT;        // [MAX_COUT] Dropout2d scales of the output channels
+    double* gst = (double*)smem;                      // [cin][4] input stats, then [cout][4] output stats
+    float* i_sc = smem + 8 * (d.cin + d.cout);
+    float* i_sh = i_sc + d.cin;
+    float* i_mean = i_sh + d.cin;
+    float* i_inv = i_mean + d.cin;
+    float* i_gam = i_inv + d.cin;
+    float* o_coef = i_gam + d.cin;                    // [cout][4]: mean, inv, mS, mSx
+    float* o_drop = o_coef + 4 * d.cout;              // [cout] Dropout2d scales of the output channels
     const bool has_gin = d.gin_off >= 0;
     const bool obn = d.gout_mode == 0;
     const int KD = d.cout * KK;                       // input-gradient reduction length
     const int KD4 = (KD + 3) & ~3;
-    float* wD = smem + pad256(BWD_HDR);               // [KD4][16]: W[co][ci][tap] at (co*KK + tap)*16 + ci, zero padded
+    float* wD = smem + bwd_hdr(d.cin, d.cout);        // [KD4][16]: W[co][ci][tap] at (co*KK + tap)*16 + ci, zero padded
     const int nwd = has_gin ? KD4 * 16 : 0;
     // S1 / UP: [KD4] output-gradient offset of reduction index k; S2: per parity class of the input
     // pixel [4][2][KD4]: (output-gradient offset, weight row) of the class's k-th valid tap
@@ -677,11 +693,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 
     float* gl = (float*)ktab + (has_gin ? pad256((S == 2 ? 8 : 1) * KD4) : 0);   // [cout][gh][PG]
     const int gplane = G.gh * G.PG;
     const int gimg = img_floats(d.cout, G.gh, G.PG);
-    float* gz = gl + gimg;                            // raw z of the output (BN-backward only)
-    float* al = gz + (obn ? gimg : 0);                // [cin][rh][P]
+    const bool zreg = G.zreg != 0;
+    float* gz = gl + gimg;                            // raw z of the output (BN-backward only, LDS form)
+    float* al = gz + ((obn && !zreg) ? gimg : 0);     // [cin][rh][P]
     // reduction scratch: aliases gz (dead after phase 3) when it is large enough -- 8 KB less LDS
     // per workgroup, one more resident workgroup per CU on the 32x32 planes
-    float* red = (obn && gimg >= BWD_RED) ? gz : al + img_floats(d.cin, G.rh, G.P);
+    // channel-sum scratch: the offset table's space, dead after the input gradient (in_bn implies has_gin)
+    float* red = (float*)ktab;
 
     const int tid = threadIdx.x;
     const int lane = tid & 63, wv = tid >> 6, kq = lane >> 4, l16 = lane & 15;
@@ -692,13 +710,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 
     const float* const zero = pin(G.zero);
     const int64_t w_off = pin(d.w_off), gout_off = pin(d.gout_off), out_off = pin(d.out_off);
     const int64_t gin_off = pin(d.gin_off);
-    const TileIdx T = tile_of(G, c.groups);
+    // split launches: workgroups [0, nblocks) compute the input gradient (+ BN-backward sums, dgamma /
+    // dbeta), [nblocks, 2 nblocks) the weight gradient of the same tiles
+    const bool wg_role = G.split && (int)blockIdx.x >= G.nblocks;
+    const bool dg_role = !wg_role;
+    const bool do_wgrad = !G.split || wg_role;
+    const int tile = wg_role ? (int)blockIdx.x - G.nblocks : (int)blockIdx.x;
+    const TileIdx T = tile_of(G, c.groups, tile);
     const int HWi = d.h_in * d.w_in, HWo = d.h_out * d.w_out;
     const float* ib = input_base(d, c, T.b);
     PHASE(1);
 
     // ---- phase 1: every global read in flight together
-    if (has_gin)
+    if (has_gin && dg_role)
         stage(wD, nwd, zero, [&](int e) -> const float* {
             const int ci = e & 15, k = e >> 4;
             const int co = k / KK, t = k - co * KK;
@@ -711,9 +735,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 
     stage_img(gl, d.cout, G.gh, G.PG, G.d_g4, G.d_PG4, G.g_sq, G.g_sr, G.g_sc, gy0, d.h_out, d.w_out, zero,
               [&](int q) -> const float* { return ws + gout_off + gbase + (int64_t)q * HWo; });
     PHASE(13);
-    if (obn)
+    f32x4 zr[ZREG];           // zreg: this thread's chunks tid + 256 u of the z image
+    if (obn && zreg) {
+        const int P4 = G.PG >> 2, plane4 = G.gh * P4, total = d.cout * plane4;
+        const int c4lo = HALO / 4, c4hi = HALO / 4 + d.w_out / 4;
+        ChunkIter it;
+        it.init(tid, plane4, P4, G.d_g4, G.d_PG4);
+#pragma unroll
+        for (int u = 0; u < ZREG; ++u) {
+            const int row = gy0 + it.r;
+            const bool ok = tid + 256 * u < total && row >= 0 && row < d.h_out && it.c4 >= c4lo && it.c4 < c4hi;
+            const float* src = ok ? ws + out_off + gbase + (int64_t)it.q * HWo + row * d.w_out + 4 * (it.c4 - c4lo)
+                                  : zero;
+            zr[u] = *as_gld((const f32x4*)src);
+            it.step(G.g_sq, G.g_sr, G.g_sc, P4, G.gh);
+        }
+    } else if (obn) {
         stage_img(gz, d.cout, G.gh, G.PG, G.d_g4, G.d_PG4, G.g_sq, G.g_sr, G.g_sc, gy0, d.h_out, d.w_out, zero,
                   [&](int q) -> const float* { return ws + out_off + gbase + (int64_t)q * HWo; });
+    }
     PHASE(14);
     int iy0, rh_;
     in_rows(K, S, UP, d.pad, T.oy0, G.th, iy0, rh_);
@@ -727,8 +767,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 
     owned_rows(S, UP, T.oy0, G.th, py0, ph_);
     // cin <= 4 at stride 1: the input gradient runs on the VALU (phase 4b'), the MFMA form would
     // leave >= 3/4 of its N = 16 columns empty
-    const bool vdg = K == 5 && S == 1 && !UP && has_gin && d.cin <= 4;
-    const int nmblk = (has_gin && !vdg && !SKIP(G, 2)) ? (G.ph * d.w_in) >> 4 : 0;
+    const bool vdg = K == 5 && S == 1 && !UP && has_gin && d.cin <= 4 && dg_role;
+    const int nmblk = (has_gin && dg_role && !vdg && !SKIP(G, 2)) ? (G.ph * d.w_in) >> 4 : 0;
     const int ci_l = min(l16, d.cin - 1);
     const bool cok = l16 < d.cin;
     const int64_t ibase = ((int64_t)T.b * d.in_ctot + d.in_c0 + ci_l) * HWi + (int64_t)py0 * d.w_in;
@@ -756,7 +796,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 
     {
         StatLoad L;
         stat_issue(c.stats, c.n_stats, T.grp, d.in_stat, d.in_bn ? d.cin : 0, gst, d.out_stat, obn ? d.cout : 0,
-                   gst + 4 * GPI_MAX_CIN, zero, L);
+                   gst + 4 * d.cin, zero, L);
         PHASE(10);
         stat_finish(L);
         PHASE(11);
@@ -776,7 +816,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 
     }
     if (obn && tid >= 64 && tid < 64 + d.cout) {
         const int co = tid - 64;
-        const double* st = gst + 4 * (GPI_MAX_CIN + co);
+        const double* st = gst + 4 * (d.cin + co);
         const double n = (double)T.gsz * HWo;
         float mean, inv;
         mean_invstd(st, n, c.bn_eps, mean, inv);
@@ -790,7 +830,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 
 
     // ---- phase 3: activations in LDS; offset table of the input-gradient reduction
     if (d.in_bn) activate_img(al, G, d, iy0, i_sc, i_sh);
-    if (has_gin && S == 2) {
+    if (has_gin && dg_role && S == 2) {
         // input pixel (py, px) = (py0 + 2a + ry, 2b + rx) receives output (oy, ox) through tap (ky, kx)
         // iff 2 oy = py + pad - ky, 2 ox = px + pad - kx: the valid taps depend on the parity class
         // (ry, rx) only.  Class table entry k: A = gl offset (co, dy = (ry + pad - ky) / 2,
@@ -811,7 +851,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 
             ktab[cls * 2 * KD4 + KD4 + k] = ob;
         }
     }
-    if (has_gin && S != 2) {
+    if (has_gin && dg_role && S != 2) {
         // A operand of reduction index k = (co, ky, kx) for owned pixel (qy, px):
         // gl[(S1) qy*PG + px | (UP) 2 qy*PG + 2 px] + ktab[k]
         const int ry0 = (UP ? 2 * py0 : py0) + d.pad - gy0;
@@ -824,7 +864,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 
             ktab[k] = o;
         }
     }
-    if (obn) {
+    if (obn && zreg) {
+        // BN-backward of the output gradient with z from registers: chunk tid + 256 u
+        const int P4 = G.PG >> 2, plane4 = G.gh * P4, total = d.cout * plane4;
+        const int c4lo = HALO / 4, c4hi = HALO / 4 + d.w_out / 4;
+        float4* g4 = reinterpret_cast<float4*>(gl);
+        ChunkIter it;
+        it.init(tid, plane4, P4, G.d_g4, G.d_PG4);
+#pragma unroll
+        for (int u = 0; u < ZREG; ++u) {
+            const int e = tid + 256 * u;
+            const int row = gy0 + it.r;
+            if (e < total && row >= 0 && row < d.h_out && it.c4 >= c4lo && it.c4 < c4hi) {
+                const float* oc = o_coef + 4 * it.q;
+                const float m = oc[0], inv = oc[1], mS = oc[2], mSx = oc[3];
+                const float ds = o_drop[it.q];
+                const float4 sv = g4[e];
+                const f32x4 zv = zr[u];
+                float4 o;
+                o.x = ds * ((sv.x - mS - ((zv[0] - m) * inv) * mSx) * inv);
+                o.y = ds * ((sv.y - mS - ((zv[1] - m) * inv) * mSx) * inv);
+                o.z = ds * ((sv.z - mS - ((zv[2] - m) * inv) * mSx) * inv);
+                o.w = ds * ((sv.w - mS - ((zv[3] - m) * inv) * mSx) * inv);
+                g4[e] = o;
+            }
+            it.step(G.g_sq, G.g_sr, G.g_sc, P4, G.gh);
+        }
+    } else if (obn) {
         const int P4 = G.PG >> 2, plane4 = G.gh * P4, total = d.cout * plane4;
         const int c4lo = HALO / 4, c4hi = HALO / 4 + d.w_out / 4;
         float4* g4 = reinterpret_cast<float4*>(gl);
@@ -885,11 +951,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 
     // and rows i >= M / columns j >= N of the tile (clamped operands) are never stored.
     const int J = d.cin * KK;
     const int rowlen = d.cout * J + (d.in_bn ? 2 * d.cin : 0);
-    float* slab = c.wpart + d.wpart_off + (int64_t)blockIdx.x * rowlen;
+    // this wave's partial-slab row: [dW partial over the wave's output rows | dgamma | dbeta partials]
+    float* slab = c.wpart + d.wpart_off + ((int64_t)tile * SLAB_ROWS + wv) * rowlen;
     // single-channel 7x7 / stride-2 input conv: weight gradient with the reduction over the tile's
     // output pixels (M = cout, N = the 49 taps in 4 column blocks, K = pixels), no zero-interleaved
     // stride-2 columns (the column-shift form below would compute ~6x the useful products here)
-    const bool vwg = K == 7 && S == 2 && !UP && d.cin == 1 && !has_gin && d.cout <= 16;
+    const bool vwg = K == 7 && S == 2 && !UP && d.cin == 1 && !has_gin && d.cout <= 16 && do_wgrad;
     if constexpr (K == 7 && S == 2 && !UP) {
         if (vwg && !SKIP(G, 1)) {
             constexpr int PADC = K / 2, NB = (KK + 15) / 16;
@@ -916,27 +983,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 
 #pragma unroll
                 for (int nb = 0; nb < NB; ++nb) acc[nb] = mfma4(a, bv[nb], acc[nb]);
             }
-            // fixed-order sum of the four waves' tiles, one column block at a time
+            // each wave stores its own tile into its slab row (the slab reduction sums the rows)
 #pragma unroll
             for (int nb = 0; nb < NB; ++nb) {
-                if (nb > 0) __syncthreads();
 #pragma unroll
-                for (int r = 0; r < 4; ++r) red[(wv * 4 + r) * 64 + lane] = acc[nb][r];
-                __syncthreads();
-                const int r = tid >> 6, ln = tid & 63;
-                const int co2 = (ln >> 4) * 4 + r, j2 = 16 * nb + (ln & 15);
-                if (co2 < d.cout && j2 < KK) {
-                    const float v = red[(0 * 4 + r) * 64 + ln] + red[(1 * 4 + r) * 64 + ln] +
-                                    red[(2 * 4 + r) * 64 + ln] + red[(3 * 4 + r) * 64 + ln];
-                    slab[co2 * J + j2] = v;
+                for (int r = 0; r < 4; ++r) {
+                    const int co2 = kq * 4 + r, j2 = 16 * nb + l16;
+                    if (co2 < d.cout && j2 < KK) slab[co2 * J + j2] = acc[nb][r];
                 }
             }
-            __syncthreads();
         }
     }
     {
         const int MI = d.cout * K, NJ = d.cin * K;
-        const int nmb = (SKIP(G, 1) || vwg) ? 0 : (MI + 15) >> 4, nnb = (NJ + 15) >> 4;
+        const int nmb = (SKIP(G, 1) || vwg || !do_wgrad) ? 0 : (MI + 15) >> 4, nnb = (NJ + 15) >> 4;
         const int XW = UP ? d.w_out + K - 1 : S * (d.w_out - 1) + K;   // virtual input columns
         const int nxs = (XW + 3) >> 2;
         for (int mb = 0; mb < nmb; ++mb) {
@@ -1032,26 +1092,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 
                 if (two) rows(BoolC<true>{});
                 else rows(BoolC<false>{});
                 const f32x4 acc[2] = {acc0, acc1};
-                // fixed-order sum of the four waves' partial tiles, one column block at a time
-                // (1024 floats of scratch)
+                // each wave stores its partial tile into its own slab row (lane (kq, l16) holds rows
+                // 4 kq + r, column l16 of the 16 x 16 block); the slab reduction sums the rows
 #pragma unroll
                 for (int u = 0; u < 2; ++u) {
                     if (u == 1 && !two) break;
-                    if (u == 1) __syncthreads();
+                    const int j2 = 16 * (nb0 + u) + l16;
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) red[(wv * 4 + r) * 64 + lane] = acc[u][r];
-                    __syncthreads();
-                    const int r = tid >> 6, ln = tid & 63;
-                    const int i2 = 16 * mb + (ln >> 4) * 4 + r;
-                    const int j2 = 16 * (nb0 + u) + (ln & 15);
-                    if (i2 < MI && j2 < NJ) {
-                        const float v = red[(0 * 4 + r) * 64 + ln] + red[(1 * 4 + r) * 64 + ln] +
-                                        red[(2 * 4 + r) * 64 + ln] + red[(3 * 4 + r) * 64 + ln];
-                        const int co2 = i2 / K, kx2 = i2 - co2 * K, ci2 = j2 / K, ky2 = j2 - ci2 * K;
-                        slab[co2 * J + ci2 * KK + ky2 * K + kx2] = v;
+                    for (int r = 0; r < 4; ++r) {
+                        const int i2 = 16 * mb + 4 * kq + r;
+                        if (i2 < MI && j2 < NJ) {
+                            const int co2 = i2 / K, kx2 = i2 - co2 * K, ci2 = j2 / K, ky2 = j2 - ci2 * K;
+                            slab[co2 * J + ci2 * KK + ky2 * K + kx2] = acc[u][r];
+                        }
                     }
                 }
-                __syncthreads();
             }
         }
     }
@@ -1252,19 +1307,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 
         else vdg_rows(IntC<4>{});
     }
     PHASE(6);
-    if (d.in_bn) {
+    if (d.in_bn && dg_role) {
+        __syncthreads();          // red aliases the offset table the input-gradient loop read
         if (vdg) {
-            // per-thread channel sums: wave sums, then the four waves in a fixed order below
+            // per-thread channel sums: wave sums -> this wave's slab row (dgamma / dbeta partials) and LDS
 #pragma unroll
             for (int ci = 0; ci < 4; ++ci) {
                 const float a = wave_sum(vsd[ci]), b = wave_sum(vsdx[ci]);
                 if (lane == 0 && ci < d.cin) {
                     red[wv * 32 + ci] = a;
                     red[128 + wv * 32 + ci] = b;
+                    slab[d.cout * J + ci] = b;
+                    slab[d.cout * J + d.cin + ci] = a;
                 }
             }
         } else {
-            // lanes 16 apart share a channel: fold them, then the four waves in a fixed order
+            // lanes 16 apart share a channel: fold them
             sd += __shfl_xor(sd, 16, 64);
             sdx += __shfl_xor(sdx, 16, 64);
             sd += __shfl_xor(sd, 32, 64);
@@ -1272,18 +1330,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 
             if (kq == 0) {
                 red[wv * 32 + l16] = sd;
                 red[128 + wv * 32 + l16] = sdx;
+                if (cok) {
+                    slab[d.cout * J + l16] = sdx;             // dgamma partial of this wave
+                    slab[d.cout * J + d.cin + l16] = sd;      // dbeta partial
+                }
             }
         }
         __syncthreads();
         if (tid < d.cin) {
+            // the four waves in a fixed order: the BN-backward sums of the input statistics
             double s_d = 0.0, s_dx = 0.0;
 #pragma unroll
             for (int w = 0; w < 4; ++w) {
                 s_d += (double)red[w * 32 + tid];
                 s_dx += (double)red[128 + w * 32 + tid];
             }
-            slab[d.cout * J + tid] = (float)s_dx;            // dgamma
-            slab[d.cout * J + d.cin + tid] = (float)s_d;     // dbeta
             gpi_stat* st = stat_slot(c, d.in_stat + tid, T.grp);
             const double gm = i_gam[tid];
             if (!SKIP(G, 4)) {
@@ -1304,9 +1365,10 @@ size_t fwd_lds(const gpi_conv_desc& d, const ConvGeom& G, int cp) {
 size_t bwd_lds(const gpi_conv_desc& d, const ConvGeom& G) {
     const int KD4 = (d.cout * d.k * d.k + 3) & ~3;
     const int gimg = img_floats(d.cout, G.gh, G.PG);
-    const bool alias = d.gout_mode == 0 && gimg >= BWD_RED;   // red inside gz (conv_bwd_kernel)
-    size_t f = (size_t)pad256(BWD_HDR) + (d.gin_off >= 0 ? pad256(KD4 * 16) + pad256((d.stride == 2 ? 8 : 1) * KD4) : 0) + gimg +
-               (d.gout_mode == 0 ? gimg : 0) + img_floats(d.cin, G.rh, G.P) + (alias ? 0 : BWD_RED);
+    const bool zimg = d.gout_mode == 0 && !G.zreg;             // z image in LDS
+    // offset table, at least BWD_RED floats: the channel-sum scratch aliases it
+    size_t f = (size_t)bwd_hdr(d.cin, d.cout) + (d.gin_off >= 0 ? pad256(KD4 * 16) + pad256((d.stride == 2 ? 8 : 1) * KD4) : 0) + gimg +
+               (zimg ? gimg : 0) + img_floats(d.cin, G.rh, G.P);
     return f * sizeof(float);
 }
 
@@ -1377,6 +1439,14 @@ int launch(const gpi_conv_desc& d, const gpi_codec_ctx& c, hipStream_t st, bool 
     G.zero = zero;
     const size_t lds = fwd ? fwd_lds(d, G, cp) : bwd_lds(d, G);
     if (lds > 160 * 1024) return GPI_ERR_UNSUPPORTED;
+    if (!fwd && d.gin_off >= 0) {
+        // resident workgroups per CU: LDS (~160 KB less a per-workgroup reserve, tools/bench_dispatch.hip)
+        // and the kernels' occupancy (6 waves per SIMD, 4 for the 5x5 kernel)
+        static const int split_env = env_int("GPI_BWD_SPLIT", 1);
+        const int per_cu = std::min((int)(160000 / std::max<size_t>(lds, 1)), d.k == 5 ? 4 : 6);
+        G.split = (split_env && 2 * G.nblocks <= per_cu * 256) ? 1 : 0;
+    }
+    const int grid = G.nblocks * (G.split ? 2 : 1);
 #ifdef GPI_PHASE_TIMING
     static const int dbg_print = env_int("GPI_DBG_PRINT", 0);
     if (dbg_print)
@@ -1388,7 +1458,7 @@ int launch(const gpi_conv_desc& d, const gpi_codec_ctx& c, hipStream_t st, bool 
         if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
             return GPI_ERR_LAUNCH;
     }
-    hipLaunchKernelGGL(k, dim3(G.nblocks), dim3(256), lds, st, d, c, G);
+    hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds, st, d, c, G);
     GPI_CHECK_LAUNCH();
     return GPI_OK;
 }
@@ -1505,8 +1575,8 @@ extern "C" int gpi_debug_phase_stamps(unsigned long long* phase, unsigned long l
 extern "C" int gpi_conv_blocks(const gpi_conv_desc* op, const gpi_groups* groups, int32_t* blocks) {
     if (!op || !groups || !blocks) return GPI_ERR_ARG;
     ConvGeom G;
-    if (!conv_geom(*op, *groups, G, false)) return GPI_ERR_UNSUPPORTED;   // backward tiling = slab rows
-    *blocks = G.nblocks;
+    if (!conv_geom(*op, *groups, G, false)) return GPI_ERR_UNSUPPORTED;   // backward tiling
+    *blocks = G.nblocks * SLAB_ROWS;                                       // one slab row per wave
     return GPI_OK;
 }
 

@@ -326,6 +326,8 @@ class ElboEngine(object):
             self.dctx.loss_scale[gi] = scale
         # ---- gradient reductions
         self.reduce_enc = self.ep.reduce_items(offE) if self.ep is not None else []
+        # slab-reduction items of the encoder's input conv (the first op; no input BN: one item)
+        self.n_reduce_in = (2 if self.ep.ops[0].bn is not None else 1) if self.ep is not None else 0
         self.reduce_dec = self.dp.reduce_items(offD)
         self.reduce_items = self.reduce_enc + self.reduce_dec
         gi = []
@@ -495,6 +497,7 @@ class ElboEngine(object):
             self._side = torch.cuda.Stream(device=torch.cuda.current_stream().device)
             self._ev_fork, self._ev_join = torch.cuda.Event(), torch.cuda.Event()
             self._ev_fork2, self._ev_join2 = torch.cuda.Event(), torch.cuda.Event()
+            self._ev_enc = torch.cuda.Event()
         return self._side
 
     def _join(self):
@@ -585,10 +588,16 @@ class ElboEngine(object):
         # done by now: run them on the side stream, concurrently with the encoder backward
         # (enqueued after it, so the encoder stays on the main chain's queue in a graph)
         self._ev_fork2.record(main)
-        if self.ep is not None:
-            _run(lib.gpi_codec_backward, self.enc_descs, len(self.enc_descs), C.byref(self.ectx), st,
-                 what='encoder backward')
-            run_reduce(self.reduce_enc, self.ws, self.flat, st)
+        n_enc = len(self.enc_descs) if self.ep is not None else 0
+        if n_enc:
+            # every encoder conv but the first (reverse order) ...
+            rest = C.cast(C.byref(self.enc_descs, C.sizeof(L.ConvDesc)), C.POINTER(L.ConvDesc))
+            _run(lib.gpi_codec_backward, rest, n_enc - 1, C.byref(self.ectx), st, what='encoder backward')
+            self._ev_enc.record(main)
+            # ... then the input conv (weight gradient only), whose slab reduction stays on the main
+            # stream while the side stream reduces the other encoder slabs concurrently
+            _run(lib.gpi_conv_backward, C.byref(self.enc_descs[0]), C.byref(self.ectx), st, what='In_conv backward')
+            run_reduce(self.reduce_enc[:self.n_reduce_in], self.ws, self.flat, st)
         side.wait_event(self._ev_fork2)
         sst = C.c_void_p(side.cuda_stream)
         if split:
@@ -604,6 +613,9 @@ class ElboEngine(object):
              C.c_void_p(self.flat.gacc.data_ptr()), sst, what='outer gemm')
         if side_extra is not None:
             side_extra(sst)
+        if n_enc:
+            side.wait_event(self._ev_enc)
+            run_reduce(self.reduce_enc[self.n_reduce_in:], self.ws, self.flat, sst)
         self._ev_join2.record(side)
         main.wait_event(self._ev_join2)
 

@@ -416,7 +416,7 @@ typedef struct gpi_bn_running_item {
 int gpi_bn_running_update(const gpi_bn_running_item* items, int n_items, int max_channels, const gpi_stat* stats,
                           int64_t n_stats, float momentum, void* stream);
 
-/* Number of workgroups (= partial-slab rows) a conv backward launch uses. */
+/* Partial-slab rows a conv backward launch writes: 4 per workgroup (one per wave). */
 int gpi_conv_blocks(const gpi_conv_desc* op, const gpi_groups* groups, int32_t* blocks);
 /* Launch geometry of one conv pass (fwd != 0: forward) for tuning / profiling tools:
  * info[0] output rows per tile, info[1] workgroups, info[2] LDS bytes per workgroup,

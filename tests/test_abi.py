@@ -59,7 +59,7 @@ def test_conv_blocks_host_query(lib):
     g.start[0], g.start[1] = 0, 288
     nb = C.c_int32()
     assert L.gpi_conv_blocks(C.byref(d), C.byref(g), C.byref(nb)) == 0
-    assert nb.value == 288 * 4          # full-width tiles of 8 rows on a 32 x 32 plane
+    assert nb.value == 288 * 4 * 4      # full-width tiles of 8 rows on a 32 x 32 plane, one slab row per wave
     d.k = 4                             # unsupported kernel size -> error code, no crash
     assert L.gpi_conv_blocks(C.byref(d), C.byref(g), C.byref(nb)) != 0
 
