@@ -1444,7 +1444,8 @@ int launch(const gpi_conv_desc& d, const gpi_codec_ctx& c, hipStream_t st, bool 
         // and the kernels' occupancy (6 waves per SIMD, 4 for the 5x5 kernel)
         static const int split_env = env_int("GPI_BWD_SPLIT", 1);
         const int per_cu = std::min((int)(160000 / std::max<size_t>(lds, 1)), d.k == 5 ? 4 : 6);
-        G.split = (split_env && 2 * G.nblocks <= per_cu * 256) ? 1 : 0;
+        // split only well under one round: 2 x 576 workgroups measured slower than 576 (r02 A/B)
+        G.split = (split_env && 2 * G.nblocks <= std::min(per_cu, 4) * 256) ? 1 : 0;
     }
     const int grid = G.nblocks * (G.split ? 2 : 1);
 #ifdef GPI_PHASE_TIMING
