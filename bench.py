@@ -336,8 +336,11 @@ def main():
     log('data ready')
     Xu, Xs, Y, F = data
     # shared subset seed: every rank draws the same global permutation and takes its slice
+    # N > 1 over RCCL: the all-reduce is a node of the step's graph (GPI_GRAPH_ALLREDUCE=0: host-side
+    # between two graphs, as with gloo)
     step = FusedElboStep(model, Xu, B_u, Xs, Y, F, lr=1e-2, seed=4321 + rank, subset_seed=777,
-                         distributed=distributed, rank=rank, world=world)
+                         distributed=distributed, rank=rank, world=world,
+                         graph_allreduce=os.environ.get('GPI_GRAPH_ALLREDUCE', '1') == '1')
     if not args.no_graph:
         step.capture()
     log('captured; warm-up')

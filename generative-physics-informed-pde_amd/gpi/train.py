@@ -49,7 +49,8 @@ class FusedElboStep(object):
     reparametrisation noise uses ``seed`` (per rank)."""
 
     def __init__(self, model, X_pool, B_u, X_s=None, Y=None, F=None, lr=1e-2, betas=(0.9, 0.999), eps=1e-8,
-                 seed=0, normalize=False, process_group=None, distributed=False, rank=0, world=1, subset_seed=None):
+                 seed=0, normalize=False, process_group=None, distributed=False, rank=0, world=1, subset_seed=None,
+                 graph_allreduce=True):
         self.model = model
         self.flat = model.native_flat()
         self.N_s = 0 if X_s is None else int(X_s.shape[0])
@@ -74,6 +75,9 @@ class FusedElboStep(object):
         self.subset_seed = int(seed if subset_seed is None else subset_seed)
         self.distributed = distributed
         self.pg = process_group
+        # RCCL all-reduce captured inside the step's graph (one replay per step, no host hop between
+        # the gradient and the update); host-side between two graphs for gloo
+        self.graph_allreduce = bool(graph_allreduce)
         self.adam = L.AdamDesc(p=self.flat.P.data_ptr(), g=self.flat.G.data_ptr(), m=self.m.data_ptr(),
                                v=self.v.data_ptr(), n=self.flat.numel, lr=self.lr.data_ptr(),
                                step=self.step_ctr.data_ptr(), beta1=betas[0], beta2=betas[1], eps=eps)
@@ -180,7 +184,9 @@ class FusedElboStep(object):
         torch.cuda.synchronize()
         self.g_fb = torch.cuda.CUDAGraph()
         self.g_up = None
-        if self.distributed:
+        self.split_graph = self.distributed and not (self.graph_allreduce and
+                                                      dist.get_backend(self.pg) == dist.Backend.NCCL)
+        if self.split_graph:
             with torch.cuda.graph(self.g_fb):
                 self.forward_backward()
             self.g_up = torch.cuda.CUDAGraph()
@@ -189,6 +195,7 @@ class FusedElboStep(object):
         else:
             with torch.cuda.graph(self.g_fb):
                 self.forward_backward()
+                self.allreduce()        # RCCL: captured as a graph node
                 self.update()
         self.graph = True
 
@@ -197,7 +204,7 @@ class FusedElboStep(object):
         if self.graph is None:
             return self.step_eager()
         self.g_fb.replay()
-        if self.distributed:
+        if self.split_graph:
             self.allreduce()
             self.g_up.replay()
 

@@ -76,3 +76,17 @@ def test_dp_two_ranks_native_step(device, tmp_path):
     # replicated shared parameters stay identical after the update
     assert np.array_equal(rk[0]['P1'][:ns], rk[1]['P1'][:ns])
     assert np.array_equal(rk[0]['P0'][:ns], rk[1]['P0'][:ns])
+
+
+def test_rccl_allreduce_captured_in_step_graph(device):
+    """The RCCL (backend 'nccl') all-reduce of the shared gradients captured inside the fused step's
+    HIP graph: replays equal eager steps bit for bit (world size 1 on this one-GPU box; the driver's
+    8-GPU node runs the same capture across ranks)."""
+    env = dict(os.environ)
+    env['PYTHONUNBUFFERED'] = '1'
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node=1',
+           '--master-addr=127.0.0.1', '--master-port=%d' % _free_port(),
+           os.path.join(os.path.dirname(HERE), 'tools', 'dist_capture_probe.py')]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert 'max |dP| = 0.000e+00' in r.stdout, r.stdout[-2000:]
