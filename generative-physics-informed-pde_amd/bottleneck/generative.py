@@ -181,7 +181,7 @@ class GenerativeModel(lamp.modules.BaseModule):
     def _elbo_engine(self, B_u, N_s, normalize, N_vo=0, vo_holdoff=False, q_unsup=None):
         flat = self.native_flat()
         return engine_for(self, ('elbo', B_u, N_s, N_vo, bool(vo_holdoff), bool(normalize), id(flat),
-                                 q_unsup is not None),
+                                 q_unsup is not None, bool(self.config['reconstruct_log_eff_property'])),
                           lambda: ElboEngine(self, B_u, N_s, normalize=normalize, N_vo=N_vo, vo_holdoff=vo_holdoff,
                                              q_unsup=q_unsup))
 
@@ -293,9 +293,6 @@ class GenerativeModel(lamp.modules.BaseModule):
         assert not (armortized_bs is not None and self.encoder is None)
         if l1_penalty is not None:
             raise NotImplementedError
-        if not self.config['reconstruct_log_eff_property']:
-            # the native decoder loss is the log-property Gaussian (generative.py:236-237, the default)
-            raise NotImplementedError('reconstruct_log_eff_property=False is not on the native path')
         N_vo = 0
         X_vo = F_vo = None
         if self._datasets.get('vo') and not disable_vo and not self.disable_elbo_vo:

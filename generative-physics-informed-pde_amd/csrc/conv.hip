@@ -550,7 +550,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void c
         const int oy = T.oy0 + ty, ox = tx;
         const bool active = pix < tp;
         float tgt = 0.f;
-        if (d.epilogue == GPI_EPI_GAUSS_LOSS && active) {
+        const bool gauss = d.epilogue == GPI_EPI_GAUSS_LOSS || d.epilogue == GPI_EPI_GAUSS_EXP_LOSS;
+        if (gauss && active) {
             int row = T.b - c.groups.start[T.grp];
             if (c.tgt_idx[T.grp]) row = c.tgt_idx[T.grp][row];
             tgt = c.tgt[T.grp][(int64_t)row * HWo + oy * d.w_out + ox];
@@ -582,15 +583,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void c
             for (int co = 0; co < CP; ++co)
                 if (co < d.cout) acc[co] *= dsl[co];
         }
-        if (d.epilogue == GPI_EPI_GAUSS_LOSS) {
+        if (gauss) {
             if (active) {
                 const float mu = acc[0], ls = acc[1];
                 const float e = expf(-2.f * ls);
-                const float r = tgt - mu;
+                // log-property Gaussian (default) or the exponentiated field's (d mean: chain factor exp(mu))
+                const bool ex = d.epilogue == GPI_EPI_GAUSS_EXP_LOSS;
+                const float emu = ex ? expf(mu) : 1.f;
+                const float r = ex ? expf(tgt) - emu : tgt - mu;
                 Lv += -0.5f * (2.f * ls + r * r * e + GPI_LOG2PI);
                 const float scl = c.loss_scale[T.grp];
                 auto go = as_gst(ws + d.gout_off + (int64_t)T.b * 2 * HWo + oy * d.w_out + ox);
-                go[0] = -scl * r * e;
+                go[0] = -scl * r * e * emu;
                 go[HWo] = scl * (1.f - r * r * e);
                 if (d.out_off >= 0) {
                     auto o = as_gst(ws + d.out_off + (int64_t)T.b * d.out_ctot * HWo + (int64_t)d.out_c0 * HWo +
@@ -617,7 +621,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void c
         }
     }
 
-    if (d.epilogue == GPI_EPI_GAUSS_LOSS) {
+    if (d.epilogue == GPI_EPI_GAUSS_LOSS || d.epilogue == GPI_EPI_GAUSS_EXP_LOSS) {
         float v[1] = {Lv};
         block_sum<1>(v, scratch, red);
         __syncthreads();
@@ -1422,7 +1426,7 @@ bool aligned_ok(const gpi_conv_desc& d, const gpi_codec_ctx& c, bool fwd) {
 int launch(const gpi_conv_desc& d, const gpi_codec_ctx& c, hipStream_t st, bool fwd) {
     ConvGeom G;
     if (!conv_geom(d, c.groups, G, fwd)) return GPI_ERR_UNSUPPORTED;
-    if (d.epilogue == GPI_EPI_GAUSS_LOSS && d.cout != 2) return GPI_ERR_ARG;
+    if ((d.epilogue == GPI_EPI_GAUSS_LOSS || d.epilogue == GPI_EPI_GAUSS_EXP_LOSS) && d.cout != 2) return GPI_ERR_ARG;
     if (d.in_off < 0 && !c.ext_in) return GPI_ERR_ARG;
     if (!aligned_ok(d, c, fwd)) return GPI_ERR_UNSUPPORTED;
     if (!fwd && d.gin_off >= 0 && ((G.ph * d.w_in) & 15)) return GPI_ERR_UNSUPPORTED;

@@ -25,7 +25,7 @@ GPI_REPLICAS = 16
 FINALIZE_ACCUMULATE = 1
 FINALIZE_ZERO = 2
 
-EPI_STORE, EPI_STORE_STATS, EPI_GAUSS_LOSS = 0, 1, 2
+EPI_STORE, EPI_STORE_STATS, EPI_GAUSS_LOSS, EPI_GAUSS_EXP_LOSS = 0, 1, 2, 3
 HEAD_ENC, HEAD_REPARAM, HEAD_QZ, HEAD_LATENT, HEAD_GP, HEAD_LOCKX = 0x01, 0x02, 0x04, 0x08, 0x10, 0x20
 HEAD_PART_ENC, HEAD_PART_Q = 0x100, 0x200
 ROM_FORWARD, ROM_LOGLIK, ROM_BACKWARD = 0, 1, 2

@@ -239,7 +239,10 @@ class ElboEngine(object):
             d_feat = 1
         # ---- decoder program (groups: unsup, sup, vo)
         dc = dec.native_config()
-        self.dp = decoder_program(final_epilogue=L.EPI_GAUSS_LOSS, **dc)
+        # the decoder likelihood of generative.py:232-239: log-property Gaussian (default) or the
+        # exponentiated field's (reconstruct_log_eff_property = False)
+        log_field = getattr(model, 'config', {}).get('reconstruct_log_eff_property', True)
+        self.dp = decoder_program(final_epilogue=L.EPI_GAUSS_LOSS if log_field else L.EPI_GAUSS_EXP_LOSS, **dc)
         self.dec_sizes = [n for n in (self.B_u, self.N_s, self.N_vo) if n > 0]
         self.g_sup = (1 if self.B_u > 0 else 0) if self.N_s > 0 else None
         self.g_vo = ((self.B_u > 0) + (self.N_s > 0)) if self.N_vo > 0 else None

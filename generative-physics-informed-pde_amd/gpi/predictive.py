@@ -83,8 +83,9 @@ def predictive_scores(Y, mean, std):
 class _EngineModel(object):
     """The attributes ElboEngine reads from a GenerativeModel."""
 
-    def __init__(self, f, gp, g, q_z, flat):
+    def __init__(self, f, gp, g, q_z, flat, config):
         self.f, self.gp, self.g = f, gp, g
+        self.config = dict(config)       # decoder likelihood choice (components.py:361)
         self.encoder = None
         self.q_z = {'vo': q_z}
         self.q_X = {'vo': None}
@@ -109,7 +110,7 @@ class PredictionEnsembleEngine(object):
         self.q_off = min(self.flat.offset(q_z._mean), self.flat.offset(q_z._logsigma))
         self.q_n = self.flat.numel - self.q_off
         assert self.q_off == self.n_dec and self.q_n == 2 * q_z._mean.numel()
-        em = _EngineModel(self.shadow, model.gp, model.g, q_z, self.flat)
+        em = _EngineModel(self.shadow, model.gp, model.g, q_z, self.flat, getattr(model, 'config', {}))
         # the PE's decoder calls are the model's decoder's in the reference (components.py:371): its BN
         # running statistics are model.f's
         self.engine = ElboEngine(em, 0, 0, N_vo=self.N, vo_holdoff=True, running_modules={'dec': model.f})

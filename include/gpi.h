@@ -49,6 +49,8 @@ extern "C" {
 #define GPI_EPI_STORE 0        /* store raw output */
 #define GPI_EPI_STORE_STATS 1  /* store raw output + per-channel fp64 sum / sum^2 (train-mode BN) */
 #define GPI_EPI_GAUSS_LOSS 2   /* cout == 2: (mean, logsigma) -> Gaussian log-lik vs target, writes d(-elbo)/d(out) */
+#define GPI_EPI_GAUSS_EXP_LOSS 3  /* as GAUSS_LOSS on the exponentiated field: N(exp(target); exp(mean), sigma^2)
+                                     (generative.py:238-239, reconstruct_log_eff_property = False) */
 
 /* Per-channel BatchNorm statistics record, one per (channel, group). */
 typedef struct gpi_stat {

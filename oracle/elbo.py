@@ -19,6 +19,14 @@ def dgll(target, mean, logvars):
     return torch.sum(-0.5 * (logvars + ((target - mean) / sigma) ** 2 + LOG2PI))
 
 
+def field_loglik(X, mx, lsx, log_field=True):
+    """GenerativeModel.random_field_likelihood (generative.py:232-239): Gaussian on the log-property
+    (reconstruct_log_eff_property=True, the default) or on the exponentiated field."""
+    if log_field:
+        return dgll(X, mx, 2 * lsx)
+    return dgll(torch.exp(X), torch.exp(mx), 2 * lsx)
+
+
 def kl_unit(mean, logvars):
     """UnitGaussianKullbackLeiblerDivergence (bottleneck/utils.py:246-248)."""
     return -0.5 * torch.sum(1 + logvars - mean.pow(2) - logvars.exp())
@@ -55,17 +63,17 @@ def rom_operator(W, M, bc_dofs, effprop, F, logsigmas_y):
     return mu, logsigmas_y.repeat(effprop.shape[0], 1)
 
 
-def elbo_unsupervised_armortized(encoder, decoder, X, eps):
+def elbo_unsupervised_armortized(encoder, decoder, X, eps, log_field=True):
     """generative.py:546-585 (normalize=False)."""
     mean, logsigma = encoder(X)
     Z = reparam(mean, logsigma, eps)
     mx, lsx = decoder(Z)
-    logL_x = dgll(X, mx, 2 * lsx)
+    logL_x = field_loglik(X, mx, lsx, log_field)
     DKL = kl_unit(mean, 2 * logsigma)
     return logL_x - DKL, dict(logL_x=logL_x, DKL=DKL)
 
 
-def elbo_supervised_freeX(decoder, gp_linear, logsigmas_X_gp, rom, qz, qX, X, Y, F, eps_z, eps_X):
+def elbo_supervised_freeX(decoder, gp_linear, logsigmas_X_gp, rom, qz, qX, X, Y, F, eps_z, eps_X, log_field=True):
     """generative.py:461-500 with independent_X=True.
 
     qz / qX : (mean, logsigma) parameter pairs [N, d]
@@ -75,7 +83,7 @@ def elbo_supervised_freeX(decoder, gp_linear, logsigmas_X_gp, rom, qz, qX, X, Y,
     Z = reparam(qz[0], qz[1], eps_z)
     Xs = reparam(qX[0], qX[1], eps_X)
     mx, lsx = decoder(Z)
-    logL_x = dgll(X, mx, 2 * lsx)
+    logL_x = field_loglik(X, mx, lsx, log_field)
     mu_X = gp_linear(Z)
     logL_X = dgll(Xs, mu_X, 2 * logsigmas_X_gp.expand(Z.shape[0], -1))
     mu_y, ls_y = rom(Xs, F)

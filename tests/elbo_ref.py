@@ -37,11 +37,11 @@ def state_of(d, dtype=torch.float64):
 
 
 def oracle_elbo(st, Xu, Xs, Y, F, eps_enc, eps_qz, eps_qX, nc, r, normalize=False, l2_penalty=None, masks=None,
-                drops=None):
+                drops=None, log_field=True):
     """ELBO of the armortized + supervised-freeX model in fp64 from the parameter dict ``st``
     (reference state_dict names) and fully injected inputs / noise; returns the 0-d ELBO (backward
     fills st[*].grad).  masks: optional {'enc', 'dec_u', 'dec_s'} ReLU decisions of the kernels
-    under test (oracle/codec.py, tests/gpu_masks.py).  drops: optional Dropout2d channel scales
+    under test (oracle/codec.py, tests/gpu_masks.py).  log_field: reconstruct_log_eff_property.  drops: optional Dropout2d channel scales
     {'enc': {conv: [B_u, C]}, 'dec': {conv: [B_u + N_s, C]}} (decoder rows: unlabeled, then labeled)."""
     mk = masks or {}
     dr = drops or {}
@@ -61,12 +61,12 @@ def oracle_elbo(st, Xu, Xs, Y, F, eps_enc, eps_qz, eps_qX, nc, r, normalize=Fals
                                              dr_u)
     dec = lambda z: ocodec.decoder_forward(dec_p, z, 8, cfg['blocks'], cfg['growth'], cfg['f0'], mk.get('dec_s'),
                                            dr_s)
-    e1, _ = oelbo.elbo_unsupervised_armortized(enc, dec_u, t(Xu), t(eps_enc))
+    e1, _ = oelbo.elbo_unsupervised_armortized(enc, dec_u, t(Xu), t(eps_enc), log_field)
     gp = lambda z: torch.nn.functional.linear(z, st['gp.fc.weight'], st['gp.fc.bias'])
     rom = lambda x, Fm: oelbo.rom_operator(W, M, bc, x, Fm, st['g.logsigmas_y'])
     e2, _ = oelbo.elbo_supervised_freeX(
         dec, gp, st['gp.logsigmas_X'], rom, (st['q_z.supervised._mean'], st['q_z.supervised._logsigma']),
-        (st['q_X.supervised._mean'], st['q_X.supervised._logsigma']), t(Xs), t(Y), t(F), t(eps_qz), t(eps_qX))
+        (st['q_X.supervised._mean'], st['q_X.supervised._logsigma']), t(Xs), t(Y), t(F), t(eps_qz), t(eps_qX), log_field)
     if normalize:        # every term divided by its own batch size (generative.py:493-499,571-574)
         e1 = e1 / len(Xu)
         e2 = e2 / len(Xs)

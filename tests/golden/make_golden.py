@@ -439,8 +439,8 @@ def make_bn_running_c32():
 
 def make_elbo_options_c32():
     """model.elbo(normalize=True) and model.elbo(l2_penalty=...) (generative.py:247-287: every term
-    divided by its batch size; minus l2_penalty * sum of the parameter norms of f and the encoder)
-    at the C32 shape of elbo_c32 -> elbo_opts_c32.npz."""
+    divided by its batch size; minus l2_penalty * sum of the parameter norms of f and the encoder),
+    and model.elbo() with reconstruct_log_eff_property=False ('expf') at the C32 shape of elbo_c32 -> elbo_opts_c32.npz."""
     phys = c32_physics()
     nc, r, mc, mf, M, W, cdofs, fdofs = phys
     n = nc * r
@@ -471,8 +471,10 @@ def make_elbo_options_c32():
         def add_scalar(self, k, v, global_step=None):
             pass
 
-    for tag, kw in (('norm', dict(normalize=True)), ('l2', dict(l2_penalty=0.05))):
+    for tag, kw in (('norm', dict(normalize=True)), ('l2', dict(l2_penalty=0.05)), ('expf', dict())):
         model.writer = _Writer() if tag == 'l2' else None
+        if tag == 'expf':            # Gaussian on the exponentiated field (generative.py:236-239)
+            model.set('reconstruct_log_eff_property', False)
         elbo, gr = _elbo_run(model, perm, eps, armortized_bs=bs, **kw)
         out.update({'%s.grad.%s' % (tag, k): v for k, v in gr.items()})
         out['%s.elbo' % tag] = np.float64(elbo.item())

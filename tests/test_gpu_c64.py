@@ -216,20 +216,23 @@ def test_fused_step_c64(device, droprate):
 
 
 # ---------------------------------------------------------------- elbo(normalize=True), elbo(l2_penalty=...)
-@pytest.mark.parametrize('opt', ['norm', 'l2'])
+@pytest.mark.parametrize('opt', ['norm', 'l2', 'expf'])
 def test_elbo_options(device, opt):
     """normalize=True (every term / its batch size) and l2_penalty (minus penalty * sum of parameter
-    norms of f and the encoder), generative.py:247-287, vs the reference run and the fp64 oracle."""
+    norms of f and the encoder), generative.py:247-287, and reconstruct_log_eff_property=False (the
+    decoder's Gaussian on exp(x), generative.py:236-239), vs the reference run and the fp64 oracle."""
     import sys
     sys.path.insert(0, __file__.rsplit('/', 1)[0])
     from test_gpu_parity import build_golden_model
     d = load('elbo_opts_c32.npz')
     model, bs = build_golden_model(d)
+    if opt == 'expf':        # Gaussian on the exponentiated field: the EPI_GAUSS_EXP_LOSS epilogue
+        model.set('reconstruct_log_eff_property', False)
     eps = (torch.cat([cuda(d['eps_enc']), cuda(d['eps_qz'])]), cuda(d['eps_qX']))
-    kw = dict(normalize=True) if opt == 'norm' else dict(l2_penalty=float(d['l2_penalty']))
+    kw = {'norm': dict(normalize=True), 'l2': dict(l2_penalty=float(d['l2_penalty'])), 'expf': {}}[opt]
     elbo = model.elbo(step=0, armortized_bs=bs, eps=eps, **kw)
     (-elbo).backward()
-    val_o, gr_o = oracle_fixture_elbo(d, **kw)
+    val_o, gr_o = oracle_fixture_elbo(d, log_field=opt != 'expf', **kw)
     assert abs(elbo.item() - val_o) <= 1e-5 * abs(val_o), (elbo.item(), val_o)
     assert abs(elbo.item() - float(d[opt + '.elbo'])) <= 2e-5 * abs(val_o)
     errs = {k: tensor_rel(p.grad.cpu(), gr_o[k]) for k, p in model.named_parameters()}

@@ -328,13 +328,14 @@ def test_elbo_c64():
     print(check_grads({k: tensor_rel(g, d['grad.' + k]) for k, g in gr.items()}))
 
 
-@pytest.mark.parametrize('opt', ['norm', 'l2'])
+@pytest.mark.parametrize('opt', ['norm', 'l2', 'expf'])
 def test_elbo_options(opt):
-    """elbo(normalize=True) and elbo(l2_penalty=0.05) (generative.py:247-287) vs the reference run."""
+    """elbo(normalize=True), elbo(l2_penalty=0.05) (generative.py:247-287) and the exponentiated-field
+    likelihood (reconstruct_log_eff_property=False, generative.py:236-239) vs the reference run."""
     from elbo_ref import oracle_fixture_elbo, tensor_rel
     d = load('elbo_opts_c32.npz')
-    kw = dict(normalize=True) if opt == 'norm' else dict(l2_penalty=float(d['l2_penalty']))
-    val, gr = oracle_fixture_elbo(d, **kw)
+    kw = {'norm': dict(normalize=True), 'l2': dict(l2_penalty=float(d['l2_penalty'])), 'expf': {}}[opt]
+    val, gr = oracle_fixture_elbo(d, log_field=opt != 'expf', **kw)
     assert abs(val - float(d[opt + '.elbo'])) <= 1e-5 * abs(float(d[opt + '.elbo']))
     bad = {k: e for k, e in ((k, tensor_rel(g, d[opt + '.grad.' + k])) for k, g in gr.items()) if e >= 2e-3}
     assert not bad, bad
