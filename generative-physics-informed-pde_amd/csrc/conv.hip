@@ -85,6 +85,7 @@ struct ConvGeom {
     int ph;         // owned input rows (backward)
     const float* zero;   // the zero page (kernel argument: no per-use address reload)
     int zreg;       // backward: the BN-backward operand z of the output in registers (<= ZREG chunks / thread)
+    int npx;        // forward: horizontally adjacent output pixels per thread (1, 2, 4)
     int split;      // backward: 2 workgroups per tile, input gradient (blockIdx < nblocks) and weight gradient
                     // (the rest) in parallel on otherwise idle CUs (launches well under one round)
     int in_sq, in_sr, in_sc;   // 256 chunks of the input image = (planes, rows, chunks)
@@ -142,7 +143,7 @@ int env_int(const char* name, int dflt) {
     return v && *v ? atoi(v) : dflt;
 }
 
-bool conv_geom(const gpi_conv_desc& d, const gpi_groups& g, ConvGeom& G, bool fwd) {
+bool conv_geom(const gpi_conv_desc& d, const gpi_groups& g, ConvGeom& G, bool fwd, bool fuse = false) {
     if (g.n_groups < 1 || g.n_groups > GPI_MAX_GROUPS) return false;
     if (d.cin < 1 || d.cin > GPI_MAX_CIN || d.cout < 1 || d.cout > GPI_MAX_COUT) return false;
     if (d.k != 1 && d.k != 3 && d.k != 5 && d.k != 7) return false;
@@ -170,12 +171,16 @@ bool conv_geom(const gpi_conv_desc& d, const gpi_groups& g, ConvGeom& G, bool fw
                      t_bwd = env_int("GPI_TILE_BWD", 512), t_s2 = env_int("GPI_TILE_S2", 128),
                      t_s2brows = env_int("GPI_TILE_S2BROWS", 4), t_s2c1 = env_int("GPI_TILE_S2C1", 256),
                      t_bwdup = env_int("GPI_TILE_BWDUP", 1024), t_bwdrows = env_int("GPI_TILE_BWDROWS", 8),
-                     t_fwdrows = env_int("GPI_TILE_FWDROWS", 8);
+                     t_fwdrows = env_int("GPI_TILE_FWDROWS", 8), t_fuse = env_int("GPI_TILE_FUSE", 1024);
     const int target = d.stride == 2 ? (d.cin == 1 ? t_s2c1 : (fwd ? t_s2 : t_s2brows * d.w_out))
                                      : (fwd ? (d.w_out >= 64 ? t_fwd64 : (d.w_out >= 32 ? t_fwdrows * d.w_out : t_fwd))
                                             : (d.upsample && d.w_out >= 32 ? t_bwdup / 64 * min(d.w_out, 64)
                                                                             : (d.w_out >= 64 ? t_bwd : t_bwdrows * d.w_out)));
-    G.th = target / d.w_out;
+    // the backward of the loss-epilogue output conv (fused with its forward, K - 1 extra forward rows
+    // per tile): 1024 px (r02 A/B: 16 rows 9 us per step faster than 8).  Keyed on the op, not on the
+    // fusion, so gpi_conv_blocks' slab rows fit both launch forms.
+    const bool loss_bwd = !fwd && (d.epilogue == GPI_EPI_GAUSS_LOSS || d.epilogue == GPI_EPI_GAUSS_EXP_LOSS);
+    G.th = (loss_bwd ? t_fuse : target) / d.w_out;
     if (G.th < 1) G.th = 1;
     if (G.th > d.h_out) G.th = d.h_out;
     if (fwd && d.stride == 1 && !d.upsample) {
@@ -195,6 +200,7 @@ bool conv_geom(const gpi_conv_desc& d, const gpi_groups& g, ConvGeom& G, bool fw
     int i0;
     in_rows(d.k, d.stride, d.upsample, d.pad, 0, G.th, i0, G.rh);
     if (d.upsample) G.rh += 1;   // parity-independent bound
+    if (fuse) G.rh += d.k - 1;   // fused output conv: the forward's input rows above and below
     G.P = d.w_in + 2 * HALO;
     g_rows(d.k, d.stride, d.pad, 0, G.th, i0, G.gh);
     G.PG = d.w_out + 2 * HALO;
@@ -207,6 +213,14 @@ bool conv_geom(const gpi_conv_desc& d, const gpi_groups& g, ConvGeom& G, bool fw
         eo * d.w_in >= lim || 256ull * G.th * d.w_out >= lim)
         return false;
     G.zero = nullptr;   // set by launch()
+    // forward: NPX adjacent output pixels per thread when the tile has >= 256 * NPX pixels (input row
+    // window and weight reads shared by the NPX pixels); GPI_FWD_NPX caps it (tuning runs only)
+    static const int npx_cap = env_int("GPI_FWD_NPX", 4);
+    G.npx = 1;
+    if (fwd) {
+        const int tp = G.th * d.w_out;
+        while (2 * G.npx <= npx_cap && tp >= 256 * 2 * G.npx && d.w_out % (2 * G.npx) == 0) G.npx *= 2;
+    }
     // the BN-backward operand image in registers when it is small: LDS = gradient + input images only
     // (one more resident workgroup per CU on the 32x32 / 64x64 decoder planes)
     G.zreg = (!fwd && d.gout_mode == 0 && (int64_t)d.cout * G.gh * (G.PG / 4) <= (int64_t)ZREG * 256) ? 1 : 0;
@@ -397,6 +411,7 @@ __device__ __forceinline__ T pin(T v) {
 }
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // Global-address-space views of (pinned, hence generic) pointers: ordinary loads and
 // stores through them stay global_load / global_store.  A flat access could alias LDS,
@@ -468,11 +483,25 @@ __device__ __forceinline__ void activate_img(float* img, const ConvGeom& G, cons
     }
 }
 
+// NPX consecutive floats of one output row (16-B / 8-B aligned: x0 is a multiple of NPX, planes are
+// multiples of 4 floats, buffers 16-B aligned -- aligned_ok)
+template <int NPX>
+__device__ __forceinline__ void store_px(float* p, const float (&v)[NPX]) {
+    if constexpr (NPX == 4) {
+        *as_gst((f32x4*)p) = f32x4{v[0], v[1], v[2], v[3]};
+    } else if constexpr (NPX == 2) {
+        *as_gst((f32x2*)p) = f32x2{v[0], v[1]};
+    } else {
+#pragma unroll
+        for (int q = 0; q < NPX; ++q) as_gst(p)[q] = v[q];
+    }
+}
+
 // ---------------------------------------------------------------------------------- forward
 // header floats: gst fp64 [4*MAX_CIN] | sc | sh [MAX_CIN] | scratch [64] | red [16] | dropout scales [8]
 constexpr int FWD_HDR = 8 * GPI_MAX_CIN + 2 * GPI_MAX_CIN + 64 + 16 + 8;
 
-template <int K, int S, int UP, int CP>
+template <int K, int S, int UP, int CP, int NPX>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void conv_fwd_kernel(gpi_conv_desc d, gpi_codec_ctx c, ConvGeom G) {
     constexpr int KK = K * K;
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -537,86 +566,218 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void c
     __syncthreads();
     PHASE(4);
 
-    // ---- phase 4: compute, one output pixel per thread and pass (two passes only for the
-    // 256-wide upsampled planes, whose tiles pair output rows)
+    // ---- phase 4: compute.  NPX == 1: one output pixel per thread and pass (two passes only for the
+    // 256-wide upsampled planes, whose tiles pair output rows).  NPX > 1: NPX horizontally adjacent
+    // pixels per thread; per (ci, ky) the thread reads the input row window the NPX x K taps cover
+    // once into registers, and every weight vector read serves NPX pixels.
     const int tp = G.th * d.w_out;
     float Lv = 0.f;
     float vst[2 * CP];
 #pragma unroll
     for (int q = 0; q < 2 * CP; ++q) vst[q] = 0.f;
-    for (int pbase = 0; pbase < tp; pbase += 256) {
-        const int pix = pbase + tid;
-        const int ty = dq(pix, G.d_wout), tx = pix - ty * d.w_out;
-        const int oy = T.oy0 + ty, ox = tx;
-        const bool active = pix < tp;
-        float tgt = 0.f;
-        const bool gauss = d.epilogue == GPI_EPI_GAUSS_LOSS || d.epilogue == GPI_EPI_GAUSS_EXP_LOSS;
-        if (gauss && active) {
-            int row = T.b - c.groups.start[T.grp];
-            if (c.tgt_idx[T.grp]) row = c.tgt_idx[T.grp][row];
-            tgt = c.tgt[T.grp][(int64_t)row * HWo + oy * d.w_out + ox];
-        }
-        PHASE(5);
-        float acc[CP];
+    const bool gauss = d.epilogue == GPI_EPI_GAUSS_LOSS || d.epilogue == GPI_EPI_GAUSS_EXP_LOSS;
+    if constexpr (NPX > 1) {
+        constexpr int PADK = K / 2;   // launch() checks pad == k / 2
+        // window column of tap kx of pixel p (x0 is a multiple of NPX, even, for the upsampling offsets)
+        constexpr int NW = UP ? ((NPX - 1 + K - 1 + (PADK & 1)) >> 1) + 1 : (NPX - 1) * S + K;
+        const int ng = tp / NPX;
+        for (int gbase = 0; gbase < ng; gbase += 256) {
+            const int g = gbase + tid;
+            const bool active = g < ng;
+            const int ty = dq(g * NPX, G.d_wout), x0 = g * NPX - ty * d.w_out;
+            const int oy = T.oy0 + ty;
+            float acc[NPX][CP];
 #pragma unroll
-        for (int co = 0; co < CP; ++co) acc[co] = 0.f;
-        if (active) {
-            const int plane = G.rh * G.P;
-            for (int ci = 0; ci < d.cin; ++ci) {
-                const float* tci = img + ci * plane;
-                const float* wci = wT + ci * KK * CP;
+            for (int p = 0; p < NPX; ++p)
 #pragma unroll
-                for (int ky = 0; ky < K; ++ky) {
-                    const int ry = UP ? (fdiv2(oy - d.pad + ky) - iy0) : (ty * S + ky);
-                    const float* trow = tci + ry * G.P;
+                for (int co = 0; co < CP; ++co) acc[p][co] = 0.f;
+            if (active) {
+                const int plane = G.rh * G.P;
+                const int cb = UP ? fdiv2(x0 - PADK) + HALO : x0 * S - PADK + HALO;
+                for (int ci = 0; ci < d.cin; ++ci) {
+                    const float* tci = img + ci * plane + cb;
+                    const float* wci = wT + ci * KK * CP;
 #pragma unroll
-                    for (int kx = 0; kx < K; ++kx) {
-                        const int col = UP ? fdiv2(ox - d.pad + kx) + HALO : ox * S - d.pad + kx + HALO;
-                        fma_vec<CP>(acc, wci + (ky * K + kx) * CP, trow[col]);
+                    for (int ky = 0; ky < K; ++ky) {
+                        const int ry = UP ? (fdiv2(oy - PADK + ky) - iy0) : (ty * S + ky);
+                        const float* trow = tci + ry * G.P;
+                        float win[NW];
+#pragma unroll
+                        for (int t = 0; t < NW; ++t) win[t] = trow[t];
+#pragma unroll
+                        for (int kx = 0; kx < K; ++kx) {
+                            float wv[CP];
+                            const float* wp = wci + (ky * K + kx) * CP;
+                            if constexpr (CP % 4 == 0) {
+#pragma unroll
+                                for (int q = 0; q < CP / 4; ++q) {
+                                    const float4 w4 = reinterpret_cast<const float4*>(wp)[q];
+                                    wv[4 * q] = w4.x;
+                                    wv[4 * q + 1] = w4.y;
+                                    wv[4 * q + 2] = w4.z;
+                                    wv[4 * q + 3] = w4.w;
+                                }
+                            } else {
+#pragma unroll
+                                for (int q = 0; q < CP / 2; ++q) {
+                                    const float2 w2 = reinterpret_cast<const float2*>(wp)[q];
+                                    wv[2 * q] = w2.x;
+                                    wv[2 * q + 1] = w2.y;
+                                }
+                            }
+#pragma unroll
+                            for (int p = 0; p < NPX; ++p) {
+                                const float v = win[UP ? ((p + kx + (PADK & 1)) >> 1) : p * S + kx];
+#pragma unroll
+                                for (int co = 0; co < CP; ++co) acc[p][co] = fmaf(wv[co], v, acc[p][co]);
+                            }
+                        }
+                    }
+                }
+            }
+            if (drop) {
+#pragma unroll
+                for (int co = 0; co < CP; ++co) {
+                    const float ds = co < d.cout ? dsl[co] : 1.f;
+#pragma unroll
+                    for (int p = 0; p < NPX; ++p) acc[p][co] *= ds;
+                }
+            }
+            const int64_t pix0 = (int64_t)oy * d.w_out + x0;
+            if (gauss) {
+                if (active) {
+                    int row = T.b - c.groups.start[T.grp];
+                    if (c.tgt_idx[T.grp]) row = c.tgt_idx[T.grp][row];
+                    const float* tg = c.tgt[T.grp] + (int64_t)row * HWo + pix0;
+                    const bool ex = d.epilogue == GPI_EPI_GAUSS_EXP_LOSS;
+                    const float scl = c.loss_scale[T.grp];
+                    float g0[NPX], g1[NPX];
+#pragma unroll
+                    for (int p = 0; p < NPX; ++p) {
+                        const float tgt = tg[p];
+                        const float mu = acc[p][0], ls = acc[p][1];
+                        const float e = expf(-2.f * ls);
+                        const float emu = ex ? expf(mu) : 1.f;
+                        const float r = ex ? expf(tgt) - emu : tgt - mu;
+                        Lv += -0.5f * (2.f * ls + r * r * e + GPI_LOG2PI);
+                        g0[p] = -scl * r * e * emu;
+                        g1[p] = scl * (1.f - r * r * e);
+                    }
+                    float* go = ws + d.gout_off + (int64_t)T.b * 2 * HWo + pix0;
+                    store_px<NPX>(go, g0);
+                    store_px<NPX>(go + HWo, g1);
+                    if (d.out_off >= 0) {
+                        float m0[NPX], m1[NPX];
+#pragma unroll
+                        for (int p = 0; p < NPX; ++p) {
+                            m0[p] = acc[p][0];
+                            m1[p] = acc[p][1];
+                        }
+                        float* o = ws + d.out_off + ((int64_t)T.b * d.out_ctot + d.out_c0) * HWo + pix0;
+                        store_px<NPX>(o, m0);
+                        store_px<NPX>(o + HWo, m1);
+                    }
+                }
+                continue;
+            }
+            if (active) {
+                float* o = ws + d.out_off + ((int64_t)T.b * d.out_ctot + d.out_c0) * HWo + pix0;
+#pragma unroll
+                for (int co = 0; co < CP; ++co) {
+                    if (co < d.cout) {
+                        float v[NPX];
+#pragma unroll
+                        for (int p = 0; p < NPX; ++p) v[p] = acc[p][co];
+                        store_px<NPX>(o + (int64_t)co * HWo, v);
+                    }
+                }
+            }
+            if (d.epilogue == GPI_EPI_STORE_STATS) {
+#pragma unroll
+                for (int co = 0; co < CP; ++co) {
+#pragma unroll
+                    for (int p = 0; p < NPX; ++p) {
+                        const float a = (active && co < d.cout) ? acc[p][co] : 0.f;
+                        vst[2 * co] += a;
+                        vst[2 * co + 1] += a * a;
                     }
                 }
             }
         }
-        PHASE(6);
-        if (drop) {
-#pragma unroll
-            for (int co = 0; co < CP; ++co)
-                if (co < d.cout) acc[co] *= dsl[co];
-        }
-        if (gauss) {
+    } else {
+        for (int pbase = 0; pbase < tp; pbase += 256) {
+            const int pix = pbase + tid;
+            const int ty = dq(pix, G.d_wout), tx = pix - ty * d.w_out;
+            const int oy = T.oy0 + ty, ox = tx;
+            const bool active = pix < tp;
+            float tgt = 0.f;
+            if (gauss && active) {
+                int row = T.b - c.groups.start[T.grp];
+                if (c.tgt_idx[T.grp]) row = c.tgt_idx[T.grp][row];
+                tgt = c.tgt[T.grp][(int64_t)row * HWo + oy * d.w_out + ox];
+            }
+            PHASE(5);
+            float acc[CP];
+    #pragma unroll
+            for (int co = 0; co < CP; ++co) acc[co] = 0.f;
             if (active) {
-                const float mu = acc[0], ls = acc[1];
-                const float e = expf(-2.f * ls);
-                // log-property Gaussian (default) or the exponentiated field's (d mean: chain factor exp(mu))
-                const bool ex = d.epilogue == GPI_EPI_GAUSS_EXP_LOSS;
-                const float emu = ex ? expf(mu) : 1.f;
-                const float r = ex ? expf(tgt) - emu : tgt - mu;
-                Lv += -0.5f * (2.f * ls + r * r * e + GPI_LOG2PI);
-                const float scl = c.loss_scale[T.grp];
-                auto go = as_gst(ws + d.gout_off + (int64_t)T.b * 2 * HWo + oy * d.w_out + ox);
-                go[0] = -scl * r * e * emu;
-                go[HWo] = scl * (1.f - r * r * e);
-                if (d.out_off >= 0) {
-                    auto o = as_gst(ws + d.out_off + (int64_t)T.b * d.out_ctot * HWo + (int64_t)d.out_c0 * HWo +
-                                 oy * d.w_out + ox);
-                    o[0] = mu;
-                    o[HWo] = ls;
+                const int plane = G.rh * G.P;
+                for (int ci = 0; ci < d.cin; ++ci) {
+                    const float* tci = img + ci * plane;
+                    const float* wci = wT + ci * KK * CP;
+    #pragma unroll
+                    for (int ky = 0; ky < K; ++ky) {
+                        const int ry = UP ? (fdiv2(oy - d.pad + ky) - iy0) : (ty * S + ky);
+                        const float* trow = tci + ry * G.P;
+    #pragma unroll
+                        for (int kx = 0; kx < K; ++kx) {
+                            const int col = UP ? fdiv2(ox - d.pad + kx) + HALO : ox * S - d.pad + kx + HALO;
+                            fma_vec<CP>(acc, wci + (ky * K + kx) * CP, trow[col]);
+                        }
+                    }
                 }
             }
-            continue;
-        }
-        if (active) {
-            auto o = as_gst(ws + d.out_off + ((int64_t)T.b * d.out_ctot + d.out_c0) * HWo + oy * d.w_out + ox);
-#pragma unroll
-            for (int co = 0; co < CP; ++co)
-                if (co < d.cout) o[(int64_t)co * HWo] = acc[co];
-        }
-        if (d.epilogue == GPI_EPI_STORE_STATS) {
-#pragma unroll
-            for (int co = 0; co < CP; ++co) {
-                const float a = (active && co < d.cout) ? acc[co] : 0.f;
-                vst[2 * co] += a;
-                vst[2 * co + 1] += a * a;
+            PHASE(6);
+            if (drop) {
+    #pragma unroll
+                for (int co = 0; co < CP; ++co)
+                    if (co < d.cout) acc[co] *= dsl[co];
+            }
+            if (gauss) {
+                if (active) {
+                    const float mu = acc[0], ls = acc[1];
+                    const float e = expf(-2.f * ls);
+                    // log-property Gaussian (default) or the exponentiated field's (d mean: chain factor exp(mu))
+                    const bool ex = d.epilogue == GPI_EPI_GAUSS_EXP_LOSS;
+                    const float emu = ex ? expf(mu) : 1.f;
+                    const float r = ex ? expf(tgt) - emu : tgt - mu;
+                    Lv += -0.5f * (2.f * ls + r * r * e + GPI_LOG2PI);
+                    const float scl = c.loss_scale[T.grp];
+                    auto go = as_gst(ws + d.gout_off + (int64_t)T.b * 2 * HWo + oy * d.w_out + ox);
+                    go[0] = -scl * r * e * emu;
+                    go[HWo] = scl * (1.f - r * r * e);
+                    if (d.out_off >= 0) {
+                        auto o = as_gst(ws + d.out_off + (int64_t)T.b * d.out_ctot * HWo + (int64_t)d.out_c0 * HWo +
+                                     oy * d.w_out + ox);
+                        o[0] = mu;
+                        o[HWo] = ls;
+                    }
+                }
+                continue;
+            }
+            if (active) {
+                auto o = as_gst(ws + d.out_off + ((int64_t)T.b * d.out_ctot + d.out_c0) * HWo + oy * d.w_out + ox);
+    #pragma unroll
+                for (int co = 0; co < CP; ++co)
+                    if (co < d.cout) o[(int64_t)co * HWo] = acc[co];
+            }
+            if (d.epilogue == GPI_EPI_STORE_STATS) {
+    #pragma unroll
+                for (int co = 0; co < CP; ++co) {
+                    const float a = (active && co < d.cout) ? acc[co] : 0.f;
+                    vst[2 * co] += a;
+                    vst[2 * co + 1] += a * a;
+                }
             }
         }
     }
@@ -673,7 +834,11 @@ struct IntC {
 // per-wave input-channel sums [2][4 waves][32] (256 floats) alias the offset table (>= 256 floats)
 constexpr int SLAB_ROWS = 4;    // partial-slab rows per workgroup: one per wave (no cross-wave dW reduction)
 
-template <int K, int S, int UP>
+// FUSE (the decoder's output conv, Gaussian-loss epilogue, no dropout): the launch computes its own
+// forward first -- output rows [oy0 - K/2, oy0 + th + K/2) from an input image K/2 rows taller on each
+// side, the log-likelihood of its owned rows and the loss gradient straight into the LDS gradient
+// image -- then runs the backward on it: no output-gradient round trip through HBM, one launch less.
+template <int K, int S, int UP, bool FUSE = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 : 6))) void conv_bwd_kernel(gpi_conv_desc d, gpi_codec_ctx c, ConvGeom G) {
     constexpr int KK = K * K;
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -700,6 +865,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 
     const bool zreg = G.zreg != 0;
     float* gz = gl + gimg;                            // raw z of the output (BN-backward only, LDS form)
     float* al = gz + ((obn && !zreg) ? gimg : 0);     // [cin][rh][P]
+    // FUSE: the image starts K/2 rows above the backward's first input row; alb is the backward's view
+    float* const alb = FUSE ? al + (K / 2) * G.P : al;
     // reduction scratch: aliases gz (dead after phase 3) when it is large enough -- 8 KB less LDS
     // per workgroup, one more resident workgroup per CU on the 32x32 planes
     // channel-sum scratch: the offset table's space, dead after the input gradient (in_bn implies has_gin)
@@ -736,8 +903,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 
     int gy0, gh_;
     g_rows(K, S, d.pad, T.oy0, G.th, gy0, gh_);
     const int64_t gbase = ((int64_t)T.b * d.out_ctot + d.out_c0) * HWo;
-    stage_img(gl, d.cout, G.gh, G.PG, G.d_g4, G.d_PG4, G.g_sq, G.g_sr, G.g_sc, gy0, d.h_out, d.w_out, zero,
-              [&](int q) -> const float* { return ws + gout_off + gbase + (int64_t)q * HWo; });
+    if constexpr (FUSE) {
+        // the gradient image is computed below: zero halo columns, out-of-plane rows and margin
+        float4* g4 = reinterpret_cast<float4*>(gl);
+        for (int e = tid; e < gimg / 4; e += 256) g4[e] = float4{0.f, 0.f, 0.f, 0.f};
+    } else {
+        stage_img(gl, d.cout, G.gh, G.PG, G.d_g4, G.d_PG4, G.g_sq, G.g_sr, G.g_sc, gy0, d.h_out, d.w_out, zero,
+                  [&](int q) -> const float* { return ws + gout_off + gbase + (int64_t)q * HWo; });
+    }
     PHASE(13);
     f32x4 zr[ZREG];           // zreg: this thread's chunks tid + 256 u of the z image
     if (obn && zreg) {
@@ -761,7 +934,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 
     PHASE(14);
     int iy0, rh_;
     in_rows(K, S, UP, d.pad, T.oy0, G.th, iy0, rh_);
-    stage_img(al, d.cin, G.rh, G.P, G.d_in4, G.d_P4, G.in_sq, G.in_sr, G.in_sc, iy0, d.h_in, d.w_in, zero,
+    const int iyA = FUSE ? iy0 - K / 2 : iy0;        // first row of the LDS input image
+    stage_img(al, d.cin, G.rh, G.P, G.d_in4, G.d_P4, G.in_sq, G.in_sr, G.in_sc, iyA, d.h_in, d.w_in, zero,
               [&](int q) -> const float* { return ib + (int64_t)q * HWi; });
     PHASE(8);
     // input-gradient epilogue operand (previous S_in, when accumulating) of this wave's first
@@ -833,7 +1007,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 
     PHASE(3);
 
     // ---- phase 3: activations in LDS; offset table of the input-gradient reduction
-    if (d.in_bn) activate_img(al, G, d, iy0, i_sc, i_sh);
+    if (d.in_bn) activate_img(al, G, d, iyA, i_sc, i_sh);
     if (has_gin && dg_role && S == 2) {
         // input pixel (py, px) = (py0 + 2a + ry, 2b + rx) receives output (oy, ox) through tap (ky, kx)
         // iff 2 oy = py + pad - ky, 2 ox = px + pad - kx: the valid taps depend on the parity class
@@ -947,6 +1121,67 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 
         }
     }
     __syncthreads();
+    if constexpr (FUSE) {
+        // ---- phase 3': forward of output rows gy0 + [0, gh) (4 adjacent pixels per thread; weights
+        // from the input-gradient table wD[(co * KK + tap) * 16 + ci]), the Gaussian log-likelihood of
+        // the owned rows, d(-logL)/d(mu, logsigma) into the gradient image
+        constexpr int NPXF = 4, PADK = K / 2, NW = (NPXF - 1) + K;
+        const int ng = G.gh * d.w_out / NPXF;
+        float Lv = 0.f;
+        int trow0 = T.b - c.groups.start[T.grp];
+        if (c.tgt_idx[T.grp]) trow0 = c.tgt_idx[T.grp][trow0];
+        const float* tg = c.tgt[T.grp] + (int64_t)trow0 * HWo;
+        const bool ex = d.epilogue == GPI_EPI_GAUSS_EXP_LOSS;
+        const float scl = c.loss_scale[T.grp];
+        for (int g = tid; g < ng; g += 256) {
+            const int j = dq(g * NPXF, G.d_wout), x0 = g * NPXF - j * d.w_out;
+            const int oy = gy0 + j;
+            if (oy < 0 || oy >= d.h_out) continue;
+            float tv[NPXF];          // targets first: their latency overlaps the compute
+#pragma unroll
+            for (int p = 0; p < NPXF; ++p) tv[p] = as_gld(tg)[oy * d.w_out + x0 + p];
+            float mu[NPXF], ls[NPXF];
+#pragma unroll
+            for (int p = 0; p < NPXF; ++p) mu[p] = ls[p] = 0.f;
+            for (int ci = 0; ci < d.cin; ++ci) {
+                const float* arow = al + (ci * G.rh + j) * G.P + HALO + x0 - PADK;
+#pragma unroll
+                for (int ky = 0; ky < K; ++ky) {
+                    float win[NW];
+#pragma unroll
+                    for (int t = 0; t < NW; ++t) win[t] = arow[ky * G.P + t];
+#pragma unroll
+                    for (int kx = 0; kx < K; ++kx) {
+                        const float w0 = wD[(ky * K + kx) * 16 + ci], w1 = wD[(KK + ky * K + kx) * 16 + ci];
+#pragma unroll
+                        for (int p = 0; p < NPXF; ++p) {
+                            mu[p] = fmaf(w0, win[p + kx], mu[p]);
+                            ls[p] = fmaf(w1, win[p + kx], ls[p]);
+                        }
+                    }
+                }
+            }
+            const bool own = j >= PADK && j < PADK + G.th;
+            float* g0 = gl + j * G.PG + HALO + x0;
+#pragma unroll
+            for (int p = 0; p < NPXF; ++p) {
+                const float tgt = tv[p];
+                const float e = expf(-2.f * ls[p]);
+                const float emu = ex ? expf(mu[p]) : 1.f;
+                const float r = ex ? expf(tgt) - emu : tgt - mu[p];
+                if (own) Lv += -0.5f * (2.f * ls[p] + r * r * e + GPI_LOG2PI);
+                g0[p] = -scl * r * e * emu;
+                g0[gplane + p] = scl * (1.f - r * r * e);
+            }
+        }
+        // one fp64 atomic per workgroup (per-wave atomics into 16 replicas serialise: 2304 x 4 adds)
+        const float lw = wave_sum(Lv);
+        if (lane == 0) o_coef[wv] = lw;       // o_coef is unused without an output BN
+        __syncthreads();
+        if (tid == 0 && !SKIP(G, 4))
+            atomicAdd(c.loss_acc + T.grp * GPI_REPLICAS + blockIdx.x % GPI_REPLICAS,
+                      (double)((o_coef[0] + o_coef[1]) + (o_coef[2] + o_coef[3])));
+    }
     PHASE(4);
 
     // ---- phase 4a: weight gradient (MFMA, column-shift form) -> slab row.
@@ -980,7 +1215,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 
                 const int px = 4 * ps + kq;
                 const int ty = dq(px, G.d_wout), ox = px - ty * d.w_out;
                 const float a = gco[ty * G.PG + ox];
-                const float* xb = al + (ty * S) * G.P + HALO + S * ox;
+                const float* xb = alb + (ty * S) * G.P + HALO + S * ox;
                 float bv[NB];
 #pragma unroll
                 for (int nb = 0; nb < NB; ++nb) bv[nb] = xb[tap_off[nb]];
@@ -1027,7 +1262,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 
 #pragma unroll
                         for (int u = 0; u < 2; ++u) {
                             const int ry = UP ? fdiv2(T.oy0 + ty - d.pad + ky[u]) - iy0 : ty * S + ky[u];
-                            brow[u] = al + (ci[u] * G.rh + ry) * G.P + HALO;
+                            brow[u] = alb + (ci[u] * G.rh + ry) * G.P + HALO;
                         }
                         // operands of four steps are read before their MFMAs (LDS read -> dependent
                         // MFMA would serialise every step)
@@ -1126,7 +1361,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 
             l_bet = i_sh[ci_l] + i_mean[ci_l] * i_sc[ci_l];     // beta
             l_rgam = 1.f / l_gam;
         }
-        const float* arow0 = al + (ci_l * G.rh + (py0 - iy0)) * G.P + HALO;   // owned row 0 of channel l16
+        const float* arow0 = alb + (ci_l * G.rh + (py0 - iy0)) * G.P + HALO;   // owned row 0 of channel l16
         const int nkd = KD4 >> 2;
         for (int round = 0; wv + 16 * round < nmblk; ++round) {
             if (round > 0 && S != 2) own_load(round);
@@ -1281,7 +1516,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 
     #pragma unroll
                 for (int ci = 0; ci < CI; ++ci) {
                     if (ci >= d.cin) break;
-                    const float* ap = al + (ci * G.rh + (py0 - iy0 + qy)) * G.P + HALO + px0;
+                    const float* ap = alb + (ci * G.rh + (py0 - iy0 + qy)) * G.P + HALO + px0;
                     const float av[2] = {ap[0], ap[1]};
                     float pv[2] = {0.f, 0.f};
                     if (d.gin_accumulate) {
@@ -1378,24 +1613,31 @@ size_t bwd_lds(const gpi_conv_desc& d, const ConvGeom& G) {
 
 typedef void (*conv_kernel_t)(gpi_conv_desc, gpi_codec_ctx, ConvGeom);
 
-template <int K, int S, int UP>
-conv_kernel_t pick(int cp, bool fwd) {
-    if (!fwd) return conv_bwd_kernel<K, S, UP>;
-    if (cp == 2) return conv_fwd_kernel<K, S, UP, 2>;
-    if (cp == 4) return conv_fwd_kernel<K, S, UP, 4>;
-    if (cp == 6) return conv_fwd_kernel<K, S, UP, 6>;
-    return conv_fwd_kernel<K, S, UP, 8>;
+template <int K, int S, int UP, int NPX>
+conv_kernel_t pick_cp(int cp) {
+    if (cp == 2) return conv_fwd_kernel<K, S, UP, 2, NPX>;
+    if (cp == 4) return conv_fwd_kernel<K, S, UP, 4, NPX>;
+    if (cp == 6) return conv_fwd_kernel<K, S, UP, 6, NPX>;
+    return conv_fwd_kernel<K, S, UP, 8, NPX>;
 }
 
-conv_kernel_t select_kernel(const gpi_conv_desc& d, int cp, bool fwd) {
+template <int K, int S, int UP>
+conv_kernel_t pick(int cp, bool fwd, int npx) {
+    if (!fwd) return conv_bwd_kernel<K, S, UP>;
+    if (npx == 4) return pick_cp<K, S, UP, 4>(cp);
+    if (npx == 2) return pick_cp<K, S, UP, 2>(cp);
+    return pick_cp<K, S, UP, 1>(cp);
+}
+
+conv_kernel_t select_kernel(const gpi_conv_desc& d, int cp, bool fwd, int npx) {
     const int key = d.k * 100 + d.stride * 10 + d.upsample;
     switch (key) {
-        case 110: return pick<1, 1, 0>(cp, fwd);
-        case 310: return pick<3, 1, 0>(cp, fwd);
-        case 311: return pick<3, 1, 1>(cp, fwd);
-        case 320: return pick<3, 2, 0>(cp, fwd);
-        case 510: return pick<5, 1, 0>(cp, fwd);
-        case 720: return pick<7, 2, 0>(cp, fwd);
+        case 110: return pick<1, 1, 0>(cp, fwd, npx);
+        case 310: return pick<3, 1, 0>(cp, fwd, npx);
+        case 311: return pick<3, 1, 1>(cp, fwd, npx);
+        case 320: return pick<3, 2, 0>(cp, fwd, npx);
+        case 510: return pick<5, 1, 0>(cp, fwd, npx);
+        case 720: return pick<7, 2, 0>(cp, fwd, npx);
         default: return nullptr;
     }
 }
@@ -1423,16 +1665,20 @@ bool aligned_ok(const gpi_conv_desc& d, const gpi_codec_ctx& c, bool fwd) {
     return true;
 }
 
-int launch(const gpi_conv_desc& d, const gpi_codec_ctx& c, hipStream_t st, bool fwd) {
+int launch(const gpi_conv_desc& d, const gpi_codec_ctx& c, hipStream_t st, bool fwd, bool fuse = false) {
     ConvGeom G;
-    if (!conv_geom(d, c.groups, G, fwd)) return GPI_ERR_UNSUPPORTED;
+    if (!conv_geom(d, c.groups, G, fwd, fuse)) return GPI_ERR_UNSUPPORTED;
+    if (fuse && (fwd || d.k != 5 || d.stride != 1 || d.upsample || d.cout != 2 || d.cin > 4 || d.drop_off >= 0 ||
+                 d.gout_mode != 1 || d.gin_off < 0 ||
+                 (d.epilogue != GPI_EPI_GAUSS_LOSS && d.epilogue != GPI_EPI_GAUSS_EXP_LOSS)))
+        return GPI_ERR_UNSUPPORTED;
     if ((d.epilogue == GPI_EPI_GAUSS_LOSS || d.epilogue == GPI_EPI_GAUSS_EXP_LOSS) && d.cout != 2) return GPI_ERR_ARG;
     if (d.in_off < 0 && !c.ext_in) return GPI_ERR_ARG;
     if (!aligned_ok(d, c, fwd)) return GPI_ERR_UNSUPPORTED;
     if (!fwd && d.gin_off >= 0 && ((G.ph * d.w_in) & 15)) return GPI_ERR_UNSUPPORTED;
     if (!fwd && d.gin_off >= 0 && d.stride == 2 && ((d.w_in & 7) || (G.ph & 1))) return GPI_ERR_UNSUPPORTED;
     const int cp = cp_of(d);
-    conv_kernel_t k = select_kernel(d, cp, fwd);
+    conv_kernel_t k = fuse ? conv_bwd_kernel<5, 1, 0, true> : select_kernel(d, cp, fwd, G.npx);
     if (!k) return GPI_ERR_UNSUPPORTED;
     static const float* zero = nullptr;
     if (!zero) {
@@ -1443,7 +1689,7 @@ int launch(const gpi_conv_desc& d, const gpi_codec_ctx& c, hipStream_t st, bool 
     G.zero = zero;
     const size_t lds = fwd ? fwd_lds(d, G, cp) : bwd_lds(d, G);
     if (lds > 160 * 1024) return GPI_ERR_UNSUPPORTED;
-    if (!fwd && d.gin_off >= 0) {
+    if (!fwd && d.gin_off >= 0 && !fuse) {
         // resident workgroups per CU: LDS (~160 KB less a per-workgroup reserve, tools/bench_dispatch.hip)
         // and the kernels' occupancy (6 waves per SIMD, 4 for the 5x5 kernel)
         static const int split_env = env_int("GPI_BWD_SPLIT", 1);
@@ -1594,6 +1840,7 @@ extern "C" int gpi_conv_launch_info(const gpi_conv_desc* op, const gpi_groups* g
     info[1] = G.nblocks;
     info[2] = (int32_t)(fwd ? fwd_lds(*op, G, cp) : bwd_lds(*op, G));
     info[3] = cp;
+    info[4] = G.npx;
     return GPI_OK;
 }
 
@@ -1605,6 +1852,11 @@ extern "C" int gpi_conv_forward(const gpi_conv_desc* op, const gpi_codec_ctx* ct
 extern "C" int gpi_conv_backward(const gpi_conv_desc* op, const gpi_codec_ctx* ctx, void* stream) {
     if (!op || !ctx) return GPI_ERR_ARG;
     return launch(*op, *ctx, (hipStream_t)stream, false);
+}
+
+extern "C" int gpi_conv_loss_fused(const gpi_conv_desc* op, const gpi_codec_ctx* ctx, void* stream) {
+    if (!op || !ctx) return GPI_ERR_ARG;
+    return launch(*op, *ctx, (hipStream_t)stream, false, true);
 }
 
 extern "C" int gpi_codec_forward(const gpi_conv_desc* ops, int n_ops, const gpi_codec_ctx* ctx, void* stream) {

@@ -176,6 +176,7 @@ SIGNATURES = {
     'gpi_error_string': (C.c_char_p, [C.c_int]),
     'gpi_conv_blocks': (C.c_int, [C.POINTER(ConvDesc), C.POINTER(Groups), C.POINTER(i32)]),
     'gpi_bn_running_update': (C.c_int, [vp, C.c_int, C.c_int, vp, i64, f32, vp]),
+    'gpi_conv_loss_fused': (C.c_int, [C.POINTER(ConvDesc), C.POINTER(CodecCtx), vp]),
     'gpi_conv_launch_info': (C.c_int, [C.POINTER(ConvDesc), C.POINTER(Groups), C.c_int, C.POINTER(i32)]),
     'gpi_conv_forward': (C.c_int, [C.POINTER(ConvDesc), C.POINTER(CodecCtx), vp]),
     'gpi_conv_backward': (C.c_int, [C.POINTER(ConvDesc), C.POINTER(CodecCtx), vp]),

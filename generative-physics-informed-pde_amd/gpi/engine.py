@@ -16,6 +16,7 @@ unsupervised term (generative.py:546-585) + the supervised freeX term
             weight-gradient slab reduction, outer-product GEMMs, finalize.
 """
 import ctypes as C
+import os
 import math
 
 import torch
@@ -247,6 +248,12 @@ class ElboEngine(object):
         self.g_sup = (1 if self.B_u > 0 else 0) if self.N_s > 0 else None
         self.g_vo = ((self.B_u > 0) + (self.N_s > 0)) if self.N_vo > 0 else None
         self.dec_descs = self.dp.layout(self.B, ws.ws, ws.stats, ws.parts, groups_struct(self.dec_sizes), offD)
+        # the loss epilogue consumes (mu, logsigma) in registers: nobody reads the output image (9.4 MB of
+        # writes per step at C64)
+        self.dec_descs[len(self.dec_descs) - 1].out_off = -1
+        # the output conv's forward and backward run as ONE launch at the end of the forward
+        # (gpi_conv_loss_fused: the loss gradient stays in LDS); GPI_FUSE_OUT=0 keeps them apart (A/B only)
+        self.n_dec_sep = len(self.dec_descs) - (1 if os.environ.get('GPI_FUSE_OUT', '1') != '0' else 0)
         # ---- dense head buffers
         d_lat = self.dp.input.per_sample
         d_x = g.dim_effective_property if self.N_q > 0 else 1
@@ -479,8 +486,10 @@ class ElboEngine(object):
             main = torch.cuda.current_stream()
             self._side_stream()
             self._ev_fork.record(main)
-        _run(lib.gpi_codec_forward, self.dec_descs, len(self.dec_descs), C.byref(self.dctx), st,
-             what='decoder forward')
+        _run(lib.gpi_codec_forward, self.dec_descs, self.n_dec_sep, C.byref(self.dctx), st, what='decoder forward')
+        if self.n_dec_sep < len(self.dec_descs):
+            _run(lib.gpi_conv_loss_fused, C.byref(self.dec_descs[self.n_dec_sep]), C.byref(self.dctx), st,
+                 what='decoder output conv (forward + loss + backward)')
         if self.roms:
             self._side.wait_event(self._ev_fork)
             for r in self.roms:
@@ -565,7 +574,7 @@ class ElboEngine(object):
         (the fused step draws the next step's noise there)."""
         lib = _lib()
         st = stream if stream is not None else L.stream_handle()
-        _run(lib.gpi_codec_backward, self.dec_descs, len(self.dec_descs), C.byref(self.dctx), st,
+        _run(lib.gpi_codec_backward, self.dec_descs, self.n_dec_sep, C.byref(self.dctx), st,
              what='decoder backward')
         P_, W_, G_ = (C.c_void_p(self.flat.P.data_ptr()), C.c_void_p(self.ws.t_ws.data_ptr()),
                       C.c_void_p(self.flat.gacc.data_ptr()))

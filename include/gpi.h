@@ -422,10 +422,18 @@ int gpi_bn_running_update(const gpi_bn_running_item* items, int n_items, int max
 int gpi_conv_blocks(const gpi_conv_desc* op, const gpi_groups* groups, int32_t* blocks);
 /* Launch geometry of one conv pass (fwd != 0: forward) for tuning / profiling tools:
  * info[0] output rows per tile, info[1] workgroups, info[2] LDS bytes per workgroup,
- * info[3] output channels per forward thread.  No device work. */
+ * info[3] output channels per forward thread, info[4] adjacent output pixels per forward thread
+ * (1 for the backward).  info holds >= 5 entries.  No device work. */
 int gpi_conv_launch_info(const gpi_conv_desc* op, const gpi_groups* groups, int fwd, int32_t* info);
 int gpi_conv_forward(const gpi_conv_desc* op, const gpi_codec_ctx* ctx, void* stream);
 int gpi_conv_backward(const gpi_conv_desc* op, const gpi_codec_ctx* ctx, void* stream);
+/* Forward AND backward of the decoder's output conv (Decoder.py:288-305 last_decoding conv3, 5x5,
+ * cout = 2) with its Gaussian-loss epilogue (generative.py:232-239, bottleneck/utils.py:231-243) in one
+ * launch: adds the log-likelihood to ctx->loss_acc and writes the weight-gradient slab rows and the
+ * input's S / BN-backward sums exactly as gpi_conv_forward followed by gpi_conv_backward would (the
+ * output gradient never leaves LDS).  op: k = 5, stride 1, no upsampling, cin <= 4, cout = 2,
+ * epilogue GPI_EPI_GAUSS_LOSS / GPI_EPI_GAUSS_EXP_LOSS, gout_mode 1, no dropout; out_off is ignored. */
+int gpi_conv_loss_fused(const gpi_conv_desc* op, const gpi_codec_ctx* ctx, void* stream);
 /* Run a codec program: ops in order (forward) / reverse order (backward). */
 int gpi_codec_forward(const gpi_conv_desc* ops, int n_ops, const gpi_codec_ctx* ctx, void* stream);
 int gpi_codec_backward(const gpi_conv_desc* ops, int n_ops, const gpi_codec_ctx* ctx, void* stream);

@@ -45,7 +45,7 @@ def main():
         for i, op in enumerate(prog.ops):
             if args and not any(a in op.name for a in args):
                 continue
-            info = (C.c_int32 * 4)()
+            info = (C.c_int32 * 8)()
             L.check(lib.gpi_conv_launch_info(C.byref(descs[i]), C.byref(ctx.groups), 1 if fwd else 0, info), 'info')
             nb = min(info[1], 4096)       # workgroups of the launch
             fn = lib.gpi_conv_forward if fwd else lib.gpi_conv_backward
