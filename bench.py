@@ -100,13 +100,20 @@ def build(cfg_name, device, seed, rank=0, world=1):
     return model, (Xu, Xs, Y, F), (B_u, N_s), physics
 
 
-def conv_bytes(d, B, fwd):
-    """Algorithmic HBM bytes of one conv launch (each tensor read / written once)."""
+def conv_bytes(d, B, fwd, fused=False):
+    """Algorithmic HBM bytes of one conv launch (each tensor read / written once).  fused: the
+    output conv's gpi_conv_loss_fused launch (input + target read, input gradient written; the
+    loss gradient never leaves LDS)."""
     hwi, hwo = d.h_in * d.w_in, d.h_out * d.w_out
+    loss = d.epilogue in (2, 3)                 # GPI_EPI_GAUSS_LOSS / GPI_EPI_GAUSS_EXP_LOSS
+    if fused:
+        return 4.0 * B * (d.cin * hwi * (3 if d.gin_accumulate else 2) + hwo)
     if fwd:
-        b = B * (d.cin * hwi + d.cout * hwo)
-        if d.epilogue == 2:
-            b += B * (hwo + 2 * hwo)             # target read + gradient write
+        b = B * d.cin * hwi
+        if loss:
+            b += B * (hwo + 2 * hwo + (d.cout * hwo if d.out_off >= 0 else 0))   # target, gradient, (mu, ls)
+        else:
+            b += B * d.cout * hwo
     else:
         b = B * (d.cin * hwi + (2 if d.gout_mode == 0 else 1) * d.cout * hwo)
         if d.gin_off >= 0:
@@ -114,34 +121,47 @@ def conv_bytes(d, B, fwd):
     return 4.0 * b
 
 
+def step_conv_launches(e):
+    """The codec launches of one ELBO step of engine e, in step order per program:
+    [(name, kind, entry point, desc, ctx, batch)] with kind 'fwd' / 'bwd', or 'fused' for the
+    output conv's single forward + loss + backward launch (engine.n_dec_sep)."""
+    import ctypes as C  # noqa: F401
+    from gpi import _lib as L
+    lib = L.lib()
+    fns = {'fwd': lib.gpi_conv_forward, 'bwd': lib.gpi_conv_backward, 'fused': lib.gpi_conv_loss_fused}
+    progs = []
+    if e.ep is not None:
+        progs.append((e.ep, e.enc_descs, e.ectx, e.B_u, len(e.enc_descs)))
+    progs.append((e.dp, e.dec_descs, e.dctx, e.B, e.n_dec_sep))
+    out = []
+    for prog, descs, ctx, B, n_sep in progs:
+        for i, op in enumerate(prog.ops):
+            for kind in (('fused',) if i >= n_sep else ('fwd', 'bwd')):
+                out.append(('%s.%s' % (op.name, kind), kind, fns[kind], descs[i], ctx, B))
+    return out
+
+
+def launch_bytes(kind, d, B):
+    return conv_bytes(d, B, kind == 'fwd', fused=kind == 'fused')
+
+
 def profile_kernels(step, reps=20):
     """Per-launch device time of every codec operator, measured with HIP events on
     the stream the kernels run on; returns [(name, ms, bytes)]."""
     import ctypes as C
     from gpi import _lib as L
-    e = step.engine
-    lib = L.lib()
     st = L.stream_handle()
     out = []
-    progs = []
-    if e.ep is not None:
-        progs.append((e.ep, e.enc_descs, e.ectx, e.B_u))
-    progs.append((e.dp, e.dec_descs, e.dctx, e.B))
-    for prog, descs, ctx, B in progs:
-        for i, op in enumerate(prog.ops):
-            for fwd in (True, False):
-                fn = lib.gpi_conv_forward if fwd else lib.gpi_conv_backward
-                d = descs[i]
-                for _ in range(3):
-                    fn(C.byref(d), C.byref(ctx), st)
-                t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                t0.record()
-                for _ in range(reps):
-                    fn(C.byref(d), C.byref(ctx), st)
-                t1.record()
-                torch.cuda.synchronize()
-                out.append(('%s.%s' % (op.name, 'fwd' if fwd else 'bwd'), t0.elapsed_time(t1) / reps,
-                            conv_bytes(d, B, fwd)))
+    for name, kind, fn, d, ctx, B in step_conv_launches(step.engine):
+        for _ in range(3):
+            fn(C.byref(d), C.byref(ctx), st)
+        t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0.record()
+        for _ in range(reps):
+            fn(C.byref(d), C.byref(ctx), st)
+        t1.record()
+        torch.cuda.synchronize()
+        out.append((name, t0.elapsed_time(t1) / reps, launch_bytes(kind, d, B)))
     return out
 
 

@@ -1,4 +1,4 @@
-"""Every codec operator of the C64 ELBO step, forward and backward, launched N times each in a
+"""Every codec launch of the C64 ELBO step (forward, backward, fused output conv), N times each in a
 fixed order after one warm step -- the workload of the per-operator PMC passes
 (tools/pmc_round.sh).  Writes the launch manifest (op, direction, launches, algorithmic bytes per
 launch) to argv[1].  usage: python tools/pmc_all.py MANIFEST.json [N]"""
@@ -25,17 +25,12 @@ def main():
     step.step_eager()
     torch.cuda.synchronize()
     e = step.engine
-    lib = L.lib()
     st = L.stream_handle()
     manifest = []
-    for prog, descs, ctx, B in ((e.ep, e.enc_descs, e.ectx, e.B_u), (e.dp, e.dec_descs, e.dctx, e.B)):
-        for i, op in enumerate(prog.ops):
-            for fwd in (True, False):
-                fn = lib.gpi_conv_forward if fwd else lib.gpi_conv_backward
-                for _ in range(n):
-                    L.check(fn(C.byref(descs[i]), C.byref(ctx), st), op.name)
-                manifest.append(dict(op='%s.%s' % (op.name, 'fwd' if fwd else 'bwd'), launches=n,
-                                     algorithmic_bytes=bench.conv_bytes(descs[i], B, fwd)))
+    for name, kind, fn, d, ctx, B in bench.step_conv_launches(e):
+        for _ in range(n):
+            L.check(fn(C.byref(d), C.byref(ctx), st), name)
+        manifest.append(dict(op=name, launches=n, algorithmic_bytes=bench.launch_bytes(kind, d, B)))
     torch.cuda.synchronize()
     with open(out, 'w') as fh:
         json.dump(dict(conv_hip_sha1=bench.conv_source_sha(), launches=manifest), fh, indent=1)
