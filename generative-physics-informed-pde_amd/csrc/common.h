@@ -61,10 +61,24 @@ __device__ __forceinline__ void block_sum(float (&v)[NV], float* scratch, float*
 __device__ __forceinline__ int floordiv2(int x) { return x >> 1; }   // arithmetic shift = floor
 __device__ __forceinline__ int ceildiv2(int x) { return -((-x) >> 1); }
 
+// Group of sample s.  Branch-free over all GPI_MAX_GROUPS starts: every start is read up front, so the
+// kernel-argument loads join the entry batch (a data-dependent loop over the by-value argument array
+// costs one dependent scalar-load round trip per iteration).
 __device__ __forceinline__ int group_of(const gpi_groups& g, int s) {
     int k = 0;
-    while (k + 1 < g.n_groups && s >= g.start[k + 1]) ++k;
+#pragma unroll
+    for (int j = 1; j < GPI_MAX_GROUPS; ++j) k += (j < g.n_groups && s >= g.start[j]) ? 1 : 0;
     return k;
+}
+
+// arr[i] of a by-value kernel-argument array with a runtime index, as a select over all entries
+// (an indexed access would be a dependent scalar load after i is known)
+template <typename T, int N>
+__device__ __forceinline__ T karg_sel(const T (&arr)[N], int i) {
+    T v = arr[0];
+#pragma unroll
+    for (int j = 1; j < N; ++j) v = (i == j) ? arr[j] : v;
+    return v;
 }
 
 // train-mode BN coefficients from fp64 sums (biased variance, torch semantics)

@@ -92,7 +92,8 @@ struct ConvGeom {
     int g_sq, g_sr, g_sc;      // ... of the output-gradient image
     Div d_in4, d_P4, d_g4, d_PG4, d_cin, d_cout, d_win, d_tp, d_wout, d_w2;
 #ifdef GPI_PHASE_TIMING
-    int dbg;   // GPI_DBG_SKIP of the timing build (never the product): 1 skip wgrad, 2 dgrad, 4 loss atomics
+    int dbg;   // GPI_DBG_SKIP of the timing build (never the product): 1 skip wgrad, 2 dgrad, 4 loss atomics,
+              // 8 return after the operand loads, 16 return at entry
 #endif
 };
 
@@ -413,6 +414,24 @@ __device__ __forceinline__ T pin(T v) {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
+// Every 64-byte line of the kernel-argument segment, touched by ONE batch of scalar loads at entry.
+// The compiler issues argument loads lazily, next to their first use, and the large by-value
+// descriptors (~0.5 KB) made that 3 to 4 dependent round trips to the argument segment before a
+// tile's operand loads were even issued (tools/prologue_waits.sh).  With every line in the scalar
+// cache after this one round trip, the later lazy loads hit it.
+template <int NBYTES>
+__device__ __forceinline__ void touch_kernargs() {
+    const __attribute__((address_space(4))) uint32_t* ka =
+        (const __attribute__((address_space(4))) uint32_t*)__builtin_amdgcn_kernarg_segment_ptr();
+    constexpr int NL = (NBYTES + 63) / 64;
+    uint32_t x[NL];
+#pragma unroll
+    for (int i = 0; i < NL; ++i) x[i] = ka[16 * i];      // all lines in flight, one wait below
+#pragma unroll
+    for (int i = 0; i < NL; ++i) asm volatile("" : : "s"(x[i]));
+}
+constexpr int CONV_KARG_BYTES = (int)(sizeof(gpi_conv_desc) + sizeof(gpi_codec_ctx) + sizeof(ConvGeom) + 16);
+
 // Global-address-space views of (pinned, hence generic) pointers: ordinary loads and
 // stores through them stay global_load / global_store.  A flat access could alias LDS,
 // so the compiler would drain every outstanding LDS-DMA (vmcnt(0)) in front of it.
@@ -435,7 +454,7 @@ __device__ __forceinline__ TileIdx tile_of(const ConvGeom& G, const gpi_groups& 
     t.b = tile / G.tiles;
     t.oy0 = (tile - t.b * G.tiles) * G.th;
     t.grp = group_of(g, t.b);
-    t.gsz = g.start[t.grp + 1] - g.start[t.grp];
+    t.gsz = karg_sel(g.start, t.grp + 1) - karg_sel(g.start, t.grp);
     return t;
 }
 
@@ -503,6 +522,8 @@ constexpr int FWD_HDR = 8 * GPI_MAX_CIN + 2 * GPI_MAX_CIN + 64 + 16 + 8;
 
 template <int K, int S, int UP, int CP, int NPX>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void conv_fwd_kernel(gpi_conv_desc d, gpi_codec_ctx c, ConvGeom G) {
+    touch_kernargs<CONV_KARG_BYTES>();
+    if (SKIP(G, 16)) return;
     constexpr int KK = K * K;
     extern __shared__ __attribute__((aligned(16))) float smem[];
     double* gst = (double*)smem;
@@ -539,8 +560,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void c
     in_rows(K, S, UP, d.pad, T.oy0, G.th, iy0, rh_);
     stage_img(img, d.cin, G.rh, G.P, G.d_in4, G.d_P4, G.in_sq, G.in_sr, G.in_sc, iy0, d.h_in, d.w_in, zero,
               [&](int q) -> const float* { return ib + (int64_t)q * HWi; });
-    if (drop && tid >= 64 && tid < 64 + d.cout)      // (after the DMA issue: its wait overlaps the stat loads)
-        dsl[tid - 64] = *as_gld(ws + d.drop_off + (int64_t)T.b * d.cout + (tid - 64));
+    // (issued after the DMA; stored to LDS only after the stat loads are issued and waited for -- an
+    // LDS store of it right here would drain every outstanding DMA first: one more round trip)
+    float dsv = 1.f;
+    if (drop && tid >= 64 && tid < 64 + d.cout) dsv = *as_gld(ws + d.drop_off + (int64_t)T.b * d.cout + (tid - 64));
     if (d.in_bn) {
         float gam = 0.f, bet = 0.f;
         if (tid < d.cin) {
@@ -551,6 +574,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void c
         stat_issue(c.stats, c.n_stats, T.grp, d.in_stat, d.cin, gst, 0, 0, nullptr, zero, L);
         stat_finish(L);
         __syncthreads();
+        if (SKIP(G, 8)) return;
         PHASE(2);
         // ---- phase 2: BN coefficients
         if (tid < d.cin) {
@@ -563,6 +587,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void c
         // ---- phase 3: BN + ReLU in LDS
         activate_img(img, G, d, iy0, sc, sh);
     }
+    if (drop && tid >= 64 && tid < 64 + d.cout) dsl[tid - 64] = dsv;
     __syncthreads();
     PHASE(4);
 
@@ -646,11 +671,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void c
             const int64_t pix0 = (int64_t)oy * d.w_out + x0;
             if (gauss) {
                 if (active) {
-                    int row = T.b - c.groups.start[T.grp];
-                    if (c.tgt_idx[T.grp]) row = c.tgt_idx[T.grp][row];
-                    const float* tg = c.tgt[T.grp] + (int64_t)row * HWo + pix0;
+                    int row = T.b - karg_sel(c.groups.start, T.grp);
+                    if (const int32_t* ti = karg_sel(c.tgt_idx, T.grp)) row = ti[row];
+                    const float* tg = karg_sel(c.tgt, T.grp) + (int64_t)row * HWo + pix0;
                     const bool ex = d.epilogue == GPI_EPI_GAUSS_EXP_LOSS;
-                    const float scl = c.loss_scale[T.grp];
+                    const float scl = karg_sel(c.loss_scale, T.grp);
                     float g0[NPX], g1[NPX];
 #pragma unroll
                     for (int p = 0; p < NPX; ++p) {
@@ -712,9 +737,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void c
             const bool active = pix < tp;
             float tgt = 0.f;
             if (gauss && active) {
-                int row = T.b - c.groups.start[T.grp];
-                if (c.tgt_idx[T.grp]) row = c.tgt_idx[T.grp][row];
-                tgt = c.tgt[T.grp][(int64_t)row * HWo + oy * d.w_out + ox];
+                int row = T.b - karg_sel(c.groups.start, T.grp);
+                if (const int32_t* ti = karg_sel(c.tgt_idx, T.grp)) row = ti[row];
+                tgt = karg_sel(c.tgt, T.grp)[(int64_t)row * HWo + oy * d.w_out + ox];
             }
             PHASE(5);
             float acc[CP];
@@ -752,7 +777,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void c
                     const float emu = ex ? expf(mu) : 1.f;
                     const float r = ex ? expf(tgt) - emu : tgt - mu;
                     Lv += -0.5f * (2.f * ls + r * r * e + GPI_LOG2PI);
-                    const float scl = c.loss_scale[T.grp];
+                    const float scl = karg_sel(c.loss_scale, T.grp);
                     auto go = as_gst(ws + d.gout_off + (int64_t)T.b * 2 * HWo + oy * d.w_out + ox);
                     go[0] = -scl * r * e * emu;
                     go[HWo] = scl * (1.f - r * r * e);
@@ -838,8 +863,13 @@ constexpr int SLAB_ROWS = 4;    // partial-slab rows per workgroup: one per wave
 // forward first -- output rows [oy0 - K/2, oy0 + th + K/2) from an input image K/2 rows taller on each
 // side, the log-likelihood of its owned rows and the loss gradient straight into the LDS gradient
 // image -- then runs the backward on it: no output-gradient round trip through HBM, one launch less.
+#ifndef GPI_FUSE_WAVES
+#define GPI_FUSE_WAVES 5
+#endif
 template <int K, int S, int UP, bool FUSE = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 : 6))) void conv_bwd_kernel(gpi_conv_desc d, gpi_codec_ctx c, ConvGeom G) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (FUSE ? GPI_FUSE_WAVES : 4) : 6))) void conv_bwd_kernel(gpi_conv_desc d, gpi_codec_ctx c, ConvGeom G) {
+    touch_kernargs<CONV_KARG_BYTES>();
+    if (SKIP(G, 16)) return;
     constexpr int KK = K * K;
     extern __shared__ __attribute__((aligned(16))) float smem[];
     double* gst = (double*)smem;                      // [cin][4] input stats, then [cout][4] output stats
@@ -969,8 +999,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 
         bet = *as_gld(params + d.beta_off + tid);
     }
     const bool drop = d.drop_off >= 0;
-    if (tid >= 128 && tid < 128 + d.cout)
-        o_drop[tid - 128] = drop ? *as_gld(ws + d.drop_off + (int64_t)T.b * d.cout + (tid - 128)) : 1.f;
+    // the dropout scale goes to LDS after the stat loads (an LDS store of it here would drain every
+    // outstanding DMA before the stat loads are even issued)
+    float odv = 1.f;
+    if (drop && tid >= 128 && tid < 128 + d.cout) odv = *as_gld(ws + d.drop_off + (int64_t)T.b * d.cout + (tid - 128));
     {
         StatLoad L;
         stat_issue(c.stats, c.n_stats, T.grp, d.in_stat, d.in_bn ? d.cin : 0, gst, d.out_stat, obn ? d.cout : 0,
@@ -979,7 +1011,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 
         stat_finish(L);
         PHASE(11);
     }
+    if (tid >= 128 && tid < 128 + d.cout) o_drop[tid - 128] = odv;
     __syncthreads();
+    if (SKIP(G, 8)) return;
     PHASE(2);
 
     // ---- phase 2: coefficients
@@ -1128,11 +1162,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 
         constexpr int NPXF = 4, PADK = K / 2, NW = (NPXF - 1) + K;
         const int ng = G.gh * d.w_out / NPXF;
         float Lv = 0.f;
-        int trow0 = T.b - c.groups.start[T.grp];
-        if (c.tgt_idx[T.grp]) trow0 = c.tgt_idx[T.grp][trow0];
-        const float* tg = c.tgt[T.grp] + (int64_t)trow0 * HWo;
+        int trow0 = T.b - karg_sel(c.groups.start, T.grp);
+        if (const int32_t* ti = karg_sel(c.tgt_idx, T.grp)) trow0 = ti[trow0];
+        const float* tg = karg_sel(c.tgt, T.grp) + (int64_t)trow0 * HWo;
         const bool ex = d.epilogue == GPI_EPI_GAUSS_EXP_LOSS;
-        const float scl = c.loss_scale[T.grp];
+        const float scl = karg_sel(c.loss_scale, T.grp);
         for (int g = tid; g < ng; g += 256) {
             const int j = dq(g * NPXF, G.d_wout), x0 = g * NPXF - j * d.w_out;
             const int oy = gy0 + j;
@@ -1145,6 +1179,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 
             for (int p = 0; p < NPXF; ++p) mu[p] = ls[p] = 0.f;
             for (int ci = 0; ci < d.cin; ++ci) {
                 const float* arow = al + (ci * G.rh + j) * G.P + HALO + x0 - PADK;
+                // the channel's 2 x K x K weights are wave-uniform: scalar loads (constant address
+                // space) into SGPRs, FMA operands straight from there -- no LDS traffic for them
+                const auto* cw0 = (const __attribute__((address_space(4))) float*)(params + w_off + (int64_t)ci * KK);
+                const auto* cw1 = cw0 + d.cin * KK;
 #pragma unroll
                 for (int ky = 0; ky < K; ++ky) {
                     float win[NW];
@@ -1152,7 +1190,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 
                     for (int t = 0; t < NW; ++t) win[t] = arow[ky * G.P + t];
 #pragma unroll
                     for (int kx = 0; kx < K; ++kx) {
-                        const float w0 = wD[(ky * K + kx) * 16 + ci], w1 = wD[(KK + ky * K + kx) * 16 + ci];
+                        const float w0 = cw0[ky * K + kx], w1 = cw1[ky * K + kx];
 #pragma unroll
                         for (int p = 0; p < NPXF; ++p) {
                             mu[p] = fmaf(w0, win[p + kx], mu[p]);
@@ -1458,12 +1496,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 
             }
         }
     }
-    // ---- phase 4b': input gradient on the VALU (cin <= 4, 5x5, stride 1): two consecutive pixels of
-    // an owned row per thread, all (<= 4) input channels at once; weights are LDS broadcasts of
-    // the same zero-padded [co * KK + tap][16] table the MFMA path uses.
+    // ---- phase 4b': input gradient on the VALU (cin <= 4, 5x5, stride 1): Q consecutive pixels of an
+    // owned row per thread (4 for cin <= 2, 2 otherwise), all (<= 4) input channels at once.  The
+    // weights W[co][ci][ky][kx] are wave-uniform: scalar loads from the parameters (constant address
+    // space, SGPR operands of the FMAs), no LDS traffic for them; the output-gradient row window of
+    // the Q pixels is read from LDS once per (co, ky).
     float vsd[4] = {0.f, 0.f, 0.f, 0.f}, vsdx[4] = {0.f, 0.f, 0.f, 0.f};
     if (vdg && !SKIP(G, 2)) {
-        const int np2 = (G.ph * d.w_in) >> 1;
         float lg[4], lb[4], lr[4];
 #pragma unroll
         for (int ci = 0; ci < 4; ++ci) {
@@ -1472,43 +1511,45 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 
             lb[ci] = d.in_bn ? i_sh[cc] + i_mean[cc] * i_sc[cc] : 0.f;
             lr[ci] = d.in_bn ? 1.f / lg[ci] : 0.f;
         }
-        // two channels' accumulators when cin <= 2 (the 5x5 output conv), four otherwise
+        const auto* wg = (const __attribute__((address_space(4))) float*)(params + w_off);
         auto vdg_rows = [&](auto ci_c) {
             constexpr int CI = decltype(ci_c)::value;
-            for (int gq = tid; gq < np2; gq += 256) {
-                const int qy = dq(2 * gq, G.d_win), px0 = 2 * gq - qy * d.w_in;
+            constexpr int Q = CI == 2 ? 4 : 2;
+            const int npq = (G.ph * d.w_in) / Q;
+            for (int gq = tid; gq < npq; gq += 256) {
+                const int qy = dq(Q * gq, G.d_win), px0 = Q * gq - qy * d.w_in;
                 const int64_t pix = (int64_t)(py0 + qy) * d.w_in + px0;
                 const int64_t gbase_in = ((int64_t)T.b * d.in_ctot + d.in_c0) * HWi + pix;
-                float acc[CI][2];
+                float acc[CI][Q];
     #pragma unroll
-                for (int ci = 0; ci < CI; ++ci) acc[ci][0] = acc[ci][1] = 0.f;
+                for (int ci = 0; ci < CI; ++ci)
+    #pragma unroll
+                    for (int q = 0; q < Q; ++q) acc[ci][q] = 0.f;
                 for (int co = 0; co < d.cout; ++co) {
     #pragma unroll 1
                     for (int ky = 0; ky < K; ++ky) {
                         const float* grow = gl + co * gplane + (qy + py0 + d.pad - ky - gy0) * G.PG + HALO + px0 +
                                             d.pad - (K - 1);
-                        float gw[K + 1];
+                        float gw[K + Q - 1];
     #pragma unroll
-                        for (int t = 0; t < K + 1; ++t) gw[t] = grow[t];
+                        for (int t = 0; t < K + Q - 1; ++t) gw[t] = grow[t];
+                        float wv[CI][K];      // SGPRs: channel ci's row ky of W[co][ci]
+    #pragma unroll
+                        for (int ci = 0; ci < CI; ++ci) {
+                            const int cc = ci < d.cin ? ci : 0;
+    #pragma unroll
+                            for (int kx = 0; kx < K; ++kx) {
+                                const float w = wg[((int64_t)co * d.cin + cc) * KK + ky * K + kx];
+                                wv[ci][kx] = ci < d.cin ? w : 0.f;
+                            }
+                        }
     #pragma unroll
                         for (int kx = 0; kx < K; ++kx) {
-                            float wv[CI];
-                            if constexpr (CI == 4) {
-                                const f32x4 w4 = *(const f32x4*)(wD + (co * KK + ky * K + kx) * 16);
-                                wv[0] = w4[0];
-                                wv[1] = w4[1];
-                                wv[2] = w4[2];
-                                wv[3] = w4[3];
-                            } else {
-                                const float2 w2 = *(const float2*)(wD + (co * KK + ky * K + kx) * 16);
-                                wv[0] = w2.x;
-                                wv[1] = w2.y;
-                            }
     #pragma unroll
-                            for (int q = 0; q < 2; ++q) {
+                            for (int q = 0; q < Q; ++q) {
                                 const float gv = gw[q + K - 1 - kx];
     #pragma unroll
-                                for (int ci = 0; ci < CI; ++ci) acc[ci][q] = fmaf(wv[ci], gv, acc[ci][q]);
+                                for (int ci = 0; ci < CI; ++ci) acc[ci][q] = fmaf(wv[ci][kx], gv, acc[ci][q]);
                             }
                         }
                     }
@@ -1517,16 +1558,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 
                 for (int ci = 0; ci < CI; ++ci) {
                     if (ci >= d.cin) break;
                     const float* ap = alb + (ci * G.rh + (py0 - iy0 + qy)) * G.P + HALO + px0;
-                    const float av[2] = {ap[0], ap[1]};
-                    float pv[2] = {0.f, 0.f};
+                    float av[Q], pv[Q], o[Q];
+    #pragma unroll
+                    for (int q = 0; q < Q; ++q) {
+                        av[q] = ap[q];
+                        pv[q] = 0.f;
+                    }
                     if (d.gin_accumulate) {
                         auto pp = as_gld(ws + gin_off + gbase_in + (int64_t)ci * HWi);
-                        pv[0] = pp[0];
-                        pv[1] = pp[1];
-                    }
-                    float o[2];
     #pragma unroll
-                    for (int q = 0; q < 2; ++q) {
+                        for (int q = 0; q < Q; ++q) pv[q] = pp[q];
+                    }
+    #pragma unroll
+                    for (int q = 0; q < Q; ++q) {
                         if (d.in_bn) {
                             const float dbn = av[q] > 0.f ? acc[ci][q] : 0.f;
                             o[q] = pv[q] + lg[ci] * dbn;
@@ -1536,9 +1580,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? 4 
                             o[q] = pv[q] + acc[ci][q];
                         }
                     }
-                    auto op = as_gst(ws + gin_off + gbase_in + (int64_t)ci * HWi);
-                    op[0] = o[0];
-                    op[1] = o[1];
+                    store_px<Q>(ws + gin_off + gbase_in + (int64_t)ci * HWi, o);
                 }
             }
         };

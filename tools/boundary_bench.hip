@@ -20,6 +20,17 @@ __global__ __launch_bounds__(256) void layer_kernel(const float4* __restrict__ s
     }
 }
 
+__global__ __launch_bounds__(256) void layer_kernel_nt(const float4* __restrict__ src, float4* __restrict__ dst, int n4) {
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n4; i += gridDim.x * 256) {
+        float4 v = src[i];
+        v.x += 1.f;
+        __builtin_nontemporal_store(v.x, &dst[i].x);
+        __builtin_nontemporal_store(v.y, &dst[i].y);
+        __builtin_nontemporal_store(v.z, &dst[i].z);
+        __builtin_nontemporal_store(v.w, &dst[i].w);
+    }
+}
+
 __device__ __forceinline__ void grid_barrier(unsigned* cnt, unsigned target) {
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -46,7 +57,7 @@ __global__ void empty_kernel() {}
 
 int main() {
     const int L = 46;
-    const size_t sizes[] = {256 << 10, 2 << 20, 10 << 20};
+    const size_t sizes[] = {256 << 10, 2 << 20, 6 << 20, 10 << 20};
     const int grids[] = {288, 1024};
     float4* bufs;
     unsigned* cnt;
@@ -92,6 +103,25 @@ int main() {
             CHECK(hipEventSynchronize(e1));
             float ms_g;
             CHECK(hipEventElapsedTime(&ms_g, e0, e1));
+            // non-temporal stores
+            float ms_nt = 0;
+            {
+                hipGraph_t g2;
+                hipGraphExec_t ge2;
+                CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeGlobal));
+                for (int l = 0; l < L; ++l)
+                    hipLaunchKernelGGL(layer_kernel_nt, dim3(G), dim3(256), 0, s, bufs + (size_t)(l & 1) * n4,
+                                       bufs + (size_t)((l + 1) & 1) * n4, n4);
+                CHECK(hipStreamEndCapture(s, &g2));
+                CHECK(hipGraphInstantiate(&ge2, g2, nullptr, nullptr, 0));
+                for (int w = 0; w < 5; ++w) CHECK(hipGraphLaunch(ge2, s));
+                CHECK(hipEventRecord(e0, s));
+                for (int r = 0; r < 20; ++r) CHECK(hipGraphLaunch(ge2, s));
+                CHECK(hipEventRecord(e1, s));
+                CHECK(hipEventSynchronize(e1));
+                CHECK(hipEventElapsedTime(&ms_nt, e0, e1));
+            }
+            printf("S %6zu KB  grid %5d: graph nt-stores %.2f us/layer\n", S >> 10, G, 1e3 * ms_nt / 20 / L);
             // persistent
             float ms_p = 0;
             CHECK(hipMemsetAsync(cnt, 0, 256, s));
