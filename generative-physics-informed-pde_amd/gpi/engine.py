@@ -136,9 +136,10 @@ def dropout_views(ws, progs):
     return out
 
 
-def draw_dropout(ws, progs, stream, seed, offset_ptr=None, sub=20):
+def draw_dropout(ws, progs, stream, seed, offset_ptr=None, sub=20, only=None):
+    """Dropout2d scales of the programs (Philox sub id sub + position); only: the positions to draw."""
     for k, prog in enumerate(progs):
-        if prog is None or prog.drop_numel == 0:
+        if prog is None or prog.drop_numel == 0 or (only is not None and k not in only):
             continue
         _run(_lib().gpi_dropout_masks, ws.fptr(prog.drop_off), prog.drop_numel, prog.drop_rate, seed,
              offset_ptr, sub + k, stream, what='dropout masks')
@@ -409,9 +410,11 @@ class ElboEngine(object):
         scales (0 or 1/(1-p)) the next forward uses."""
         return dropout_views(self.ws, (('enc', self.ep, self.B_u), ('dec', self.dp, self.B)))
 
-    def draw_dropout(self, stream, seed, offset_ptr=None, sub=20):
-        """Fresh Dropout2d scales for every dropout conv of both codecs (device Philox)."""
-        draw_dropout(self.ws, (self.ep, self.dp), stream, seed, offset_ptr, sub)
+    def draw_dropout(self, stream, seed, offset_ptr=None, sub=20, codecs=('enc', 'dec')):
+        """Fresh Dropout2d scales for every dropout conv of the codecs (device Philox; the encoder's
+        stream is sub, the decoder's sub + 1 whichever are drawn)."""
+        draw_dropout(self.ws, (self.ep, self.dp), stream, seed, offset_ptr, sub,
+                     only=[k for k, c in enumerate(('enc', 'dec')) if c in codecs])
 
     def eps_x(self):
         """[N_ex, d_x] q_X noise (supervised rows, then VO rows unless held off; none in lockX)."""
@@ -568,10 +571,12 @@ class ElboEngine(object):
                     out['vo_entropy'] = float(t[T_ENT2]) + self.N_vo * ENT_CONST
         return out
 
-    def backward(self, stream=None, side_extra=None):
+    def backward(self, stream=None, side_extra=None, side_late=None):
         """Gradients of -ELBO into flat.gacc (fp64).  side_extra(side_stream_handle) is launched on
-        the side stream after the decoder's reductions, concurrently with the encoder backward
-        (the fused step draws the next step's noise there)."""
+        the side stream after the decoder's reductions, concurrently with the encoder backward, and
+        side_late(side_stream_handle) after every encoder launch (the fused step draws the next
+        step's noise and decoder masks in the first, the encoder's dropout masks -- read by the
+        encoder backward -- in the second)."""
         lib = _lib()
         st = stream if stream is not None else L.stream_handle()
         _run(lib.gpi_codec_backward, self.dec_descs, self.n_dec_sep, C.byref(self.dctx), st,
@@ -628,6 +633,8 @@ class ElboEngine(object):
         if n_enc:
             side.wait_event(self._ev_enc)
             run_reduce(self.reduce_enc[self.n_reduce_in:], self.ws, self.flat, sst)
+        if side_late is not None:
+            side_late(sst)
         self._ev_join2.record(side)
         main.wait_event(self._ev_join2)
 

@@ -107,12 +107,16 @@ class FusedElboStep(object):
         self._launch_noise(L.stream_handle(), self.idx, sub0=100)
 
     # ------------------------------------------------------------------
-    def _launch_noise(self, st, idx, sub0=0):
+    def _launch_noise(self, st, idx, sub0=0, codecs=('enc', 'dec'), masks_only=False):
         """Random subset into ``idx`` and the reparametrisation noise into the engine's eps
         buffers.  Philox streams: the step's offset (advanced by Adam at the end of every step)
         and sub ids sub0 + {1, 2, 3}; the noise drawn during step k (for step k+1) therefore
         differs from step k's own, which was drawn during step k-1 or by the prologue (sub0 = 100)."""
         lib = L.lib()
+        if self.engine.has_dropout and codecs:   # Dropout2d channel scales (sub ids sub0 + 4 enc, + 5 dec)
+            self.engine.draw_dropout(st, self.seed, L.ptr(self.rng_off), sub0 + 4, codecs=codecs)
+        if masks_only:
+            return
         if self.B_u:
             L.check(lib.gpi_random_subset(L.ptr(idx), self.n_pool, self.n_sub, self.subset_seed, L.ptr(self.rng_off),
                                           sub0 + 1, st), 'random subset')
@@ -121,8 +125,6 @@ class FusedElboStep(object):
         if self.engine.N_ex:
             ex = self.engine.eps_x()
             L.check(lib.gpi_randn(L.ptr(ex), ex.numel(), self.seed, L.ptr(self.rng_off), sub0 + 3, st), 'randn x')
-        if self.engine.has_dropout:      # Dropout2d channel scales of both codecs (sub ids sub0 + 4, + 5)
-            self.engine.draw_dropout(st, self.seed, L.ptr(self.rng_off), sub0 + 4)
 
     def forward_backward(self, stream=None):
         """One step without the parameter update.  The step's noise and subset were drawn by the
@@ -131,7 +133,11 @@ class FusedElboStep(object):
         reset, subset hand-over) is one launch."""
         st = stream if stream is not None else L.stream_handle()
         self.engine.forward(st, compute_value=False, zero_gacc=False, zero_scratch=False, running='defer')
-        self.engine.backward(st, side_extra=lambda sst: self._launch_noise(sst, self.idx_next))
+        # next step's subset / noise / decoder masks concurrently with the encoder backward; the
+        # encoder's masks once the encoder backward (which reads this step's) is done
+        self.engine.backward(st, side_extra=lambda sst: self._launch_noise(sst, self.idx_next, codecs=('dec',)),
+                             side_late=lambda sst: self._launch_noise(sst, self.idx_next, codecs=('enc',),
+                                                                      masks_only=True))
         L.check(L.lib().gpi_step_epilogue(C.byref(self.epi), st), 'step epilogue')
 
     def allreduce(self):
