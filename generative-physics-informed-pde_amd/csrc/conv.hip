@@ -93,7 +93,8 @@ struct ConvGeom {
     Div d_in4, d_P4, d_g4, d_PG4, d_cin, d_cout, d_win, d_tp, d_wout, d_w2;
 #ifdef GPI_PHASE_TIMING
     int dbg;   // GPI_DBG_SKIP of the timing build (never the product): 1 skip wgrad, 2 dgrad, 4 loss atomics,
-              // 8 return after the operand loads, 16 return at entry
+              // 8 return after the operand loads, 16 return at entry, 32 forward returns after its loads,
+              // 64 forward skips its compute loop, 128 forward skips its statistics epilogue
 #endif
 };
 
@@ -574,7 +575,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void c
         stat_issue(c.stats, c.n_stats, T.grp, d.in_stat, d.cin, gst, 0, 0, nullptr, zero, L);
         stat_finish(L);
         __syncthreads();
-        if (SKIP(G, 8)) return;
+        if (SKIP(G, 8) || SKIP(G, 32)) return;
         PHASE(2);
         // ---- phase 2: BN coefficients
         if (tid < d.cin) {
@@ -616,7 +617,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void c
             for (int p = 0; p < NPX; ++p)
 #pragma unroll
                 for (int co = 0; co < CP; ++co) acc[p][co] = 0.f;
-            if (active) {
+            if (active && !SKIP(G, 64)) {
                 const int plane = G.rh * G.P;
                 const int cb = UP ? fdiv2(x0 - PADK) + HALO : x0 * S - PADK + HALO;
                 for (int ci = 0; ci < d.cin; ++ci) {
@@ -745,7 +746,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void c
             float acc[CP];
     #pragma unroll
             for (int co = 0; co < CP; ++co) acc[co] = 0.f;
-            if (active) {
+            if (active && !SKIP(G, 64)) {
                 const int plane = G.rh * G.P;
                 for (int ci = 0; ci < d.cin; ++ci) {
                     const float* tci = img + ci * plane;
@@ -809,16 +810,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void c
 
     if (d.epilogue == GPI_EPI_GAUSS_LOSS || d.epilogue == GPI_EPI_GAUSS_EXP_LOSS) {
         float v[1] = {Lv};
-        block_sum<1>(v, scratch, red);
-        __syncthreads();
+        block_sum<1>(v, scratch, red);      // thread 0 wrote red[0] itself: no barrier before reading it
         if (tid == 0 && !SKIP(G, 4)) atomicAdd(c.loss_acc + T.grp * GPI_REPLICAS + blockIdx.x % GPI_REPLICAS, (double)red[0]);
         PHASE(7);
         RTSTAMP(1);
         return;
     }
-    if (d.epilogue == GPI_EPI_STORE_STATS) {
-        block_sum<2 * CP>(vst, scratch, red);
-        __syncthreads();
+    if (d.epilogue == GPI_EPI_STORE_STATS && !SKIP(G, 128)) {
+        block_sum<2 * CP>(vst, scratch, red);   // thread t < 2 CP wrote red[t] itself: no barrier
         if (tid < 2 * d.cout && !SKIP(G, 4)) {
             gpi_stat* st = stat_slot(c, d.out_stat + (tid >> 1), T.grp);
             atomicAdd((tid & 1) ? &st->sumsq : &st->sum, (double)red[tid]);
