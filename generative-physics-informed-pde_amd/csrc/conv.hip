@@ -974,8 +974,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
     owned_rows(S, UP, T.oy0, G.th, py0, ph_);
     // cin <= 4 at stride 1: the input gradient runs on the VALU (phase 4b'), the MFMA form would
     // leave >= 3/4 of its N = 16 columns empty
-    const bool vdg = K == 5 && S == 1 && !UP && has_gin && d.cin <= 4 && dg_role;
-    const int nmblk = (has_gin && dg_role && !vdg && !SKIP(G, 2)) ? (G.ph * d.w_in) >> 4 : 0;
+    // (FUSE: always the VALU input gradient -- launch() checks cin <= 4 -- so the MFMA input-gradient
+    // path and its operand registers compile away)
+    const bool vdg = FUSE || (K == 5 && S == 1 && !UP && has_gin && d.cin <= 4 && dg_role);
+    const int nmblk = (!FUSE && has_gin && dg_role && !vdg && !SKIP(G, 2)) ? (G.ph * d.w_in) >> 4 : 0;
     const int ci_l = min(l16, d.cin - 1);
     const bool cok = l16 < d.cin;
     const int64_t ibase = ((int64_t)T.b * d.in_ctot + d.in_c0 + ci_l) * HWi + (int64_t)py0 * d.w_in;
