@@ -42,14 +42,35 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 
 // Block-wide sum of NV per-thread values into red[0..NV) (caller syncs after).
 // scratch: >= NV * (blockDim/64) floats.
+// The NV wave sums run step-major (every value through one DPP step before the next step): NV
+// independent DPP ops per step keep the VALU busy instead of one dependent ladder per value with
+// the DPP wait states in between (value-major took ~1500 cycles for 16 values).
+template <int CTRL, int ROW_MASK, int NV>
+__device__ __forceinline__ void dpp_step(float (&v)[NV]) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] = dpp_add<CTRL, ROW_MASK>(v[i]);
+}
+
+// v[i] <- wave sum of v[i] (uniform), for NV values at once (step-major).
+template <int NV>
+__device__ __forceinline__ void wave_sums(float (&v)[NV]) {
+    dpp_step<0xb1, 0xf>(v);    // quad_perm [1,0,3,2]
+    dpp_step<0x4e, 0xf>(v);    // quad_perm [2,3,0,1]
+    dpp_step<0x124, 0xf>(v);   // row_ror:4
+    dpp_step<0x128, 0xf>(v);   // row_ror:8
+    dpp_step<0x142, 0xa>(v);   // row_bcast:15 into rows 1, 3
+    dpp_step<0x143, 0xc>(v);   // row_bcast:31 into rows 2, 3
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v[i]), 63));
+}
+
 template <int NV>
 __device__ __forceinline__ void block_sum(float (&v)[NV], float* scratch, float* red) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    wave_sums(v);
 #pragma unroll
-    for (int i = 0; i < NV; ++i) {
-        float s = wave_sum(v[i]);
-        if (lane == 0) scratch[i * nw + wid] = s;
-    }
+    for (int i = 0; i < NV; ++i)
+        if (lane == 0) scratch[i * nw + wid] = v[i];
     __syncthreads();
     if ((int)threadIdx.x < NV) {
         float s = 0.f;

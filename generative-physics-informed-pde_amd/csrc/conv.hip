@@ -1593,9 +1593,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
         __syncthreads();          // red aliases the offset table the input-gradient loop read
         if (vdg) {
             // per-thread channel sums: wave sums -> this wave's slab row (dgamma / dbeta partials) and LDS
+            float ws8[8] = {vsd[0], vsd[1], vsd[2], vsd[3], vsdx[0], vsdx[1], vsdx[2], vsdx[3]};
+            wave_sums(ws8);
 #pragma unroll
             for (int ci = 0; ci < 4; ++ci) {
-                const float a = wave_sum(vsd[ci]), b = wave_sum(vsdx[ci]);
+                const float a = ws8[ci], b = ws8[4 + ci];
                 if (lane == 0 && ci < d.cin) {
                     red[wv * 32 + ci] = a;
                     red[128 + wv * 32 + ci] = b;
