@@ -503,6 +503,28 @@ __device__ __forceinline__ void activate_img(float* img, const ConvGeom& G, cons
     }
 }
 
+// win[t] = p[t], t < NW, where p - OFF is 16-byte aligned (OFF in 0..3): whole 16-B LDS reads.
+// A wave's lanes take 4-pixel groups of consecutive rows; single-dword window reads of such a
+// layout hit 16 distinct banks 4 ways (rows 8 banks apart, lanes 4 apart), 16-B reads of 16 lanes
+// cover all 64 banks once.  Reads up to 4 * ceil((OFF + NW) / 4) floats from p - OFF (callers keep
+// that inside the row pitch).
+template <int NW, int OFF>
+__device__ __forceinline__ void lds_window(const float* p, float (&win)[NW]) {
+    constexpr int NCH = (OFF + NW + 3) / 4;
+    const float4* q = reinterpret_cast<const float4*>(p - OFF);
+    float buf[4 * NCH];
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+        const float4 v = q[c];
+        buf[4 * c] = v.x;
+        buf[4 * c + 1] = v.y;
+        buf[4 * c + 2] = v.z;
+        buf[4 * c + 3] = v.w;
+    }
+#pragma unroll
+    for (int t = 0; t < NW; ++t) win[t] = buf[OFF + t];
+}
+
 // NPX consecutive floats of one output row (16-B / 8-B aligned: x0 is a multiple of NPX, planes are
 // multiples of 4 floats, buffers 16-B aligned -- aligned_ok)
 template <int NPX>
@@ -628,8 +650,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void c
                         const int ry = UP ? (fdiv2(oy - PADK + ky) - iy0) : (ty * S + ky);
                         const float* trow = tci + ry * G.P;
                         float win[NW];
+                        if constexpr (!UP && (NPX * S) % 4 == 0) {
+                            // x0 * S is a multiple of 4: the window starts (HALO - K/2) mod 4 past a 16-B boundary
+                            lds_window<NW, (HALO - PADK) & 3>(trow, win);
+                        } else {
 #pragma unroll
-                        for (int t = 0; t < NW; ++t) win[t] = trow[t];
+                            for (int t = 0; t < NW; ++t) win[t] = trow[t];
+                        }
 #pragma unroll
                         for (int kx = 0; kx < K; ++kx) {
                             float wv[CP];
@@ -1187,8 +1214,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
 #pragma unroll
                 for (int ky = 0; ky < K; ++ky) {
                     float win[NW];
-#pragma unroll
-                    for (int t = 0; t < NW; ++t) win[t] = arow[ky * G.P + t];
+                    lds_window<NW, (HALO - PADK) & 3>(arow + ky * G.P, win);   // x0 multiple of 4
 #pragma unroll
                     for (int kx = 0; kx < K; ++kx) {
                         const float w0 = cw0[ky * K + kx], w1 = cw1[ky * K + kx];
@@ -1532,8 +1558,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
                         const float* grow = gl + co * gplane + (qy + py0 + d.pad - ky - gy0) * G.PG + HALO + px0 +
                                             d.pad - (K - 1);
                         float gw[K + Q - 1];
+                        if constexpr (Q == 4) {
+                            // px0 multiple of 4: the window starts (HALO + pad - (K - 1)) mod 4 past a 16-B boundary
+                            lds_window<K + Q - 1, (HALO + K / 2 - (K - 1)) & 3>(grow, gw);
+                        } else {
     #pragma unroll
-                        for (int t = 0; t < K + Q - 1; ++t) gw[t] = grow[t];
+                            for (int t = 0; t < K + Q - 1; ++t) gw[t] = grow[t];
+                        }
                         float wv[CI][K];      // SGPRs: channel ci's row ky of W[co][ci]
     #pragma unroll
                         for (int ci = 0; ci < CI; ++ci) {

@@ -557,3 +557,25 @@ def test_bn_running_statistics_match_reference(device):
             np.testing.assert_allclose(got, v, rtol=2e-5, atol=2e-6, err_msg=name)
         n += 1
     assert n > 0
+
+
+def test_fused_output_conv_matches_separate_launches(device, monkeypatch):
+    """gpi_conv_loss_fused (the decoder output conv's forward + Gaussian loss + backward in one launch,
+    the loss gradient kept in LDS) against the separate forward and backward launches of the same op
+    (GPI_FUSE_OUT=0 at engine construction): same ELBO (1e-6, the loss block-sum order differs) and
+    the same gradients of every parameter (1e-6 of each tensor's max)."""
+    d = load('elbo_c32.npz')
+    eps = (torch.cat([cuda(d['eps_enc']), cuda(d['eps_qz'])]), cuda(d['eps_qX']))
+    out = {}
+    for tag, env in (('fused', '1'), ('separate', '0')):
+        monkeypatch.setenv('GPI_FUSE_OUT', env)
+        model, bs = build_golden_model(d)
+        elbo = model.elbo(step=0, armortized_bs=bs, eps=eps)
+        (-elbo).backward()
+        eng = model._elbo_engine(bs, int(d['cfg'][5]), False)
+        assert eng.n_dec_sep == len(eng.dec_descs) - (1 if env == '1' else 0)
+        out[tag] = (elbo.item(), {k: p.grad.detach().cpu().numpy().copy() for k, p in model.named_parameters()})
+    (v1, g1), (v0, g0) = out['fused'], out['separate']
+    assert abs(v1 - v0) <= 1e-6 * abs(v0), (v1, v0)
+    for k in g0:
+        assert np.abs(g1[k] - g0[k]).max() <= 1e-6 * max(np.abs(g0[k]).max(), 1e-30), k
