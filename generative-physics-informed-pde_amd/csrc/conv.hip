@@ -145,6 +145,8 @@ int env_int(const char* name, int dflt) {
     return v && *v ? atoi(v) : dflt;
 }
 
+size_t bwd_lds_floats(const gpi_conv_desc& d, int rh, int P, int gh, int PG, int zreg, int split);
+
 bool conv_geom(const gpi_conv_desc& d, const gpi_groups& g, ConvGeom& G, bool fwd, bool fuse = false) {
     if (g.n_groups < 1 || g.n_groups > GPI_MAX_GROUPS) return false;
     if (d.cin < 1 || d.cin > GPI_MAX_CIN || d.cout < 1 || d.cout > GPI_MAX_COUT) return false;
@@ -1677,14 +1679,18 @@ size_t fwd_lds(const gpi_conv_desc& d, const ConvGeom& G, int cp) {
            ((size_t)pad256(FWD_HDR) + pad256(d.cin * d.k * d.k * cp) + img_floats(d.cin, G.rh, G.P));
 }
 
-size_t bwd_lds(const gpi_conv_desc& d, const ConvGeom& G) {
+size_t bwd_lds_floats(const gpi_conv_desc& d, int rh, int P, int gh, int PG, int zreg, int split) {
+    (void)split;
     const int KD4 = (d.cout * d.k * d.k + 3) & ~3;
-    const int gimg = img_floats(d.cout, G.gh, G.PG);
-    const bool zimg = d.gout_mode == 0 && !G.zreg;             // z image in LDS
+    const int gimg = img_floats(d.cout, gh, PG);
+    const bool zimg = d.gout_mode == 0 && !zreg;             // z image in LDS
     // offset table, at least BWD_RED floats: the channel-sum scratch aliases it
-    size_t f = (size_t)bwd_hdr(d.cin, d.cout) + (d.gin_off >= 0 ? pad256(KD4 * 16) + pad256((d.stride == 2 ? 8 : 1) * KD4) : 0) + gimg +
-               (zimg ? gimg : 0) + img_floats(d.cin, G.rh, G.P);
-    return f * sizeof(float);
+    return (size_t)bwd_hdr(d.cin, d.cout) + (d.gin_off >= 0 ? pad256(KD4 * 16) + pad256((d.stride == 2 ? 8 : 1) * KD4) : 0) +
+           gimg + (zimg ? gimg : 0) + img_floats(d.cin, rh, P);
+}
+
+size_t bwd_lds(const gpi_conv_desc& d, const ConvGeom& G) {
+    return sizeof(float) * bwd_lds_floats(d, G.rh, G.P, G.gh, G.PG, G.zreg, G.split);
 }
 
 typedef void (*conv_kernel_t)(gpi_conv_desc, gpi_codec_ctx, ConvGeom);
@@ -1917,6 +1923,8 @@ extern "C" int gpi_conv_launch_info(const gpi_conv_desc* op, const gpi_groups* g
     info[2] = (int32_t)(fwd ? fwd_lds(*op, G, cp) : bwd_lds(*op, G));
     info[3] = cp;
     info[4] = G.npx;
+    info[5] = G.P;
+    info[6] = G.PG;
     return GPI_OK;
 }
 

@@ -423,7 +423,8 @@ int gpi_conv_blocks(const gpi_conv_desc* op, const gpi_groups* groups, int32_t* 
 /* Launch geometry of one conv pass (fwd != 0: forward) for tuning / profiling tools:
  * info[0] output rows per tile, info[1] workgroups, info[2] LDS bytes per workgroup,
  * info[3] output channels per forward thread, info[4] adjacent output pixels per forward thread
- * (1 for the backward).  info holds >= 5 entries.  No device work. */
+ * (1 for the backward), info[5] / info[6] LDS row pitch (floats) of the input / output-gradient
+ * images.  info holds >= 7 entries.  No device work. */
 int gpi_conv_launch_info(const gpi_conv_desc* op, const gpi_groups* groups, int fwd, int32_t* info);
 int gpi_conv_forward(const gpi_conv_desc* op, const gpi_codec_ctx* ctx, void* stream);
 int gpi_conv_backward(const gpi_conv_desc* op, const gpi_codec_ctx* ctx, void* stream);

@@ -32,11 +32,11 @@ def main(cfg='c64', vgpr_wgs=(6, 4)):
             for fwd in (1, 0):
                 info = (C.c_int32 * 8)()
                 L.check(lib.gpi_conv_launch_info(C.byref(descs[i]), C.byref(g), fwd, info), op.name)
-                th, nb, lds, cp, npx = list(info)[:5]
+                th, nb, lds, cp, npx, P, PG = list(info)[:7]
                 per_cu = min(LDS_CU // max(lds, 1), vgpr_wgs[1] if (op.k == 5 and not fwd) else vgpr_wgs[0])
-                print('%s %-40s %s k%d s%d up%d %2d->%-2d %3dx%-3d th %3d npx %d blocks %5d lds %6d  wg/cu %d  rounds %.2f' % (
+                print('%s %-40s %s k%d s%d up%d %2d->%-2d %3dx%-3d th %3d npx %d P %3d PG %3d blocks %5d lds %6d  wg/cu %d  rounds %.2f' % (
                     kind, op.name, 'fwd' if fwd else 'bwd', op.k, op.stride, op.upsample, op.cin, op.cout,
-                    op.dst.H, op.dst.W, th, npx, nb, lds, per_cu, nb / (per_cu * CUS)))
+                    op.dst.H, op.dst.W, th, npx, P, PG, nb, lds, per_cu, nb / (per_cu * CUS)))
 
 
 if __name__ == '__main__':
