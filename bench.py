@@ -327,10 +327,12 @@ def main():
     ap.add_argument('--no-roofline', action='store_true')
     ap.add_argument('--kprof', default=None, help='write the per-operator HIP-event profile (JSON) here')
     args = ap.parse_args()
-    dbg = sorted(k for k in os.environ if k.startswith('GPI_DBG_'))
+    dbg = sorted(k for k in os.environ if k.startswith('GPI_DBG_') or k == 'GPI_PHASE_TIMING')
     if dbg:
-        raise SystemExit('bench.py refuses to report with %s set (timing-build switches that skip work)' % dbg)
-    tuning = {k: os.environ[k] for k in sorted(os.environ) if k.startswith('GPI_TILE_')}
+        raise SystemExit('bench.py refuses to report with %s set (timing build / switches that skip work)' % dbg)
+    # any other GPI_* variable is a tuning knob (tiles, pixel blocking, role split, output-conv fusion,
+    # graph all-reduce, an A/B build of the library): recorded in the JSON line
+    tuning = {k: os.environ[k] for k in sorted(os.environ) if k.startswith('GPI_')}
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
