@@ -335,9 +335,11 @@ __global__ __launch_bounds__(256) void vo_moments_kernel(gpi_vo_moments_desc d, 
 constexpr int LT = 32;   // Lambda tile
 
 // Lambda[a][b] = sum_i Gamma[a][i] cov_i Gamma[b][i] (+ vo_var on the diagonal), lower tiles
-// (ta >= tb) computed and mirrored.  cov_i = 1 / (double) prec_i.
+// (ta >= tb) computed and mirrored.  cov_i = 1 / (double) prec_i, formed once per k-step by 32
+// threads (not per tile element).  The next k-step's Gamma tiles are loaded into registers while
+// the current one is multiplied (one global round trip per k-step hidden behind the FMAs).
 __global__ __launch_bounds__(256) void vo_lambda_kernel(gpi_vo_condition_desc d) {
-    __shared__ double As[LT][LT + 1], Bs[LT][LT + 1];
+    __shared__ double As[LT][LT + 1], Bs[LT][LT + 1], cv[LT];
     const int j = blockIdx.y;
     int t = blockIdx.x, ta = 0;
     while (t > ta) { t -= ta + 1; ++ta; }
@@ -347,20 +349,28 @@ __global__ __launch_bounds__(256) void vo_lambda_kernel(gpi_vo_condition_desc d)
     const float* prec = d.prec + (int64_t)j * dy;
     const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
     double acc[2][2] = {{0.0, 0.0}, {0.0, 0.0}};
-    for (int k0 = 0; k0 < dy; k0 += LT) {
-        for (int e = threadIdx.x; e < LT * LT; e += 256) {
-            const int rr = e / LT, cc = e - rr * LT;
-            const int i = k0 + cc;
-            const int a = ta * LT + rr, b = tb * LT + rr;
-            double av = 0.0, bv = 0.0;
-            if (i < dy) {
-                const double cov = 1.0 / (double)prec[i];
-                if (a < m) av = gam[(int64_t)a * dy + i] * cov;
-                if (b < m) bv = gam[(int64_t)b * dy + i];
-            }
-            As[rr][cc] = av;
-            Bs[rr][cc] = bv;
+    // this thread's 4 elements of each 32 x 32 tile: rows rr = (tid >> 5) + 8 u, column cc = tid & 31
+    const int cc = threadIdx.x & 31, r0 = threadIdx.x >> 5;
+    double pa[4], pb[4], pc = 0.0;
+    auto fetch = [&](int k0) {
+        const int i = k0 + cc;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int a = ta * LT + r0 + 8 * u, b = tb * LT + r0 + 8 * u;
+            pa[u] = (i < dy && a < m) ? gam[(int64_t)a * dy + i] : 0.0;
+            pb[u] = (i < dy && b < m) ? gam[(int64_t)b * dy + i] : 0.0;
         }
+        pc = (threadIdx.x < LT && k0 + (int)threadIdx.x < dy) ? (double)prec[k0 + threadIdx.x] : 1.0;
+    };
+    fetch(0);
+    for (int k0 = 0; k0 < dy; k0 += LT) {
+        if (threadIdx.x < LT) cv[threadIdx.x] = 1.0 / pc;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) Bs[r0 + 8 * u][cc] = pb[u];
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < 4; ++u) As[r0 + 8 * u][cc] = pa[u] * cv[cc];
+        if (k0 + LT < dy) fetch(k0 + LT);      // next tiles in flight during the FMAs below
         __syncthreads();
 #pragma unroll 8
         for (int c = 0; c < LT; ++c) {
