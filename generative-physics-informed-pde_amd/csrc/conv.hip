@@ -145,7 +145,6 @@ int env_int(const char* name, int dflt) {
     return v && *v ? atoi(v) : dflt;
 }
 
-size_t bwd_lds_floats(const gpi_conv_desc& d, int rh, int P, int gh, int PG, int zreg, int split);
 
 bool conv_geom(const gpi_conv_desc& d, const gpi_groups& g, ConvGeom& G, bool fwd, bool fuse = false) {
     if (g.n_groups < 1 || g.n_groups > GPI_MAX_GROUPS) return false;
@@ -1679,8 +1678,7 @@ size_t fwd_lds(const gpi_conv_desc& d, const ConvGeom& G, int cp) {
            ((size_t)pad256(FWD_HDR) + pad256(d.cin * d.k * d.k * cp) + img_floats(d.cin, G.rh, G.P));
 }
 
-size_t bwd_lds_floats(const gpi_conv_desc& d, int rh, int P, int gh, int PG, int zreg, int split) {
-    (void)split;
+size_t bwd_lds_floats(const gpi_conv_desc& d, int rh, int P, int gh, int PG, int zreg) {
     const int KD4 = (d.cout * d.k * d.k + 3) & ~3;
     const int gimg = img_floats(d.cout, gh, PG);
     const bool zimg = d.gout_mode == 0 && !zreg;             // z image in LDS
@@ -1690,7 +1688,7 @@ size_t bwd_lds_floats(const gpi_conv_desc& d, int rh, int P, int gh, int PG, int
 }
 
 size_t bwd_lds(const gpi_conv_desc& d, const ConvGeom& G) {
-    return sizeof(float) * bwd_lds_floats(d, G.rh, G.P, G.gh, G.PG, G.zreg, G.split);
+    return sizeof(float) * bwd_lds_floats(d, G.rh, G.P, G.gh, G.PG, G.zreg);
 }
 
 typedef void (*conv_kernel_t)(gpi_conv_desc, gpi_codec_ctx, ConvGeom);
