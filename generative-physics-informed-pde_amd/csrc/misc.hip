@@ -28,6 +28,15 @@ __global__ __launch_bounds__(256) void step_epilogue_kernel(gpi_step_epilogue_de
         d.scratch[i] = 0.0;
     }
     if (i < d.n_idx) d.idx_dst[i] = d.idx_src[i];
+    if (i * 4 < d.drop_n) {                      // gpi_dropout_masks' draw, Philox block i
+        const uint64_t base = d.drop_offset ? *d.drop_offset : 0;
+        const uint4_ r = philox(base + (uint64_t)i, d.drop_sub, d.drop_seed);
+        const float u[4] = {u01(r.x), u01(r.y), u01(r.z), u01(r.w)};
+        const float scale = 1.f / (1.f - d.drop_p);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (i * 4 + k < d.drop_n) d.drop_out[i * 4 + k] = u[k] < d.drop_p ? 0.f : scale;
+    }
 }
 
 // torch.optim.Adam single-tensor math (torch/optim/adam.py, defaults:
@@ -157,8 +166,10 @@ extern "C" int gpi_step_epilogue(const gpi_step_epilogue_desc* d, void* stream) 
     if ((d->n && (!d->gacc || !d->grad)) || (d->n_scratch && !d->scratch) || (d->n_terms && !d->terms_dst) ||
         (d->n_idx && (!d->idx_src || !d->idx_dst)))
         return GPI_ERR_ARG;
+    if (d->drop_n < 0 || (d->drop_n && (!d->drop_out || !(d->drop_p >= 0.f && d->drop_p < 1.f)))) return GPI_ERR_ARG;
     int64_t m = d->n > d->n_scratch ? d->n : d->n_scratch;
     if (d->n_idx > m) m = d->n_idx;
+    if ((d->drop_n + 3) / 4 > m) m = (d->drop_n + 3) / 4;
     const int64_t nb = m > 0 ? (m + 255) / 256 : 1;
     hipLaunchKernelGGL(step_epilogue_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, *d);
     GPI_CHECK_LAUNCH();

@@ -152,7 +152,8 @@ class VoGalerkinDesc(C.Structure):
 class StepEpilogueDesc(C.Structure):
     _fields_ = [('gacc', vp), ('grad', vp), ('n', i64), ('flags', i32), ('n_terms', i32), ('step', vp),
                 ('scratch', vp), ('n_scratch', i64), ('terms_dst', vp), ('idx_src', vp), ('idx_dst', vp),
-                ('n_idx', i64)]
+                ('n_idx', i64), ('drop_out', vp), ('drop_n', i64), ('drop_p', f32), ('_pad2', i32),
+                ('drop_seed', u64), ('drop_offset', vp), ('drop_sub', u64)]
 
 
 class FomDesc(C.Structure):

@@ -571,12 +571,11 @@ class ElboEngine(object):
                     out['vo_entropy'] = float(t[T_ENT2]) + self.N_vo * ENT_CONST
         return out
 
-    def backward(self, stream=None, side_extra=None, side_late=None):
+    def backward(self, stream=None, side_extra=None):
         """Gradients of -ELBO into flat.gacc (fp64).  side_extra(side_stream_handle) is launched on
-        the side stream after the decoder's reductions, concurrently with the encoder backward, and
-        side_late(side_stream_handle) after every encoder launch (the fused step draws the next
-        step's noise and decoder masks in the first, the encoder's dropout masks -- read by the
-        encoder backward -- in the second)."""
+        the side stream after the decoder's reductions, concurrently with the encoder backward (the
+        fused step draws the next step's subset, noise and decoder dropout masks there; nothing it
+        writes may be read by the encoder backward)."""
         lib = _lib()
         st = stream if stream is not None else L.stream_handle()
         _run(lib.gpi_codec_backward, self.dec_descs, self.n_dec_sep, C.byref(self.dctx), st,
@@ -633,8 +632,6 @@ class ElboEngine(object):
         if n_enc:
             side.wait_event(self._ev_enc)
             run_reduce(self.reduce_enc[self.n_reduce_in:], self.ws, self.flat, sst)
-        if side_late is not None:
-            side_late(sst)
         self._ev_join2.record(side)
         main.wait_event(self._ev_join2)
 

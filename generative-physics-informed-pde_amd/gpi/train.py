@@ -102,12 +102,22 @@ class FusedElboStep(object):
                                       n_scratch=ws.t_scr.numel(), terms_dst=self.last_terms.data_ptr(),
                                       idx_src=self.idx_next.data_ptr(), idx_dst=self.idx.data_ptr(),
                                       n_idx=self.n_sub if self.B_u else 0)
+        # the next step's encoder Dropout2d masks: drawn by the epilogue (after the encoder backward,
+        # which reads this step's), Philox sub id 4 as _launch_noise(sub0=0) would
+        ep = self.engine.ep
+        if ep is not None and ep.drop_numel > 0:
+            self.epi.drop_out = self.engine.ws.fptr(ep.drop_off).value
+            self.epi.drop_n = ep.drop_numel
+            self.epi.drop_p = ep.drop_rate
+            self.epi.drop_seed = self.seed
+            self.epi.drop_offset = self.rng_off.data_ptr()
+            self.epi.drop_sub = 4
         self.graph = None
         # the first step's noise; every step then draws the next step's during its backward
         self._launch_noise(L.stream_handle(), self.idx, sub0=100)
 
     # ------------------------------------------------------------------
-    def _launch_noise(self, st, idx, sub0=0, codecs=('enc', 'dec'), masks_only=False):
+    def _launch_noise(self, st, idx, sub0=0, codecs=('enc', 'dec')):
         """Random subset into ``idx`` and the reparametrisation noise into the engine's eps
         buffers.  Philox streams: the step's offset (advanced by Adam at the end of every step)
         and sub ids sub0 + {1, 2, 3}; the noise drawn during step k (for step k+1) therefore
@@ -115,8 +125,6 @@ class FusedElboStep(object):
         lib = L.lib()
         if self.engine.has_dropout and codecs:   # Dropout2d channel scales (sub ids sub0 + 4 enc, + 5 dec)
             self.engine.draw_dropout(st, self.seed, L.ptr(self.rng_off), sub0 + 4, codecs=codecs)
-        if masks_only:
-            return
         if self.B_u:
             L.check(lib.gpi_random_subset(L.ptr(idx), self.n_pool, self.n_sub, self.subset_seed, L.ptr(self.rng_off),
                                           sub0 + 1, st), 'random subset')
@@ -134,10 +142,8 @@ class FusedElboStep(object):
         st = stream if stream is not None else L.stream_handle()
         self.engine.forward(st, compute_value=False, zero_gacc=False, zero_scratch=False, running='defer')
         # next step's subset / noise / decoder masks concurrently with the encoder backward; the
-        # encoder's masks once the encoder backward (which reads this step's) is done
-        self.engine.backward(st, side_extra=lambda sst: self._launch_noise(sst, self.idx_next, codecs=('dec',)),
-                             side_late=lambda sst: self._launch_noise(sst, self.idx_next, codecs=('enc',),
-                                                                      masks_only=True))
+        # encoder's masks by the epilogue below (the encoder backward reads this step's)
+        self.engine.backward(st, side_extra=lambda sst: self._launch_noise(sst, self.idx_next, codecs=('dec',)))
         L.check(L.lib().gpi_step_epilogue(C.byref(self.epi), st), 'step epilogue')
 
     def allreduce(self):

@@ -485,6 +485,16 @@ typedef struct gpi_step_epilogue_desc {
     const int32_t* idx_src;
     int32_t* idx_dst;
     int64_t n_idx;
+    /* optional Dropout2d draw folded into the epilogue (exactly gpi_dropout_masks(drop_out, drop_n,
+     * drop_p, drop_seed, drop_offset, drop_sub)): the fused step draws the next step's encoder masks
+     * here, after the encoder backward that reads the current ones, without a launch of its own */
+    float* drop_out;
+    int64_t drop_n;            /* 0: no draw */
+    float drop_p;
+    int32_t _pad2;
+    uint64_t drop_seed;
+    const uint64_t* drop_offset;
+    uint64_t drop_sub;
 } gpi_step_epilogue_desc;
 int gpi_step_epilogue(const gpi_step_epilogue_desc* d, void* stream);
 int gpi_adam(const gpi_adam_desc* d, void* stream);
