@@ -192,6 +192,19 @@ def test_fused_step_c64(device, droprate):
         masks = engine_relu_masks(ref_model._elbo_engine(bs, int(d['cfg'][5]), False))
         step.forward_backward()
         torch.cuda.synchronize()
+        if droprate > 0:
+            # the next step's masks, drawn during this step (decoder: side stream; encoder: the step
+            # epilogue) = gpi_dropout_masks at this step's Philox offset, sub ids 4 (enc) / 5 (dec)
+            from gpi import _lib as L
+            for k, sub in (('enc', 4), ('dec', 5)):
+                prog = e.ep if k == 'enc' else e.dp
+                ref_m = torch.empty(prog.drop_numel, dtype=torch.float32, device='cuda')
+                L.check(L.lib().gpi_dropout_masks(L.ptr(ref_m), prog.drop_numel, prog.drop_rate, step.seed,
+                                                  L.ptr(step.rng_off), sub, L.stream_handle()), 'masks')
+                torch.cuda.synchronize()
+                got_m = e.ws.view(prog.drop_off, prog.drop_numel)
+                assert torch.equal(got_m, ref_m), k
+                assert not all(torch.equal(v, drops[k][n]) for n, v in e.dropout_views()[k].items()), k
         ocodec.MASK_AUDIT.clear()
         val = oracle_elbo(st, d['Xu'][idx], d['Xs'], d['Y'], d['F'], eps_z[:bs], eps_z[bs:], eps_x, nc, n // nc,
                           masks=masks, drops={k: {n: v.double().cpu() for n, v in dd.items()}
