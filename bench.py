@@ -310,10 +310,14 @@ def step_bytes(model, B_u, N_s, physics):
 
 
 def conv_source_sha():
-    """sha1 of csrc/conv.hip: PMC traffic figures are only used for the code they were measured on."""
+    """sha1 of csrc/conv.hip + csrc/common.h (the conv kernels' sources): PMC traffic figures are only
+    used for the code they were measured on."""
     import hashlib
-    with open(os.path.join(PKG, 'csrc', 'conv.hip'), 'rb') as fh:
-        return hashlib.sha1(fh.read()).hexdigest()
+    h = hashlib.sha1()
+    for f in ('conv.hip', 'common.h'):
+        with open(os.path.join(PKG, 'csrc', f), 'rb') as fh:
+            h.update(fh.read())
+    return h.hexdigest()
 
 
 def main():
