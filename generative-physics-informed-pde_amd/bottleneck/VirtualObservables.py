@@ -491,6 +491,7 @@ class QuerryEnsemble(object):
                                       for n, q in enumerate(self._querries)):
             self._gamma = torch.stack([q.Gamma for q in self._querries]).contiguous()
             self._alpha = torch.stack([q.alpha for q in self._querries]).contiguous()
+            self.generation = getattr(self, 'generation', 0) + 1
         return self._gamma
 
     @property
@@ -768,6 +769,9 @@ class VirtualObservablesEnsemble(BaseVirtualObservablesEnsemble):
         self._logsig32 = torch.zeros(N, dy, dtype=torch.float32, device=device)
         self._has_posterior = False
         self._ws = None
+        self.sparse = True          # column-sparse kernels when Gamma's columns allow (CGR / flux rows)
+        self._plan = None
+        self._plan_key = None
         self._mean_vo_variances = self._get_mean_vo_variances()
         self._set_member_variance_values(self._mean_vo_variances)
         self._precision_initialized = False
@@ -819,6 +823,19 @@ class VirtualObservablesEnsemble(BaseVirtualObservablesEnsemble):
             vo._vars = self._vars64[n]
 
     # ------------------------------------------------------------------ updates
+    def _sparse_plan(self):
+        """SparsePlan of the ensemble's Gamma, rebuilt when Gamma is replaced; None when disabled or when
+        Gamma has test-function rows (dense, and redrawn in place by resample)."""
+        qe = self._QuerryEnsemble
+        if not self.sparse or getattr(qe, '_aux', None):
+            return None
+        gamma = qe.gamma
+        key = (gamma.data_ptr(), tuple(gamma.shape), getattr(qe, 'generation', 0))
+        if key != self._plan_key:
+            self._plan = V.SparsePlan.build(gamma)
+            self._plan_key = key
+        return self._plan
+
     def update(self, G, PREC, iteration, writer=None):
         self.update_vo_precision(iteration, writer)
         qe = self._QuerryEnsemble
@@ -827,7 +844,8 @@ class VirtualObservablesEnsemble(BaseVirtualObservablesEnsemble):
             self._ws = V.ConditionWorkspace(self.N, self.m, self.dim_out, gamma.device)
         V.vo_condition(gamma, alpha, G.detach().to(torch.float32).contiguous(),
                        PREC.detach().to(torch.float32).contiguous(), self._mean_vo_variances.contiguous(),
-                       self._mean64, self._vars64, self._mean32, self._logsig32, ws=self._ws)
+                       self._mean64, self._vars64, self._mean32, self._logsig32, ws=self._ws,
+                       sparse=self._sparse_plan())
         self._has_posterior = True
         self._bind_members()
         self.flush_cache()
@@ -853,7 +871,7 @@ class VirtualObservablesEnsemble(BaseVirtualObservablesEnsemble):
             vo_var = torch.empty_like(beta)
             inf = self.infinite_precision_mask.to(torch.int32).contiguous()
             V.vo_precision(qe.gamma, qe.alpha, self._mean64, self._vars64, inf, beta, vo_var,
-                           alpha0=self._alpha_0, beta0=self._beta_0)
+                           alpha0=self._alpha_0, beta0=self._beta_0, sparse=self._sparse_plan())
             self._prec_beta = beta
             self._mean_vo_variances = vo_var
             self._set_member_variance_values(self._mean_vo_variances)

@@ -135,7 +135,8 @@ extern "C" int gpi_struct_sizes(int64_t* out, int n) {
                          (int64_t)sizeof(gpi_vo_moments_desc), (int64_t)sizeof(gpi_vo_condition_desc),
                          (int64_t)sizeof(gpi_vo_precision_desc), (int64_t)sizeof(gpi_gp_sample_desc),
                          (int64_t)sizeof(gpi_vo_galerkin_desc), (int64_t)sizeof(gpi_step_epilogue_desc),
-                         (int64_t)sizeof(gpi_fom_desc), (int64_t)sizeof(gpi_random_field_desc)};
+                         (int64_t)sizeof(gpi_fom_desc), (int64_t)sizeof(gpi_random_field_desc),
+                         (int64_t)sizeof(gpi_vo_sparse)};
     const int k = (int)(sizeof(s) / sizeof(s[0]));
     if (!out || n < k) return GPI_ERR_ARG;
     for (int i = 0; i < k; ++i) out[i] = s[i];

@@ -498,14 +498,18 @@ __global__ __launch_bounds__(256) void vo_chol_kernel(gpi_vo_condition_desc d) {
     else chol_block(A, m, bad);
     if (bad && d.flag && tid == 0) atomicOr(d.flag, 1);
     if (!LDS) return;       // large m: b by vo_rhs_kernel, solves by vo_solvec_kernel
-    // b = Gamma g - alpha
-    const double* gam = d.gamma + (int64_t)j * m * dy;
-    const float* g = d.g + (int64_t)j * dy;
-    for (int a = wid; a < m; a += 4) {
-        double s = 0.0;
-        for (int i = lane; i < dy; i += 64) s = fma(gam[(int64_t)a * dy + i], (double)g[i], s);
-        s = wave_sum_d(s);
-        if (lane == 0) b[a] = s - d.alpha[(int64_t)j * m + a];
+    // b = Gamma g - alpha (column-sparse path: already in solvec, vo_rhs_sparse_kernel)
+    if (d.sparse) {
+        for (int a = tid; a < m; a += 256) b[a] = d.solvec[(int64_t)j * m + a];
+    } else {
+        const double* gam = d.gamma + (int64_t)j * m * dy;
+        const float* g = d.g + (int64_t)j * dy;
+        for (int a = wid; a < m; a += 4) {
+            double s = 0.0;
+            for (int i = lane; i < dy; i += 64) s = fma(gam[(int64_t)a * dy + i], (double)g[i], s);
+            s = wave_sum_d(s);
+            if (lane == 0) b[a] = s - d.alpha[(int64_t)j * m + a];
+        }
     }
     __syncthreads();
     // L z = b, L^T x = z
@@ -714,6 +718,176 @@ __global__ __launch_bounds__(256) void vo_columns_kernel(gpi_vo_condition_desc d
     if (d.logsig32) d.logsig32[o] = 0.5f * logf((float)var);
 }
 
+// ---------------------------------------------------------------- column-sparse conditioning
+// With gpi_vo_sparse (CGR / flux rows: <= VS_R nonzeros per column, the same rows in every sample):
+//   Lambda      one thread per (pair (a, b), sample): sum over the columns holding both rows
+//   b           one wave per (row a, sample) over the row's nonzeros
+//   Lambda^-1   U U^T with U = L^-T (upper triangle of lam after vo_linv), 32 x 32 tiles
+//   columns     one thread per (column i, sample): Gamma_i . solvec and Gamma_i^T Lambda^-1 Gamma_i
+//               from the column's <= VS_R slots (|L^-1 Gamma_i|^2 without forming L^-1 Gamma_i)
+// Every sum runs in a fixed order (reproducible).
+constexpr int VS_R = 16;
+
+// nz[a, i] = 1 if gamma[j, a, i] != 0 for some sample j (16 loads in flight per thread)
+__global__ __launch_bounds__(256) void vo_nz_kernel(const double* gamma, int n, int m, int dy, uint8_t* nz) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= (int64_t)m * dy) return;
+    const int64_t plane = (int64_t)m * dy;
+    bool any = false;
+    for (int j0 = 0; j0 < n && !any; j0 += 16) {
+        double v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[u] = (j0 + u < n) ? gamma[(int64_t)(j0 + u) * plane + e] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) any = any || (v[u] != 0.0);
+    }
+    nz[e] = any ? 1 : 0;
+}
+
+__global__ __launch_bounds__(256) void vo_pattern_kernel(const uint8_t* nz, int m, int dy, int r, int32_t* rows,
+                                                         int32_t* count) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= dy) return;
+    int c = 0;
+    for (int a = 0; a < m; ++a)
+        if (nz[(int64_t)a * dy + i]) {
+            if (c < r) rows[(int64_t)i * r + c] = a;
+            ++c;
+        }
+    for (int s = c; s < r; ++s) rows[(int64_t)i * r + s] = -1;
+    count[i] = c;
+}
+
+__global__ __launch_bounds__(256) void vo_sparse_values_kernel(const double* gamma, int n, int m, int dy,
+                                                               gpi_vo_sparse sp) {
+    const int i = blockIdx.x * 256 + threadIdx.x, j = blockIdx.y;
+    if (i >= dy) return;
+    const double* gj = gamma + (int64_t)j * m * dy;
+    double* out = const_cast<double*>(sp.vals) + ((int64_t)j * dy + i) * sp.r;
+    for (int s = 0; s < sp.r; ++s) {
+        const int a = sp.rows[(int64_t)i * sp.r + s];
+        out[s] = a >= 0 ? gj[(int64_t)a * dy + i] : 0.0;
+    }
+}
+
+__global__ __launch_bounds__(256) void vo_lambda_sparse_kernel(gpi_vo_condition_desc d, gpi_vo_sparse sp) {
+    const int p = blockIdx.x * 256 + threadIdx.x, j = blockIdx.y;
+    if (p >= sp.n_pairs) return;
+    const int m = d.m, r = sp.r, rr = r * r;
+    const double* v = sp.vals + (int64_t)j * d.d_y * r;
+    const float* prec = d.prec + (int64_t)j * d.d_y;
+    double acc = 0.0;
+    const int e1 = sp.pair_ptr[p + 1];
+    for (int e = sp.pair_ptr[p]; e < e1; ++e) {
+        const int src = sp.pair_src[e];
+        const int i = src / rr, st = src - i * rr, s = st / r, t = st - s * r;
+        acc = fma(v[i * r + s] / (double)prec[i], v[i * r + t], acc);
+    }
+    const int ab = sp.pair_ab[p], a = ab / m, b = ab - a * m;
+    if (a == b) acc += d.vo_var[a];
+    double* lam = d.lam + (int64_t)j * m * m;
+    lam[(int64_t)a * m + b] = acc;
+    lam[(int64_t)b * m + a] = acc;
+}
+
+// b = Gamma g - alpha into solvec, one wave per (row a, sample j)
+__global__ __launch_bounds__(256) void vo_rhs_sparse_kernel(gpi_vo_condition_desc d, gpi_vo_sparse sp) {
+    const int lane = threadIdx.x & 63, a = blockIdx.x * 4 + (threadIdx.x >> 6), j = blockIdx.y;
+    if (a >= d.m) return;                                  // wave-uniform
+    const double* v = sp.vals + (int64_t)j * d.d_y * sp.r;
+    const float* g = d.g + (int64_t)j * d.d_y;
+    double s = 0.0;
+    const int e1 = sp.row_ptr[a + 1];
+    for (int e = sp.row_ptr[a] + lane; e < e1; e += 64) {
+        const int src = sp.row_src[e];
+        s = fma(v[src], (double)g[src / sp.r], s);
+    }
+    s = wave_sum_d(s);
+    if (lane == 0) d.solvec[(int64_t)j * d.m + a] = s - d.alpha[(int64_t)j * d.m + a];
+}
+
+// Lambda^-1 = L^-T L^-1 = U U^T, U[a][c] = (L^-1)_{ca}: lam[a m + c] for c > a, 1 / lam[a m + a] at c = a;
+// lower 32 x 32 tiles (ta >= tb) computed and mirrored; the c-loop starts at row tile ta (U is upper).
+__global__ __launch_bounds__(256) void vo_inv_kernel(gpi_vo_condition_desc d, gpi_vo_sparse sp) {
+    __shared__ double As[LT][LT + 1], Bs[LT][LT + 1];
+    const int j = blockIdx.y;
+    int t = blockIdx.x, ta = 0;
+    while (t > ta) { t -= ta + 1; ++ta; }
+    const int tb = t, m = d.m;
+    const double* lam = d.lam + (int64_t)j * m * m;
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+    const int cc = threadIdx.x & 31, r0 = threadIdx.x >> 5;
+    auto U = [&](int a, int c) -> double {
+        if (a >= m || c >= m || c < a) return 0.0;
+        const double x = lam[(int64_t)a * m + c];
+        return c == a ? 1.0 / x : x;
+    };
+    double acc[2][2] = {{0.0, 0.0}, {0.0, 0.0}};
+    for (int c0 = ta * LT; c0 < m; c0 += LT) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            As[r0 + 8 * u][cc] = U(ta * LT + r0 + 8 * u, c0 + cc);
+            Bs[r0 + 8 * u][cc] = U(tb * LT + r0 + 8 * u, c0 + cc);
+        }
+        __syncthreads();
+#pragma unroll 8
+        for (int c = 0; c < LT; ++c) {
+            const double a0 = As[ty][c], a1 = As[ty + 16][c];
+            const double b0 = Bs[tx][c], b1 = Bs[tx + 16][c];
+            acc[0][0] = fma(a0, b0, acc[0][0]);
+            acc[0][1] = fma(a0, b1, acc[0][1]);
+            acc[1][0] = fma(a1, b0, acc[1][0]);
+            acc[1][1] = fma(a1, b1, acc[1][1]);
+        }
+        __syncthreads();
+    }
+    double* inv = sp.inv + (int64_t)j * m * m;
+    for (int u = 0; u < 2; ++u)
+        for (int v = 0; v < 2; ++v) {
+            const int a = ta * LT + ty + 16 * u, b = tb * LT + tx + 16 * v;
+            if (a >= m || b >= m || b > a) continue;
+            inv[(int64_t)a * m + b] = acc[u][v];
+            inv[(int64_t)b * m + a] = acc[u][v];
+        }
+}
+
+// Posterior of column i of sample j from its slots: mean_i = g_i - cov_i Gamma_i . solvec,
+// vars_i = cov_i - cov_i^2 Gamma_i^T Lambda^-1 Gamma_i.
+__global__ __launch_bounds__(256) void vo_columns_sparse_kernel(gpi_vo_condition_desc d, gpi_vo_sparse sp) {
+    const int i = blockIdx.x * 256 + threadIdx.x, j = blockIdx.y;
+    if (i >= d.d_y) return;
+    const int m = d.m, r = sp.r;
+    int rw[VS_R];
+    double v[VS_R];
+#pragma unroll
+    for (int s = 0; s < VS_R; ++s) {
+        rw[s] = s < r ? sp.rows[(int64_t)i * r + s] : -1;
+        v[s] = rw[s] >= 0 ? sp.vals[((int64_t)j * d.d_y + i) * r + s] : 0.0;
+    }
+    const double* inv = sp.inv + (int64_t)j * m * m;
+    const double* sv = d.solvec + (int64_t)j * m;
+    double smv = 0.0, qn = 0.0;
+#pragma unroll
+    for (int s = 0; s < VS_R; ++s) {
+        if (rw[s] < 0) continue;
+        const double* ia = inv + (int64_t)rw[s] * m;
+        smv = fma(v[s], sv[rw[s]], smv);
+        double off = 0.0;
+#pragma unroll
+        for (int t = 0; t < s; ++t)
+            if (rw[t] >= 0) off = fma(v[t], ia[rw[t]], off);
+        qn = fma(v[s], fma(2.0, off, v[s] * ia[rw[s]]), qn);
+    }
+    const int64_t o = (int64_t)j * d.d_y + i;
+    const double cov = 1.0 / (double)d.prec[o];
+    const double mean = (double)d.g[o] - cov * smv;
+    const double var = cov - cov * cov * qn;
+    d.mean[o] = mean;
+    d.vars[o] = var;
+    if (d.mean32) d.mean32[o] = (float)mean;
+    if (d.logsig32) d.logsig32[o] = 0.5f * logf((float)var);
+}
+
 // ---------------------------------------------------------------- precision
 // One workgroup per (row a, VO sample j): its term (Gamma_j mean_j - alpha_j)_a^2 + (Gamma_j^2 vars_j)_a
 // into terms[a, j]; vo_precision_final sums them over j in order (reproducible) into beta / vo_var.
@@ -739,6 +913,29 @@ __global__ __launch_bounds__(256) void vo_precision_kernel(gpi_vo_precision_desc
         const double r1 = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]) - d.alpha[(int64_t)j * m + a];
         const double r2 = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
         d.terms[(int64_t)a * d.n + j] = r1 * r1 + r2;
+    }
+}
+
+// The same terms from the column-sparse view: one wave per (row a, sample j) over the row's nonzeros.
+__global__ __launch_bounds__(256) void vo_precision_sparse_kernel(gpi_vo_precision_desc d, gpi_vo_sparse sp) {
+    const int lane = threadIdx.x & 63, a = blockIdx.x, j = blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (j >= d.n) return;                                  // wave-uniform
+    const double* v = sp.vals + (int64_t)j * d.d_y * sp.r;
+    const double* mu = d.mean + (int64_t)j * d.d_y;
+    const double* va = d.vars + (int64_t)j * d.d_y;
+    double s1 = 0.0, s2 = 0.0;
+    const int e1 = sp.row_ptr[a + 1];
+    for (int e = sp.row_ptr[a] + lane; e < e1; e += 64) {
+        const int src = sp.row_src[e], i = src / sp.r;
+        const double gv = v[src];
+        s1 = fma(gv, mu[i], s1);
+        s2 = fma(gv * gv, va[i], s2);
+    }
+    s1 = wave_sum_d(s1);
+    s2 = wave_sum_d(s2);
+    if (lane == 0) {
+        const double r1 = s1 - d.alpha[(int64_t)j * d.m + a];
+        d.terms[(int64_t)a * d.n + j] = r1 * r1 + s2;
     }
 }
 
@@ -897,23 +1094,43 @@ extern "C" int gpi_vo_moments(const gpi_vo_moments_desc* d, void* stream) {
     return GPI_OK;
 }
 
+static bool sparse_ok(const gpi_vo_sparse& sp, int m) {
+    return sp.r >= 1 && sp.r <= VS_R && sp.n_pairs >= m && sp.rows && sp.vals && sp.pair_ptr && sp.pair_ab &&
+           sp.pair_src && sp.row_ptr && sp.row_src;
+}
+
 extern "C" int gpi_vo_condition(const gpi_vo_condition_desc* d, void* stream) {
-    if (!d || !d->gamma || !d->alpha || !d->g || !d->prec || !d->vo_var || !d->lam || !d->solvec || !d->mean ||
-        !d->vars || d->n < 0 || d->m < 1 || d->d_y < 1)
+    if (!d || !d->alpha || !d->g || !d->prec || !d->vo_var || !d->lam || !d->solvec || !d->mean || !d->vars ||
+        d->n < 0 || d->m < 1 || d->d_y < 1 || (!d->gamma && !d->sparse))
         return GPI_ERR_ARG;
+    if (d->sparse && (!sparse_ok(*d->sparse, d->m) || !d->sparse->inv)) return GPI_ERR_ARG;
     if (d->m > VS_MAXM) return GPI_ERR_UNSUPPORTED;
     if (d->n == 0) return GPI_OK;
     const hipStream_t st = (hipStream_t)stream;
     const int T = (d->m + LT - 1) / LT;
-    hipLaunchKernelGGL(vo_lambda_kernel, dim3(T * (T + 1) / 2, d->n), dim3(256), 0, st, *d);
-    GPI_CHECK_LAUNCH();
     const size_t lds_small = sizeof(double) * ((size_t)d->m * d->m + d->m);
-    if (lds_small <= 64 * 1024) {
-        hipLaunchKernelGGL(vo_chol_kernel<true>, dim3(d->n), dim3(256), lds_small, st, *d);
-    } else {
-        hipLaunchKernelGGL(vo_rhs_kernel, dim3(d->m, d->n), dim3(256), 0, st, *d);
+    if (d->sparse) {
+        const gpi_vo_sparse sp = *d->sparse;
+        if (hipMemsetAsync(d->lam, 0, sizeof(double) * (size_t)d->n * d->m * d->m, st) != hipSuccess)
+            return GPI_ERR_LAUNCH;
+        hipLaunchKernelGGL(vo_lambda_sparse_kernel, dim3((sp.n_pairs + 255) / 256, d->n), dim3(256), 0, st, *d, sp);
         GPI_CHECK_LAUNCH();
-        hipLaunchKernelGGL(vo_chol_kernel<false>, dim3(d->n), dim3(256), sizeof(double) * d->m, st, *d);
+        hipLaunchKernelGGL(vo_rhs_sparse_kernel, dim3((d->m + 3) / 4, d->n), dim3(256), 0, st, *d, sp);
+        GPI_CHECK_LAUNCH();
+        if (lds_small <= 64 * 1024)
+            hipLaunchKernelGGL(vo_chol_kernel<true>, dim3(d->n), dim3(256), lds_small, st, *d);
+        else
+            hipLaunchKernelGGL(vo_chol_kernel<false>, dim3(d->n), dim3(256), sizeof(double) * d->m, st, *d);
+    } else {
+        hipLaunchKernelGGL(vo_lambda_kernel, dim3(T * (T + 1) / 2, d->n), dim3(256), 0, st, *d);
+        GPI_CHECK_LAUNCH();
+        if (lds_small <= 64 * 1024) {
+            hipLaunchKernelGGL(vo_chol_kernel<true>, dim3(d->n), dim3(256), lds_small, st, *d);
+        } else {
+            hipLaunchKernelGGL(vo_rhs_kernel, dim3(d->m, d->n), dim3(256), 0, st, *d);
+            GPI_CHECK_LAUNCH();
+            hipLaunchKernelGGL(vo_chol_kernel<false>, dim3(d->n), dim3(256), sizeof(double) * d->m, st, *d);
+        }
     }
     GPI_CHECK_LAUNCH();
     if (d->m <= 256) hipLaunchKernelGGL(vo_linv_wave_kernel, dim3((d->m + 3) / 4, d->n), dim3(256), 0, st, *d);
@@ -921,18 +1138,52 @@ extern "C" int gpi_vo_condition(const gpi_vo_condition_desc* d, void* stream) {
     GPI_CHECK_LAUNCH();
     if (lds_small > 64 * 1024) hipLaunchKernelGGL(vo_solvec_kernel, dim3(d->n), dim3(256), 0, st, *d);
     GPI_CHECK_LAUNCH();
-    hipLaunchKernelGGL(vo_columns_kernel, dim3((d->d_y + VC_BN - 1) / VC_BN, d->n), dim3(256), 0, st, *d);
+    if (d->sparse) {
+        const gpi_vo_sparse sp = *d->sparse;
+        hipLaunchKernelGGL(vo_inv_kernel, dim3(T * (T + 1) / 2, d->n), dim3(256), 0, st, *d, sp);
+        GPI_CHECK_LAUNCH();
+        hipLaunchKernelGGL(vo_columns_sparse_kernel, dim3((d->d_y + 255) / 256, d->n), dim3(256), 0, st, *d, sp);
+    } else {
+        hipLaunchKernelGGL(vo_columns_kernel, dim3((d->d_y + VC_BN - 1) / VC_BN, d->n), dim3(256), 0, st, *d);
+    }
+    GPI_CHECK_LAUNCH();
+    return GPI_OK;
+}
+
+extern "C" int gpi_vo_pattern(const double* gamma, int32_t n, int32_t m, int32_t d_y, int32_t r, int32_t* rows,
+                              int32_t* count, uint8_t* work, void* stream) {
+    if (!gamma || !rows || !count || !work || n < 1 || m < 1 || d_y < 1 || r < 1) return GPI_ERR_ARG;
+    const hipStream_t st = (hipStream_t)stream;
+    const int64_t md = (int64_t)m * d_y;
+    hipLaunchKernelGGL(vo_nz_kernel, dim3((unsigned)((md + 255) / 256)), dim3(256), 0, st, gamma, n, m, d_y, work);
+    GPI_CHECK_LAUNCH();
+    hipLaunchKernelGGL(vo_pattern_kernel, dim3((d_y + 255) / 256), dim3(256), 0, st, work, m, d_y, r, rows, count);
+    GPI_CHECK_LAUNCH();
+    return GPI_OK;
+}
+
+extern "C" int gpi_vo_sparse_values(const double* gamma, int32_t n, int32_t m, int32_t d_y, const gpi_vo_sparse* sp,
+                                    void* stream) {
+    if (!gamma || !sp || !sp->rows || !sp->vals || sp->r < 1 || n < 0 || m < 1 || d_y < 1) return GPI_ERR_ARG;
+    if (n == 0) return GPI_OK;
+    hipLaunchKernelGGL(vo_sparse_values_kernel, dim3((d_y + 255) / 256, n), dim3(256), 0, (hipStream_t)stream, gamma,
+                       n, m, d_y, *sp);
     GPI_CHECK_LAUNCH();
     return GPI_OK;
 }
 
 extern "C" int gpi_vo_precision(const gpi_vo_precision_desc* d, void* stream) {
-    if (!d || !d->gamma || !d->alpha || !d->mean || !d->vars || !d->beta || !d->vo_var || d->n < 0 || d->m < 1 ||
-        d->d_y < 1 || (d->n > 0 && !d->terms))
+    if (!d || (!d->gamma && !d->sparse) || !d->alpha || !d->mean || !d->vars || !d->beta || !d->vo_var || d->n < 0 ||
+        d->m < 1 || d->d_y < 1 || (d->n > 0 && !d->terms))
         return GPI_ERR_ARG;
+    if (d->sparse && !sparse_ok(*d->sparse, d->m)) return GPI_ERR_ARG;
     const hipStream_t st = (hipStream_t)stream;
     if (d->n > 0) {
-        hipLaunchKernelGGL(vo_precision_kernel, dim3(d->m, d->n), dim3(256), 0, st, *d);
+        if (d->sparse)
+            hipLaunchKernelGGL(vo_precision_sparse_kernel, dim3(d->m, (d->n + 3) / 4), dim3(256), 0, st, *d,
+                               *d->sparse);
+        else
+            hipLaunchKernelGGL(vo_precision_kernel, dim3(d->m, d->n), dim3(256), 0, st, *d);
         GPI_CHECK_LAUNCH();
     }
     hipLaunchKernelGGL(vo_precision_final, dim3((d->m + 255) / 256), dim3(256), 0, st, *d);

@@ -128,13 +128,19 @@ class VoMomentsDesc(C.Structure):
 class VoConditionDesc(C.Structure):
     _fields_ = [('n', i32), ('m', i32), ('d_y', i32), ('_pad', i32),
                 ('gamma', vp), ('alpha', vp), ('g', vp), ('prec', vp), ('vo_var', vp), ('lam', vp), ('solvec', vp),
-                ('mean', vp), ('vars', vp), ('mean32', vp), ('logsig32', vp), ('flag', vp)]
+                ('mean', vp), ('vars', vp), ('mean32', vp), ('logsig32', vp), ('flag', vp), ('sparse', vp)]
 
 
 class VoPrecisionDesc(C.Structure):
     _fields_ = [('n', i32), ('m', i32), ('d_y', i32), ('_pad', i32),
                 ('gamma', vp), ('alpha', vp), ('mean', vp), ('vars', vp), ('infinite', vp),
-                ('alpha0', C.c_double), ('beta0', C.c_double), ('beta', vp), ('vo_var', vp), ('terms', vp)]
+                ('alpha0', C.c_double), ('beta0', C.c_double), ('beta', vp), ('vo_var', vp), ('terms', vp),
+                ('sparse', vp)]
+
+
+class VoSparse(C.Structure):
+    _fields_ = [('r', i32), ('n_pairs', i32), ('rows', vp), ('vals', vp), ('pair_ptr', vp), ('pair_ab', vp),
+                ('pair_src', vp), ('row_ptr', vp), ('row_src', vp), ('inv', vp)]
 
 
 class GpSampleDesc(C.Structure):
@@ -168,7 +174,7 @@ class RandomFieldDesc(C.Structure):
 
 STRUCTS = [Stat, Groups, ConvDesc, CodecCtx, ReduceItem, HeadDesc, GemmItem, RomDesc, ResidualDesc, AdamDesc,
            VoQueryDesc, VoMomentsDesc, VoConditionDesc, VoPrecisionDesc, GpSampleDesc,
-           VoGalerkinDesc, StepEpilogueDesc, FomDesc, RandomFieldDesc]
+           VoGalerkinDesc, StepEpilogueDesc, FomDesc, RandomFieldDesc, VoSparse]
 
 # name -> (restype, argtypes)
 SIGNATURES = {
@@ -205,6 +211,8 @@ SIGNATURES = {
     'gpi_vo_galerkin': (C.c_int, [C.POINTER(VoGalerkinDesc), vp]),
     'gpi_vo_condition': (C.c_int, [C.POINTER(VoConditionDesc), vp]),
     'gpi_vo_precision': (C.c_int, [C.POINTER(VoPrecisionDesc), vp]),
+    'gpi_vo_pattern': (C.c_int, [vp, i32, i32, i32, i32, vp, vp, vp, vp]),
+    'gpi_vo_sparse_values': (C.c_int, [vp, i32, i32, i32, C.POINTER(VoSparse), vp]),
     'gpi_gauss_sample': (C.c_int, [vp, vp, vp, i64, i32, i32, vp, u64, vp, u64, vp]),
     'gpi_gp_sample': (C.c_int, [C.POINTER(GpSampleDesc), vp]),
     'gpi_predictive_scores': (C.c_int, [vp, vp, vp, i32, i32, vp, vp]),

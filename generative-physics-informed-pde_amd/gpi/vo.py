@@ -6,6 +6,7 @@ what the kernels assume.
 """
 import ctypes as C
 
+import numpy as np
 import torch
 
 from . import _lib as L
@@ -93,6 +94,85 @@ def vo_moments(uc, nc, refine, n, n_mc, logsig_y=None, eps=None, seed=0, offset=
     return mean, std, prec
 
 
+VS_R = 16        # slots per column of the column-sparse view (csrc/vo.hip VS_R)
+
+
+def sparse_index_lists(rows, m):
+    """Index lists of the column-sparse view (include/gpi.h gpi_vo_sparse) from the column pattern
+    rows [d_y, r] (ascending row per slot, -1 = empty): the contributions of every column to the
+    Lambda entries (a >= b, all diagonals present) grouped by entry, and the nonzeros of every row.
+    Host bookkeeping only (once per Gamma); every sum over them runs on the device."""
+    rows = np.asarray(rows, dtype=np.int64)
+    dy, r = rows.shape
+    S, T = np.tril_indices(r)                       # s >= t: rows[i, s] >= rows[i, t]
+    a, b = rows[:, S], rows[:, T]
+    ok = (a >= 0) & (b >= 0)
+    ii = np.broadcast_to(np.arange(dy)[:, None], a.shape)
+    key = (a * m + b)[ok]
+    src = ((ii * r + S[None, :]) * r + T[None, :])[ok]
+    diag = np.arange(m, dtype=np.int64) * (m + 1)
+    pair_ab = np.union1d(key, diag)
+    pidx = np.searchsorted(pair_ab, key)
+    order = np.lexsort((src, pidx))
+    pair_src = src[order]
+    pair_ptr = np.zeros(len(pair_ab) + 1, dtype=np.int64)
+    np.cumsum(np.bincount(pidx, minlength=len(pair_ab)), out=pair_ptr[1:])
+    ra = rows.reshape(-1)
+    rsrc = np.nonzero(ra >= 0)[0]
+    rorder = np.lexsort((rsrc, ra[rsrc]))
+    row_src = rsrc[rorder]
+    row_ptr = np.zeros(m + 1, dtype=np.int64)
+    np.cumsum(np.bincount(ra[rsrc], minlength=m), out=row_ptr[1:])
+    i32 = lambda x: np.ascontiguousarray(x, dtype=np.int32)
+    return dict(pair_ab=i32(pair_ab), pair_ptr=i32(pair_ptr), pair_src=i32(pair_src), row_ptr=i32(row_ptr),
+                row_src=i32(row_src))
+
+
+class SparsePlan(object):
+    """Column-sparse view of a Gamma [N, m, d_y] whose columns have <= VS_R nonzero rows in the union
+    over samples (CGR / flux rows); ``build`` returns None for denser Gamma (the dense kernels then run).
+    Tied to the values of the Gamma it was built from: rebuild after Gamma changes."""
+
+    @classmethod
+    def build(cls, gamma, r_max=VS_R):
+        _dev(gamma)
+        assert gamma.dtype == torch.float64 and gamma.is_contiguous() and gamma.dim() == 3
+        N, m, dy = gamma.shape
+        r_max = min(int(r_max), VS_R)
+        rows = torch.empty(dy, r_max, dtype=torch.int32, device=gamma.device)
+        count = torch.empty(dy, dtype=torch.int32, device=gamma.device)
+        work = torch.empty(m, dy, dtype=torch.uint8, device=gamma.device)
+        L.check(L.lib().gpi_vo_pattern(_p(gamma), N, m, dy, r_max, _p(rows), _p(count), _p(work),
+                                       L.stream_handle()), 'vo pattern')
+        cmax = int(count.max().item())
+        if cmax > r_max:
+            return None
+        self = cls()
+        self.r = max(cmax, 1)
+        rows_h = rows[:, :self.r].cpu().numpy()
+        lists = sparse_index_lists(rows_h, m)
+        dev = gamma.device
+        self.rows = torch.from_numpy(np.ascontiguousarray(rows_h, dtype=np.int32)).to(dev)
+        for k, v in lists.items():
+            setattr(self, k, torch.from_numpy(v).to(dev))
+        self.n_pairs = int(len(lists['pair_ab']))
+        self.vals = torch.empty(N, dy, self.r, dtype=torch.float64, device=dev)
+        self.inv = torch.empty(N, m, m, dtype=torch.float64, device=dev)
+        self.shape = (N, m, dy)
+        self.desc = L.VoSparse(r=self.r, n_pairs=self.n_pairs, rows=_p(self.rows), vals=_p(self.vals),
+                               pair_ptr=_p(self.pair_ptr), pair_ab=_p(self.pair_ab), pair_src=_p(self.pair_src),
+                               row_ptr=_p(self.row_ptr), row_src=_p(self.row_src), inv=_p(self.inv))
+        self.refresh(gamma)
+        return self
+
+    def refresh(self, gamma):
+        """Re-gather the slot values from gamma (same pattern)."""
+        assert tuple(gamma.shape) == self.shape and gamma.is_contiguous()
+        N, m, dy = self.shape
+        L.check(L.lib().gpi_vo_sparse_values(_p(gamma), N, m, dy, C.byref(self.desc), L.stream_handle()),
+                'vo sparse values')
+
+
 class ConditionWorkspace(object):
     def __init__(self, N, m, dy, device):
         self.lam = torch.empty(N, m, m, dtype=torch.float64, device=device)
@@ -100,8 +180,9 @@ class ConditionWorkspace(object):
         self.flag = torch.zeros(1, dtype=torch.int32, device=device)
 
 
-def vo_condition(gamma, alpha, g, prec, vo_var, mean, vars_, mean32=None, logsig32=None, ws=None):
-    """VirtualObservable.update for every VO sample (VirtualObservables.py:642-669)."""
+def vo_condition(gamma, alpha, g, prec, vo_var, mean, vars_, mean32=None, logsig32=None, ws=None, sparse=None):
+    """VirtualObservable.update for every VO sample (VirtualObservables.py:642-669); ``sparse``: a
+    SparsePlan of gamma (column-sparse kernels)."""
     _dev(gamma, alpha, g, prec, vo_var, mean, vars_, mean32, logsig32)
     N, m, dy = gamma.shape
     assert alpha.shape == (N, m) and vo_var.shape == (m,)
@@ -113,12 +194,15 @@ def vo_condition(gamma, alpha, g, prec, vo_var, mean, vars_, mean32=None, logsig
         ws = ConditionWorkspace(N, m, dy, gamma.device)
     d = L.VoConditionDesc(n=N, m=m, d_y=dy, gamma=_p(gamma), alpha=_p(alpha), g=_p(g), prec=_p(prec),
                           vo_var=_p(vo_var), lam=_p(ws.lam), solvec=_p(ws.solvec), mean=_p(mean), vars=_p(vars_),
-                          mean32=_p(mean32), logsig32=_p(logsig32), flag=_p(ws.flag))
+                          mean32=_p(mean32), logsig32=_p(logsig32), flag=_p(ws.flag),
+                          sparse=C.addressof(sparse.desc) if sparse is not None else None)
+    if sparse is not None:
+        assert sparse.shape == (N, m, dy)
     L.check(L.lib().gpi_vo_condition(C.byref(d), L.stream_handle()), 'vo condition')
     return ws
 
 
-def vo_precision(gamma, alpha, mean, vars_, infinite, beta, vo_var, alpha0=ALPHA0, beta0=BETA0):
+def vo_precision(gamma, alpha, mean, vars_, infinite, beta, vo_var, alpha0=ALPHA0, beta0=BETA0, sparse=None):
     """update_vo_precision + _get_mean_vo_variances (VirtualObservables.py:960-998)."""
     _dev(gamma, alpha, mean, vars_, infinite, beta, vo_var)
     N, m, dy = gamma.shape
@@ -127,7 +211,9 @@ def vo_precision(gamma, alpha, mean, vars_, infinite, beta, vo_var, alpha0=ALPHA
     terms = torch.empty(m, max(N, 1), dtype=torch.float64, device=beta.device)
     d = L.VoPrecisionDesc(n=N, m=m, d_y=dy, gamma=_p(gamma), alpha=_p(alpha), mean=_p(mean), vars=_p(vars_),
                           infinite=_p(infinite), alpha0=alpha0, beta0=beta0, beta=_p(beta), vo_var=_p(vo_var),
-                          terms=_p(terms))
+                          terms=_p(terms), sparse=C.addressof(sparse.desc) if sparse is not None else None)
+    if sparse is not None:
+        assert sparse.shape == (N, m, dy)
     L.check(L.lib().gpi_vo_precision(C.byref(d), L.stream_handle()), 'vo precision')
 
 

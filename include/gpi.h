@@ -309,6 +309,26 @@ typedef struct gpi_vo_moments_desc {
     float* prec;               /* [n, d_y] out (optional) */
 } gpi_vo_moments_desc;
 
+/* Column-sparse view of Gamma [n, m, d_y] (optional, for gpi_vo_condition / gpi_vo_precision).
+ * The CGR and flux rows (VirtualObservables.py:297-321, flux.py:81-158) give every column i (a fine
+ * node) <= ~11 nonzero rows, the same rows in every sample; with this view Lambda, Gamma g - alpha,
+ * the column posteriors and the precision terms cost O(nnz) instead of O(m d_y) (the dense path reads
+ * all of Gamma, 0.9 GB at 64^2 x 128 VO samples, in each of them).  Built once per Gamma:
+ * gpi_vo_pattern (rows / counts), the caller's index lists (gpi/vo.py SparsePlan), then
+ * gpi_vo_sparse_values.  Empty slots: rows = -1, vals = 0. */
+typedef struct gpi_vo_sparse {
+    int32_t r;                 /* slots per column */
+    int32_t n_pairs;           /* Lambda entries (a >= b) that receive a contribution (all diagonals included) */
+    const int32_t* rows;       /* [d_y, r] row of slot s of column i, ascending, -1 = empty */
+    const double* vals;        /* [n, d_y, r] Gamma[j, rows[i, s], i] */
+    const int32_t* pair_ptr;   /* [n_pairs + 1] contribution ranges */
+    const int32_t* pair_ab;    /* [n_pairs] a * m + b, a >= b */
+    const int32_t* pair_src;   /* [pair_ptr[n_pairs]] (i * r + s) * r + t: column i, slots s >= t */
+    const int32_t* row_ptr;    /* [m + 1] */
+    const int32_t* row_src;    /* [row_ptr[m]] i * r + s: the nonzeros of row a, ascending i */
+    double* inv;               /* workspace [n, m, m]: Lambda^{-1} (gpi_vo_condition only) */
+} gpi_vo_sparse;
+
 /* Gaussian conditioning of every VO sample (VirtualObservable.update,
  * VirtualObservables.py:642-669): prior N(g, diag(1/prec)), observation
  * Gamma y = alpha + N(0, diag(vo_var)):
@@ -331,6 +351,7 @@ typedef struct gpi_vo_condition_desc {
     float* logsig32;           /* optional [n, d_y] out: 0.5 log((float) vars)  (ensemble .logsigma) */
     int32_t* flag;             /* optional: set to 1 if a Lambda is not positive definite
                                   (torch.cholesky raises there; checked lazily by the caller) */
+    const gpi_vo_sparse* sparse; /* optional column-sparse view of gamma (then gamma itself is not read) */
 } gpi_vo_condition_desc;
 
 /* VO precision update (VirtualObservablesEnsemble.update_vo_precision,
@@ -349,6 +370,7 @@ typedef struct gpi_vo_precision_desc {
     double* vo_var;            /* [m] out (mean VO variances) */
     double* terms;             /* [m, n] workspace: per-(row, VO sample) terms, summed over samples in a
                                   fixed order (bitwise reproducible beta / vo_var) */
+    const gpi_vo_sparse* sparse; /* optional column-sparse view of gamma (then gamma itself is not read) */
 } gpi_vo_precision_desc;
 
 /* Predictive effective properties (Analysis.sample_predictive_y's first two stages,
@@ -453,6 +475,14 @@ int gpi_vo_query(const gpi_vo_query_desc* d, void* stream);
 int gpi_vo_galerkin(const gpi_vo_galerkin_desc* d, void* stream);
 int gpi_vo_moments(const gpi_vo_moments_desc* d, void* stream);
 int gpi_vo_condition(const gpi_vo_condition_desc* d, void* stream);
+/* Column pattern of gamma [n, m, d_y]: rows[i, s] = the s-th row a (ascending) with gamma[j, a, i] != 0
+ * for some j (s < r; -1 beyond), count[i] = the number of such rows (may exceed r: the caller then
+ * keeps the dense path).  work: [m, d_y] bytes. */
+int gpi_vo_pattern(const double* gamma, int32_t n, int32_t m, int32_t d_y, int32_t r, int32_t* rows, int32_t* count,
+                   uint8_t* work, void* stream);
+/* sp->vals[j, i, s] = gamma[j, sp->rows[i, s], i] (0 on empty slots); only sp->r, rows, vals are used. */
+int gpi_vo_sparse_values(const double* gamma, int32_t n, int32_t m, int32_t d_y, const gpi_vo_sparse* sp,
+                         void* stream);
 int gpi_vo_precision(const gpi_vo_precision_desc* d, void* stream);
 /* Reparametrised Gaussian rows (bottleneck/utils.py:216-219, components.py:174-180):
  * out[r, t] = mean[r / rep, t] + exp(logsigma[r / rep, t]) * N(0,1), normals from

@@ -125,12 +125,15 @@ def test_vo_moments(device):
     assert rel(std0.cpu(), y0.std(1, ddof=1)) < 1e-5
 
 
+@pytest.mark.parametrize('sparse', [False, True], ids=['dense', 'sparse'])
 @pytest.mark.parametrize('m_kind', ['cgr', 'cgr_flux_c64', 'cgr_flux_nc16'])
-def test_vo_condition_vs_oracle(device, m_kind):
+def test_vo_condition_vs_oracle(device, m_kind, sparse):
     """Conditioning kernel vs the oracle restatement of VirtualObservable.update on the same
     fp32-rounded prior (the reference casts its fp32 Y_mean / PREC to double).  m = 25 keeps Lambda in
-    LDS; m = 209 (CGR + flux at 64x64) takes the global-memory Cholesky and the 107 KB column kernel."""
-    from gpi.vo import vo_condition
+    LDS; m = 209 (CGR + flux at 64x64) takes the global-memory Cholesky and the 107 KB column kernel;
+    m = 801 (nc = 16) the one-thread-per-column L^-1.  ``sparse``: the column-sparse kernels
+    (SparsePlan of the same Gamma)."""
+    from gpi.vo import vo_condition, SparsePlan
     if m_kind == 'cgr':
         d = load('vo_c32.npz')
         G, A = d['Gamma'], d['alpha']
@@ -156,8 +159,12 @@ def test_vo_condition_vs_oracle(device, m_kind):
     vars_ = torch.empty_like(mean)
     m32 = torch.empty(N, dy, device='cuda')
     l32 = torch.empty(N, dy, device='cuda')
-    ws = vo_condition(cuda(G, torch.float64), cuda(A, torch.float64), cuda(g), cuda(p), cuda(vv, torch.float64),
-                      mean, vars_, m32, l32)
+    Gd = cuda(G, torch.float64)
+    plan = SparsePlan.build(Gd) if sparse else None
+    if sparse:
+        assert plan is not None and plan.r <= 16
+    ws = vo_condition(Gd, cuda(A, torch.float64), cuda(g), cuda(p), cuda(vv, torch.float64),
+                      mean, vars_, m32, l32, sparse=plan)
     assert ws.flag.item() == 0
     for i in range(N):
         mo, vo = oelbo.vo_condition(torch.tensor(G[i]), torch.tensor(A[i]), torch.tensor(g[i]).double(),
@@ -187,6 +194,43 @@ def test_vo_precision_vs_oracle(device):
     assert rel(beta.cpu(), d['prec_beta']) < 1e-12
     ref = oelbo.vo_mean_variances(torch.tensor(d['prec_beta']), G.shape[0], inf.cpu().bool())
     assert rel(vv.cpu(), ref) < 1e-12
+    # column-sparse view of the same Gamma
+    from gpi.vo import SparsePlan
+    plan = SparsePlan.build(G)
+    assert plan is not None
+    beta3, vv3 = torch.empty_like(beta), torch.empty_like(vv)
+    vo_precision(G, A, mu, va, inf, beta3, vv3, sparse=plan)
+    assert rel(beta3.cpu(), d['prec_beta']) < 1e-12
+    assert rel(vv3.cpu(), ref) < 1e-12
+
+
+@pytest.mark.parametrize('nc,r', [(4, 8), (8, 8)])
+def test_vo_sparse_pattern(device, nc, r):
+    """gpi_vo_pattern / gpi_vo_sparse_values on CGR + flux rows: the slots hold exactly the nonzeros of
+    every column (union over samples, ascending rows), and a Gamma with a denser column is refused."""
+    from gpi import _lib as L
+    from gpi.vo import vo_query, SparsePlan
+    rng = np.random.default_rng(5)
+    n = nc * r
+    N = 3
+    x = rng.normal(0.4, 0.8, (N, 2 * n * n))
+    u = rng.uniform(-0.5, 0.5, (N, 4))
+    G, _ = vo_query(cuda(x, torch.float64), cuda(u, torch.float64), n, nc, L.VO_CGR | L.VO_FLUX)
+    plan = SparsePlan.build(G)
+    assert plan is not None
+    Gh = G.cpu().numpy()
+    nz = (Gh != 0).any(0)
+    rows = plan.rows.cpu().numpy()
+    vals = plan.vals.cpu().numpy()
+    assert plan.r == int(nz.sum(0).max())
+    for i in range(Gh.shape[2]):
+        a = np.nonzero(nz[:, i])[0]
+        assert np.array_equal(rows[i, :len(a)], a) and np.all(rows[i, len(a):] == -1)
+        np.testing.assert_array_equal(vals[:, i, :len(a)], Gh[:, a, i])
+        assert np.all(vals[:, i, len(a):] == 0)
+    G2 = G.clone()
+    G2[0, :, 7] = 1.0                              # one dense column
+    assert SparsePlan.build(G2) is None
 
 
 # ---------------------------------------------------------------- the model path

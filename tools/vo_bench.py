@@ -55,16 +55,29 @@ def run(ident, N_vo, N_mc, reps, dev):
     ens = VO.VirtualObservablesEnsemble(QPE, QE, dtype=torch.float32, device=dev)
     t = lambda a: torch.tensor(a, dtype=torch.float32, device=dev)
     model.register_datasets({'vo': _DS(X=t(X), Y=t(np.zeros((N_vo, (n + 1) * (n - 1)))), F_ROM_BC=t(F))}, ens)
-    model.update_virtual_observables(N_mc, step=0)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for it in range(reps):
-        model.update_virtual_observables(N_mc, step=it + 1)
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / reps
+    times, post = {}, {}
+    for mode in ('dense', 'sparse'):            # same updates (same seeds) through both conditioning paths
+        ens.sparse = mode == 'sparse'
+        torch.manual_seed(1)
+        model.update_virtual_observables(N_mc, step=0)
+        model.update_virtual_observables(N_mc, step=1)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for it in range(reps):
+            model.update_virtual_observables(N_mc, step=it + 2)
+        torch.cuda.synchronize()
+        times[mode] = (time.perf_counter() - t0) / reps
+        torch.manual_seed(2)
+        model.update_virtual_observables(N_mc, step=reps + 2)
+        post[mode] = (ens._mean64.clone(), ens._vars64.clone())
+    dm = ((post['dense'][0] - post['sparse'][0]).abs().max() / post['dense'][0].abs().max()).item()
+    dv = ((post['dense'][1] - post['sparse'][1]).abs().max() / post['dense'][1].abs().max()).item()
+    dt = times['sparse']
     m = int(ens._QuerryEnsemble.gamma.shape[1])
     return dict(grid=n, nc=nc, N_vo=N_vo, N_mc=N_mc, m=m, ms_per_update=round(dt * 1e3, 3),
-                vo_samples_per_s=round(N_vo / dt, 1)), (model, ens, X, U, F, physics)
+                vo_samples_per_s=round(N_vo / dt, 1), conditioning='column-sparse (SparsePlan r=%d)'
+                % ens._plan.r, ms_per_update_dense=round(times['dense'] * 1e3, 3),
+                sparse_vs_dense_rel_diff=dict(mean=dm, vars=dv)), (model, ens, X, U, F, physics)
 
 
 def cpu_port(state, N_vo_cpu, N_mc):
