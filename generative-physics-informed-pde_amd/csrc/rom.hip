@@ -381,6 +381,128 @@ __global__ __launch_bounds__(ROM_NT) void rom_kernel(gpi_rom_desc d, RomDims D) 
     }
 }
 
+// Coarse solutions only (FORWARD without mu_y: the VO MC predictive, N_vo x N_mc samples), nc = 4 / 8:
+// ONE LANE PER SAMPLE.  rom_kernel runs the banded Cholesky in one lane of a 256-thread workgroup per
+// sample; here every lane of a wave64 factors its own sample's system with the same register window
+// (chol_band_seq), the forward substitution fused into the factorisation (row k of L is final when
+// the window reaches it) and the band rows / right-hand side in LDS interleaved by lane ([entry][64]:
+// conflict-free).  Slot 0 of each stored L row holds 1 / L(k,k).
+template <int NC>
+__global__ __launch_bounds__(64) void rom_lane_kernel(gpi_rom_desc d) {
+    constexpr int W = NC, BW = NC - 1, NI = (NC - 1) * (NC + 1), NN = (NC + 1) * (NC + 1);
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float* Ls = sm;                       // [NI * W][64]
+    float* Bs = sm + NI * W * 64;         // [NI][64]
+    const int lane = threadIdx.x;
+    const int s = blockIdx.x * 64 + lane;
+    const bool act = s < d.n;
+    const int sc = act ? s : 0;
+    const float* __restrict__ x = d.x + (int64_t)sc * d.x_stride;
+    const float* __restrict__ F = d.F + (int64_t)sc * NN;
+    auto kap = [&](int I, int J, int ul) -> float {
+        const float v = x[2 * (I + NC * J) + ul];
+        return d.input_kappa ? v : expf(v) + 1e-8f;
+    };
+    auto ch = [&](int I, int J) -> float {        // horizontal edge (I,J)-(I+1,J)
+        float c = 0.f;
+        if (J < NC) c += kap(I, J, 0);
+        if (J > 0) c += kap(I, J - 1, 1);
+        return 0.5f * c;
+    };
+    auto cv = [&](int I, int J) -> float {        // vertical edge (I,J)-(I,J+1)
+        float c = 0.f;
+        if (I > 0) c += kap(I - 1, J, 0);
+        if (I < NC) c += kap(I, J, 1);
+        return 0.5f * c;
+    };
+    bool bad = false;
+#pragma unroll
+    for (int t = 0; t < 2 * NC * NC; ++t) {
+        const float v = x[t];
+        bad |= !((d.input_kappa ? v : expf(v) + 1e-8f) > 1e-12f);
+    }
+    if (act && bad && d.flag) atomicOr(d.flag, 1);
+    // ---- assemble the interior rows (banded lower) + rhs
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+        const int J = k / (NC - 1), I = k - J * (NC - 1) + 1, p = I + (NC + 1) * J;
+        const float chl = ch(I - 1, J), chr = ch(I, J);
+        const float cvd = J > 0 ? cv(I, J - 1) : 0.f, cvu = J < NC ? cv(I, J) : 0.f;
+#pragma unroll
+        for (int t = 0; t < W; ++t) {
+            float v = 0.f;
+            if (t == 0) v = chl + chr + cvd + cvu;
+            if (t == 1 && I - 1 >= 1) v += -chl;
+            if (t == BW && J >= 1) v += -cvd;
+            Ls[(k * W + t) * 64 + lane] = v;
+        }
+        float rhs = F[p];
+        if (I - 1 == 0) rhs += chl * F[p - 1];
+        if (I + 1 == NC) rhs += chr * F[p + 1];
+        Bs[k * 64 + lane] = rhs;
+    }
+    // ---- factorisation + forward substitution (register window, see chol_band_seq)
+    float win[W][W];   // win[a][t] = L(k + a, k + a - t)
+    float h[BW];       // h[t-1] = y[k - t]
+#pragma unroll
+    for (int a = 0; a < W; ++a)
+#pragma unroll
+        for (int t = 0; t < W; ++t) win[a][t] = a < NI ? Ls[(a * W + t) * 64 + lane] : 0.f;
+#pragma unroll
+    for (int t = 0; t < BW; ++t) h[t] = 0.f;
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+        const float dk = sqrtf(win[0][0]);
+        const float inv = 1.f / dk;
+#pragma unroll
+        for (int a = 1; a < W; ++a) win[a][a] *= inv;                       // L(k+a, k)
+#pragma unroll
+        for (int a = 1; a < W; ++a)
+#pragma unroll
+            for (int b = 1; b <= a; ++b) win[a][a - b] = fmaf(-win[a][a], win[b][b], win[a][a - b]);
+        float y = Bs[k * 64 + lane];
+#pragma unroll
+        for (int t = 1; t <= BW; ++t)
+            if (k - t >= 0) y = fmaf(-win[0][t], h[t - 1], y);
+        y *= inv;
+        Bs[k * 64 + lane] = y;
+#pragma unroll
+        for (int t = BW - 1; t > 0; --t) h[t] = h[t - 1];
+        h[0] = y;
+        Ls[(k * W) * 64 + lane] = inv;
+#pragma unroll
+        for (int t = 1; t < W; ++t) Ls[(k * W + t) * 64 + lane] = win[0][t];
+#pragma unroll
+        for (int a = 0; a + 1 < W; ++a)
+#pragma unroll
+            for (int t = 0; t < W; ++t) win[a][t] = win[a + 1][t];
+#pragma unroll
+        for (int t = 0; t < W; ++t) win[W - 1][t] = (k + W < NI) ? Ls[((k + W) * W + t) * 64 + lane] : 0.f;
+    }
+    // ---- back substitution L^T x = y
+#pragma unroll
+    for (int t = 0; t < BW; ++t) h[t] = 0.f;        // h[t-1] = x[k + t]
+#pragma unroll
+    for (int k = NI - 1; k >= 0; --k) {
+        float a = Bs[k * 64 + lane];
+#pragma unroll
+        for (int t = 1; t <= BW; ++t)
+            if (k + t < NI) a = fmaf(-Ls[((k + t) * W + t) * 64 + lane], h[t - 1], a);
+        a *= Ls[(k * W) * 64 + lane];
+        Bs[k * 64 + lane] = a;
+#pragma unroll
+        for (int t = BW - 1; t > 0; --t) h[t] = h[t - 1];
+        h[0] = a;
+    }
+    if (!act) return;
+    float* uc = d.uc + (int64_t)s * NN;
+#pragma unroll
+    for (int e = 0; e < NN; ++e) {
+        const int I = e % (NC + 1), J = e / (NC + 1);
+        uc[e] = (I == 0 || I == NC) ? F[e] : Bs[(J * (NC - 1) + (I - 1)) * 64 + lane];
+    }
+}
+
 }  // namespace
 
 extern "C" int gpi_rom(const gpi_rom_desc* d, void* stream) {
@@ -397,6 +519,17 @@ extern "C" int gpi_rom(const gpi_rom_desc* d, void* stream) {
     D.r = d->refine;
     D.n = d->nc * d->refine;
     D.dy = (D.n + 1) * (D.n - 1);
+    if (d->mode == GPI_ROM_FORWARD && !d->mu_y && d->uc && (d->nc == 4 || d->nc == 8)) {
+        const size_t lds = sizeof(float) * 64 * (D.nI * (D.bw + 1) + D.nI);
+        const void* k = d->nc == 8 ? (const void*)rom_lane_kernel<8> : (const void*)rom_lane_kernel<4>;
+        if (lds > 64 * 1024 && hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+            return GPI_ERR_LAUNCH;
+        const dim3 grid((d->n + 63) / 64);
+        if (d->nc == 8) hipLaunchKernelGGL(rom_lane_kernel<8>, grid, dim3(64), lds, (hipStream_t)stream, *d);
+        else hipLaunchKernelGGL(rom_lane_kernel<4>, grid, dim3(64), lds, (hipStream_t)stream, *d);
+        GPI_CHECK_LAUNCH();
+        return GPI_OK;
+    }
     const size_t lds = sizeof(float) * (D.nT + D.nI * (D.bw + 1) + 4 * D.nn + 2 * D.nI + 2 * (ROM_NT / 64) + 4);
     hipLaunchKernelGGL(rom_kernel, dim3(d->n), dim3(ROM_NT), lds, (hipStream_t)stream, *d, D);
     GPI_CHECK_LAUNCH();

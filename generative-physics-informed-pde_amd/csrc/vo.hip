@@ -298,31 +298,31 @@ __global__ __launch_bounds__(256) void vo_moments_kernel(gpi_vo_moments_desc d, 
     }
     const uint64_t base = d.offset ? *d.offset : 0;
     const int64_t row0 = (int64_t)j * d.n_mc;
-    double mean = 0.0, ssd = 0.0;
-    for (int pass = 0; pass < 2; ++pass) {
-        double acc = 0.0;
-        for (int s0 = 0; s0 < d.n_mc; s0 += MOM_CH) {
-            const int ns = min(MOM_CH, d.n_mc - s0);
-            __syncthreads();
-            for (int e = threadIdx.x; e < ns * nn; e += 256) su[e] = d.uc[(row0 + s0) * nn + e];
-            __syncthreads();
-            if (!act) continue;
-            for (int s = 0; s < ns; ++s) {
-                const float* us = su + s * nn;
-                float y = w[0] * us[kk[0]] + w[1] * us[kk[1]] + w[2] * us[kk[2]];
-                if (d.logsig_y) {
-                    const int64_t rr = row0 + s0 + s;
-                    const float e = d.eps ? d.eps[rr * G.dy + p]
-                                          : normal_at(base + (uint64_t)(rr * G.dy + p), d.sub, d.seed);
-                    y = fmaf(sig, e, y);
-                }
-                if (pass == 0) acc += (double)y;
-                else { const double t = (double)y - mean; acc += t * t; }
+    // one pass (each draw made once): fp64 sums of y - K and (y - K)^2, shifted by the first sample K
+    double s1 = 0.0, s2 = 0.0, K = 0.0;
+    for (int s0 = 0; s0 < d.n_mc; s0 += MOM_CH) {
+        const int ns = min(MOM_CH, d.n_mc - s0);
+        __syncthreads();
+        for (int e = threadIdx.x; e < ns * nn; e += 256) su[e] = d.uc[(row0 + s0) * nn + e];
+        __syncthreads();
+        if (!act) continue;
+        for (int s = 0; s < ns; ++s) {
+            const float* us = su + s * nn;
+            float y = w[0] * us[kk[0]] + w[1] * us[kk[1]] + w[2] * us[kk[2]];
+            if (d.logsig_y) {
+                const int64_t rr = row0 + s0 + s;
+                const float e = d.eps ? d.eps[rr * G.dy + p]
+                                      : normal_at(base + (uint64_t)(rr * G.dy + p), d.sub, d.seed);
+                y = fmaf(sig, e, y);
             }
+            if (s0 + s == 0) K = (double)y;
+            const double t = (double)y - K;
+            s1 += t;
+            s2 = fma(t, t, s2);
         }
-        if (pass == 0) mean = acc / (double)d.n_mc;
-        else ssd = acc;
     }
+    const double mean = K + s1 / (double)d.n_mc;
+    const double ssd = fmax(s2 - s1 * (s1 / (double)d.n_mc), 0.0);
     if (!act) return;
     const float sd = (float)sqrt(ssd / (double)(d.n_mc - 1));
     const int64_t o = (int64_t)j * G.dy + p;
@@ -580,6 +580,69 @@ __global__ __launch_bounds__(256) void vo_linv_wave_kernel(gpi_vo_condition_desc
     for (int k = 0; k < 4; ++k) {
         const int a = lane + 64 * k;
         if (a > c && a < m) lam[(int64_t)c * m + a] = x[k];
+    }
+}
+
+// The same by 32 x 32 blocks (m <= 256), one workgroup per (block column jb, sample): block row ib of
+// column block jb of L^-1 is X_ib = L_ib,ib^-1 (delta_ib,jb I - sum_{kb=jb}^{ib-1} L_ib,kb X_kb): the sum as
+// LDS tile products, the triangular solve with one barrier per row (thread (tr, tc) keeps rows tr + 8u of
+// column tc in registers; the owner of row k publishes x_k).  The finished blocks stay in LDS for the
+// block rows below and are written transposed into lam's strict upper triangle (only the lower
+// triangle is read here, so workgroups never race).
+constexpr int TI = 32;
+__global__ __launch_bounds__(256) void vo_linv_block_kernel(gpi_vo_condition_desc d) {
+    extern __shared__ double xs[];                       // [nb - jb][TI][TI + 1]
+    __shared__ double Ls[TI][TI + 1];
+    const int jb = blockIdx.x, j = blockIdx.y, m = d.m, nb = (m + TI - 1) / TI;
+    double* lam = d.lam + (int64_t)j * m * m;
+    const int tid = threadIdx.x, tc = tid & 31, tr = tid >> 5;
+    for (int ib = jb; ib < nb; ++ib) {
+        double* Xi = xs + (ib - jb) * TI * (TI + 1);
+        double acc[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc[u] = (ib == jb && tr + 8 * u == tc && ib * TI + tc < m) ? 1.0 : 0.0;
+        for (int kb = jb; kb < ib; ++kb) {
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int a = ib * TI + tr + 8 * u, b = kb * TI + tc;
+                Ls[tr + 8 * u][tc] = (a < m && b < m) ? lam[(int64_t)a * m + b] : 0.0;
+            }
+            __syncthreads();
+            const double* Xk = xs + (kb - jb) * TI * (TI + 1);
+#pragma unroll 8
+            for (int c = 0; c < TI; ++c) {
+                const double xv = Xk[c * (TI + 1) + tc];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) acc[u] = fma(-Ls[tr + 8 * u][c], xv, acc[u]);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {                    // diagonal block (identity on rows past m)
+            const int r = tr + 8 * u, a = ib * TI + r, b = ib * TI + tc;
+            Ls[r][tc] = (a < m && b < m) ? (tc <= r ? lam[(int64_t)a * m + b] : 0.0) : (r == tc ? 1.0 : 0.0);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < 4; ++u) Xi[(tr + 8 * u) * (TI + 1) + tc] = acc[u];
+        for (int k = 0; k < TI; ++k) {                   // rows below k take x_k; row k itself is final
+            __syncthreads();
+            const double xk = Xi[k * (TI + 1) + tc] / Ls[k][k];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (tr + 8 * u > k) Xi[(tr + 8 * u) * (TI + 1) + tc] = fma(-Ls[tr + 8 * u][k], xk,
+                                                                           Xi[(tr + 8 * u) * (TI + 1) + tc]);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < 4; ++u) Xi[(tr + 8 * u) * (TI + 1) + tc] /= Ls[tr + 8 * u][tr + 8 * u];
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {                    // lam[c m + a] = X[a][c], a > c (rows r fastest)
+            const int r = tc, cl = tr + 8 * u, a = ib * TI + r, c = jb * TI + cl;
+            if (a < m && c < m && a > c) lam[(int64_t)c * m + a] = Xi[r * (TI + 1) + cl];
+        }
     }
 }
 
@@ -1133,8 +1196,13 @@ extern "C" int gpi_vo_condition(const gpi_vo_condition_desc* d, void* stream) {
         }
     }
     GPI_CHECK_LAUNCH();
-    if (d->m <= 256) hipLaunchKernelGGL(vo_linv_wave_kernel, dim3((d->m + 3) / 4, d->n), dim3(256), 0, st, *d);
-    else hipLaunchKernelGGL(vo_linv_kernel, dim3(d->n), dim3(256), 0, st, *d);
+    if (d->m <= 256) {
+        const int nb = (d->m + TI - 1) / TI;
+        hipLaunchKernelGGL(vo_linv_block_kernel, dim3(nb, d->n), dim3(256), sizeof(double) * nb * TI * (TI + 1), st,
+                           *d);
+    } else {
+        hipLaunchKernelGGL(vo_linv_kernel, dim3(d->n), dim3(256), 0, st, *d);
+    }
     GPI_CHECK_LAUNCH();
     if (lds_small > 64 * 1024) hipLaunchKernelGGL(vo_solvec_kernel, dim3(d->n), dim3(256), 0, st, *d);
     GPI_CHECK_LAUNCH();

@@ -126,6 +126,36 @@ def test_rom_c64_fused_loglik(device):
     assert flag.item() == 0
 
 
+@pytest.mark.parametrize('nc', [4, 8])
+def test_rom_coarse_solutions_lane_per_sample(device, nc):
+    """gpi_rom FORWARD without mu_y (the VO MC predictive's coarse solves: rom_lane_kernel, one lane per
+    sample, 16 384 samples at the notebook's 128 x 128) vs the workgroup-per-sample kernel (FORWARD with
+    mu_y) on the same inputs, and a subset vs the fp64 oracle solve (ROM.py:59-100)."""
+    from gpi.engine import rom_call
+    from gpi import _lib as L
+    r = 8
+    M, W, bc = physics(nc, r)
+    rng = np.random.default_rng(nc)
+    N = 16384 + 37                                   # a ragged last wave
+    x = cuda(rng.normal(0.3, 0.7, (N, 2 * nc * nc)))
+    F = torch.zeros(N, (nc + 1) ** 2, device='cuda')
+    Fh = np.zeros((N, (nc + 1) ** 2), dtype=np.float32)
+    bnodes = [e for e in range((nc + 1) ** 2) if e % (nc + 1) in (0, nc)]
+    Fh[:, bnodes] = rng.uniform(-0.5, 0.5, (N, len(bnodes)))
+    F.copy_(torch.from_numpy(Fh))
+    uc_lane = torch.empty(N, (nc + 1) ** 2, device='cuda')
+    rom_call(nc, r, x, F, False, L.ROM_FORWARD, uc=uc_lane)
+    uc_wg = torch.empty_like(uc_lane)
+    mu = torch.empty(N, (nc * r + 1) * (nc * r - 1), device='cuda')
+    rom_call(nc, r, x, F, False, L.ROM_FORWARD, mu_y=mu, uc=uc_wg)
+    assert tensor_rel(uc_lane.cpu(), uc_wg.cpu().numpy().astype(np.float64)) < 2e-6
+    sel = [0, 1, 777, N - 1]
+    e64 = torch.tensor(x[sel].cpu().numpy(), dtype=torch.float64)
+    u = oelbo.rom_solve(torch.tensor(M), torch.exp(e64) + 1e-8, torch.tensor(Fh[sel], dtype=torch.float64),
+                        torch.tensor(bc))
+    assert tensor_rel(uc_lane[sel].cpu(), u) < 1e-5
+
+
 # ---------------------------------------------------------------- the ELBO step at the bench shape
 def test_elbo_c64_module_path(device):
     """GenerativeModel.elbo + backward (the drop-in module path) at B_u = 256, N_s = 32 with the
