@@ -434,20 +434,31 @@ __device__ void chol_panel(double* A, int m, bool& bad) {
             P[r][c] = c < w ? A[(int64_t)(R0 + r) * m + K0 + c] : 0.0;
         }
         __syncthreads();
-        for (int k = 0; k < w; ++k) {               // diagonal block
-            const double akk = D[k][k];
-            if (!(akk > 0.0)) bad = true;
-            const double dk = sqrt(akk);
-            __syncthreads();
-            if (tid > k && tid < w) D[tid][k] /= dk;
-            if (tid == 0) D[k][k] = dk;
-            __syncthreads();
-            if (tid < CP_W * CP_W) {
-                const int r = tid / CP_W, c = tid - r * CP_W;
-                if (r > k && c > k && c <= r && r < w) D[r][c] -= D[r][k] * D[c][k];
+        if (tid < 64) {                             // diagonal block: wave 0, lane r holds row r, no barriers
+            const int r = tid & (CP_W - 1);
+            double row[CP_W];
+#pragma unroll
+            for (int c = 0; c < CP_W; ++c) row[c] = D[r][c];
+#pragma unroll
+            for (int k = 0; k < CP_W; ++k) {
+                if (k < w) {
+                    const double akk = __shfl(row[k], k, 64);
+                    if (!(akk > 0.0)) bad = true;
+                    const double dk = sqrt(akk);
+                    if (r == k) row[k] = dk;
+                    else if (r > k) row[k] /= dk;
+#pragma unroll
+                    for (int c = k + 1; c < CP_W; ++c) {
+                        const double lc = __shfl(row[k], c, 64);
+                        if (r >= c && r > k) row[c] = fma(-row[k], lc, row[c]);
+                    }
+                }
             }
-            __syncthreads();
+            if (tid < CP_W)
+#pragma unroll
+                for (int c = 0; c < CP_W; ++c) D[r][c] = row[c];
         }
+        __syncthreads();
         if (tid < R) {                              // panel rows: x L11^T = a
             for (int c = 0; c < w; ++c) {
                 double a = P[tid][c];
@@ -585,17 +596,20 @@ __global__ __launch_bounds__(256) void vo_linv_wave_kernel(gpi_vo_condition_desc
 
 // The same by 32 x 32 blocks (m <= 256), one workgroup per (block column jb, sample): block row ib of
 // column block jb of L^-1 is X_ib = L_ib,ib^-1 (delta_ib,jb I - sum_{kb=jb}^{ib-1} L_ib,kb X_kb): the sum as
-// LDS tile products, the triangular solve with one barrier per row (thread (tr, tc) keeps rows tr + 8u of
-// column tc in registers; the owner of row k publishes x_k).  The finished blocks stay in LDS for the
-// block rows below and are written transposed into lam's strict upper triangle (only the lower
-// triangle is read here, so workgroups never race).
+// LDS tile products, the triangular solve per column inside one wave (thread (tc, tr) = (tid / 8, tid % 8)
+// keeps rows tr + 8u of column tc in registers; the owner of row k hands x_k to the column's 8 lanes by a
+// shuffle, no barrier).  The finished blocks stay in LDS for the block rows below and are written
+// transposed into lam's strict upper triangle (only the lower triangle is read here, so workgroups never
+// race).
 constexpr int TI = 32;
 __global__ __launch_bounds__(256) void vo_linv_block_kernel(gpi_vo_condition_desc d) {
     extern __shared__ double xs[];                       // [nb - jb][TI][TI + 1]
     __shared__ double Ls[TI][TI + 1];
     const int jb = blockIdx.x, j = blockIdx.y, m = d.m, nb = (m + TI - 1) / TI;
     double* lam = d.lam + (int64_t)j * m * m;
-    const int tid = threadIdx.x, tc = tid & 31, tr = tid >> 5;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int tc = tid >> 3, tr = tid & 7;               // compute layout
+    const int lc = tid & 31, lr = tid >> 5;              // tile-load layout (rows of 32 contiguous)
     for (int ib = jb; ib < nb; ++ib) {
         double* Xi = xs + (ib - jb) * TI * (TI + 1);
         double acc[4];
@@ -605,8 +619,8 @@ __global__ __launch_bounds__(256) void vo_linv_block_kernel(gpi_vo_condition_des
             __syncthreads();
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                const int a = ib * TI + tr + 8 * u, b = kb * TI + tc;
-                Ls[tr + 8 * u][tc] = (a < m && b < m) ? lam[(int64_t)a * m + b] : 0.0;
+                const int a = ib * TI + lr + 8 * u, b = kb * TI + lc;
+                Ls[lr + 8 * u][lc] = (a < m && b < m) ? lam[(int64_t)a * m + b] : 0.0;
             }
             __syncthreads();
             const double* Xk = xs + (kb - jb) * TI * (TI + 1);
@@ -620,27 +634,25 @@ __global__ __launch_bounds__(256) void vo_linv_block_kernel(gpi_vo_condition_des
         __syncthreads();
 #pragma unroll
         for (int u = 0; u < 4; ++u) {                    // diagonal block (identity on rows past m)
-            const int r = tr + 8 * u, a = ib * TI + r, b = ib * TI + tc;
-            Ls[r][tc] = (a < m && b < m) ? (tc <= r ? lam[(int64_t)a * m + b] : 0.0) : (r == tc ? 1.0 : 0.0);
+            const int r = lr + 8 * u, a = ib * TI + r, b = ib * TI + lc;
+            Ls[r][lc] = (a < m && b < m) ? (lc <= r ? lam[(int64_t)a * m + b] : 0.0) : (r == lc ? 1.0 : 0.0);
         }
         __syncthreads();
 #pragma unroll
-        for (int u = 0; u < 4; ++u) Xi[(tr + 8 * u) * (TI + 1) + tc] = acc[u];
-        for (int k = 0; k < TI; ++k) {                   // rows below k take x_k; row k itself is final
-            __syncthreads();
-            const double xk = Xi[k * (TI + 1) + tc] / Ls[k][k];
+        for (int k = 0; k < TI; ++k) {
+            const double cand = acc[k >> 3] / Ls[k][k];
+            const double xk = __shfl(cand, (lane & ~7) | (k & 7), 64);
+            if (tr == (k & 7)) acc[k >> 3] = xk;
 #pragma unroll
             for (int u = 0; u < 4; ++u)
-                if (tr + 8 * u > k) Xi[(tr + 8 * u) * (TI + 1) + tc] = fma(-Ls[tr + 8 * u][k], xk,
-                                                                           Xi[(tr + 8 * u) * (TI + 1) + tc]);
+                if (tr + 8 * u > k) acc[u] = fma(-Ls[tr + 8 * u][k], xk, acc[u]);
         }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) Xi[(tr + 8 * u) * (TI + 1) + tc] = acc[u];
         __syncthreads();
 #pragma unroll
-        for (int u = 0; u < 4; ++u) Xi[(tr + 8 * u) * (TI + 1) + tc] /= Ls[tr + 8 * u][tr + 8 * u];
-        __syncthreads();
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {                    // lam[c m + a] = X[a][c], a > c (rows r fastest)
-            const int r = tc, cl = tr + 8 * u, a = ib * TI + r, c = jb * TI + cl;
+        for (int u = 0; u < 4; ++u) {                    // lam[c m + a] = X[a][c], a > c (rows fastest)
+            const int r = lc, cl = lr + 8 * u, a = ib * TI + r, c = jb * TI + cl;
             if (a < m && c < m && a > c) lam[(int64_t)c * m + a] = Xi[r * (TI + 1) + cl];
         }
     }
