@@ -823,13 +823,12 @@ class VirtualObservablesEnsemble(BaseVirtualObservablesEnsemble):
             vo._vars = self._vars64[n]
 
     # ------------------------------------------------------------------ updates
-    def _sparse_plan(self):
-        """SparsePlan of the ensemble's Gamma, rebuilt when Gamma is replaced; None when disabled or when
-        Gamma has test-function rows (dense, and redrawn in place by resample)."""
+    def _sparse_plan(self, gamma):
+        """SparsePlan of the ensemble's Gamma (``gamma`` = qe.gamma), rebuilt when Gamma is replaced; None when
+        disabled or when Gamma has test-function rows (dense, and redrawn in place by resample)."""
         qe = self._QuerryEnsemble
         if not self.sparse or getattr(qe, '_aux', None):
             return None
-        gamma = qe.gamma
         key = (gamma.data_ptr(), tuple(gamma.shape), getattr(qe, 'generation', 0))
         if key != self._plan_key:
             self._plan = V.SparsePlan.build(gamma)
@@ -839,13 +838,14 @@ class VirtualObservablesEnsemble(BaseVirtualObservablesEnsemble):
     def update(self, G, PREC, iteration, writer=None):
         self.update_vo_precision(iteration, writer)
         qe = self._QuerryEnsemble
-        gamma, alpha = qe.gamma, qe.alpha
+        gamma = qe.gamma
+        alpha = qe._alpha
         if self._ws is None:
             self._ws = V.ConditionWorkspace(self.N, self.m, self.dim_out, gamma.device)
         V.vo_condition(gamma, alpha, G.detach().to(torch.float32).contiguous(),
                        PREC.detach().to(torch.float32).contiguous(), self._mean_vo_variances.contiguous(),
                        self._mean64, self._vars64, self._mean32, self._logsig32, ws=self._ws,
-                       sparse=self._sparse_plan())
+                       sparse=self._sparse_plan(gamma))
         self._has_posterior = True
         self._bind_members()
         self.flush_cache()
@@ -870,8 +870,9 @@ class VirtualObservablesEnsemble(BaseVirtualObservablesEnsemble):
             beta = torch.empty(self.m, dtype=torch.float64, device=self.device)
             vo_var = torch.empty_like(beta)
             inf = self.infinite_precision_mask.to(torch.int32).contiguous()
-            V.vo_precision(qe.gamma, qe.alpha, self._mean64, self._vars64, inf, beta, vo_var,
-                           alpha0=self._alpha_0, beta0=self._beta_0, sparse=self._sparse_plan())
+            gamma = qe.gamma
+            V.vo_precision(gamma, qe._alpha, self._mean64, self._vars64, inf, beta, vo_var,
+                           alpha0=self._alpha_0, beta0=self._beta_0, sparse=self._sparse_plan(gamma))
             self._prec_beta = beta
             self._mean_vo_variances = vo_var
             self._set_member_variance_values(self._mean_vo_variances)

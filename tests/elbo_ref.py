@@ -13,7 +13,8 @@ from oracle import fem
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
 
 # codec hyper-parameters of the fixtures (factories/model.py:187-257)
-CODEC = {32: dict(blocks=[1, 1], growth=4, f0=4), 64: dict(blocks=[1, 2, 1], growth=4, f0=6)}
+CODEC = {32: dict(blocks=[1, 1], growth=4, f0=4), 64: dict(blocks=[1, 2, 1], growth=4, f0=6),
+         128: dict(blocks=[1, 2, 2, 1], growth=4, f0=6), 256: dict(blocks=[1, 2, 2, 2, 1], growth=4, f0=6)}
 _PHYS = {}
 
 

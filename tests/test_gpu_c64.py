@@ -280,3 +280,66 @@ def test_elbo_options(device, opt):
     assert abs(elbo.item() - float(d[opt + '.elbo'])) <= 2e-5 * abs(val_o)
     errs = {k: tensor_rel(p.grad.cpu(), gr_o[k]) for k, p in model.named_parameters()}
     print(check_grads(errs))
+
+
+# ---------------------------------------------------------------- scale-up grids (BASELINE configs 4 / 5)
+@pytest.mark.parametrize('ident,n', [('highres128', 128), ('highres256', 256)])
+def test_fused_step_scaleup_grids(device, ident, n):
+    """FusedElboStep at 128^2 (highres128: blocks [1,2,2,1]) and 256^2 (highres256: [1,2,2,2,1]), ROM 8x8,
+    droprate 0.2 (device-drawn Dropout2d), small batch (B_u = 4 of a pool of 8, N_s = 2), random-init
+    parameters and synthetic fields: one step's ELBO vs the fp64 oracle (1e-5) and every gradient tensor
+    vs the oracle with the kernels' ReLU tie decisions and dropout scales."""
+    from gpu_masks import engine_relu_masks
+    from factories.model import ModelFactory
+    from gpi.train import FusedElboStep
+    import copy
+    torch.manual_seed(3)
+    fac = ModelFactory.FromIdentifier(ident)
+    fac.set('device', 'cuda')
+    physics_, model, _, encoder, _, _ = fac.setup()
+    model.encoder = encoder.cuda()
+    nc = physics_['rom'].grid.n
+    assert physics_['fom'].grid.n == n
+    rng = np.random.default_rng(n)
+    Nu, bs, Ns = 8, 4, 2
+    Xu = rng.normal(0.3, 0.6, (Nu, n, n)).astype(np.float32)
+    Xs = rng.normal(0.3, 0.6, (Ns, n, n)).astype(np.float32)
+    Y = rng.normal(0.0, 0.3, (Ns, (n + 1) * (n - 1))).astype(np.float32)
+    F = np.zeros((Ns, (nc + 1) ** 2), dtype=np.float32)
+    bnodes = [e for e in range((nc + 1) ** 2) if e % (nc + 1) in (0, nc)]
+    F[:, bnodes] = rng.uniform(-0.5, 0.5, (Ns, len(bnodes)))
+    model.register_datasets({'supervised': _DS(X=cuda(Xs), Y=cuda(Y), F_ROM_BC=cuda(F)),
+                             'unsupervised': _DS(perm=torch.arange(Nu, device='cuda'), X=cuda(Xu))}, None,
+                            create_unsupervised_variational_approximation=False)
+    model.cuda()
+    ref_model = copy.deepcopy(model)
+    step = FusedElboStep(model, cuda(Xu), bs, cuda(Xs), cuda(Y), cuda(F), lr=1e-3, seed=5)
+    e = step.engine
+    eps_z_t, eps_x_t = e.eps_z().clone(), e.eps_x().clone()
+    drops_t = {k: {nm: v.clone() for nm, v in dd.items()} for k, dd in e.dropout_views().items()}
+    assert drops_t
+    idx_t = step.idx.clone().long()
+    st = {k: torch.tensor(p.detach().cpu().numpy(), dtype=torch.float64, requires_grad=True)
+          for k, p in model.named_parameters()}
+    # the module path on the same inputs gives the kernels' ReLU decisions for the oracle
+    ref_model._datasets['unsupervised'].perm = idx_t
+    ref = ref_model.elbo(step=0, armortized_bs=bs, eps=(eps_z_t, eps_x_t), dropout=drops_t)
+    masks = engine_relu_masks(ref_model._elbo_engine(bs, Ns, False))
+    step.forward_backward()
+    torch.cuda.synchronize()
+    eps_z = eps_z_t.cpu().numpy().astype(np.float64)
+    eps_x = eps_x_t.cpu().numpy().astype(np.float64)
+    idx = idx_t.cpu().numpy()
+    drops = {k: {nm: v.double().cpu() for nm, v in dd.items()} for k, dd in drops_t.items()}
+    ocodec.MASK_AUDIT.clear()
+    val = oracle_elbo(st, Xu[idx], Xs, Y, F, eps_z[:bs], eps_z[bs:], eps_x, nc, n // nc, masks=masks, drops=drops)
+    check_mask_audit()
+    (-val).backward()
+    got = step.elbo().item()
+    assert abs(got - val.item()) <= 1e-5 * abs(val.item()), (got, val.item())
+    assert abs(got - ref.item()) <= 1e-6 * abs(val.item()), (got, ref.item())
+    G = step.flat.G
+    off = step.flat.name_offsets
+    errs = {k: tensor_rel(G[off[k]:off[k] + st[k].numel()].cpu().numpy().reshape(st[k].shape), st[k].grad.numpy())
+            for k in st}
+    print(check_grads(errs, tol_all=5e-5, frac_tight=1.0))
