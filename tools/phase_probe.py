@@ -49,6 +49,8 @@ def main():
             L.check(lib.gpi_conv_launch_info(C.byref(descs[i]), C.byref(ctx.groups), 1 if fwd else 0, info), 'info')
             nb = min(info[1], 4096)       # workgroups of the launch
             fn = lib.gpi_conv_forward if fwd else lib.gpi_conv_backward
+            if prog is e.dp and i == e.n_dec_sep and e.n_dec_sep < len(e.dec_descs) and not fwd:
+                fn = lib.gpi_conv_loss_fused          # the decoder output conv runs fused in the step
             torch.cuda.synchronize()
             L.check(stamps(ph.ctypes.data, rt.ctypes.data), 'stamps')     # clears the device stamps
             for _ in range(3):     # the last launch's stamps remain
