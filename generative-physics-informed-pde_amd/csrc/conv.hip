@@ -1185,59 +1185,68 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
     }
     __syncthreads();
     if constexpr (FUSE) {
-        // ---- phase 3': forward of output rows gy0 + [0, gh) (4 adjacent pixels per thread; weights
-        // from the input-gradient table wD[(co * KK + tap) * 16 + ci]), the Gaussian log-likelihood of
-        // the owned rows, d(-logL)/d(mu, logsigma) into the gradient image
-        constexpr int NPXF = 4, PADK = K / 2, NW = (NPXF - 1) + K;
-        const int ng = G.gh * d.w_out / NPXF;
+        // ---- phase 3': forward of output rows gy0 + [0, gh) (weights as SGPR operands from scalar
+        // loads), the Gaussian log-likelihood of the owned rows, d(-logL)/d(mu, logsigma) into the
+        // gradient image
+        constexpr int PADK = K / 2;
         float Lv = 0.f;
         int trow0 = T.b - karg_sel(c.groups.start, T.grp);
         if (const int32_t* ti = karg_sel(c.tgt_idx, T.grp)) trow0 = ti[trow0];
         const float* tg = karg_sel(c.tgt, T.grp) + (int64_t)trow0 * HWo;
         const bool ex = d.epilogue == GPI_EPI_GAUSS_EXP_LOSS;
         const float scl = karg_sel(c.loss_scale, T.grp);
-        for (int g = tid; g < ng; g += 256) {
-            const int j = dq(g * NPXF, G.d_wout), x0 = g * NPXF - j * d.w_out;
-            const int oy = gy0 + j;
-            if (oy < 0 || oy >= d.h_out) continue;
-            float tv[NPXF];          // targets first: their latency overlaps the compute
+        // RPF vertically adjacent pixels of one column per thread: items (column, row group) fill the
+        // 256 lanes exactly on 64-wide planes (20 rows = 4 groups x 64 columns with 16-row tiles; the
+        // horizontal 4-pixel form left 64 of 320 groups for a second, quarter-full pass).  Per (ci, kx)
+        // the column's RPF + K - 1 input values are read once (lanes on consecutive columns: one
+        // 256-B LDS row per read, no bank conflicts) and serve the RPF x K taps.
+        constexpr int RPF = 5;
+        const int nrg = (G.gh + RPF - 1) / RPF, nitem = nrg * d.w_out;
+        for (int it = tid; it < nitem; it += 256) {
+            const int rg = dq(it, G.d_wout), x = it - rg * d.w_out;
+            const int j0 = rg * RPF;
+            float tv[RPF];
 #pragma unroll
-            for (int p = 0; p < NPXF; ++p) tv[p] = as_gld(tg)[oy * d.w_out + x0 + p];
-            float mu[NPXF], ls[NPXF];
+            for (int p = 0; p < RPF; ++p) {
+                const int oy = gy0 + j0 + p;
+                const bool ok = j0 + p < G.gh && oy >= 0 && oy < d.h_out;
+                tv[p] = ok ? as_gld(tg)[oy * d.w_out + x] : 0.f;
+            }
+            float mu[RPF], ls[RPF];
 #pragma unroll
-            for (int p = 0; p < NPXF; ++p) mu[p] = ls[p] = 0.f;
+            for (int p = 0; p < RPF; ++p) mu[p] = ls[p] = 0.f;
             for (int ci = 0; ci < d.cin; ++ci) {
-                const float* arow = al + (ci * G.rh + j) * G.P + HALO + x0 - PADK;
-                // the channel's 2 x K x K weights are wave-uniform: scalar loads (constant address
-                // space) into SGPRs, FMA operands straight from there -- no LDS traffic for them
+                const float* acol = al + ci * G.rh * G.P + HALO + x - PADK;
                 const auto* cw0 = (const __attribute__((address_space(4))) float*)(params + w_off + (int64_t)ci * KK);
                 const auto* cw1 = cw0 + d.cin * KK;
 #pragma unroll
-                for (int ky = 0; ky < K; ++ky) {
-                    float win[NW];
-                    lds_window<NW, (HALO - PADK) & 3>(arow + ky * G.P, win);   // x0 multiple of 4
+                for (int kx = 0; kx < K; ++kx) {
+                    // input row j0 + r feeds pixel p through tap ky = r - p: one value live at a time
 #pragma unroll
-                    for (int kx = 0; kx < K; ++kx) {
-                        const float w0 = cw0[ky * K + kx], w1 = cw1[ky * K + kx];
+                    for (int r = 0; r < RPF + K - 1; ++r) {
+                        const float v = acol[min(j0 + r, G.rh - 1) * G.P + kx];
 #pragma unroll
-                        for (int p = 0; p < NPXF; ++p) {
-                            mu[p] = fmaf(w0, win[p + kx], mu[p]);
-                            ls[p] = fmaf(w1, win[p + kx], ls[p]);
+                        for (int p = 0; p < RPF; ++p) {
+                            const int ky = r - p;
+                            if (ky < 0 || ky >= K) continue;
+                            mu[p] = fmaf(cw0[ky * K + kx], v, mu[p]);
+                            ls[p] = fmaf(cw1[ky * K + kx], v, ls[p]);
                         }
                     }
                 }
             }
-            const bool own = j >= PADK && j < PADK + G.th;
-            float* g0 = gl + j * G.PG + HALO + x0;
 #pragma unroll
-            for (int p = 0; p < NPXF; ++p) {
-                const float tgt = tv[p];
+            for (int p = 0; p < RPF; ++p) {
+                const int j = j0 + p, oy = gy0 + j;
+                if (j >= G.gh || oy < 0 || oy >= d.h_out) continue;
+                const bool own = j >= PADK && j < PADK + G.th;
                 const float e = expf(-2.f * ls[p]);
                 const float emu = ex ? expf(mu[p]) : 1.f;
-                const float r = ex ? expf(tgt) - emu : tgt - mu[p];
+                const float r = ex ? expf(tv[p]) - emu : tv[p] - mu[p];
                 if (own) Lv += -0.5f * (2.f * ls[p] + r * r * e + GPI_LOG2PI);
-                g0[p] = -scl * r * e * emu;
-                g0[gplane + p] = scl * (1.f - r * r * e);
+                float* g0 = gl + j * G.PG + HALO + x;
+                g0[0] = -scl * r * e * emu;
+                g0[gplane] = scl * (1.f - r * r * e);
             }
         }
         // one fp64 atomic per workgroup (per-wave atomics into 16 replicas serialise: 2304 x 4 adds)

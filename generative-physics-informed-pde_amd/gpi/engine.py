@@ -396,6 +396,14 @@ class ElboEngine(object):
         self.running = BnRunning([(self.ep, run_mods.get('enc', enc), [(0, self.B_u)]),
                                   (self.dp, run_mods.get('dec', dec), list(enumerate(self.dec_sizes)))], ws, dev)
         self._running_pending = False
+        # encoder slab reduction: all on the main stream after the input conv's backward ('main'), or
+        # split ('split': the input conv's slabs on the main stream, the rest on the side stream
+        # concurrently with the input conv's backward)
+        self.enc_reduce = 'split'
+        # side-stream priority (torch: lower = higher priority; 0 = default)
+        self.side_priority = 0
+        # ROM launches enqueued before the decoder forward (capture order) instead of after it
+        self.rom_first = False
 
     # ------------------------------------------------------------------
     def eps_z(self):
@@ -489,16 +497,14 @@ class ElboEngine(object):
             main = torch.cuda.current_stream()
             self._side_stream()
             self._ev_fork.record(main)
+            if self.rom_first:
+                self._launch_roms()
         _run(lib.gpi_codec_forward, self.dec_descs, self.n_dec_sep, C.byref(self.dctx), st, what='decoder forward')
         if self.n_dec_sep < len(self.dec_descs):
             _run(lib.gpi_conv_loss_fused, C.byref(self.dec_descs[self.n_dec_sep]), C.byref(self.dctx), st,
                  what='decoder output conv (forward + loss + backward)')
-        if self.roms:
-            self._side.wait_event(self._ev_fork)
-            for r in self.roms:
-                _run(lib.gpi_rom, C.byref(r), C.c_void_p(self._side.cuda_stream), what='rom')
-            self._ev_join.record(self._side)
-            self._pending_join = True
+        if self.roms and not self.rom_first:
+            self._launch_roms()
         if running == 'now':
             self.running.launch(st)
         self._running_pending = running == 'defer'
@@ -507,9 +513,16 @@ class ElboEngine(object):
             return self.elbo_value()
         return None
 
+    def _launch_roms(self):
+        self._side.wait_event(self._ev_fork)
+        for r in self.roms:
+            _run(_lib().gpi_rom, C.byref(r), C.c_void_p(self._side.cuda_stream), what='rom')
+        self._ev_join.record(self._side)
+        self._pending_join = True
+
     def _side_stream(self):
         if self._side is None:
-            self._side = torch.cuda.Stream(device=torch.cuda.current_stream().device)
+            self._side = torch.cuda.Stream(device=torch.cuda.current_stream().device, priority=self.side_priority)
             self._ev_fork, self._ev_join = torch.cuda.Event(), torch.cuda.Event()
             self._ev_fork2, self._ev_join2 = torch.cuda.Event(), torch.cuda.Event()
             self._ev_enc = torch.cuda.Event()
@@ -609,11 +622,13 @@ class ElboEngine(object):
             # every encoder conv but the first (reverse order) ...
             rest = C.cast(C.byref(self.enc_descs, C.sizeof(L.ConvDesc)), C.POINTER(L.ConvDesc))
             _run(lib.gpi_codec_backward, rest, n_enc - 1, C.byref(self.ectx), st, what='encoder backward')
-            self._ev_enc.record(main)
+            enc_split = self.enc_reduce == 'split'
+            if enc_split:
+                self._ev_enc.record(main)
             # ... then the input conv (weight gradient only), whose slab reduction stays on the main
             # stream while the side stream reduces the other encoder slabs concurrently
             _run(lib.gpi_conv_backward, C.byref(self.enc_descs[0]), C.byref(self.ectx), st, what='In_conv backward')
-            run_reduce(self.reduce_enc[:self.n_reduce_in], self.ws, self.flat, st)
+            run_reduce(self.reduce_enc[:self.n_reduce_in] if enc_split else self.reduce_enc, self.ws, self.flat, st)
         side.wait_event(self._ev_fork2)
         sst = C.c_void_p(side.cuda_stream)
         if split:
@@ -629,7 +644,7 @@ class ElboEngine(object):
              C.c_void_p(self.flat.gacc.data_ptr()), sst, what='outer gemm')
         if side_extra is not None:
             side_extra(sst)
-        if n_enc:
+        if n_enc and self.enc_reduce == 'split':
             side.wait_event(self._ev_enc)
             run_reduce(self.reduce_enc[self.n_reduce_in:], self.ws, self.flat, sst)
         self._ev_join2.record(side)

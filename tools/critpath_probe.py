@@ -25,6 +25,12 @@ def main():
         e.early_rom = False
     if variant in ('no_noise', 'no_side'):
         step._launch_noise = lambda *a, **k: None
+    if variant == 'rom_first':
+        e.rom_first = True
+    if variant == 'side_prio':
+        e.side_priority = -1
+    if variant == 'enc_reduce_main':
+        e.enc_reduce = 'main'
     step.capture()
     for _ in range(30):
         step.step()
