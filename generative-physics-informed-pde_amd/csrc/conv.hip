@@ -86,6 +86,8 @@ struct ConvGeom {
     const float* zero;   // the zero page (kernel argument: no per-use address reload)
     int zreg;       // backward: the BN-backward operand z of the output in registers (<= ZREG chunks / thread)
     int npx;        // forward: horizontally adjacent output pixels per thread (1, 2, 4)
+    int cg;         // forward, tiles of <= 128 pixels: input-channel groups computing partial sums in parallel
+                    // (256 / pixels threads per pixel instead of one busy wave), summed through LDS
     int split;      // backward: 2 workgroups per tile, input gradient (blockIdx < nblocks) and weight gradient
                     // (the rest) in parallel on otherwise idle CUs (launches well under one round)
     int in_sq, in_sr, in_sc;   // 256 chunks of the input image = (planes, rows, chunks)
@@ -223,6 +225,12 @@ bool conv_geom(const gpi_conv_desc& d, const gpi_groups& g, ConvGeom& G, bool fw
     if (fwd) {
         const int tp = G.th * d.w_out;
         while (2 * G.npx <= npx_cap && tp >= 256 * 2 * G.npx && d.w_out % (2 * G.npx) == 0) G.npx *= 2;
+    }
+    G.cg = 1;
+    if (fwd && G.npx == 1 && d.epilogue != GPI_EPI_GAUSS_LOSS && d.epilogue != GPI_EPI_GAUSS_EXP_LOSS) {
+        static const int cg_on = env_int("GPI_FWD_CG", 1);
+        const int tp = G.th * d.w_out;
+        if (cg_on && tp <= 128 && 256 % tp == 0 && !d.upsample && d.k <= 3) G.cg = std::min(256 / tp, d.cin);
     }
     // the BN-backward operand image in registers when it is small: LDS = gradient + input images only
     // (one more resident workgroup per CU on the 32x32 / 64x64 decoder planes)
@@ -526,17 +534,42 @@ __device__ __forceinline__ void lds_window(const float* p, float (&win)[NW]) {
     for (int t = 0; t < NW; ++t) win[t] = buf[OFF + t];
 }
 
+// Activation / gradient stores of the conv epilogues: write-through (sc1) stores, which leave no dirty
+// line in the XCD's L2 for the kernel-end release to write back (the next launch reads them from memory
+// either way: other XCDs' L2s never see this one's lines).  C64 step 0.6267 vs 0.6346 ms with plain
+// stores (r02 A/B, 3 x 300 replays each; 0.630 vs 0.633 on a second box); GPI_PLAIN_STORES builds the
+// plain form for A/B runs.  The weight-gradient slab partials (scattered dwords) stay plain: write-through
+// measured slower there (0.636-0.652 ms).
+#ifndef GPI_PLAIN_STORES
+// relaxed agent-scope atomic stores lower to global_store_dword[x2] sc1 (the compiler schedules and
+// allocates them like ordinary stores)
+__device__ __forceinline__ void st2(float* p, f32x2 v) {
+    __hip_atomic_store((uint64_t*)p, __builtin_bit_cast(uint64_t, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st4(float* p, f32x4 v) {
+    // no 16-byte atomic store exists to lower it from; as two 8-byte halves it measured slower
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(p), "v"(v));
+}
+__device__ __forceinline__ void st1(float* p, float v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+#else
+__device__ __forceinline__ void st4(float* p, f32x4 v) { *as_gst((f32x4*)p) = v; }
+__device__ __forceinline__ void st2(float* p, f32x2 v) { *as_gst((f32x2*)p) = v; }
+__device__ __forceinline__ void st1(float* p, float v) { *as_gst(p) = v; }
+#endif
+
 // NPX consecutive floats of one output row (16-B / 8-B aligned: x0 is a multiple of NPX, planes are
 // multiples of 4 floats, buffers 16-B aligned -- aligned_ok)
 template <int NPX>
 __device__ __forceinline__ void store_px(float* p, const float (&v)[NPX]) {
     if constexpr (NPX == 4) {
-        *as_gst((f32x4*)p) = f32x4{v[0], v[1], v[2], v[3]};
+        st4(p, f32x4{v[0], v[1], v[2], v[3]});
     } else if constexpr (NPX == 2) {
-        *as_gst((f32x2*)p) = f32x2{v[0], v[1]};
+        st2(p, f32x2{v[0], v[1]});
     } else {
 #pragma unroll
-        for (int q = 0; q < NPX; ++q) as_gst(p)[q] = v[q];
+        for (int q = 0; q < NPX; ++q) st1(p + q, v[q]);
     }
 }
 
@@ -545,7 +578,8 @@ __device__ __forceinline__ void store_px(float* p, const float (&v)[NPX]) {
 constexpr int FWD_HDR = 8 * GPI_MAX_CIN + 2 * GPI_MAX_CIN + 64 + 16 + 8;
 
 template <int K, int S, int UP, int CP, int NPX>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void conv_fwd_kernel(gpi_conv_desc d, gpi_codec_ctx c, ConvGeom G) {
+// (the channel-group instantiation NPX == 0 runs one workgroup per CU: no occupancy target)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NPX == 0 ? 1 : 5))) void conv_fwd_kernel(gpi_conv_desc d, gpi_codec_ctx c, ConvGeom G) {
     touch_kernargs<CONV_KARG_BYTES>();
     if (SKIP(G, 16)) return;
     constexpr int KK = K * K;
@@ -759,11 +793,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void c
             }
         }
     } else {
+        // NPX == 0: the channel-group instantiation (G.cg > 1), otherwise one group (folds away)
+        const int cg = NPX == 0 ? G.cg : 1;
         for (int pbase = 0; pbase < tp; pbase += 256) {
-            const int pix = pbase + tid;
+            // cg > 1 (tp <= 128, one pass): thread = (channel group, pixel)
+            const int grp = NPX == 0 ? dq(tid, G.d_tp) : 0;
+            const int pix = NPX == 0 ? tid - grp * tp : pbase + tid;
             const int ty = dq(pix, G.d_wout), tx = pix - ty * d.w_out;
             const int oy = T.oy0 + ty, ox = tx;
-            const bool active = pix < tp;
+            bool active = pix < tp && grp < cg;
             float tgt = 0.f;
             if (gauss && active) {
                 int row = T.b - karg_sel(c.groups.start, T.grp);
@@ -776,7 +814,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void c
             for (int co = 0; co < CP; ++co) acc[co] = 0.f;
             if (active && !SKIP(G, 64)) {
                 const int plane = G.rh * G.P;
-                for (int ci = 0; ci < d.cin; ++ci) {
+                for (int ci = grp; ci < d.cin; ci += cg) {
                     const float* tci = img + ci * plane;
                     const float* wci = wT + ci * KK * CP;
     #pragma unroll
@@ -790,6 +828,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void c
                         }
                     }
                 }
+            }
+            if (NPX == 0 && cg > 1) {
+                // channel-group partials [grp - 1][pix][CP] after the image; group 0 sums them in group order
+                float* part = img + img_floats(d.cin, G.rh, G.P);
+                if (active && grp > 0) {
+    #pragma unroll
+                    for (int co = 0; co < CP; ++co) part[((grp - 1) * tp + pix) * CP + co] = acc[co];
+                }
+                __syncthreads();
+                if (active && grp == 0) {
+                    for (int g = 1; g < cg; ++g) {
+    #pragma unroll
+                        for (int co = 0; co < CP; ++co) acc[co] += part[((g - 1) * tp + pix) * CP + co];
+                    }
+                }
+                active = active && grp == 0;
             }
             PHASE(6);
             if (drop) {
@@ -820,10 +874,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void c
                 continue;
             }
             if (active) {
-                auto o = as_gst(ws + d.out_off + ((int64_t)T.b * d.out_ctot + d.out_c0) * HWo + oy * d.w_out + ox);
+                float* o = ws + d.out_off + ((int64_t)T.b * d.out_ctot + d.out_c0) * HWo + oy * d.w_out + ox;
     #pragma unroll
                 for (int co = 0; co < CP; ++co)
-                    if (co < d.cout) o[(int64_t)co * HWo] = acc[co];
+                    if (co < d.cout) st1(o + (int64_t)co * HWo, acc[co]);
             }
             if (d.epilogue == GPI_EPI_STORE_STATS) {
     #pragma unroll
@@ -1507,7 +1561,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
                             } else {
                                 o = pa + acc[q];
                             }
-                            *as_gst(ws + gin_off + go) = o;
+                            *as_gst(ws + gin_off + go) = o;   // every other pixel: plain (sc1 measured slower)
                         }
                     } else if (cok) {
                         float* gp = ws + gin_off + ibase + 16 * m + 4 * kq;
@@ -1527,7 +1581,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
                                 o[q] = pa[q] + acc[q];
                             }
                         }
-                        *as_gst((f32x4*)gp) = f32x4{o[0], o[1], o[2], o[3]};
+                        st4(gp, f32x4{o[0], o[1], o[2], o[3]});
                     }
                 }
             }
@@ -1683,8 +1737,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
 }
 
 size_t fwd_lds(const gpi_conv_desc& d, const ConvGeom& G, int cp) {
-    return sizeof(float) *
-           ((size_t)pad256(FWD_HDR) + pad256(d.cin * d.k * d.k * cp) + img_floats(d.cin, G.rh, G.P));
+    return sizeof(float) * ((size_t)pad256(FWD_HDR) + pad256(d.cin * d.k * d.k * cp) + img_floats(d.cin, G.rh, G.P) +
+                            (G.cg > 1 ? (size_t)(G.cg - 1) * G.th * d.w_out * cp : 0));
 }
 
 size_t bwd_lds_floats(const gpi_conv_desc& d, int rh, int P, int gh, int PG, int zreg) {
@@ -1715,6 +1769,9 @@ conv_kernel_t pick(int cp, bool fwd, int npx) {
     if (!fwd) return conv_bwd_kernel<K, S, UP>;
     if (npx == 4) return pick_cp<K, S, UP, 4>(cp);
     if (npx == 2) return pick_cp<K, S, UP, 2>(cp);
+    if constexpr (!UP && K <= 3) {   // channel-group instantiation: the small-plane codec convs only
+        if (npx == 0) return pick_cp<K, S, UP, 0>(cp);
+    }
     return pick_cp<K, S, UP, 1>(cp);
 }
 
@@ -1767,7 +1824,8 @@ int launch(const gpi_conv_desc& d, const gpi_codec_ctx& c, hipStream_t st, bool 
     if (!fwd && d.gin_off >= 0 && ((G.ph * d.w_in) & 15)) return GPI_ERR_UNSUPPORTED;
     if (!fwd && d.gin_off >= 0 && d.stride == 2 && ((d.w_in & 7) || (G.ph & 1))) return GPI_ERR_UNSUPPORTED;
     const int cp = cp_of(d);
-    conv_kernel_t k = fuse ? conv_bwd_kernel<5, 1, 0, true> : select_kernel(d, cp, fwd, G.npx);
+    conv_kernel_t k = fuse ? conv_bwd_kernel<5, 1, 0, true>
+                           : select_kernel(d, cp, fwd, G.cg > 1 ? 0 : G.npx);
     if (!k) return GPI_ERR_UNSUPPORTED;
     static const float* zero = nullptr;
     if (!zero) {
