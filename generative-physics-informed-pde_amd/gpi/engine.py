@@ -404,6 +404,8 @@ class ElboEngine(object):
         self.side_priority = 0
         # ROM launches enqueued before the decoder forward (capture order) instead of after it
         self.rom_first = False
+        # callable(side stream handle) launched on the side stream ahead of the ROM (fused step)
+        self.side_pre = None
 
     # ------------------------------------------------------------------
     def eps_z(self):
@@ -515,6 +517,8 @@ class ElboEngine(object):
 
     def _launch_roms(self):
         self._side.wait_event(self._ev_fork)
+        if self.side_pre is not None:
+            self.side_pre(C.c_void_p(self._side.cuda_stream))
         for r in self.roms:
             _run(_lib().gpi_rom, C.byref(r), C.c_void_p(self._side.cuda_stream), what='rom')
         self._ev_join.record(self._side)

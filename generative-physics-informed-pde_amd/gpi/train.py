@@ -82,6 +82,8 @@ class FusedElboStep(object):
                                v=self.v.data_ptr(), n=self.flat.numel, lr=self.lr.data_ptr(),
                                step=self.step_ctr.data_ptr(), beta1=betas[0], beta2=betas[1], eps=eps)
         self.idx_next = torch.zeros_like(self.idx)
+        # A/B switch (tools/critpath_probe.py): draw the next step's subset on the side stream ahead of the ROM
+        self.subset_early = False
         my_idx = self.idx[self.rank * self.B_u:(self.rank + 1) * self.B_u] if self.B_u else None
         self.engine.bind(X_u=self.X_pool, u_index=my_idx, X_s=X_s, Y=Y, F=F)
         n_pool = self.X_pool.shape[0] if self.X_pool is not None else 0
@@ -117,7 +119,12 @@ class FusedElboStep(object):
         self._launch_noise(L.stream_handle(), self.idx, sub0=100)
 
     # ------------------------------------------------------------------
-    def _launch_noise(self, st, idx, sub0=0, codecs=('enc', 'dec')):
+    def _launch_subset(self, st, idx, sub0=0):
+        if self.B_u:
+            L.check(L.lib().gpi_random_subset(L.ptr(idx), self.n_pool, self.n_sub, self.subset_seed,
+                                              L.ptr(self.rng_off), sub0 + 1, st), 'random subset')
+
+    def _launch_noise(self, st, idx, sub0=0, codecs=('enc', 'dec'), subset=True):
         """Random subset into ``idx`` and the reparametrisation noise into the engine's eps
         buffers.  Philox streams: the step's offset (advanced by Adam at the end of every step)
         and sub ids sub0 + {1, 2, 3}; the noise drawn during step k (for step k+1) therefore
@@ -125,9 +132,8 @@ class FusedElboStep(object):
         lib = L.lib()
         if self.engine.has_dropout and codecs:   # Dropout2d channel scales (sub ids sub0 + 4 enc, + 5 dec)
             self.engine.draw_dropout(st, self.seed, L.ptr(self.rng_off), sub0 + 4, codecs=codecs)
-        if self.B_u:
-            L.check(lib.gpi_random_subset(L.ptr(idx), self.n_pool, self.n_sub, self.subset_seed, L.ptr(self.rng_off),
-                                          sub0 + 1, st), 'random subset')
+        if subset:
+            self._launch_subset(st, idx, sub0)
         ez = self.engine.eps_z()
         L.check(lib.gpi_randn(L.ptr(ez), ez.numel(), self.seed, L.ptr(self.rng_off), sub0 + 2, st), 'randn z')
         if self.engine.N_ex:
@@ -140,10 +146,14 @@ class FusedElboStep(object):
         the head backward has consumed this step's; the epilogue (gradient finalisation, scratch
         reset, subset hand-over) is one launch."""
         st = stream if stream is not None else L.stream_handle()
+        # subset_early: the next step's subset (it writes only idx_next) ahead of the ROM on the side stream
+        early = self.subset_early and bool(self.engine.roms)
+        self.engine.side_pre = (lambda sst: self._launch_subset(sst, self.idx_next)) if early else None
         self.engine.forward(st, compute_value=False, zero_gacc=False, zero_scratch=False, running='defer')
         # next step's subset / noise / decoder masks concurrently with the encoder backward; the
         # encoder's masks by the epilogue below (the encoder backward reads this step's)
-        self.engine.backward(st, side_extra=lambda sst: self._launch_noise(sst, self.idx_next, codecs=('dec',)))
+        self.engine.backward(st, side_extra=lambda sst: self._launch_noise(sst, self.idx_next, codecs=('dec',),
+                                                                           subset=not early))
         L.check(L.lib().gpi_step_epilogue(C.byref(self.epi), st), 'step epilogue')
 
     def allreduce(self):

@@ -25,6 +25,8 @@ def main():
         e.early_rom = False
     if variant in ('no_noise', 'no_side'):
         step._launch_noise = lambda *a, **k: None
+    if variant == 'subset_early':
+        step.subset_early = True
     if variant == 'rom_first':
         e.rom_first = True
     if variant == 'side_prio':
