@@ -25,6 +25,10 @@ def main():
         e.early_rom = False
     if variant in ('no_noise', 'no_side'):
         step._launch_noise = lambda *a, **k: None
+    if variant == 'two_graphs':
+        step.n_graphs = 2
+    if variant == 'side_split':
+        e.side_split = True
     if variant == 'subset_early':
         step.subset_early = True
     if variant == 'rom_first':
