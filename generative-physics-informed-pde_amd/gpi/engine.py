@@ -400,15 +400,10 @@ class ElboEngine(object):
         # split ('split': the input conv's slabs on the main stream, the rest on the side stream
         # concurrently with the input conv's backward)
         self.enc_reduce = 'split'
-        # side-stream priority (torch: lower = higher priority; 0 = default)
-        self.side_priority = 0
         # ROM launches enqueued before the decoder forward (capture order) instead of after it
         self.rom_first = False
         # callable(side stream handle) launched on the side stream ahead of the ROM (fused step)
         self.side_pre = None
-        # A/B switch: split the backward's side work over two side streams (see backward)
-        self.side_split = False
-        self._side2 = None
 
     # ------------------------------------------------------------------
     def eps_z(self):
@@ -527,15 +522,9 @@ class ElboEngine(object):
         self._ev_join.record(self._side)
         self._pending_join = True
 
-    def _side2_stream(self):
-        if self._side2 is None:
-            self._side2 = torch.cuda.Stream(device=torch.cuda.current_stream().device)
-            self._ev_a1, self._ev_a = torch.cuda.Event(), torch.cuda.Event()
-        return self._side2
-
     def _side_stream(self):
         if self._side is None:
-            self._side = torch.cuda.Stream(device=torch.cuda.current_stream().device, priority=self.side_priority)
+            self._side = torch.cuda.Stream(device=torch.cuda.current_stream().device)
             self._ev_fork, self._ev_join = torch.cuda.Event(), torch.cuda.Event()
             self._ev_fork2, self._ev_join2 = torch.cuda.Event(), torch.cuda.Event()
             self._ev_enc = torch.cuda.Event()
@@ -649,31 +638,6 @@ class ElboEngine(object):
             hq.flags |= L.HEAD_PART_Q
             _run(lib.gpi_head_backward, C.byref(hq), P_, W_, G_, sst, what='head backward (variational samples)')
             self._pending_join = False          # joined below with the rest of the side work
-        if self.side_split:
-            # two side streams: the ROM chain (variational head backward -> dense weight GEMM) and the rest
-            # (decoder slab reduction, BN running statistics, next-step draws once the head backward has
-            # read this step's noise, encoder slab reduction), which does not wait for the ROM
-            s2 = self._side2_stream()
-            self._ev_a1.record(side)
-            _run(lib.gpi_outer_gemm, self.gemm_items, len(self.gemm_items), C.c_void_p(self.ws.t_ws.data_ptr()),
-                 C.c_void_p(self.flat.gacc.data_ptr()), sst, what='outer gemm')
-            self._ev_a.record(side)
-            s2.wait_event(self._ev_fork2)
-            sst2 = C.c_void_p(s2.cuda_stream)
-            run_reduce(self.reduce_dec, self.ws, self.flat, sst2)
-            if self._running_pending:
-                self.running.launch(sst2)
-                self._running_pending = False
-            if side_extra is not None:
-                s2.wait_event(self._ev_a1)
-                side_extra(sst2)
-            if n_enc and self.enc_reduce == 'split':
-                s2.wait_event(self._ev_enc)
-                run_reduce(self.reduce_enc[self.n_reduce_in:], self.ws, self.flat, sst2)
-            s2.wait_event(self._ev_a)
-            self._ev_join2.record(s2)
-            main.wait_event(self._ev_join2)
-            return
         run_reduce(self.reduce_dec, self.ws, self.flat, sst)
         if self._running_pending:
             self.running.launch(sst)

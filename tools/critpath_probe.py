@@ -1,6 +1,9 @@
 """Critical-path probe of the fused C64 step (timing experiments only; variants skip work, so their
 ELBO values are meaningless): ms per graph replay of the full step and of variants without the
-side-stream ROM ('no_rom'), without the next-step noise draws ('no_noise'), or without both.
+side-stream ROM ('no_rom'), without the next-step noise draws ('no_noise'), or without both; and
+schedule variants that do all the work: 'enc_reduce_main' (encoder slab reduction on the main stream),
+'rom_first' (ROM captured before the decoder forward), 'subset_early' (next-step subset ahead of the ROM),
+'two_graphs' (two graph instances replayed alternately).
 usage: python tools/critpath_probe.py VARIANT [steps]"""
 import os
 import sys
@@ -27,14 +30,10 @@ def main():
         step._launch_noise = lambda *a, **k: None
     if variant == 'two_graphs':
         step.n_graphs = 2
-    if variant == 'side_split':
-        e.side_split = True
     if variant == 'subset_early':
         step.subset_early = True
     if variant == 'rom_first':
         e.rom_first = True
-    if variant == 'side_prio':
-        e.side_priority = -1
     if variant == 'enc_reduce_main':
         e.enc_reduce = 'main'
     step.capture()
