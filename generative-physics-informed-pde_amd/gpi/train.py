@@ -84,7 +84,6 @@ class FusedElboStep(object):
         self.idx_next = torch.zeros_like(self.idx)
         # A/B switch (tools/critpath_probe.py): draw the next step's subset on the side stream ahead of the ROM
         self.subset_early = False
-        self.n_graphs = 1               # A/B switch: 2 = two graph instances replayed alternately
         my_idx = self.idx[self.rank * self.B_u:(self.rank + 1) * self.B_u] if self.B_u else None
         self.engine.bind(X_u=self.X_pool, u_index=my_idx, X_s=X_s, Y=Y, F=F)
         n_pool = self.X_pool.shape[0] if self.X_pool is not None else 0
@@ -220,27 +219,13 @@ class FusedElboStep(object):
                 self.forward_backward()
                 self.allreduce()        # RCCL: captured as a graph node
                 self.update()
-            # n_graphs = 2 (A/B): a second instance of the same step, replayed alternately, so that the
-            # runtime can prepare one replay while the other still runs
-            self._g_alt = None
-            if self.n_graphs == 2:
-                self._g_alt = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(self._g_alt):
-                    self.forward_backward()
-                    self.allreduce()
-                    self.update()
-            self._flip = False
         self.graph = True
 
     def step(self):
         self.sync_lr()
         if self.graph is None:
             return self.step_eager()
-        if getattr(self, '_g_alt', None) is not None and self._flip:
-            self._g_alt.replay()
-        else:
-            self.g_fb.replay()
-        self._flip = not getattr(self, '_flip', False)
+        self.g_fb.replay()
         if self.split_graph:
             self.allreduce()
             self.g_up.replay()

@@ -2,8 +2,7 @@
 ELBO values are meaningless): ms per graph replay of the full step and of variants without the
 side-stream ROM ('no_rom'), without the next-step noise draws ('no_noise'), or without both; and
 schedule variants that do all the work: 'enc_reduce_main' (encoder slab reduction on the main stream),
-'rom_first' (ROM captured before the decoder forward), 'subset_early' (next-step subset ahead of the ROM),
-'two_graphs' (two graph instances replayed alternately).
+'rom_first' (ROM captured before the decoder forward), 'subset_early' (next-step subset ahead of the ROM).
 usage: python tools/critpath_probe.py VARIANT [steps]"""
 import os
 import sys
@@ -28,8 +27,6 @@ def main():
         e.early_rom = False
     if variant in ('no_noise', 'no_side'):
         step._launch_noise = lambda *a, **k: None
-    if variant == 'two_graphs':
-        step.n_graphs = 2
     if variant == 'subset_early':
         step.subset_early = True
     if variant == 'rom_first':
