@@ -147,21 +147,33 @@ def launch_bytes(kind, d, B):
 
 def profile_kernels(step, reps=20):
     """Per-launch device time of every codec operator, measured with HIP events on
-    the stream the kernels run on; returns [(name, ms, bytes)]."""
+    the stream the kernels run on; returns [(name, ms, bytes)].  The reps launches of an
+    operator are captured into one HIP graph and timed as two replays of it: back to back on
+    the device, so a slow host (eager launches through ctypes cost about as much as the
+    smallest kernels) cannot stretch the measured time."""
     import ctypes as C
     from gpi import _lib as L
-    st = L.stream_handle()
     out = []
     for name, kind, fn, d, ctx, B in step_conv_launches(step.engine):
+        st = L.stream_handle()
         for _ in range(3):
             fn(C.byref(d), C.byref(ctx), st)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            cst = L.stream_handle()
+            for _ in range(reps):
+                fn(C.byref(d), C.byref(ctx), cst)
+        g.replay()
+        torch.cuda.synchronize()
         t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0.record()
-        for _ in range(reps):
-            fn(C.byref(d), C.byref(ctx), st)
+        g.replay()
+        g.replay()
         t1.record()
         torch.cuda.synchronize()
-        out.append((name, t0.elapsed_time(t1) / reps, launch_bytes(kind, d, B)))
+        out.append((name, t0.elapsed_time(t1) / (2 * reps), launch_bytes(kind, d, B)))
+        del g
     return out
 
 
@@ -323,8 +335,8 @@ def conv_source_sha():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=50)
-    ap.add_argument('--warmup', type=int, default=30)
+    ap.add_argument('--steps', type=int, default=200)
+    ap.add_argument('--warmup', type=int, default=200)
     ap.add_argument('--config', default='c64', choices=sorted(CONFIGS))
     ap.add_argument('--no-graph', action='store_true')
     ap.add_argument('--no-cpu-baseline', action='store_true')
