@@ -160,8 +160,8 @@ def profile_kernels(step, reps=20):
             fn(C.byref(d), C.byref(ctx), st)
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            cst = L.stream_handle()
+        with torch.cuda.graph(g, capture_error_mode='thread_local'):   # (rank 0 of a DP job: other
+            cst = L.stream_handle()                                      # threads may touch the device)
             for _ in range(reps):
                 fn(C.byref(d), C.byref(ctx), cst)
         g.replay()
