@@ -543,15 +543,18 @@ __device__ __forceinline__ void lds_window(const float* p, float (&win)[NW]) {
 #ifndef GPI_PLAIN_STORES
 // relaxed agent-scope atomic stores lower to global_store_dword[x2] sc1 (the compiler schedules and
 // allocates them like ordinary stores)
+// (global address space: a generic pointer would make them flat stores, which also count against the LDS
+// counter and are ordered against LDS traffic)
 __device__ __forceinline__ void st2(float* p, f32x2 v) {
-    __hip_atomic_store((uint64_t*)p, __builtin_bit_cast(uint64_t, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((__attribute__((address_space(1))) uint64_t*)p, __builtin_bit_cast(uint64_t, v),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ void st4(float* p, f32x4 v) {
     // no 16-byte atomic store exists to lower it from; as two 8-byte halves it measured slower
     asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(p), "v"(v));
 }
 __device__ __forceinline__ void st1(float* p, float v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((__attribute__((address_space(1))) float*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 #else
 __device__ __forceinline__ void st4(float* p, f32x4 v) { *as_gst((f32x4*)p) = v; }
