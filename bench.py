@@ -7,15 +7,20 @@ step   : random armortized subset + reparametrisation noise + ELBO forward
          gradients] + Adam over every parameter  (training.py:405-417 without
          the PredictionEnsemble / monitoring extras).
 work   : per GPU B_u = 256 unlabeled + N_s = 32 labeled 64x64 samples
-         (highres codec, ROM 8x8, drop_rate 0), weak scaling over GPUs.
+         (highres codec, ROM 8x8, the factory's Dropout2d rate 0.2), weak
+         scaling over GPUs.
 
-Usage: python bench.py [--gpus N --steps K --warmup W]; for N > 1 launch one
-process per GPU with torch.distributed.run (RCCL backend).
+Usage: python bench.py [--gpus N --steps K --warmup W].  With N > 1 and no
+torch.distributed environment, this process starts ``torch.distributed.run
+--nproc-per-node N`` as a CHILD (before it touches the GPU) and relays rank 0's
+JSON line; under torchrun (WORLD_SIZE set) WORLD_SIZE must equal N.
 """
 import argparse
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -332,6 +337,33 @@ def conv_source_sha():
     return h.hexdigest()
 
 
+def free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """--gpus n > 1 without a torch.distributed environment: one process per GPU through
+    torch.distributed.run, started as a child process of this one (which has not touched the GPU:
+    no exec from a GPU-initialised process).  Rank 0's stdout (the JSON line) is relayed; the
+    ranks' stderr goes straight through.  Returns the launcher's exit code."""
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', str(n),
+           '--master-addr', '127.0.0.1', '--master-port', str(free_port()),
+           os.path.abspath(__file__)] + list(argv)
+    log('launching %d ranks: %s' % (n, ' '.join(cmd[1:])))
+    env = dict(os.environ)
+    env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')     # dmabuf IPC (RCCL across processes)
+    proc = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, text=True)
+    for line in proc.stdout.splitlines():
+        if line.startswith('{'):
+            print(line)
+            sys.stdout.flush()
+        elif line.strip():
+            sys.stderr.write(line + '\n')
+    return proc.returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -350,6 +382,14 @@ def main():
     # graph all-reduce, an A/B build of the library): recorded in the JSON line
     tuning = {k: os.environ[k] for k in sorted(os.environ) if k.startswith('GPI_')}
 
+    if args.gpus < 1:
+        raise SystemExit('--gpus must be >= 1')
+    if 'WORLD_SIZE' not in os.environ:
+        if args.gpus > 1:
+            sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    elif int(os.environ['WORLD_SIZE']) != args.gpus:
+        raise SystemExit('bench.py: WORLD_SIZE=%s differs from --gpus %d (refusing to report a line for a '
+                         'different GPU count)' % (os.environ['WORLD_SIZE'], args.gpus))
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
@@ -453,7 +493,11 @@ def main():
                                    'ROM %dx%d, fused native step' % (CONFIG_TAG[args.config], args.config, B_u, N_s,
                                                                      physics['rom'].grid.n, physics['rom'].grid.n),
                        'global_batch': world * per_step, 'grid': physics['fom'].grid.n,
-                       'parallelism': 'dp%d' % world, 'graph': not args.no_graph},
+                       'parallelism': 'dp%d' % world, 'graph': not args.no_graph,
+                       'world': world, 'backend': backend if distributed else None,
+                       'allreduce': None if not distributed else
+                       ('host-side between graphs' if args.no_graph or step.split_graph else 'in-graph'),
+                       'bn': 'replica' if not getattr(step, 'sync_bn', False) else 'sync'},
             'elbo_last': elbo,
             'host_enqueue_ms_per_step': round(1e3 * (t_enq - t0) / args.steps, 4),
             'roofline': roof,

@@ -384,7 +384,8 @@ class Analysis(object):
         relerr_y, logscore_y, r2_y = predictive_scores(Y, y_mean, y_std)
         if iteration is None:
             if return_mean_std:
-                raise RuntimeError('nope')
+                # the reference refuses this combination as well (components.py:516-517)
+                raise RuntimeError('eval_all_y: return_mean_std=True needs an iteration to record the scores at')
             return logscore_y, r2_y, relerr_y
         self.data['relerr_y'].append(iteration, relerr_y)
         self.data['logscore_y'].append(iteration, logscore_y)

@@ -338,7 +338,10 @@ class ElboEngine(object):
         # ---- gradient reductions
         self.reduce_enc = self.ep.reduce_items(offE) if self.ep is not None else []
         # slab-reduction items of the encoder's input conv (the first op; no input BN: one item)
-        self.n_reduce_in = (2 if self.ep.ops[0].bn is not None else 1) if self.ep is not None else 0
+        # (counted per op: 1 for the weight, +1 or +2 for an input BN whose gamma / beta are (not)
+        # adjacent; a miscount would leave one of its items to the side stream while the main
+        # stream's input-conv backward still writes that slab)
+        self.n_reduce_in = self.ep.reduce_counts(offE)[0] if self.ep is not None else 0
         self.reduce_dec = self.dp.reduce_items(offD)
         self.reduce_items = self.reduce_enc + self.reduce_dec
         gi = []

@@ -193,6 +193,17 @@ class CodecProgram(object):
                     item(base + op.numel + op.cin, b, op.cin, op.rowlen, op.blocks)
         return items
 
+    def reduce_counts(self, param_offset):
+        """Number of reduce_items() entries each op contributes, in op order."""
+        out = []
+        for op in self.ops:
+            n = 1
+            if op.bn is not None:
+                g, b = param_offset(op.bn + '.weight'), param_offset(op.bn + '.bias')
+                n += 1 if b == g + op.cin else 2
+            out.append(n)
+        return out
+
 
 # --------------------------------------------------------------------------
 def encoder_program(imsize, blocks, growth, init_features, bn_size=8, bottleneck=True, drop_rate=0.0):

@@ -57,6 +57,10 @@ class FusedElboStep(object):
         self.B_u = int(B_u)
         self.rank, self.world = int(rank), int(world)
         assert 0 <= self.rank < self.world
+        if subset_seed is None and self.world > 1 and self.B_u > 0:
+            # every rank must draw the SAME global permutation (its B_u-slice of it); the per-rank
+            # noise seed would give overlapping / duplicated slices without any error
+            raise ValueError('FusedElboStep: world > 1 needs an explicit subset_seed shared by all ranks')
         self.engine = ElboEngine(model, self.B_u, self.N_s, normalize=normalize)
         dev = self.flat.P.device
         self.X_pool = X_pool.contiguous().float() if X_pool is not None else None
@@ -175,6 +179,7 @@ class FusedElboStep(object):
         self.forward_backward()
         self.allreduce()
         self.update()
+        self.optimizer.step()      # no-op; tells torch LR schedulers that an optimizer step happened
 
     # ------------------------------------------------------------------
     def _mutable_state(self):
@@ -229,6 +234,7 @@ class FusedElboStep(object):
         if self.split_graph:
             self.allreduce()
             self.g_up.replay()
+        self.optimizer.step()
 
     def elbo(self):
         """ELBO value of the last completed step (0-d tensor)."""

@@ -47,6 +47,12 @@ def main(out):
     model, _ = shard_model(d, rank)
     ds = model._datasets['supervised']
     Xu = torch.tensor(d['Xu'], device='cuda')
+    try:        # world > 1 without a shared subset seed: refused (ranks would draw different permutations)
+        FusedElboStep(model, Xu, B_U, ds.get('X'), ds.get('Y'), ds.get('F_ROM_BC'), seed=50 + rank,
+                      distributed=True, rank=rank, world=world)
+        raise AssertionError('FusedElboStep accepted world > 1 without subset_seed')
+    except ValueError:
+        pass
     step = FusedElboStep(model, Xu, B_U, ds.get('X'), ds.get('Y'), ds.get('F_ROM_BC'), lr=1e-3, seed=50 + rank,
                          subset_seed=9, distributed=True, rank=rank, world=world)
     e = step.engine

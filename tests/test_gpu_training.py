@@ -77,10 +77,15 @@ def test_trainer_loop_fused_step(device, tmp_path):
     sw.register_optimizer(step.optimizer, 'training')
     step.capture()
     elbos = []
-    for n in range(N_STEPS):
-        step.step()
-        sw.step('training', metric=None)
-        elbos.append(step.elbo())
+    import warnings
+    with warnings.catch_warnings():
+        # the fused step reports its optimizer step to torch's scheduler hook (no "lr_scheduler.step()
+        # before optimizer.step()" warning)
+        warnings.filterwarnings('error', message='.*lr_scheduler.step.*')
+        for n in range(N_STEPS):
+            step.step()
+            sw.step('training', metric=None)
+            elbos.append(step.elbo())
     elbos = [float(e.item()) for e in elbos]
     assert all(math.isfinite(e) for e in elbos)
     assert np.mean(elbos[-10:]) > np.mean(elbos[:10]), elbos
