@@ -88,6 +88,118 @@ def oracle_fixture_elbo(d, **kw):
     return float(val.item()), {k: v.grad.numpy() for k, v in st.items() if v.grad is not None}
 
 
+def _c32_codecs(st, masks, n=32):
+    mk = masks or {}
+    cfg = CODEC[n]
+    enc_p = {k[8:]: v for k, v in st.items() if k.startswith('encoder.')}
+    dec_p = {k[2:]: v for k, v in st.items() if k.startswith('f.')}
+    enc = lambda x: ocodec.encoder_forward(enc_p, x, n, cfg['blocks'], cfg['growth'], cfg['f0'], mk.get('enc'))
+    dec = {g: (lambda z, g=g: ocodec.decoder_forward(dec_p, z, 8, cfg['blocks'], cfg['growth'], cfg['f0'],
+                                                     mk.get(g)))
+           for g in ('dec_u', 'dec_s', 'dec_v')}
+    return enc, dec
+
+
+def oracle_vo_fixture_elbo(d, vo_mean, vo_vars, masks=None, lockx=False, holdoff=False):
+    """fp64 oracle of GenerativeModel.elbo with the VO term (armortized unsupervised + supervised +
+    virtual observables; generative.py:247-287, freeX :341-392 / :461-500, lockX :300-339 / :429-459)
+    on vo_elbo(_lockx)_c32.npz's state, data and injected noise.  vo_mean / vo_vars: the VO posterior
+    the kernels conditioned (VirtualObservablesEnsemble.mean / .vars, fp32); the VO target is
+    reparametrize(mean, 0.5 log vars) (generative.py:311,356).  masks: the kernels' ReLU decisions per
+    codec call {'enc', 'dec_u', 'dec_s', 'dec_v'}.  holdoff: the VO term keeps logL_x - KL only.
+    Returns (elbo float, {name: grad of -elbo})."""
+    n, nc, dz, Nu, bs, Ns, Nvo, Nmc = [int(v) for v in d['cfg']]
+    st = state_of(d)
+    t = lambda k: torch.as_tensor(np.asarray(d[k]), dtype=torch.float64)
+    M, W, bc = t('M'), t('W'), torch.as_tensor(d['bc_dofs'])
+    enc, dec = _c32_codecs(st, masks, n)
+    gp = lambda z: torch.nn.functional.linear(z, st['gp.fc.weight'], st['gp.fc.bias'])
+    rom = lambda x, F: oelbo.rom_operator(W, M, bc, x, F, st['g.logsigmas_y'])
+    qz = lambda key: (st['q_z.%s._mean' % key], st['q_z.%s._logsigma' % key])
+    qx = lambda key: (st['q_X.%s._mean' % key], st['q_X.%s._logsigma' % key])
+    pre = 'epsh' if holdoff else 'eps'
+    e = lambda i: t('%s%d' % (pre, i))
+    Xu = t('Xu')[torch.as_tensor(d['perm'][:bs])]
+    e1, _ = oelbo.elbo_unsupervised_armortized(enc, dec['dec_u'], Xu, e(0))
+    if lockx:
+        e2, _ = oelbo.elbo_supervised_lockX(dec['dec_s'], gp, rom, qz('supervised'), t('Xs'), t('Ys'), t('Fs'), e(1))
+        i_qz, i_y = 2, 3
+    else:
+        e2, _ = oelbo.elbo_supervised_freeX(dec['dec_s'], gp, st['gp.logsigmas_X'], rom, qz('supervised'),
+                                            qx('supervised'), t('Xs'), t('Ys'), t('Fs'), e(1), e(2))
+        i_qz, i_y = 3, 5
+    if holdoff:
+        z = oelbo.reparam(*qz('vo'), e(i_qz))
+        mx, lsx = dec['dec_v'](z)
+        e3 = oelbo.dgll(t('Xv'), mx, 2 * lsx) - oelbo.kl_unit(qz('vo')[0], 2 * qz('vo')[1])
+    else:
+        vm = torch.as_tensor(np.asarray(vo_mean), dtype=torch.float64)
+        vv = torch.as_tensor(np.asarray(vo_vars), dtype=torch.float64)
+        y = vm + torch.sqrt(vv) * e(i_y)
+        if lockx:
+            e3, _ = oelbo.elbo_supervised_lockX(dec['dec_v'], gp, rom, qz('vo'), t('Xv'), y, t('Fv'), e(i_qz))
+        else:
+            e3, _ = oelbo.elbo_supervised_freeX(dec['dec_v'], gp, st['gp.logsigmas_X'], rom, qz('vo'), qx('vo'),
+                                                t('Xv'), y, t('Fv'), e(i_qz), e(4))
+    val = e1 + e2 + e3
+    (-val).backward()
+    return float(val.item()), {k: v.grad.numpy() for k, v in st.items() if v.grad is not None}
+
+
+def oracle_vo_updates(d, lockx=False, n_updates=2):
+    """fp64 oracle of update_virtual_observables x n_updates (generative.py:182-222: MC predictive through
+    the ROM with the fixture's injected draws; VirtualObservables.py:642-669 conditioning, :971-998
+    precision update between updates) on vo_elbo(_lockx)_c32.npz.  Returns a list of dicts
+    {Y_mean, Y_std, vo_var, mean, vars} per update and the final prec_beta."""
+    n, nc, dz, Nu, bs, Ns, Nvo, Nmc = [int(v) for v in d['cfg']]
+    st = {k: v.detach() for k, v in state_of(d).items()}
+    t = lambda k: torch.as_tensor(np.asarray(d[k]), dtype=torch.float64)
+    M, W, bc = t('M'), t('W'), torch.as_tensor(d['bc_dofs'])
+    G, A = t('Gamma'), t('alpha')
+    m = G.shape[1]
+    infinite = torch.zeros(m, dtype=torch.bool)
+    infinite[:(nc + 1) ** 2] = True             # CGR rows: infinite precision; flux rows learnable
+    vo_var = oelbo.vo_mean_variances(torch.ones(m, dtype=torch.float64), Nvo, infinite)
+    gp = (lambda z: torch.nn.functional.linear(z, st['gp.fc.weight'], st['gp.fc.bias'])) if lockx else None
+    qkey = 'q_z.vo' if lockx else 'q_X.vo'
+    out, beta = [], None
+    for it in range(n_updates):
+        ex = t('upd%d.eps_X' % it).view(Nvo, Nmc, -1)
+        ey = t('upd%d.eps_y' % it).view(Nvo, Nmc, -1)
+        Ym, Ys = oelbo.vo_predictive(W, M, bc, st[qkey + '._mean'], st[qkey + '._logsigma'], t('Fv'),
+                                     st['g.logsigmas_y'], ex, ey, gp_linear=gp)
+        if it > 0:
+            beta = oelbo.vo_precision_beta(list(G), list(A), list(out[-1]['mean']), list(out[-1]['vars']))
+            vo_var = oelbo.vo_mean_variances(beta, Nvo, infinite)
+        res = [oelbo.vo_condition(G[i], A[i], Ym[i], 1 / Ys[i] ** 2, vo_var) for i in range(Nvo)]
+        out.append(dict(Y_mean=Ym, Y_std=Ys, vo_var=vo_var.clone(), mean=torch.stack([r[0] for r in res]),
+                        vars=torch.stack([r[1] for r in res])))
+    return out, beta
+
+
+def oracle_nonarm_fixture_elbo(d, masks=None):
+    """fp64 oracle of elbo_unsupervised (generative.py:515-544: per-sample q_z['unsupervised'] rows, the
+    KL of q_z['supervised'], sic :525) + supervised freeX on elbo_nonarm_c32.npz; masks {'dec_u',
+    'dec_s'}.  Returns (elbo float, {name: grad of -elbo})."""
+    n, nc, dz, Nu, Ns = [int(v) for v in d['cfg']]
+    st = state_of(d)
+    t = lambda k: torch.as_tensor(np.asarray(d[k]), dtype=torch.float64)
+    _, dec = _c32_codecs(st, masks, n)
+    qzs = (st['q_z.supervised._mean'], st['q_z.supervised._logsigma'])
+    Zu = oelbo.reparam(st['q_z.unsupervised._mean'], st['q_z.unsupervised._logsigma'], t('eps_u'))
+    mx, lsx = dec['dec_u'](Zu)
+    e1 = oelbo.dgll(t('Xu'), mx, 2 * lsx) - oelbo.kl_unit(qzs[0], 2 * qzs[1])
+    e2, _ = oelbo.elbo_supervised_freeX(
+        dec['dec_s'], lambda z: torch.nn.functional.linear(z, st['gp.fc.weight'], st['gp.fc.bias']),
+        st['gp.logsigmas_X'], lambda x, F: oelbo.rom_operator(t('W'), t('M'), torch.as_tensor(d['bc_dofs']), x, F,
+                                                              st['g.logsigmas_y']),
+        qzs, (st['q_X.supervised._mean'], st['q_X.supervised._logsigma']), t('Xs'), t('Y'), t('F'), t('eps_qz'),
+        t('eps_qX'))
+    val = e1 + e2
+    (-val).backward()
+    return float(val.item()), {k: v.grad.numpy() for k, v in st.items() if v.grad is not None}
+
+
 def tensor_rel(g, ref):
     """Per-tensor relative error max|g - ref| / max|ref| (no absolute floor)."""
     g = np.asarray(g, dtype=np.float64)

@@ -67,4 +67,8 @@ def engine_relu_masks(engine):
     if engine.N_s > 0:
         masks['dec_s'] = _program_masks(engine.dp, ws_np, stats, P, slice(engine.B_u, engine.B_u + engine.N_s), g,
                                         engine.N_s)
+        g += 1
+    if getattr(engine, 'N_vo', 0) > 0:       # the VO term's decoder batch: the third BN group
+        r0 = engine.B_u + engine.N_s
+        masks['dec_v'] = _program_masks(engine.dp, ws_np, stats, P, slice(r0, r0 + engine.N_vo), g, engine.N_vo)
     return masks

@@ -365,3 +365,51 @@ def test_codec_dropout():
     np.testing.assert_allclose(Z.grad.numpy(), d['grad_Z'], rtol=1e-3, atol=1e-4)
     for k, p in pd.items():
         np.testing.assert_allclose(p.grad.numpy(), d['dec.grad.' + k], rtol=1e-3, atol=2e-3, err_msg=k)
+
+
+# ---------------------------------------------------------------- the GPU tests' fp64 oracle helpers
+@pytest.mark.parametrize('lockx', [False, True], ids=['freeX', 'lockX'])
+@pytest.mark.parametrize('holdoff', [False, True], ids=['vo', 'holdoff'])
+def test_oracle_vo_fixture_elbo_helper(lockx, holdoff):
+    """tests/elbo_ref.py oracle_vo_fixture_elbo (what the GPU VO-ELBO tests compare the kernels with)
+    reproduces the reference run it restates: value 2e-5, gradients 2e-4 of max(|ref|, 1)."""
+    from elbo_ref import oracle_vo_fixture_elbo
+    d = load('vo_elbo_lockx_c32.npz' if lockx else 'vo_elbo_c32.npz')
+    val, gr = oracle_vo_fixture_elbo(d, d['upd1.mean'], d['upd1.vars'], lockx=lockx, holdoff=holdoff)
+    key = 'elbo_holdoff' if holdoff else 'elbo'
+    np.testing.assert_allclose(val, float(d[key]), rtol=2e-5)
+    pre = 'gradh.' if holdoff else 'grad.'
+    for k in {k[len(pre):] for k in d if k.startswith(pre)} | set(gr):
+        ref = d.get(pre + k)
+        if ref is None:
+            assert not np.abs(gr[k]).any(), k
+            continue
+        got = gr.get(k, np.zeros_like(ref))
+        scale = max(np.abs(ref).max(), 1.0)
+        np.testing.assert_allclose(got / scale, ref / scale, atol=2e-4, err_msg=k)
+
+
+def test_oracle_nonarm_fixture_elbo_helper():
+    from elbo_ref import oracle_nonarm_fixture_elbo
+    d = load('elbo_nonarm_c32.npz')
+    val, gr = oracle_nonarm_fixture_elbo(d)
+    np.testing.assert_allclose(val, float(d['elbo']), rtol=2e-5)
+    for k, g in gr.items():
+        ref = d['grad.' + k]
+        scale = max(np.abs(ref).max(), 1.0)
+        np.testing.assert_allclose(g / scale, ref / scale, atol=2e-4, err_msg=k)
+
+
+@pytest.mark.parametrize('lockx', [False, True], ids=['freeX', 'lockX'])
+def test_oracle_vo_updates_helper(lockx):
+    """tests/elbo_ref.py oracle_vo_updates (fp64 end to end) vs the reference's fp32 VO updates."""
+    from elbo_ref import oracle_vo_updates
+    d = load('vo_elbo_lockx_c32.npz' if lockx else 'vo_elbo_c32.npz')
+    ups, beta = oracle_vo_updates(d, lockx=lockx)
+    rel = lambda a, b: float(np.abs(np.asarray(a) - b).max() / np.abs(b).max())
+    for it, u in enumerate(ups):
+        assert rel(u['Y_mean'], d['upd%d.Y_mean' % it]) < 1e-5
+        assert rel(u['Y_std'], d['upd%d.Y_std' % it]) < 1e-4
+        assert rel(u['mean'], d['upd%d.mean' % it]) < 1e-5
+        assert rel(u['vars'], d['upd%d.vars' % it]) < 1e-4
+    assert rel(beta, d['upd1.prec_beta']) < 1e-4
