@@ -283,12 +283,16 @@ def test_elbo_options(device, opt):
 
 
 # ---------------------------------------------------------------- scale-up grids (BASELINE configs 4 / 5)
-@pytest.mark.parametrize('ident,n', [('highres128', 128), ('highres256', 256)])
-def test_fused_step_scaleup_grids(device, ident, n):
+@pytest.mark.parametrize('ident,n,Nu,bs,Ns', [('highres128', 128, 8, 4, 2), ('highres256', 256, 8, 4, 2),
+                                               ('highres128', 128, 512, 256, 32)],
+                         ids=['c128-small', 'c256-small', 'c128-config4'])
+def test_fused_step_scaleup_grids(device, ident, n, Nu, bs, Ns):
     """FusedElboStep at 128^2 (highres128: blocks [1,2,2,1]) and 256^2 (highres256: [1,2,2,2,1]), ROM 8x8,
-    droprate 0.2 (device-drawn Dropout2d), small batch (B_u = 4 of a pool of 8, N_s = 2), random-init
-    parameters and synthetic fields: one step's ELBO vs the fp64 oracle (1e-5) and every gradient tensor
-    vs the oracle with the kernels' ReLU tie decisions and dropout scales."""
+    droprate 0.2 (device-drawn Dropout2d), random-init parameters and synthetic fields: one step's ELBO
+    vs the fp64 oracle (1e-5) and every gradient tensor vs the oracle with the kernels' ReLU tie
+    decisions and dropout scales (5e-5 per tensor).  Small batches (B_u = 4 of a pool of 8, N_s = 2) and
+    BASELINE config 4's own shape (128^2, B_u = 256 of 512, N_s = 32: the launch geometry bench.py
+    --config c128 times)."""
     from gpu_masks import engine_relu_masks
     from factories.model import ModelFactory
     from gpi.train import FusedElboStep
@@ -301,7 +305,6 @@ def test_fused_step_scaleup_grids(device, ident, n):
     nc = physics_['rom'].grid.n
     assert physics_['fom'].grid.n == n
     rng = np.random.default_rng(n)
-    Nu, bs, Ns = 8, 4, 2
     Xu = rng.normal(0.3, 0.6, (Nu, n, n)).astype(np.float32)
     Xs = rng.normal(0.3, 0.6, (Ns, n, n)).astype(np.float32)
     Y = rng.normal(0.0, 0.3, (Ns, (n + 1) * (n - 1))).astype(np.float32)
