@@ -88,6 +88,7 @@ struct ConvGeom {
     int npx;        // forward: horizontally adjacent output pixels per thread (1, 2, 4)
     int cg;         // forward, tiles of <= 128 pixels: input-channel groups computing partial sums in parallel
                     // (256 / pixels threads per pixel instead of one busy wave), summed through LDS
+    int fuse;       // backward: the fused output-conv launch (forward + loss + backward, gpi_conv_loss_fused)
     int split;      // backward: 2 workgroups per tile, input gradient (blockIdx < nblocks) and weight gradient
                     // (the rest) in parallel on otherwise idle CUs (launches well under one round)
     int in_sq, in_sr, in_sc;   // 256 chunks of the input image = (planes, rows, chunks)
@@ -236,6 +237,7 @@ bool conv_geom(const gpi_conv_desc& d, const gpi_groups& g, ConvGeom& G, bool fw
     // (one more resident workgroup per CU on the 32x32 / 64x64 decoder planes)
     G.zreg = (!fwd && d.gout_mode == 0 && (int64_t)d.cout * G.gh * (G.PG / 4) <= (int64_t)ZREG * 256) ? 1 : 0;
     G.split = 0;   // decided by launch() from the LDS footprint
+    G.fuse = fuse ? 1 : 0;
 #ifdef GPI_PHASE_TIMING
     static const int dbg = env_int("GPI_DBG_SKIP", 0);
     G.dbg = dbg;
@@ -930,6 +932,16 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
 // launches: <= 31 KB gives 5 workgroups per CU, measured tools/bench_dispatch.hip)
 __host__ __device__ inline int pad64(int n) { return (n + 63) & ~63; }
 __host__ __device__ inline int bwd_hdr(int cin, int cout) { return pad64(8 * (cin + cout) + 5 * cin + 5 * cout); }
+// ops whose backward takes the VALU input gradient with SGPR weights (the decoder's 5x5 output conv)
+__host__ __device__ inline bool vop_op(const gpi_conv_desc& d) {
+    return d.k == 5 && d.stride == 1 && !d.upsample && d.gin_off >= 0 && d.cin <= 4 && d.cout <= 2;
+}
+__host__ __device__ inline int bwd_rowlen(const gpi_conv_desc& d) {
+    return d.cout * d.cin * d.k * d.k + (d.in_bn ? 2 * d.cin : 0);
+}
+// LDS of such an op between the header and the gradient image: [fuse: target rows] | channel-sum scratch
+// (256) + SLAB_ROWS weight-gradient partial rows
+__host__ __device__ inline int vop_mid_floats(int gh, int w_out, int rowlen, bool fuse);
 template <bool B>
 struct BoolC {
     static constexpr bool value = B;
@@ -941,7 +953,13 @@ struct IntC {
 };
 
 // per-wave input-channel sums [2][4 waves][32] (256 floats) alias the offset table (>= 256 floats)
-constexpr int SLAB_ROWS = 4;    // partial-slab rows per workgroup: one per wave (no cross-wave dW reduction)
+constexpr int SLAB_ROWS = 4;    // partial-slab rows per workgroup: one per wave (no cross-wave dW reduction;
+                                // vop ops: summed in LDS, one row per workgroup)
+// [WB: input-gradient weights, <= 200 floats | WF (fuse): forward weights, later the channel-sum scratch (256) |
+//  SLAB_ROWS weight-gradient partial rows]
+__host__ __device__ inline int vop_mid_floats(int gh, int w_out, int rowlen, bool fuse) {
+    return pad256(512 + SLAB_ROWS * rowlen);
+}
 
 // FUSE (the decoder's output conv, Gaussian-loss epilogue, no dropout): the launch computes its own
 // forward first -- output rows [oy0 - K/2, oy0 + th + K/2) from an input image K/2 rows taller on each
@@ -968,12 +986,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
     const bool obn = d.gout_mode == 0;
     const int KD = d.cout * KK;                       // input-gradient reduction length
     const int KD4 = (KD + 3) & ~3;
+    // vop: the VALU input gradient (5x5, stride 1, cin <= 4; always with FUSE) takes its weights from
+    // SGPRs, so there is no wD / offset table; that LDS region (`mid`) holds instead [FUSE: the Gaussian
+    // target rows of the tile, [gh][w_out], staged with the operand images] and, once those are dead,
+    // the channel-sum scratch (256) and the four waves' weight-gradient partial rows, summed in LDS
+    // into ONE slab row per tile (a quarter of the slab bytes, one coalesced store)
+    const bool vop = FUSE || (K == 5 && S == 1 && !UP && has_gin && d.cin <= 4 && d.cout <= 2);
+    const int J = d.cin * KK;
+    const int rowlen = d.cout * J + (d.in_bn ? 2 * d.cin : 0);
     float* wD = smem + bwd_hdr(d.cin, d.cout);        // [KD4][16]: W[co][ci][tap] at (co*KK + tap)*16 + ci, zero padded
-    const int nwd = has_gin ? KD4 * 16 : 0;
+    const int nwd = (has_gin && !vop) ? KD4 * 16 : 0;
+    float* const mid = wD;
+    const int nmid = vop ? vop_mid_floats(G.gh, d.w_out, rowlen, FUSE) : 0;
     // S1 / UP: [KD4] output-gradient offset of reduction index k; S2: per parity class of the input
     // pixel [4][2][KD4]: (output-gradient offset, weight row) of the class's k-th valid tap
-    int* ktab = (int*)(wD + pad256(nwd));
-    float* gl = (float*)ktab + (has_gin ? pad256((S == 2 ? 8 : 1) * KD4) : 0);   // [cout][gh][PG]
+    int* ktab = (int*)(wD + pad256(nwd) + nmid);
+    float* gl = (float*)ktab + ((has_gin && !vop) ? pad256((S == 2 ? 8 : 1) * KD4) : 0);   // [cout][gh][PG]
     const int gplane = G.gh * G.PG;
     const int gimg = img_floats(d.cout, G.gh, G.PG);
     const bool zreg = G.zreg != 0;
@@ -983,8 +1011,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
     float* const alb = FUSE ? al + (K / 2) * G.P : al;
     // reduction scratch: aliases gz (dead after phase 3) when it is large enough -- 8 KB less LDS
     // per workgroup, one more resident workgroup per CU on the 32x32 planes
-    // channel-sum scratch: the offset table's space, dead after the input gradient (in_bn implies has_gin)
-    float* red = (float*)ktab;
+    // channel-sum scratch: the offset table's space, dead after the input gradient (in_bn implies has_gin);
+    // FUSE: the target image's (>= 256 floats, dead after the loss phase)
+    float* red = vop ? mid + 256 : (float*)ktab;
 
     const int tid = threadIdx.x;
     const int lane = tid & 63, wv = tid >> 6, kq = lane >> 4, l16 = lane & 15;
@@ -1007,7 +1036,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
     PHASE(1);
 
     // ---- phase 1: every global read in flight together
-    if (has_gin && dg_role)
+    // (LDS stores first: an LDS store behind an outstanding LDS-DMA waits for that DMA)
+    if constexpr (FUSE) {
+        // the gradient image is computed in phase 3': zero halo columns, out-of-plane rows and margin
+        float4* g4 = reinterpret_cast<float4*>(gl);
+        for (int e = tid; e < gimg / 4; e += 256) g4[e] = float4{0.f, 0.f, 0.f, 0.f};
+    }
+    const int CIV = d.cin <= 2 ? 2 : 4;      // vop: input channels per weight vector (zero padded)
+    if (vop) {
+        // weights W[co][ci][ky][kx] transposed for the packed (v_pk_fma_f32) loops: input gradient
+        // WB[((co K + ky) K + kx) CIV + ci]; FUSE forward WF[((ci K + kx) K + ky) 2 + co]
+        stage(mid, d.cout * KK * CIV, zero, [&](int e) -> const float* {
+            const int ci = e % CIV, t = e / CIV, co = t / KK, tap = t - co * KK;
+            return ci < d.cin ? params + w_off + ((int64_t)co * d.cin + ci) * KK + tap : nullptr;
+        });
+        if (FUSE)
+            stage(mid + 256, d.cin * KK * 2, zero, [&](int e) -> const float* {
+                const int co = e & 1, t = e >> 1, ci = t / KK, r = t - ci * KK, kx = r / K, ky = r - kx * K;
+                return params + w_off + ((int64_t)co * d.cin + ci) * KK + ky * K + kx;
+            });
+    }
+    if (has_gin && dg_role && !vop)
         stage(wD, nwd, zero, [&](int e) -> const float* {
             const int ci = e & 15, k = e >> 4;
             const int co = k / KK, t = k - co * KK;
@@ -1017,10 +1066,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
     int gy0, gh_;
     g_rows(K, S, d.pad, T.oy0, G.th, gy0, gh_);
     const int64_t gbase = ((int64_t)T.b * d.out_ctot + d.out_c0) * HWo;
+    // FUSE: the Gaussian target of this thread's first forward item (column x, RPF rows), loaded with the
+    // operand images into registers (one global round trip less inside the loss phase)
+    constexpr int RPF = 5;                    // FUSE: vertically adjacent output pixels per forward item
+    float tv0[FUSE ? RPF : 1];
+    const float* tg = zero;
     if constexpr (FUSE) {
-        // the gradient image is computed below: zero halo columns, out-of-plane rows and margin
-        float4* g4 = reinterpret_cast<float4*>(gl);
-        for (int e = tid; e < gimg / 4; e += 256) g4[e] = float4{0.f, 0.f, 0.f, 0.f};
+        int trow0 = T.b - karg_sel(c.groups.start, T.grp);
+        if (const int32_t* ti = karg_sel(c.tgt_idx, T.grp)) trow0 = ti[trow0];
+        tg = karg_sel(c.tgt, T.grp) + (int64_t)trow0 * HWo;
+        const int nitem = ((G.gh + RPF - 1) / RPF) * d.w_out;
+        const int rg = dq(tid, G.d_wout), x = tid - rg * d.w_out;
+#pragma unroll
+        for (int p = 0; p < RPF; ++p) {
+            const int oy = gy0 + rg * RPF + p;
+            const bool ok = tid < nitem && rg * RPF + p < G.gh && oy >= 0 && oy < d.h_out;
+            tv0[p] = *as_gld(ok ? tg + oy * d.w_out + x : zero);
+        }
     } else {
         stage_img(gl, d.cout, G.gh, G.PG, G.d_g4, G.d_PG4, G.g_sq, G.g_sr, G.g_sc, gy0, d.h_out, d.w_out, zero,
                   [&](int q) -> const float* { return ws + gout_off + gbase + (int64_t)q * HWo; });
@@ -1061,7 +1123,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
     // leave >= 3/4 of its N = 16 columns empty
     // (FUSE: always the VALU input gradient -- launch() checks cin <= 4 -- so the MFMA input-gradient
     // path and its operand registers compile away)
-    const bool vdg = FUSE || (K == 5 && S == 1 && !UP && has_gin && d.cin <= 4 && dg_role);
+    const bool vdg = vop && dg_role;     // (launch() never splits a vop op: dg_role holds)
     const int nmblk = (!FUSE && has_gin && dg_role && !vdg && !SKIP(G, 2)) ? (G.ph * d.w_in) >> 4 : 0;
     const int ci_l = min(l16, d.cin - 1);
     const bool cok = l16 < d.cin;
@@ -1149,7 +1211,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
             ktab[cls * 2 * KD4 + KD4 + k] = ob;
         }
     }
-    if (has_gin && dg_role && S != 2) {
+    if (has_gin && dg_role && S != 2 && !vop) {
         // A operand of reduction index k = (co, ky, kx) for owned pixel (qy, px):
         // gl[(S1) qy*PG + px | (UP) 2 qy*PG + 2 px] + ktab[k]
         const int ry0 = (UP ? 2 * py0 : py0) + d.pad - gy0;
@@ -1242,70 +1304,89 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
     }
     __syncthreads();
     if constexpr (FUSE) {
-        // ---- phase 3': forward of output rows gy0 + [0, gh) (weights as SGPR operands from scalar
-        // loads), the Gaussian log-likelihood of the owned rows, d(-logL)/d(mu, logsigma) into the
-        // gradient image
+        // ---- phase 3': forward of output rows gy0 + [0, gh), the Gaussian log-likelihood of the owned
+        // rows, d(-logL)/d(mu, logsigma) into the gradient image.  (mu, logsigma) of a pixel is one packed
+        // pair: every tap is ONE v_pk_fma_f32 with the (co 0, co 1) weight pair of the tap, read from
+        // LDS (WF, uniform address: a broadcast read) -- no scalar loads in the loop, whose lgkmcnt
+        // waits used to drain the LDS reads as well (r03: 22.5 k cycles per workgroup for this phase)
         constexpr int PADK = K / 2;
         float Lv = 0.f;
-        int trow0 = T.b - karg_sel(c.groups.start, T.grp);
-        if (const int32_t* ti = karg_sel(c.tgt_idx, T.grp)) trow0 = ti[trow0];
-        const float* tg = karg_sel(c.tgt, T.grp) + (int64_t)trow0 * HWo;
         const bool ex = d.epilogue == GPI_EPI_GAUSS_EXP_LOSS;
         const float scl = karg_sel(c.loss_scale, T.grp);
         // RPF vertically adjacent pixels of one column per thread: items (column, row group) fill the
-        // 256 lanes exactly on 64-wide planes (20 rows = 4 groups x 64 columns with 16-row tiles; the
-        // horizontal 4-pixel form left 64 of 320 groups for a second, quarter-full pass).  Per (ci, kx)
-        // the column's RPF + K - 1 input values are read once (lanes on consecutive columns: one
-        // 256-B LDS row per read, no bank conflicts) and serve the RPF x K taps.
-        constexpr int RPF = 5;
+        // 256 lanes exactly on 64-wide planes (20 rows = 4 groups x 64 columns with 16-row tiles).  Per
+        // (ci, kx) the column's RPF + K - 1 input values are read once (lanes on consecutive columns: one
+        // 256-B LDS row per read, no bank conflicts) and serve the RPF x K taps.  The weights: lane l
+        // holds WF[64 j + l] in wr[j] (one LDS read each), a tap's (co 0, co 1) pair is taken by two
+        // v_readlane into SGPRs -- VALU work instead of 50 broadcast LDS reads per item (the phase was
+        // LDS-bound: r03c 15.6 k cycles per workgroup)
         const int nrg = (G.gh + RPF - 1) / RPF, nitem = nrg * d.w_out;
-        for (int it = tid; it < nitem; it += 256) {
-            const int rg = dq(it, G.d_wout), x = it - rg * d.w_out;
-            const int j0 = rg * RPF;
-            float tv[RPF];
+        auto fwd_items = [&](auto ci_c) {
+            constexpr int CIN = decltype(ci_c)::value;
+            constexpr int NWR = (CIN * KK * 2 + 63) / 64;
+            float wr[NWR];
 #pragma unroll
-            for (int p = 0; p < RPF; ++p) {
-                const int oy = gy0 + j0 + p;
-                const bool ok = j0 + p < G.gh && oy >= 0 && oy < d.h_out;
-                tv[p] = ok ? as_gld(tg)[oy * d.w_out + x] : 0.f;
-            }
-            float mu[RPF], ls[RPF];
+            for (int j = 0; j < NWR; ++j) wr[j] = mid[256 + 64 * j + lane];
+            for (int it = tid; it < nitem; it += 256) {
+                const int rg = dq(it, G.d_wout), x = it - rg * d.w_out;
+                const int j0 = rg * RPF;
+                float tv[RPF];
 #pragma unroll
-            for (int p = 0; p < RPF; ++p) mu[p] = ls[p] = 0.f;
-            for (int ci = 0; ci < d.cin; ++ci) {
-                const float* acol = al + ci * G.rh * G.P + HALO + x - PADK;
-                const auto* cw0 = (const __attribute__((address_space(4))) float*)(params + w_off + (int64_t)ci * KK);
-                const auto* cw1 = cw0 + d.cin * KK;
+                for (int p = 0; p < RPF; ++p) {
+                    const int oy = gy0 + j0 + p;
+                    const bool ok = j0 + p < G.gh && oy >= 0 && oy < d.h_out;
+                    tv[p] = it == tid ? tv0[p] : (ok ? as_gld(tg)[oy * d.w_out + x] : 0.f);
+                }
+                f32x2 acc[RPF];
 #pragma unroll
-                for (int kx = 0; kx < K; ++kx) {
-                    // input row j0 + r feeds pixel p through tap ky = r - p: one value live at a time
+                for (int p = 0; p < RPF; ++p) acc[p] = f32x2{0.f, 0.f};
 #pragma unroll
-                    for (int r = 0; r < RPF + K - 1; ++r) {
-                        const float v = acol[min(j0 + r, G.rh - 1) * G.P + kx];
+                for (int ci = 0; ci < CIN; ++ci) {
+                    if (ci >= d.cin) break;
+                    const float* acol = al + ci * G.rh * G.P + HALO + x - PADK;
 #pragma unroll
-                        for (int p = 0; p < RPF; ++p) {
-                            const int ky = r - p;
-                            if (ky < 0 || ky >= K) continue;
-                            mu[p] = fmaf(cw0[ky * K + kx], v, mu[p]);
-                            ls[p] = fmaf(cw1[ky * K + kx], v, ls[p]);
+                    for (int kx = 0; kx < K; ++kx) {
+                        float v[RPF + K - 1];
+#pragma unroll
+                        for (int r = 0; r < RPF + K - 1; ++r) v[r] = acol[min(j0 + r, G.rh - 1) * G.P + kx];
+                        f32x2 w[K];
+#pragma unroll
+                        for (int ky = 0; ky < K; ++ky) {
+                            const int i = ((ci * K + kx) * K + ky) * 2;
+                            w[ky][0] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wr[i >> 6]), i & 63));
+                            w[ky][1] = __int_as_float(
+                                __builtin_amdgcn_readlane(__float_as_int(wr[(i + 1) >> 6]), (i + 1) & 63));
+                        }
+                        // input row j0 + r feeds pixel p through tap ky = r - p
+#pragma unroll
+                        for (int r = 0; r < RPF + K - 1; ++r) {
+#pragma unroll
+                            for (int p = 0; p < RPF; ++p) {
+                                const int ky = r - p;
+                                if (ky < 0 || ky >= K) continue;
+                                acc[p] = __builtin_elementwise_fma(w[ky], f32x2{v[r], v[r]}, acc[p]);
+                            }
                         }
                     }
                 }
-            }
 #pragma unroll
-            for (int p = 0; p < RPF; ++p) {
-                const int j = j0 + p, oy = gy0 + j;
-                if (j >= G.gh || oy < 0 || oy >= d.h_out) continue;
-                const bool own = j >= PADK && j < PADK + G.th;
-                const float e = expf(-2.f * ls[p]);
-                const float emu = ex ? expf(mu[p]) : 1.f;
-                const float r = ex ? expf(tv[p]) - emu : tv[p] - mu[p];
-                if (own) Lv += -0.5f * (2.f * ls[p] + r * r * e + GPI_LOG2PI);
-                float* g0 = gl + j * G.PG + HALO + x;
-                g0[0] = -scl * r * e * emu;
-                g0[gplane] = scl * (1.f - r * r * e);
+                for (int p = 0; p < RPF; ++p) {
+                    const int j = j0 + p, oy = gy0 + j;
+                    if (j >= G.gh || oy < 0 || oy >= d.h_out) continue;
+                    const bool own = j >= PADK && j < PADK + G.th;
+                    const float mu = acc[p][0], ls = acc[p][1];
+                    const float e = expf(-2.f * ls);
+                    const float emu = ex ? expf(mu) : 1.f;
+                    const float r = ex ? expf(tv[p]) - emu : tv[p] - mu;
+                    if (own) Lv += -0.5f * (2.f * ls + r * r * e + GPI_LOG2PI);
+                    float* g0 = gl + j * G.PG + HALO + x;
+                    g0[0] = -scl * r * e * emu;
+                    g0[gplane] = scl * (1.f - r * r * e);
+                }
             }
-        }
+        };
+        if (d.cin <= 2) fwd_items(IntC<2>{});
+        else fwd_items(IntC<4>{});
         // one fp64 atomic per workgroup (per-wave atomics into 16 replicas serialise: 2304 x 4 adds)
         const float lw = wave_sum(Lv);
         if (lane == 0) o_coef[wv] = lw;       // o_coef is unused without an output BN
@@ -1320,10 +1401,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
     // Stride 1 / upsampling: no masks in the loop -- the zero halos and tail margins of the
     // images make every out-of-range read a zero or a finite value multiplied by a zero,
     // and rows i >= M / columns j >= N of the tile (clamped operands) are never stored.
-    const int J = d.cin * KK;
-    const int rowlen = d.cout * J + (d.in_bn ? 2 * d.cin : 0);
     // this wave's partial-slab row: [dW partial over the wave's output rows | dgamma | dbeta partials]
-    float* slab = c.wpart + d.wpart_off + ((int64_t)tile * SLAB_ROWS + wv) * rowlen;
+    // (vop: in LDS, summed below into the tile's one slab row)
+    float* slab = vop ? mid + 512 + wv * rowlen : c.wpart + d.wpart_off + ((int64_t)tile * SLAB_ROWS + wv) * rowlen;
     // single-channel 7x7 / stride-2 input conv: weight gradient with the reduction over the tile's
     // output pixels (M = cout, N = the 49 taps in 4 column blocks, K = pixels), no zero-interleaved
     // stride-2 columns (the column-shift form below would compute ~6x the useful products here)
@@ -1605,22 +1685,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
             lb[ci] = d.in_bn ? i_sh[cc] + i_mean[cc] * i_sc[cc] : 0.f;
             lr[ci] = d.in_bn ? 1.f / lg[ci] : 0.f;
         }
-        const auto* wg = (const __attribute__((address_space(4))) float*)(params + w_off);
+        // packed over input-channel pairs: WB[((co K + ky) K + kx) CIV + ci]; lane l holds WB[64 j + l] in
+        // wb[j], a tap's channel pair is taken by v_readlane (no LDS traffic for the weights in the loop)
         auto vdg_rows = [&](auto ci_c) {
-            constexpr int CI = decltype(ci_c)::value;
+            constexpr int CI = decltype(ci_c)::value;     // == CIV
+            constexpr int CH = CI / 2;
             constexpr int Q = CI == 2 ? 4 : 2;
+            constexpr int NWB = (2 * KK * CI + 63) / 64;   // cout <= 2 (vop)
+            float wb[NWB];
+    #pragma unroll
+            for (int j = 0; j < NWB; ++j) wb[j] = mid[64 * j + lane];
             const int npq = (G.ph * d.w_in) / Q;
             for (int gq = tid; gq < npq; gq += 256) {
                 const int qy = dq(Q * gq, G.d_win), px0 = Q * gq - qy * d.w_in;
                 const int64_t pix = (int64_t)(py0 + qy) * d.w_in + px0;
                 const int64_t gbase_in = ((int64_t)T.b * d.in_ctot + d.in_c0) * HWi + pix;
-                float acc[CI][Q];
+                f32x2 acc2[CH][Q];
     #pragma unroll
-                for (int ci = 0; ci < CI; ++ci)
+                for (int h = 0; h < CH; ++h)
     #pragma unroll
-                    for (int q = 0; q < Q; ++q) acc[ci][q] = 0.f;
-                for (int co = 0; co < d.cout; ++co) {
-    #pragma unroll 1
+                    for (int q = 0; q < Q; ++q) acc2[h][q] = f32x2{0.f, 0.f};
+    #pragma unroll
+                for (int co = 0; co < 2; ++co) {
+                    if (co >= d.cout) break;
+    #pragma unroll
                     for (int ky = 0; ky < K; ++ky) {
                         const float* grow = gl + co * gplane + (qy + py0 + d.pad - ky - gy0) * G.PG + HALO + px0 +
                                             d.pad - (K - 1);
@@ -1632,27 +1720,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
     #pragma unroll
                             for (int t = 0; t < K + Q - 1; ++t) gw[t] = grow[t];
                         }
-                        float wv[CI][K];      // SGPRs: channel ci's row ky of W[co][ci]
-    #pragma unroll
-                        for (int ci = 0; ci < CI; ++ci) {
-                            const int cc = ci < d.cin ? ci : 0;
-    #pragma unroll
-                            for (int kx = 0; kx < K; ++kx) {
-                                const float w = wg[((int64_t)co * d.cin + cc) * KK + ky * K + kx];
-                                wv[ci][kx] = ci < d.cin ? w : 0.f;
-                            }
-                        }
     #pragma unroll
                         for (int kx = 0; kx < K; ++kx) {
+                            f32x2 w[CH];
+    #pragma unroll
+                            for (int h = 0; h < CH; ++h) {
+                                const int i = ((co * K + ky) * K + kx) * CI + 2 * h;
+                                w[h][0] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wb[i >> 6]), i & 63));
+                                w[h][1] = __int_as_float(
+                                    __builtin_amdgcn_readlane(__float_as_int(wb[(i + 1) >> 6]), (i + 1) & 63));
+                            }
     #pragma unroll
                             for (int q = 0; q < Q; ++q) {
                                 const float gv = gw[q + K - 1 - kx];
     #pragma unroll
-                                for (int ci = 0; ci < CI; ++ci) acc[ci][q] = fmaf(wv[ci][kx], gv, acc[ci][q]);
+                                for (int h = 0; h < CH; ++h)
+                                    acc2[h][q] = __builtin_elementwise_fma(w[h], f32x2{gv, gv}, acc2[h][q]);
                             }
                         }
                     }
                 }
+                float acc[CI][Q];
+    #pragma unroll
+                for (int ci = 0; ci < CI; ++ci)
+    #pragma unroll
+                    for (int q = 0; q < Q; ++q) acc[ci][q] = acc2[ci >> 1][q][ci & 1];
     #pragma unroll
                 for (int ci = 0; ci < CI; ++ci) {
                     if (ci >= d.cin) break;
@@ -1735,6 +1827,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
             }
         }
     }
+    if (vop) {
+        // the four waves' partial rows in a fixed order -> the tile's slab row
+        __syncthreads();
+        float* srow = c.wpart + d.wpart_off + (int64_t)tile * rowlen;
+        for (int e = tid; e < rowlen; e += 256) {
+            const float* r = mid + 512 + e;
+            srow[e] = (r[0] + r[rowlen]) + (r[2 * rowlen] + r[3 * rowlen]);
+        }
+    }
     PHASE(7);
     RTSTAMP(1);
 }
@@ -1744,17 +1845,19 @@ size_t fwd_lds(const gpi_conv_desc& d, const ConvGeom& G, int cp) {
                             (G.cg > 1 ? (size_t)(G.cg - 1) * G.th * d.w_out * cp : 0));
 }
 
-size_t bwd_lds_floats(const gpi_conv_desc& d, int rh, int P, int gh, int PG, int zreg) {
+size_t bwd_lds_floats(const gpi_conv_desc& d, int rh, int P, int gh, int PG, int zreg, bool fuse) {
     const int KD4 = (d.cout * d.k * d.k + 3) & ~3;
     const int gimg = img_floats(d.cout, gh, PG);
     const bool zimg = d.gout_mode == 0 && !zreg;             // z image in LDS
-    // offset table, at least BWD_RED floats: the channel-sum scratch aliases it
-    return (size_t)bwd_hdr(d.cin, d.cout) + (d.gin_off >= 0 ? pad256(KD4 * 16) + pad256((d.stride == 2 ? 8 : 1) * KD4) : 0) +
-           gimg + (zimg ? gimg : 0) + img_floats(d.cin, rh, P);
+    // offset table, at least BWD_RED floats: the channel-sum scratch aliases it (fuse: the target image
+    // [gh][w_out] in place of the MFMA input-gradient weights and offset table)
+    const size_t mid = vop_op(d) ? vop_mid_floats(gh, d.w_out, bwd_rowlen(d), fuse)
+                                 : (d.gin_off >= 0 ? pad256(KD4 * 16) + pad256((d.stride == 2 ? 8 : 1) * KD4) : 0);
+    return (size_t)bwd_hdr(d.cin, d.cout) + mid + gimg + (zimg ? gimg : 0) + img_floats(d.cin, rh, P);
 }
 
 size_t bwd_lds(const gpi_conv_desc& d, const ConvGeom& G) {
-    return sizeof(float) * bwd_lds_floats(d, G.rh, G.P, G.gh, G.PG, G.zreg);
+    return sizeof(float) * bwd_lds_floats(d, G.rh, G.P, G.gh, G.PG, G.zreg, G.fuse != 0);
 }
 
 typedef void (*conv_kernel_t)(gpi_conv_desc, gpi_codec_ctx, ConvGeom);
@@ -1839,7 +1942,7 @@ int launch(const gpi_conv_desc& d, const gpi_codec_ctx& c, hipStream_t st, bool 
     G.zero = zero;
     const size_t lds = fwd ? fwd_lds(d, G, cp) : bwd_lds(d, G);
     if (lds > 160 * 1024) return GPI_ERR_UNSUPPORTED;
-    if (!fwd && d.gin_off >= 0 && !fuse) {
+    if (!fwd && d.gin_off >= 0 && !fuse && !vop_op(d)) {
         // resident workgroups per CU: LDS (~160 KB less a per-workgroup reserve, tools/bench_dispatch.hip)
         // and the kernels' occupancy (6 waves per SIMD, 4 for the 5x5 kernel)
         static const int split_env = env_int("GPI_BWD_SPLIT", 1);
@@ -1977,7 +2080,7 @@ extern "C" int gpi_conv_blocks(const gpi_conv_desc* op, const gpi_groups* groups
     if (!op || !groups || !blocks) return GPI_ERR_ARG;
     ConvGeom G;
     if (!conv_geom(*op, *groups, G, false)) return GPI_ERR_UNSUPPORTED;   // backward tiling
-    *blocks = G.nblocks * SLAB_ROWS;                                       // one slab row per wave
+    *blocks = G.nblocks * (vop_op(*op) ? 1 : SLAB_ROWS);    // one slab row per wave (vop ops: per workgroup)
     return GPI_OK;
 }
 
