@@ -44,6 +44,20 @@ def main():
     fwd.uc = uc.data_ptr()
     solve_us = timed(lambda: L.check(lib.gpi_rom(C.byref(fwd), st), 'rom fwd'), reps)
     print('rom coarse solve only (FORWARD, no prolongation): %.1f us' % solve_us)
+    if os.environ.get('GPI_LIB_VARIANT') == 'timing':
+        import numpy as np
+        f = lib.gpi_debug_rom_stamps
+        f.restype, f.argtypes = C.c_int, [C.c_void_p]
+        ph = np.zeros((256, 8), np.uint64)
+        L.check(f(ph.ctypes.data), 'stamps')          # clear
+        L.check(lib.gpi_rom(C.byref(e.rom), st), 'rom')
+        torch.cuda.synchronize()
+        L.check(f(ph.ctypes.data), 'stamps')
+        p = ph[:e.rom.n][:, [0, 1, 6, 2, 3, 4, 5]].astype(np.int64)
+        names = ['load+assemble', 'cholesky', 'solves', 'prolong+loglik', 'adjoint', 'dJ/dx']
+        dd = np.diff(p, axis=1).mean(0)
+        print('rom_kernel phases (cycles, mean over %d workgroups): %s; total %.0f' % (
+            e.rom.n, ', '.join('%s %.0f' % (n, v) for n, v in zip(names, dd)), (p[:, 6] - p[:, 0]).mean()))
     step.capture()
     step_us = timed(step.step, reps)
     print('variant %s: rom %.1f us, step %.1f us (%.0f samples/s)' % (
