@@ -16,10 +16,25 @@
 //     dJ/dc_pq = -(lambda_p - lambda_q)(u_p - u_q), dJ/dkappa_t = 1/2 sum over
 //     its two legs, dJ/dx = dJ/dkappa * exp(x).
 #include "common.h"
+#include <stdlib.h>
 
 using namespace gpi;
 
 namespace {
+
+// Phase stamps of the timing build (make timing; tools/rom_probe.py): thread 0 of workgroup b writes
+// the shader clock at phase boundary i to g_rom_phase[b % 256][i].  Compiled out of the product.
+#ifdef GPI_PHASE_TIMING
+__device__ unsigned long long g_rom_phase[256 * 8];
+#define RPHASE(i)                                                                                       \
+    do {                                                                                                \
+        if (threadIdx.x == 0) g_rom_phase[(blockIdx.x & 255) * 8 + (i)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define RPHASE(i) \
+    do {          \
+    } while (0)
+#endif
 
 struct RomDims {
     int nc, nn, nT, nI, bw, n, dy, r;
@@ -198,6 +213,7 @@ __global__ __launch_bounds__(ROM_NT) void rom_kernel(gpi_rom_desc d, RomDims D) 
     const int nc = D.nc;
     const float* x = d.x + (int64_t)s * d.x_stride;
     const float* F = d.F + (int64_t)s * D.nn;
+    RPHASE(0);
 
     bool bad = false;
     for (int t = tid; t < D.nT; t += NT) {
@@ -230,6 +246,7 @@ __global__ __launch_bounds__(ROM_NT) void rom_kernel(gpi_rom_desc d, RomDims D) 
         b[ii] = rhs;
     }
     __syncthreads();
+    RPHASE(1);
     if (nc == 8 || nc == 4) {
         if (tid == 0) {
             if (nc == 8) { chol_band_seq<8>(L, dinv); solve_band_seq<8>(L, dinv, b); }
@@ -245,6 +262,7 @@ __global__ __launch_bounds__(ROM_NT) void rom_kernel(gpi_rom_desc d, RomDims D) 
         u[e] = (I == 0 || I == nc) ? F[e] : b[J * (nc - 1) + (I - 1)];
     }
     __syncthreads();
+    RPHASE(2);
     if (d.uc) for (int e = tid; e < D.nn; e += NT) d.uc[(int64_t)s * D.nn + e] = u[e];
     if (d.mode == GPI_ROM_FORWARD && !d.mu_y) return;   // coarse solutions only (VO MC predictive)
 
@@ -305,7 +323,9 @@ __global__ __launch_bounds__(ROM_NT) void rom_kernel(gpi_rom_desc d, RomDims D) 
                         const float rr = yv[k] - mu;
                         Lsum += -0.5f * (2.f * lv[k] + rr * rr * ee + GPI_LOG2PI);
                         g = -d.loss_scale * rr * ee;
-                        atomicAdd(d.gacc_logsig + pp[k], (double)(d.loss_scale * (1.f - rr * rr * ee)));
+                        const float gl = d.loss_scale * (1.f - rr * rr * ee);
+                        if (d.gls_part) d.gls_part[(int64_t)s * D.dy + pp[k]] = gl;
+                        else atomicAdd(d.gacc_logsig + pp[k], (double)gl);
                     } else {
                         g = gv[k];
                     }
@@ -343,6 +363,7 @@ __global__ __launch_bounds__(ROM_NT) void rom_kernel(gpi_rom_desc d, RomDims D) 
     }
     if (d.mode == GPI_ROM_FORWARD) return;
     __syncthreads();
+    RPHASE(3);
 
     // ---- adjoint
     for (int ii = tid; ii < D.nI; ii += NT) {
@@ -359,6 +380,7 @@ __global__ __launch_bounds__(ROM_NT) void rom_kernel(gpi_rom_desc d, RomDims D) 
     } else {
         solve_band(L, b, D);
     }
+    RPHASE(4);
     for (int ii = tid; ii < D.nI; ii += NT) {
         const int J = ii / (nc - 1), I = ii - J * (nc - 1) + 1;
         lam[I + (nc + 1) * J] = b[ii];
@@ -379,6 +401,382 @@ __global__ __launch_bounds__(ROM_NT) void rom_kernel(gpi_rom_desc d, RomDims D) 
         float* gp = d.gx + (int64_t)s * d.gx_stride + t;
         *gp = (d.gx_accumulate ? *gp : 0.f) + g;
     }
+    RPHASE(5);
+}
+
+// ---------------------------------------------------------------------------------------------
+// rom_kernel_fast<NC> (nc = 4 / 8, one 256-thread workgroup per sample): the same result as
+// rom_kernel with the sequential chains cut (r03 phase stamps of rom_kernel at C64: Cholesky + solve
+// 83 k cycles, adjoint solve 55 k, prolongation 19 k of 162 k):
+//   * the banded Cholesky by one lane with the register window, the pivot by v_rsq (no IEEE sqrt /
+//     division sequences in the chain) and the next band row loaded two steps ahead;
+//   * K^{-1} by ONE wave: lane j < NI solves K x = e_j, lane NI solves K u = b -- 64 independent
+//     forward / back substitutions with the band rows as broadcast LDS reads and the solution in
+//     registers, so the coarse solution and the inverse cost one solve's latency; the adjoint
+//     lambda = K^{-1} W^T dmu is then a parallel mat-vec instead of two more sequential sweeps;
+//   * the Y / logsigma_y loads of the prolongation are issued at entry (in flight during the
+//     factorisation).
+template <int NC>
+__device__ __forceinline__ void chol_band_fast(float* __restrict__ L, float* __restrict__ dinv) {
+    constexpr int W = NC, NI = (NC - 1) * (NC + 1);
+    float win[W][W];   // win[a][t] = L(k + a, k + a - t)
+    float nxt[2][W];   // rows k + W, k + W + 1 (prefetched)
+#pragma unroll
+    for (int a = 0; a < W; ++a)
+#pragma unroll
+        for (int t = 0; t < W; ++t) win[a][t] = a < NI ? L[a * W + t] : 0.f;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int t = 0; t < W; ++t) nxt[u][t] = (W + u < NI) ? L[(W + u) * W + t] : 0.f;
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+        const float inv = __builtin_amdgcn_rsqf(win[0][0]);
+        win[0][0] = win[0][0] * inv;
+        dinv[k] = inv;
+#pragma unroll
+        for (int a = 1; a < W; ++a) win[a][a] *= inv;                       // L(k+a, k)
+#pragma unroll
+        for (int a = 1; a < W; ++a)
+#pragma unroll
+            for (int b = 1; b <= a; ++b) win[a][a - b] = fmaf(-win[a][a], win[b][b], win[a][a - b]);
+#pragma unroll
+        for (int t = 0; t < W; ++t) L[k * W + t] = win[0][t];
+#pragma unroll
+        for (int a = 0; a + 1 < W; ++a)
+#pragma unroll
+            for (int t = 0; t < W; ++t) win[a][t] = win[a + 1][t];
+#pragma unroll
+        for (int t = 0; t < W; ++t) {
+            win[W - 1][t] = nxt[0][t];
+            nxt[0][t] = nxt[1][t];
+            nxt[1][t] = (k + W + 2 < NI) ? L[(k + W + 2) * W + t] : 0.f;
+        }
+    }
+}
+
+// The same factorisation by one wave with the (W x W) window spread over the lanes: lane R W + t holds
+// window entry (a, t) = L(k + a, k + a - t) of the physical row R, a = (R - k) mod W (the rows rotate,
+// nothing is shifted); per step the pivot is read by v_readlane, the column is scaled, and the rank-1
+// update takes its two column values by ds_bpermute.  The finished row goes to L, its lanes take the
+// band row k + W (loaded a step ahead).  Critical path per step ~ readlane, rsq, mul, bpermute, fma.
+template <int NC>
+__device__ __forceinline__ void chol_band_wave(float* __restrict__ L, float* __restrict__ dinv) {
+    constexpr int W = NC, NI = (NC - 1) * (NC + 1);
+    const int lane = threadIdx.x & 63;
+    const int R = lane / W, t = lane - R * W;
+    const bool act = lane < W * W;
+    float v = (act && R < NI) ? L[R * W + t] : 0.f;            // rows 0 .. W-1 (R == a at k = 0)
+    float nx = (act && W + R < NI) ? L[(W + R) * W + t] : 0.f;  // row W + R: replaces row R after step R
+    for (int k = 0; k < NI; ++k) {
+        const int R0 = k % W;
+        const int a = (R - R0 + W) % W;
+        const float p = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), R0 * W));
+        const float inv = __builtin_amdgcn_rsqf(p);
+        if (a >= 1 && t == a) v *= inv;                          // column k: L(k + a, k)
+        // rank-1 update of entries (a, t), 0 <= t < a: -= L(k+a, k) L(k+a-t, k)
+        const int b = a - t;
+        const int s1 = R * W + a;                                // (a, a): this row's column entry
+        const int s2 = ((R0 + b) % W) * W + b;                   // (b, b)
+        const float c1 = __shfl(v, s1, 64), c2 = __shfl(v, s2, 64);
+        if (a >= 1 && t < a) v = fmaf(-c1, c2, v);
+        if (R == R0) {
+            // row k is final: store it (pivot -> sqrt(p) = p * rsq(p)), take row k + W
+            const float o = t == 0 ? p * inv : v;
+            L[k * W + t] = o;
+            if (t == 0) dinv[k] = inv;
+            v = nx;
+            nx = (act && k + 2 * W < NI) ? L[(k + 2 * W) * W + t] : 0.f;
+        }
+    }
+}
+
+constexpr int KINV_P = 65;     // pitch of the K^{-1} image (conflict-free row and column access)
+
+template <int NC>
+__global__ __launch_bounds__(ROM_NT) void rom_kernel_fast(gpi_rom_desc d, RomDims D, int chol_wave) {
+    constexpr int W = NC, BW = NC - 1, NI = (NC - 1) * (NC + 1), NN = (NC + 1) * (NC + 1), NT2 = 2 * NC * NC;
+    constexpr int PF = 3 * ROM_U;            // prefetched fine nodes per thread (a square holds <= (r+1) r)
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float* kp = sm;                   // [NT2] kappa
+    float* L = kp + NT2;              // [NI * W]
+    float* u = L + NI * W;            // [NN]
+    float* b = u + NN;                // [NI]
+    float* lam = b + NI;              // [NN]
+    float* dinv = lam + NN;           // [NI]
+    float* kinv = dinv + NI;          // [NI][KINV_P]
+    double* du = (double*)(sm + ((NT2 + NI * W + 2 * NN + 2 * NI + NI * KINV_P + 1) & ~1));   // [NN]
+    double* lred = du + NN;           // [ROM_NT / 64]
+    const int s = blockIdx.x;
+    const int tid = threadIdx.x;
+    const float* x = d.x + (int64_t)s * d.x_stride;
+    const float* F = d.F + (int64_t)s * NN;
+    const int nf = D.n, r = D.r;
+    RPHASE(0);
+
+    // ---- entry: every global read in flight (kappa, F, and this thread's first PF fine nodes)
+    const int q0 = tid >> 2, sub = tid & 3;
+    float ypf[PF], lpf[PF];
+    {
+        const bool okq = q0 < NC * NC && d.mode == GPI_ROM_LOGLIK;
+        const int I = q0 % NC, J = q0 / NC;
+        const int i0 = I == 0 ? 1 : I * r, i1 = (I + 1) * r - 1;
+        const int rows = J == NC - 1 ? r + 1 : r;
+        const int ncol = i1 - i0 + 1, total = rows * ncol;
+        const uint32_t mcol = (ncol > 1 ? (uint32_t)(((1ull << 32) + ncol - 1) / ncol) : 0u);   // e / ncol = umulhi(e, mcol), e < 2^16
+#pragma unroll
+        for (int k = 0; k < PF; ++k) {
+            const int e = sub + 4 * k;
+            const bool ok = okq && e < total;
+            const int jj = ok ? (mcol ? (int)__umulhi((uint32_t)e, mcol) : e) : 0, ii = ok ? e - jj * ncol : 0;
+            const int pp = (J * r + jj) * (nf - 1) + (i0 + ii - 1);
+            ypf[k] = ok ? d.Y[(int64_t)s * D.dy + pp] : 0.f;
+            lpf[k] = ok ? d.logsig_y[pp] : 0.f;
+        }
+    }
+    bool bad = false;
+    for (int t = tid; t < NT2; t += ROM_NT) {
+        const float kv = d.input_kappa ? x[t] : expf(x[t]) + 1e-8f;
+        bad |= !(kv > 1e-12f);
+        kp[t] = kv;
+    }
+    if (bad && d.flag) atomicOr(d.flag, 1);
+    for (int e = tid; e < NN; e += ROM_NT) {
+        du[e] = (d.mode == GPI_ROM_BACKWARD && d.duc) ? (double)d.duc[(int64_t)s * NN + e] : 0.0;
+        lam[e] = 0.f;
+    }
+    __syncthreads();
+    // ---- assemble the interior system (banded lower) + rhs
+    for (int ii = tid; ii < NI; ii += ROM_NT) {
+        const int J = ii / (NC - 1), I = ii - J * (NC - 1) + 1;
+        const int p = I + (NC + 1) * J;
+        const float chl = c_h(kp, NC, I - 1, J), chr = c_h(kp, NC, I, J);
+        const float cvd = J > 0 ? c_v(kp, NC, I, J - 1) : 0.f;
+        const float cvu = J < NC ? c_v(kp, NC, I, J) : 0.f;
+        float* row = L + ii * W;
+#pragma unroll
+        for (int t = 0; t < W; ++t) row[t] = 0.f;
+        row[0] = chl + chr + cvd + cvu;
+        if (I - 1 >= 1) row[1] += -chl;
+        if (J >= 1) row[BW] += -cvd;
+        float rhs = F[p];
+        if (I - 1 == 0) rhs += chl * F[p - 1];
+        if (I + 1 == NC) rhs += chr * F[p + 1];
+        b[ii] = rhs;
+    }
+    __syncthreads();
+    RPHASE(1);
+    // the prefetched Y / logsigma_y values in registers from here on (issued at entry, they arrived with
+    // kappa and F): otherwise the compiler sinks the loads to the prolongation, a round trip there
+#pragma unroll
+    for (int k = 0; k < PF; ++k) asm volatile("" : : "v"(ypf[k]), "v"(lpf[k]));
+    static_assert(NC * NC <= 64, "window per wave");
+    if (chol_wave) {
+        if (tid < 64) chol_band_wave<NC>(L, dinv);
+    } else if (tid == 0) {
+        chol_band_fast<NC>(L, dinv);
+    }
+    __syncthreads();
+    RPHASE(6);
+    // ---- wave 0: lane j < NI solves K x = e_j (column j of K^{-1}), lane NI solves K u = b.  The band
+    // factor (NI W floats), 1 / L(k,k) and b sit spread over the wave's lanes in registers (lane l holds
+    // entry 64 v + l of register v) and every coefficient of the fully unrolled sweeps is taken by
+    // v_readlane (uniform, an SGPR operand): no LDS round trip in the sweeps' dependency chains
+    // (the LDS form: 62.7 k cycles for the two sweeps, r03f); the solution y[NI] stays in registers.
+    if (tid < 64) {
+        constexpr int NLR = (NI * W + 63) / 64;
+        const int j = tid;
+        float lr[NLR];
+#pragma unroll
+        for (int v = 0; v < NLR; ++v) lr[v] = (64 * v + j < NI * W) ? L[64 * v + j] : 0.f;
+        const float dr = j < NI ? dinv[j] : 0.f;
+        const float br = j < NI ? b[j] : 0.f;
+        auto Lk = [&](int idx) -> float {       // L[idx], idx compile-time after unrolling
+            return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lr[idx >> 6]), idx & 63));
+        };
+        auto rl = [&](float v, int l) -> float { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); };
+        float y[NI];
+#pragma unroll
+        for (int k = 0; k < NI; ++k) {
+            __builtin_amdgcn_sched_barrier(0);  // keep each step's readlanes next to their use (SGPR pressure)
+            const float bk = rl(br, k);
+            float a = j == k ? 1.f : 0.f;
+            a = j == NI ? bk : a;
+            float a2 = 0.f;                     // two partial sums: a shorter dependency chain
+#pragma unroll
+            for (int t = 1; t <= BW; ++t) {
+                if (k - t < 0) continue;
+                if (t & 1) a = fmaf(-Lk(k * W + t), y[k - t], a);
+                else a2 = fmaf(-Lk(k * W + t), y[k - t], a2);
+            }
+            y[k] = (a + a2) * rl(dr, k);
+        }
+#pragma unroll
+        for (int k = NI - 1; k >= 0; --k) {
+            __builtin_amdgcn_sched_barrier(0);
+            float a = y[k], a2 = 0.f;
+#pragma unroll
+            for (int t = 1; t <= BW; ++t) {
+                if (k + t >= NI) continue;
+                if (t & 1) a = fmaf(-Lk((k + t) * W + t), y[k + t], a);
+                else a2 = fmaf(-Lk((k + t) * W + t), y[k + t], a2);
+            }
+            y[k] = (a + a2) * rl(dr, k);
+        }
+        if (j <= NI) {
+#pragma unroll
+            for (int i = 0; i < NI; ++i) kinv[i * KINV_P + j] = y[i];
+        }
+    }
+    __syncthreads();
+    RPHASE(2);
+    for (int e = tid; e < NN; e += ROM_NT) {
+        const int I = e % (NC + 1), J = e / (NC + 1);
+        u[e] = (I == 0 || I == NC) ? F[e] : kinv[(J * (NC - 1) + (I - 1)) * KINV_P + NI];
+    }
+    __syncthreads();
+    if (d.uc) for (int e = tid; e < NN; e += ROM_NT) d.uc[(int64_t)s * NN + e] = u[e];
+
+    // ---- prolongation (+ log-likelihood, + W^T of the output gradient), as rom_kernel; the first
+    // PF nodes of every thread's square from the entry prefetch
+    const float rinv = 1.f / (float)r;
+    float Lsum = 0.f;
+    const bool want_g = d.mode == GPI_ROM_LOGLIK || (d.mode == GPI_ROM_BACKWARD && d.dmu);
+    for (int qb = 0; qb < NC * NC; qb += ROM_NT / 4) {
+        const int q = qb + q0;
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+        int v0 = 0;
+        if (q < NC * NC) {
+            const int I = q % NC, J = q / NC;
+            v0 = I + (NC + 1) * J;
+            const float u0 = u[v0], u1 = u[v0 + 1], u2 = u[v0 + NC + 1], u3 = u[v0 + NC + 2];
+            const int i0 = I == 0 ? 1 : I * r, i1 = (I + 1) * r - 1;
+            const int rows = J == NC - 1 ? r + 1 : r;
+            const int ncol = i1 - i0 + 1, total = rows * ncol;
+            const uint32_t mcol = (ncol > 1 ? (uint32_t)(((1ull << 32) + ncol - 1) / ncol) : 0u);
+            for (int e0 = sub; e0 < total; e0 += 4 * ROM_U) {
+                const int bi = (e0 - sub) / (4 * ROM_U);
+                const bool pre = qb == 0 && bi < PF / ROM_U;
+                int pp[ROM_U];
+                float yv[ROM_U], lv[ROM_U], gv[ROM_U];
+#pragma unroll
+                for (int k = 0; k < ROM_U; ++k) {
+                    const int e = min(e0 + 4 * k, total - 1);
+                    const int jj = (mcol ? (int)__umulhi((uint32_t)e, mcol) : e), ii = e - jj * ncol;
+                    pp[k] = (J * r + jj) * (nf - 1) + (i0 + ii - 1);
+                }
+                if (d.mode == GPI_ROM_LOGLIK) {
+                    if (pre) {
+#pragma unroll
+                        for (int k = 0; k < ROM_U; ++k) {
+                            yv[k] = bi == 0 ? ypf[k] : (bi == 1 ? ypf[ROM_U + k] : ypf[2 * ROM_U + k]);
+                            lv[k] = bi == 0 ? lpf[k] : (bi == 1 ? lpf[ROM_U + k] : lpf[2 * ROM_U + k]);
+                        }
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < ROM_U; ++k) {
+                            yv[k] = d.Y[(int64_t)s * D.dy + pp[k]];
+                            lv[k] = d.logsig_y[pp[k]];
+                        }
+                    }
+                } else if (want_g) {
+#pragma unroll
+                    for (int k = 0; k < ROM_U; ++k) gv[k] = d.dmu[(int64_t)s * D.dy + pp[k]];
+                }
+#pragma unroll
+                for (int k = 0; k < ROM_U; ++k) {
+                    const int e = e0 + 4 * k;
+                    if (e >= total) break;
+                    const int jj = (mcol ? (int)__umulhi((uint32_t)e, mcol) : e), ii = e - jj * ncol;
+                    const float xi = (float)(i0 + ii - I * r) * rinv, eta = (float)jj * rinv;
+                    float w0, w1, w2, w3;
+                    if (xi >= eta) { w0 = 1.f - xi; w1 = xi - eta; w2 = 0.f; w3 = eta; }
+                    else { w0 = 1.f - eta; w1 = 0.f; w2 = eta - xi; w3 = xi; }
+                    const float mu = w0 * u0 + (w1 * u1 + w2 * u2) + w3 * u3;
+                    if (d.mu_y) d.mu_y[(int64_t)s * D.dy + pp[k]] = mu;
+                    if (!want_g) continue;
+                    float g;
+                    if (d.mode == GPI_ROM_LOGLIK) {
+                        const float ee = expf(-2.f * lv[k]);
+                        const float rr = yv[k] - mu;
+                        Lsum += -0.5f * (2.f * lv[k] + rr * rr * ee + GPI_LOG2PI);
+                        g = -d.loss_scale * rr * ee;
+                        const float gl = d.loss_scale * (1.f - rr * rr * ee);
+                        if (d.gls_part) d.gls_part[(int64_t)s * D.dy + pp[k]] = gl;
+                        else atomicAdd(d.gacc_logsig + pp[k], (double)gl);
+                    } else {
+                        g = gv[k];
+                    }
+                    acc[0] += w0 * g;
+                    acc[1] += w1 * g;
+                    acc[2] += w2 * g;
+                    acc[3] += w3 * g;
+                }
+            }
+        }
+        if (want_g) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                acc[c] += __shfl_xor(acc[c], 1, 64);
+                acc[c] += __shfl_xor(acc[c], 2, 64);
+            }
+            if (q < NC * NC && sub == 0) {
+                atomicAdd(&du[v0], (double)acc[0]);
+                atomicAdd(&du[v0 + 1], (double)acc[1]);
+                atomicAdd(&du[v0 + NC + 1], (double)acc[2]);
+                atomicAdd(&du[v0 + NC + 2], (double)acc[3]);
+            }
+        }
+    }
+    RPHASE(7);
+    if (d.mode == GPI_ROM_LOGLIK) {
+        Lsum = wave_sum(Lsum);
+        if ((tid & 63) == 0) lred[tid >> 6] = (double)Lsum;
+        __syncthreads();
+        if (tid == 0 && d.loss_acc) {
+            double t = lred[0];
+#pragma unroll
+            for (int w = 1; w < ROM_NT / 64; ++w) t += lred[w];
+            atomicAdd(d.loss_acc + blockIdx.x % GPI_REPLICAS, t);
+        }
+    }
+    if (d.mode == GPI_ROM_FORWARD) return;
+    __syncthreads();
+    RPHASE(3);
+    // ---- adjoint lambda = K^{-1} (W^T dmu)_interior: thread i < NI takes row i (K^{-1} symmetric:
+    // kinv[i][j] is column i's entry j, read along j -- consecutive threads, consecutive banks)
+    if (tid < NI) {
+        float a = 0.f;
+#pragma unroll 9
+        for (int jj = 0; jj < NI; ++jj) {
+            const int J = jj / (NC - 1), I = jj - J * (NC - 1) + 1;
+            a = fmaf(kinv[jj * KINV_P + tid], (float)du[I + (NC + 1) * J], a);
+        }
+        const int J = tid / (NC - 1), I = tid - J * (NC - 1) + 1;
+        lam[I + (NC + 1) * J] = a;
+    }
+    __syncthreads();
+    RPHASE(4);
+    // ---- dJ/dx per coarse triangle
+    for (int t = tid; t < NT2; t += ROM_NT) {
+        const int q = t >> 1, ul = t & 1;
+        const int I = q % NC, J = q / NC;
+        const int v0 = I + (NC + 1) * J, v1 = v0 + 1, v2 = v0 + (NC + 1), v3 = v2 + 1;
+        float dk;
+        if (!ul) dk = -(lam[v0] - lam[v1]) * (u[v0] - u[v1]) - (lam[v1] - lam[v3]) * (u[v1] - u[v3]);
+        else dk = -(lam[v2] - lam[v3]) * (u[v2] - u[v3]) - (lam[v0] - lam[v2]) * (u[v0] - u[v2]);
+        const float g = 0.5f * dk * (d.input_kappa ? 1.f : (kp[t] - 1e-8f));
+        float* gp = d.gx + (int64_t)s * d.gx_stride + t;
+        *gp = (d.gx_accumulate ? *gp : 0.f) + g;
+    }
+    RPHASE(5);
+}
+
+template <int NC>
+size_t rom_fast_lds() {
+    constexpr int W = NC, NI = (NC - 1) * (NC + 1), NN = (NC + 1) * (NC + 1), NT2 = 2 * NC * NC;
+    const size_t fl = ((NT2 + NI * W + 2 * NN + 2 * NI + NI * KINV_P + 1) & ~1);
+    return sizeof(float) * fl + sizeof(double) * (NN + ROM_NT / 64);
 }
 
 // Coarse solutions only (FORWARD without mu_y: the VO MC predictive, N_vo x N_mc samples), nc = 4 / 8:
@@ -505,9 +903,20 @@ __global__ __launch_bounds__(64) void rom_lane_kernel(gpi_rom_desc d) {
 
 }  // namespace
 
+#ifdef GPI_PHASE_TIMING
+// timing build only (not declared in gpi.h): copy the ROM phase stamps out and clear them
+extern "C" int gpi_debug_rom_stamps(unsigned long long* out) {
+    static unsigned long long zeros[256 * 8];
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rom_phase), sizeof(zeros)) != hipSuccess) return GPI_ERR_LAUNCH;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_rom_phase), zeros, sizeof(zeros)) != hipSuccess) return GPI_ERR_LAUNCH;
+    return GPI_OK;
+}
+#endif
+
 extern "C" int gpi_rom(const gpi_rom_desc* d, void* stream) {
     if (!d || !d->x || !d->F || d->nc < 2 || d->nc > 12 || d->refine < 1 || d->n < 0) return GPI_ERR_ARG;
-    if (d->mode == GPI_ROM_LOGLIK && (!d->Y || !d->logsig_y || !d->gacc_logsig || !d->gx)) return GPI_ERR_ARG;
+    if (d->mode == GPI_ROM_LOGLIK && (!d->Y || !d->logsig_y || (!d->gacc_logsig && !d->gls_part) || !d->gx))
+        return GPI_ERR_ARG;
     if (d->mode == GPI_ROM_BACKWARD && ((!d->dmu && !d->duc) || !d->gx)) return GPI_ERR_ARG;
     if (d->n == 0) return GPI_OK;
     RomDims D;
@@ -527,6 +936,17 @@ extern "C" int gpi_rom(const gpi_rom_desc* d, void* stream) {
         const dim3 grid((d->n + 63) / 64);
         if (d->nc == 8) hipLaunchKernelGGL(rom_lane_kernel<8>, grid, dim3(64), lds, (hipStream_t)stream, *d);
         else hipLaunchKernelGGL(rom_lane_kernel<4>, grid, dim3(64), lds, (hipStream_t)stream, *d);
+        GPI_CHECK_LAUNCH();
+        return GPI_OK;
+    }
+    static const bool slow = getenv("GPI_ROM_SLOW") && atoi(getenv("GPI_ROM_SLOW"));   // A/B: the r02 kernel
+    if ((d->nc == 8 || d->nc == 4) && !slow) {
+        const size_t lds = d->nc == 8 ? rom_fast_lds<8>() : rom_fast_lds<4>();
+        static const int chol_wave = getenv("GPI_ROM_CHOL") ? atoi(getenv("GPI_ROM_CHOL")) : 0;   // A/B only
+        if (d->nc == 8)
+            hipLaunchKernelGGL(rom_kernel_fast<8>, dim3(d->n), dim3(ROM_NT), lds, (hipStream_t)stream, *d, D, chol_wave);
+        else
+            hipLaunchKernelGGL(rom_kernel_fast<4>, dim3(d->n), dim3(ROM_NT), lds, (hipStream_t)stream, *d, D, chol_wave);
         GPI_CHECK_LAUNCH();
         return GPI_OK;
     }

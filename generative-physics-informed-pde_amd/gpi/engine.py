@@ -269,6 +269,12 @@ class ElboEngine(object):
                         ('y_vo', (self.N_vo if not self.vo_holdoff else 0) * self.d_y)):
             hb[name] = ws.alloc(max(n, 1))
         self.hb = hb
+        # ROM log-likelihood: per-sample d/dlogsigma_y rows (plain stores), reduced into gacc with the
+        # decoder slabs (gpi_rom gls_part) -- instead of n x d_y same-address fp64 atomics
+        self.gls_off = {}
+        for key, n in (('sup', self.N_s), ('vo', 0 if self.vo_holdoff else self.N_vo)):
+            if n > 0:
+                self.gls_off[key] = ws.parts.alloc(n * self.d_y)
         ws.materialize(dev)
         P = lambda mod, n: flat.offset(mod.get_parameter(n))
         h = L.HeadDesc()
@@ -379,7 +385,15 @@ class ElboEngine(object):
             r.mu_y = None
             r.uc = None
             r.dmu = None
+            key = 'sup' if slot == T_LOGL_Y else 'vo'
+            r.gls_part = ws.t_parts.data_ptr() + 4 * self.gls_off[key]
+            it = L.ReduceItem()
+            it.part_off, it.w_off, it.numel, it.row_stride, it.blocks = (self.gls_off[key], flat.offset(g.logsigmas_y),
+                                                                         self.d_y, self.d_y, n)
+            self.rom_reduce.append(it)
             return r
+
+        self.rom_reduce = []
 
         self.roms = []
         self.rom = self.rom_vo = None
@@ -390,6 +404,9 @@ class ElboEngine(object):
             self.rom_vo = rom_desc(self.N_s, self.N_vo, sv, T_LOGL_Y2)
             self.rom_vo.Y = ws.fptr(hb['y_vo']).value
             self.roms.append(self.rom_vo)
+        # the ROMs' d/dlogsigma_y rows are reduced with the decoder slabs (after the ROMs on the side stream)
+        self.reduce_dec = self.reduce_dec + self.rom_reduce
+        self.reduce_items = self.reduce_enc + self.reduce_dec
         self._fixed = (self.B_u, self.N_s, self.N_vo)
         self._side = None
         self._pending_join = False
@@ -824,7 +841,8 @@ def ROM_NN(nc):
 
 
 def rom_call(nc, refine, x, F, input_kappa, mode, mu_y=None, uc=None, dmu=None, duc=None, gx=None, Y=None,
-             logsig_y=None, gacc_logsig=None, loss_acc=None, flag=None, loss_scale=1.0, gx_accumulate=False):
+             logsig_y=None, gacc_logsig=None, loss_acc=None, flag=None, loss_scale=1.0, gx_accumulate=False,
+             gls_part=None):
     """Thin launcher of gpi_rom for the standalone ROM / ReducedOrderModelOperator."""
     for t in (x, F):
         L.require_device(t)
@@ -834,7 +852,7 @@ def rom_call(nc, refine, x, F, input_kappa, mode, mu_y=None, uc=None, dmu=None, 
     p = lambda t: t.data_ptr() if t is not None else None
     r.mu_y, r.uc, r.dmu, r.duc, r.gx, r.Y, r.logsig_y = p(mu_y), p(uc), p(dmu), p(duc), p(gx), p(Y), p(logsig_y)
     r.gx_stride = gx.stride(0) if gx is not None else 0
-    r.gacc_logsig, r.loss_acc, r.flag = p(gacc_logsig), p(loss_acc), p(flag)
+    r.gacc_logsig, r.loss_acc, r.flag, r.gls_part = p(gacc_logsig), p(loss_acc), p(flag), p(gls_part)
     r.loss_scale, r.gx_accumulate = loss_scale, 1 if gx_accumulate else 0
     _run(_lib().gpi_rom, C.byref(r), L.stream_handle(), what='rom')
 

@@ -221,6 +221,9 @@ typedef struct gpi_rom_desc {
     double* loss_acc;          /* [GPI_REPLICAS] sum log-lik (LOGLIK) */
     int32_t* flag;             /* set to 1 if any kappa <= 1e-12 (ROM.py:74-76), checked lazily */
     float* uc;                 /* optional [n, (nc+1)^2] coarse solution */
+    float* gls_part;           /* optional [n, d_y] (LOGLIK): per-sample d/d logsigma_y contributions written with
+                                  plain stores instead of the fp64 atomics into gacc_logsig (32 x 4095 same-address
+                                  atomics per C64 step); the caller reduces the n rows (gpi_wgrad_reduce item) */
 } gpi_rom_desc;
 
 /* Coarse-grained residual on the fine grid (VirtualObservables CGR query,

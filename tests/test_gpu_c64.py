@@ -124,6 +124,14 @@ def test_rom_c64_fused_loglik(device):
     assert tensor_rel(gx.cpu(), e64.grad) < 1e-4
     assert tensor_rel(gls.cpu(), ls64.grad) < 1e-5
     assert flag.item() == 0
+    # gls_part: the same contributions as per-sample rows (plain stores; the engine reduces them)
+    part = torch.full((x.shape[0], ls.shape[0]), float('nan'), device='cuda')
+    gx2 = torch.zeros_like(x)
+    acc2 = torch.zeros_like(acc)
+    rom_call(nc, r, x, F, False, L.ROM_LOGLIK, Y=Y, logsig_y=ls, gx=gx2, gls_part=part, loss_acc=acc2, flag=flag)
+    assert torch.isfinite(part).all()
+    assert tensor_rel(part.double().sum(0).cpu(), ls64.grad) < 1e-5
+    assert torch.equal(gx2, gx) and torch.equal(acc2, acc)
 
 
 @pytest.mark.parametrize('nc', [4, 8])

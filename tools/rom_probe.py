@@ -53,11 +53,11 @@ def main():
         L.check(lib.gpi_rom(C.byref(e.rom), st), 'rom')
         torch.cuda.synchronize()
         L.check(f(ph.ctypes.data), 'stamps')
-        p = ph[:e.rom.n][:, [0, 1, 6, 2, 3, 4, 5]].astype(np.int64)
-        names = ['load+assemble', 'cholesky', 'solves', 'prolong+loglik', 'adjoint', 'dJ/dx']
+        p = ph[:e.rom.n][:, [0, 1, 6, 2, 7, 3, 4, 5]].astype(np.int64)
+        names = ['load+assemble', 'cholesky', 'solves', 'prolong+loglik', 'loss sum', 'adjoint', 'dJ/dx']
         dd = np.diff(p, axis=1).mean(0)
         print('rom_kernel phases (cycles, mean over %d workgroups): %s; total %.0f' % (
-            e.rom.n, ', '.join('%s %.0f' % (n, v) for n, v in zip(names, dd)), (p[:, 6] - p[:, 0]).mean()))
+            e.rom.n, ', '.join('%s %.0f' % (n, v) for n, v in zip(names, dd)), (p[:, 7] - p[:, 0]).mean()))
     step.capture()
     step_us = timed(step.step, reps)
     print('variant %s: rom %.1f us, step %.1f us (%.0f samples/s)' % (
