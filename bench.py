@@ -374,6 +374,8 @@ def main():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-roofline', action='store_true')
     ap.add_argument('--kprof', default=None, help='write the per-operator HIP-event profile (JSON) here')
+    ap.add_argument('--sync-bn', action='store_true',
+                    help='SyncBN: BN statistics over the union of the ranks\' batches (N > 1; default replica-BN)')
     args = ap.parse_args()
     dbg = sorted(k for k in os.environ if k.startswith('GPI_DBG_') or k == 'GPI_PHASE_TIMING')
     if dbg:
@@ -418,8 +420,8 @@ def main():
     # between two graphs, as with gloo)
     step = FusedElboStep(model, Xu, B_u, Xs, Y, F, lr=1e-2, seed=4321 + rank, subset_seed=777,
                          distributed=distributed, rank=rank, world=world,
-                         graph_allreduce=os.environ.get('GPI_GRAPH_ALLREDUCE', '1') == '1')
-    if not args.no_graph:
+                         graph_allreduce=os.environ.get('GPI_GRAPH_ALLREDUCE', '1') == '1', sync_bn=args.sync_bn)
+    if not args.no_graph and not (step.sync_bn and backend != 'nccl'):
         step.capture()
     log('captured; warm-up')
     for _ in range(args.warmup):
@@ -493,10 +495,10 @@ def main():
                                    'ROM %dx%d, fused native step' % (CONFIG_TAG[args.config], args.config, B_u, N_s,
                                                                      physics['rom'].grid.n, physics['rom'].grid.n),
                        'global_batch': world * per_step, 'grid': physics['fom'].grid.n,
-                       'parallelism': 'dp%d' % world, 'graph': not args.no_graph,
+                       'parallelism': 'dp%d' % world, 'graph': step.graph is not None,
                        'world': world, 'backend': backend if distributed else None,
                        'allreduce': None if not distributed else
-                       ('host-side between graphs' if args.no_graph or step.split_graph else 'in-graph'),
+                       ('host-side between graphs' if args.no_graph or getattr(step, 'split_graph', True) else 'in-graph'),
                        'bn': 'replica' if not getattr(step, 'sync_bn', False) else 'sync'},
             'elbo_last': elbo,
             'host_enqueue_ms_per_step': round(1e3 * (t_enq - t0) / args.steps, 4),

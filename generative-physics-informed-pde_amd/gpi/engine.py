@@ -424,6 +424,9 @@ class ElboEngine(object):
         self.rom_first = False
         # callable(side stream handle) launched on the side stream ahead of the ROM (fused step)
         self.side_pre = None
+        # SyncBN (set_sync_bn): None = replica-BN, per-rank batch statistics
+        self.bn_sync = None
+        self.bn_world = 1
 
     # ------------------------------------------------------------------
     def eps_z(self):
@@ -500,8 +503,7 @@ class ElboEngine(object):
         if zero_gacc:
             self.flat.gacc.zero_()
         if self.ep is not None:
-            _run(lib.gpi_codec_forward, self.enc_descs, len(self.enc_descs), C.byref(self.ectx), st,
-                 what='encoder forward')
+            self._codec_forward(self.enc_descs, 0, len(self.enc_descs), self.ectx, st, 'encoder forward')
         if not self.armortized and self.B_u > 0:
             # q_z['unsupervised'] rows as the "encoder" outputs of the head's first segment
             # (torch copies on the current stream, which the launches use)
@@ -519,7 +521,7 @@ class ElboEngine(object):
             self._ev_fork.record(main)
             if self.rom_first:
                 self._launch_roms()
-        _run(lib.gpi_codec_forward, self.dec_descs, self.n_dec_sep, C.byref(self.dctx), st, what='decoder forward')
+        self._codec_forward(self.dec_descs, 0, self.n_dec_sep, self.dctx, st, 'decoder forward')
         if self.n_dec_sep < len(self.dec_descs):
             _run(lib.gpi_conv_loss_fused, C.byref(self.dec_descs[self.n_dec_sep]), C.byref(self.dctx), st,
                  what='decoder output conv (forward + loss + backward)')
@@ -532,6 +534,59 @@ class ElboEngine(object):
             self._join()
             return self.elbo_value()
         return None
+
+    # ------------------------------------------------------------------ SyncBN (optional)
+    def set_sync_bn(self, allreduce, world):
+        """SyncBN mode (the exact-parity alternative to replica-BN): every BN
+        layer normalises over the union of the ranks' batches of its codec call, as the reference does
+        over its one process's batch (codec.py:164-173 in train mode).  allreduce(t): in-place SUM
+        over the ranks.  After each producing conv the fp64 channel sums {sum x, sum x^2} of its output
+        are all-reduced (forward), and before each conv whose output feeds a BN the BN-backward sums
+        {sum S, sum S x-hat} of that output (backward) -- once per channel and phase.  The sums are
+        divided by the world size: the kernels divide by their per-rank count, so equal per-rank
+        batches give the global means.  The codec launches then go one by one (host hook between
+        them); running_var's Bessel factor keeps the per-rank count (N/(N-1) for N = per-rank
+        samples x pixels, >= 16384 here: a <1e-4 relative difference in the running buffer only)."""
+        self.bn_sync = allreduce
+        self.bn_world = int(world)
+
+    def _stats_view(self):
+        R, G = L.GPI_REPLICAS, L.GPI_MAX_GROUPS
+        o = N_TERMS * R
+        return self.ws.t_scr[o:o + R * G * self.ws.n_stats * 4].view(R, G, self.ws.n_stats, 4)
+
+    def _sync_stats(self, stat0, n, f0):
+        v = self._stats_view()
+        sub = v[:, :, stat0:stat0 + n, f0:f0 + 2].sum(0)        # replicas folded: [groups, n, 2]
+        self.bn_sync(sub)
+        sub.div_(self.bn_world)
+        v[:, :, stat0:stat0 + n, f0:f0 + 2] = 0.0
+        v[0, :, stat0:stat0 + n, f0:f0 + 2] = sub
+
+    def _codec_forward(self, descs, i0, i1, ctx, st, what):
+        lib = _lib()
+        if self.bn_sync is None:
+            ptr = C.cast(C.byref(descs, i0 * C.sizeof(L.ConvDesc)), C.POINTER(L.ConvDesc))
+            _run(lib.gpi_codec_forward, ptr, i1 - i0, C.byref(ctx), st, what=what)
+            return
+        for i in range(i0, i1):
+            d = descs[i]
+            _run(lib.gpi_conv_forward, C.byref(d), C.byref(ctx), st, what=what)
+            if d.epilogue == L.EPI_STORE_STATS and d.out_stat >= 0:
+                self._sync_stats(d.out_stat, d.cout, 0)
+
+    def _codec_backward(self, descs, i0, i1, ctx, st, what):
+        """descs[i1 - 1] down to descs[i0] (gpi_codec_backward's order)."""
+        lib = _lib()
+        if self.bn_sync is None:
+            ptr = C.cast(C.byref(descs, i0 * C.sizeof(L.ConvDesc)), C.POINTER(L.ConvDesc))
+            _run(lib.gpi_codec_backward, ptr, i1 - i0, C.byref(ctx), st, what=what)
+            return
+        for i in range(i1 - 1, i0 - 1, -1):
+            d = descs[i]
+            if d.gout_mode == 0:          # its output feeds a BN: that BN's backward sums are complete
+                self._sync_stats(d.out_stat, d.cout, 2)
+            _run(lib.gpi_conv_backward, C.byref(d), C.byref(ctx), st, what=what)
 
     def _launch_roms(self):
         self._side.wait_event(self._ev_fork)
@@ -613,8 +668,7 @@ class ElboEngine(object):
         writes may be read by the encoder backward)."""
         lib = _lib()
         st = stream if stream is not None else L.stream_handle()
-        _run(lib.gpi_codec_backward, self.dec_descs, self.n_dec_sep, C.byref(self.dctx), st,
-             what='decoder backward')
+        self._codec_backward(self.dec_descs, 0, self.n_dec_sep, self.dctx, st, 'decoder backward')
         P_, W_, G_ = (C.c_void_p(self.flat.P.data_ptr()), C.c_void_p(self.ws.t_ws.data_ptr()),
                       C.c_void_p(self.flat.gacc.data_ptr()))
         main = torch.cuda.current_stream()
@@ -642,13 +696,14 @@ class ElboEngine(object):
         n_enc = len(self.enc_descs) if self.ep is not None else 0
         if n_enc:
             # every encoder conv but the first (reverse order) ...
-            rest = C.cast(C.byref(self.enc_descs, C.sizeof(L.ConvDesc)), C.POINTER(L.ConvDesc))
-            _run(lib.gpi_codec_backward, rest, n_enc - 1, C.byref(self.ectx), st, what='encoder backward')
+            self._codec_backward(self.enc_descs, 1, n_enc, self.ectx, st, 'encoder backward')
             enc_split = self.enc_reduce == 'split'
             if enc_split:
                 self._ev_enc.record(main)
             # ... then the input conv (weight gradient only), whose slab reduction stays on the main
             # stream while the side stream reduces the other encoder slabs concurrently
+            if self.bn_sync is not None and self.enc_descs[0].gout_mode == 0:
+                self._sync_stats(self.enc_descs[0].out_stat, self.enc_descs[0].cout, 2)
             _run(lib.gpi_conv_backward, C.byref(self.enc_descs[0]), C.byref(self.ectx), st, what='In_conv backward')
             run_reduce(self.reduce_enc[:self.n_reduce_in] if enc_split else self.reduce_enc, self.ws, self.flat, st)
         side.wait_event(self._ev_fork2)

@@ -50,7 +50,7 @@ class FusedElboStep(object):
 
     def __init__(self, model, X_pool, B_u, X_s=None, Y=None, F=None, lr=1e-2, betas=(0.9, 0.999), eps=1e-8,
                  seed=0, normalize=False, process_group=None, distributed=False, rank=0, world=1, subset_seed=None,
-                 graph_allreduce=True):
+                 graph_allreduce=True, sync_bn=False):
         self.model = model
         self.flat = model.native_flat()
         self.N_s = 0 if X_s is None else int(X_s.shape[0])
@@ -62,6 +62,12 @@ class FusedElboStep(object):
             # noise seed would give overlapping / duplicated slices without any error
             raise ValueError('FusedElboStep: world > 1 needs an explicit subset_seed shared by all ranks')
         self.engine = ElboEngine(model, self.B_u, self.N_s, normalize=normalize)
+        # SyncBN: every codec call's BN statistics over the union of the ranks' batches (ElboEngine.set_sync_bn);
+        # default replica-BN (per-rank batch statistics, no collective in the codec)
+        self.sync_bn = bool(sync_bn) and bool(distributed) and self.world > 1
+        if self.sync_bn:
+            pg = process_group
+            self.engine.set_sync_bn(lambda t: dist.all_reduce(t, op=dist.ReduceOp.SUM, group=pg), self.world)
         dev = self.flat.P.device
         self.X_pool = X_pool.contiguous().float() if X_pool is not None else None
         self.X_s, self.Y, self.F = X_s, Y, F
@@ -202,6 +208,8 @@ class FusedElboStep(object):
         The two warm-up steps run on snapshots: capture() leaves parameters, optimizer state,
         step counter, random stream and the pre-drawn subset / noise exactly as it found them, so
         the first replayed step is the step an eager loop would take next."""
+        if self.sync_bn and dist.get_backend(self.pg) != dist.Backend.NCCL:
+            raise RuntimeError('FusedElboStep.capture: SyncBN with a host-side backend (gloo) runs eagerly only')
         torch.cuda.synchronize()
         saved = [t.clone() for t in self._mutable_state()]
         s = torch.cuda.Stream()

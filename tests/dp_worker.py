@@ -37,8 +37,9 @@ def shard_model(d, rank, B_u=B_U, ns=NS_RANK):
     return build_golden_model(e)
 
 
-def main(out):
+def main(out, mode='replica'):
     rank, world = int(os.environ['RANK']), int(os.environ['WORLD_SIZE'])
+    sync_bn = mode == 'sync'     # SyncBN: BN statistics over both ranks' batches (eager: gloo)
     torch.cuda.set_device(0)                      # every rank on the one GPU of the box
     dist.init_process_group('gloo')
     from elbo_ref import load
@@ -54,7 +55,8 @@ def main(out):
     except ValueError:
         pass
     step = FusedElboStep(model, Xu, B_U, ds.get('X'), ds.get('Y'), ds.get('F_ROM_BC'), lr=1e-3, seed=50 + rank,
-                         subset_seed=9, distributed=True, rank=rank, world=world)
+                         subset_seed=9, distributed=True, rank=rank, world=world, sync_bn=sync_bn)
+    assert step.sync_bn == sync_bn
     e = step.engine
     rec = dict(idx=step.idx.cpu().numpy(), eps_z=e.eps_z().cpu().numpy(), eps_x=e.eps_x().cpu().numpy(),
                P0=step.flat.P.cpu().numpy())
@@ -78,4 +80,4 @@ def main(out):
 
 
 if __name__ == '__main__':
-    main(sys.argv[1])
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else 'replica')

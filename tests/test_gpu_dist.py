@@ -78,6 +78,70 @@ def test_dp_two_ranks_native_step(device, tmp_path):
     assert np.array_equal(rk[0]['P0'][:ns], rk[1]['P0'][:ns])
 
 
+def test_dp_two_ranks_sync_bn(device, tmp_path):
+    """SyncBN (FusedElboStep(sync_bn=True)): with every BN layer normalised over
+    both ranks' batches, the all-reduced shared gradient of two gloo ranks equals the gradient of ONE
+    process running the union batch (the reference's semantics at the global batch: train-mode BN over
+    the whole codec call, codec.py:164-173), and each rank's q rows equal the union's rows of its
+    labeled shard.  Tolerance 5e-5 per tensor (fp32 sums in another order); the ELBO halves sum to the
+    union ELBO within 1e-5."""
+    from dp_worker import B_U, NS_RANK
+    from test_gpu_parity import build_golden_model
+    env = dict(os.environ)
+    env['PYTHONUNBUFFERED'] = '1'
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node=2',
+           '--master-addr=127.0.0.1', '--master-port=%d' % _free_port(), os.path.join(HERE, 'dp_worker.py'),
+           str(tmp_path), 'sync']
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    rk = [dict(np.load(str(tmp_path / ('rank%d.npz' % i)))) for i in range(2)]
+    idx = rk[0]['idx']
+    ns = int(rk[0]['n_shared'])
+    d = load('elbo_c32.npz')
+    e = dict(d)
+    e['cfg'] = np.array([int(d['cfg'][0]), int(d['cfg'][1]), int(d['cfg'][2]), int(d['cfg'][3]), 2 * B_U,
+                         2 * NS_RANK])
+    for k in ('Xs', 'Y', 'F'):
+        e[k] = d[k][:2 * NS_RANK]
+    model, _ = build_golden_model(e)
+    model._datasets['unsupervised'].perm = torch.tensor(idx[:2 * B_U], device='cuda').long()
+    dz = rk[0]['eps_z'].shape[1]
+    ez = np.concatenate([rk[0]['eps_z'][:B_U], rk[1]['eps_z'][:B_U], rk[0]['eps_z'][B_U:], rk[1]['eps_z'][B_U:]])
+    ex = np.concatenate([rk[0]['eps_x'], rk[1]['eps_x']])
+    assert ez.shape == (2 * (B_U + NS_RANK), dz)
+    names = list(rk[0]['names'])
+    with torch.no_grad():       # the ranks' initial parameters (shared: identical; q rows: shard rows)
+        for k, p in model.named_parameters():
+            i = names.index(k)
+            o = [int(rk[j]['offsets'][i]) for j in range(2)]
+            if k.startswith(('q_z.', 'q_X.')):
+                parts = [rk[j]['P0'][o[j]:o[j] + p.numel() // 2] for j in range(2)]
+                p.copy_(torch.tensor(np.concatenate(parts).reshape(p.shape)))
+            else:
+                p.copy_(torch.tensor(rk[0]['P0'][o[0]:o[0] + p.numel()].reshape(p.shape)))
+    elbo = model.elbo(step=0, armortized_bs=2 * B_U, eps=(torch.tensor(ez, device='cuda'),
+                                                          torch.tensor(ex, device='cuda')))
+    (-elbo).backward()
+    tot = float(rk[0]['elbo']) + float(rk[1]['elbo'])
+    assert abs(tot - elbo.item()) <= 1e-5 * abs(elbo.item()), (tot, elbo.item())
+    errs = {}
+    for k, p in model.named_parameters():
+        i = names.index(k)
+        g = p.grad.cpu().numpy().ravel()
+        if k.startswith(('q_z.', 'q_X.')):
+            half = p.numel() // 2
+            for j in range(2):
+                o = int(rk[j]['offsets'][i])
+                errs['%s[rank%d]' % (k, j)] = tensor_rel(rk[j]['G_red'][o:o + half], g[j * half:(j + 1) * half])
+        else:
+            o = int(rk[0]['offsets'][i])
+            assert o + p.numel() <= ns
+            errs[k] = tensor_rel(rk[0]['G_red'][o:o + p.numel()], g)
+            assert np.array_equal(rk[0]['G_red'][o:o + p.numel()], rk[1]['G_red'][o:o + p.numel()])
+    bad = {k: v for k, v in errs.items() if v >= 5e-5}
+    assert not bad, (bad, sorted(errs.items(), key=lambda kv: -kv[1])[:8])
+
+
 def test_rccl_allreduce_captured_in_step_graph(device):
     """The RCCL (backend 'nccl') all-reduce of the shared gradients captured inside the fused step's
     HIP graph: replays equal eager steps bit for bit (world size 1 on this one-GPU box; the driver's
