@@ -407,18 +407,32 @@ __global__ __launch_bounds__(ROM_NT) void rom_kernel(gpi_rom_desc d, RomDims D) 
 // ---------------------------------------------------------------------------------------------
 // rom_kernel_fast<NC> (nc = 4 / 8, one 256-thread workgroup per sample): the same result as
 // rom_kernel with the sequential chains cut (r03 phase stamps of rom_kernel at C64: Cholesky + solve
-// 83 k cycles, adjoint solve 55 k, prolongation 19 k of 162 k):
-//   * the banded Cholesky by one lane with the register window, the pivot by v_rsq (no IEEE sqrt /
-//     division sequences in the chain) and the next band row loaded two steps ahead;
-//   * K^{-1} by ONE wave: lane j < NI solves K x = e_j, lane NI solves K u = b -- 64 independent
-//     forward / back substitutions with the band rows as broadcast LDS reads and the solution in
-//     registers, so the coarse solution and the inverse cost one solve's latency; the adjoint
-//     lambda = K^{-1} W^T dmu is then a parallel mat-vec instead of two more sequential sweeps;
+// 83 k cycles, adjoint solve 55 k, prolongation 19 k of 162 k; 72.8 us per launch):
+//   * wave 0 factors K = L L^T and forms Z = L^{-1} in ONE pass (chol_inv_wave): the factorisation runs
+//     redundantly in every lane and lane j takes the forward substitution of e_j as each row of L
+//     becomes final; u = K^{-1} b and the adjoint lambda = K^{-1} W^T dmu are then Z^T (Z v) mat-vecs
+//     over the four waves (kinv_apply) instead of sequential triangular sweeps;
 //   * the Y / logsigma_y loads of the prolongation are issued at entry (in flight during the
-//     factorisation).
+//     factorisation);
+//   * d/dlogsigma_y per sample and node goes to a row of gls_part (plain stores) when given, reduced
+//     with the decoder slabs, instead of 4095 same-address fp64 atomics per sample.
+// (r03 A/B: a wave-parallel factorisation with rotating window rows and ds_bpermute took 23.7 k cycles,
+// the redundant form 13.9 k; 64 independent register solves with v_readlane coefficients 17.5 k for the
+// sweeps vs 3.7 k for the two Z mat-vecs.)  21.3 us per launch at C64.
+
+constexpr int KINV_P = 65;     // pitch of the Z = L^{-1} image (conflict-free row and column access)
+
+// Z = L^{-1} (K = L L^T) by ONE wave: every lane runs the same banded factorisation (chol_band_seq's
+// register window, the pivot by v_rsq instead of IEEE sqrt + division; the values are uniform, the band
+// rows come by broadcast LDS reads) and, as row k of L becomes final at step k, lane j takes
+// forward-substitution step k of L y = e_j -- the factorisation instructions serve all 64 right-hand
+// sides at once (SIMT: an instruction costs the same with one lane active or 64), no LDS or cross-lane
+// traffic in the substitution.  Column j of Z goes to z[k][j] (pitch KINV_P).  Then
+// K^{-1} v = Z^T (Z v): two parallel triangular mat-vecs per solve.
 template <int NC>
-__device__ __forceinline__ void chol_band_fast(float* __restrict__ L, float* __restrict__ dinv) {
-    constexpr int W = NC, NI = (NC - 1) * (NC + 1);
+__device__ __forceinline__ void chol_inv_wave(const float* __restrict__ L, float* __restrict__ z) {
+    constexpr int W = NC, BW = NC - 1, NI = (NC - 1) * (NC + 1);
+    const int j = threadIdx.x & 63;
     float win[W][W];   // win[a][t] = L(k + a, k + a - t)
     float nxt[2][W];   // rows k + W, k + W + 1 (prefetched)
 #pragma unroll
@@ -429,19 +443,32 @@ __device__ __forceinline__ void chol_band_fast(float* __restrict__ L, float* __r
     for (int u = 0; u < 2; ++u)
 #pragma unroll
         for (int t = 0; t < W; ++t) nxt[u][t] = (W + u < NI) ? L[(W + u) * W + t] : 0.f;
+    float h[BW];       // h[t-1] = y[k - t] of this lane's right-hand side e_j
+#pragma unroll
+    for (int t = 0; t < BW; ++t) h[t] = 0.f;
 #pragma unroll
     for (int k = 0; k < NI; ++k) {
         const float inv = __builtin_amdgcn_rsqf(win[0][0]);
-        win[0][0] = win[0][0] * inv;
-        dinv[k] = inv;
+        // forward substitution step k (row k of L is final: L(k, k - t) = win[0][t], 1 / L(k,k) = inv)
+        float y = j == k ? 1.f : 0.f, y2 = 0.f;
+#pragma unroll
+        for (int t = 1; t <= BW; ++t) {
+            if (k - t < 0) continue;
+            if (t & 1) y = fmaf(-win[0][t], h[t - 1], y);
+            else y2 = fmaf(-win[0][t], h[t - 1], y2);
+        }
+        y = (y + y2) * inv;
+        z[k * KINV_P + j] = y;
+#pragma unroll
+        for (int t = BW - 1; t > 0; --t) h[t] = h[t - 1];
+        h[0] = y;
+        // factorisation step k
 #pragma unroll
         for (int a = 1; a < W; ++a) win[a][a] *= inv;                       // L(k+a, k)
 #pragma unroll
         for (int a = 1; a < W; ++a)
 #pragma unroll
             for (int b = 1; b <= a; ++b) win[a][a - b] = fmaf(-win[a][a], win[b][b], win[a][a - b]);
-#pragma unroll
-        for (int t = 0; t < W; ++t) L[k * W + t] = win[0][t];
 #pragma unroll
         for (int a = 0; a + 1 < W; ++a)
 #pragma unroll
@@ -455,46 +482,38 @@ __device__ __forceinline__ void chol_band_fast(float* __restrict__ L, float* __r
     }
 }
 
-// The same factorisation by one wave with the (W x W) window spread over the lanes: lane R W + t holds
-// window entry (a, t) = L(k + a, k + a - t) of the physical row R, a = (R - k) mod W (the rows rotate,
-// nothing is shifted); per step the pivot is read by v_readlane, the column is scaled, and the rank-1
-// update takes its two column values by ds_bpermute.  The finished row goes to L, its lanes take the
-// band row k + W (loaded a step ahead).  Critical path per step ~ readlane, rsq, mul, bpermute, fma.
+// out[i] = (Z^T (Z v))_i = (K^{-1} v)_i for i < NI (v, out in LDS; out may alias v; part: 4 x 64 floats of
+// scratch).  All ROM_NT = 256 threads call it: wave p sums the terms k = p (mod 4) of every row i = lane
+// (fully unrolled, conflict-free: bank (i + k) mod 64), the four partial sums meet in LDS; three barriers.
 template <int NC>
-__device__ __forceinline__ void chol_band_wave(float* __restrict__ L, float* __restrict__ dinv) {
-    constexpr int W = NC, NI = (NC - 1) * (NC + 1);
-    const int lane = threadIdx.x & 63;
-    const int R = lane / W, t = lane - R * W;
-    const bool act = lane < W * W;
-    float v = (act && R < NI) ? L[R * W + t] : 0.f;            // rows 0 .. W-1 (R == a at k = 0)
-    float nx = (act && W + R < NI) ? L[(W + R) * W + t] : 0.f;  // row W + R: replaces row R after step R
-    for (int k = 0; k < NI; ++k) {
-        const int R0 = k % W;
-        const int a = (R - R0 + W) % W;
-        const float p = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), R0 * W));
-        const float inv = __builtin_amdgcn_rsqf(p);
-        if (a >= 1 && t == a) v *= inv;                          // column k: L(k + a, k)
-        // rank-1 update of entries (a, t), 0 <= t < a: -= L(k+a, k) L(k+a-t, k)
-        const int b = a - t;
-        const int s1 = R * W + a;                                // (a, a): this row's column entry
-        const int s2 = ((R0 + b) % W) * W + b;                   // (b, b)
-        const float c1 = __shfl(v, s1, 64), c2 = __shfl(v, s2, 64);
-        if (a >= 1 && t < a) v = fmaf(-c1, c2, v);
-        if (R == R0) {
-            // row k is final: store it (pivot -> sqrt(p) = p * rsq(p)), take row k + W
-            const float o = t == 0 ? p * inv : v;
-            L[k * W + t] = o;
-            if (t == 0) dinv[k] = inv;
-            v = nx;
-            nx = (act && k + 2 * W < NI) ? L[(k + 2 * W) * W + t] : 0.f;
-        }
+__device__ __forceinline__ void kinv_apply(const float* __restrict__ z, const float* v, float* part, float* out) {
+    constexpr int NI = (NC - 1) * (NC + 1), NM = (NI + 3) / 4;
+    const int i = threadIdx.x & 63, p = threadIdx.x >> 6;
+    float a = 0.f;
+#pragma unroll
+    for (int m = 0; m < NM; ++m) {            // (Z v)_i = sum_{k <= i} Z[i][k] v_k
+        const int k = 4 * m + p;
+        if (k < NI) a = fmaf((k <= i && i < NI) ? z[i * KINV_P + k] : 0.f, v[k], a);
     }
+    part[p * 64 + i] = a;
+    __syncthreads();
+    float* w = part + 256;                    // (Z v), 64 floats
+    if (threadIdx.x < 64) w[i] = (part[i] + part[64 + i]) + (part[128 + i] + part[192 + i]);
+    __syncthreads();
+    a = 0.f;
+#pragma unroll
+    for (int m = 0; m < NM; ++m) {            // (Z^T w)_i = sum_{k >= i} Z[k][i] w_k
+        const int k = 4 * m + p;
+        if (k < NI) a = fmaf((k >= i && i < NI) ? z[k * KINV_P + i] : 0.f, w[k], a);
+    }
+    part[p * 64 + i] = a;
+    __syncthreads();
+    if (threadIdx.x < NI) out[i] = (part[i] + part[64 + i]) + (part[128 + i] + part[192 + i]);
+    __syncthreads();
 }
 
-constexpr int KINV_P = 65;     // pitch of the K^{-1} image (conflict-free row and column access)
-
 template <int NC>
-__global__ __launch_bounds__(ROM_NT) void rom_kernel_fast(gpi_rom_desc d, RomDims D, int chol_wave) {
+__global__ __launch_bounds__(ROM_NT) void rom_kernel_fast(gpi_rom_desc d, RomDims D) {
     constexpr int W = NC, BW = NC - 1, NI = (NC - 1) * (NC + 1), NN = (NC + 1) * (NC + 1), NT2 = 2 * NC * NC;
     constexpr int PF = 3 * ROM_U;            // prefetched fine nodes per thread (a square holds <= (r+1) r)
     extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -504,8 +523,9 @@ __global__ __launch_bounds__(ROM_NT) void rom_kernel_fast(gpi_rom_desc d, RomDim
     float* b = u + NN;                // [NI]
     float* lam = b + NI;              // [NN]
     float* dinv = lam + NN;           // [NI]
-    float* kinv = dinv + NI;          // [NI][KINV_P]
-    double* du = (double*)(sm + ((NT2 + NI * W + 2 * NN + 2 * NI + NI * KINV_P + 1) & ~1));   // [NN]
+    float* kinv = dinv + NI;          // [NI][KINV_P]: Z = L^{-1}
+    float* part = kinv + NI * KINV_P; // [320] kinv_apply scratch
+    double* du = (double*)(sm + ((NT2 + NI * W + 2 * NN + 2 * NI + NI * KINV_P + 320 + 1) & ~1));   // [NN]
     double* lred = du + NN;           // [ROM_NT / 64]
     const int s = blockIdx.x;
     const int tid = threadIdx.x;
@@ -571,68 +591,16 @@ __global__ __launch_bounds__(ROM_NT) void rom_kernel_fast(gpi_rom_desc d, RomDim
 #pragma unroll
     for (int k = 0; k < PF; ++k) asm volatile("" : : "v"(ypf[k]), "v"(lpf[k]));
     static_assert(NC * NC <= 64, "window per wave");
-    if (chol_wave) {
-        if (tid < 64) chol_band_wave<NC>(L, dinv);
-    } else if (tid == 0) {
-        chol_band_fast<NC>(L, dinv);
-    }
-    __syncthreads();
+    // every lane of wave 0: the factorisation (uniform) + forward substitution of e_lane -> Z = L^{-1}
+    if (tid < 64) chol_inv_wave<NC>(L, kinv);
     RPHASE(6);
-    // ---- wave 0: lane j < NI solves K x = e_j (column j of K^{-1}), lane NI solves K u = b.  The band
-    // factor (NI W floats), 1 / L(k,k) and b sit spread over the wave's lanes in registers (lane l holds
-    // entry 64 v + l of register v) and every coefficient of the fully unrolled sweeps is taken by
-    // v_readlane (uniform, an SGPR operand): no LDS round trip in the sweeps' dependency chains
-    // (the LDS form: 62.7 k cycles for the two sweeps, r03f); the solution y[NI] stays in registers.
-    if (tid < 64) {
-        constexpr int NLR = (NI * W + 63) / 64;
-        const int j = tid;
-        float lr[NLR];
-#pragma unroll
-        for (int v = 0; v < NLR; ++v) lr[v] = (64 * v + j < NI * W) ? L[64 * v + j] : 0.f;
-        const float dr = j < NI ? dinv[j] : 0.f;
-        const float br = j < NI ? b[j] : 0.f;
-        auto Lk = [&](int idx) -> float {       // L[idx], idx compile-time after unrolling
-            return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lr[idx >> 6]), idx & 63));
-        };
-        auto rl = [&](float v, int l) -> float { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); };
-        float y[NI];
-#pragma unroll
-        for (int k = 0; k < NI; ++k) {
-            __builtin_amdgcn_sched_barrier(0);  // keep each step's readlanes next to their use (SGPR pressure)
-            const float bk = rl(br, k);
-            float a = j == k ? 1.f : 0.f;
-            a = j == NI ? bk : a;
-            float a2 = 0.f;                     // two partial sums: a shorter dependency chain
-#pragma unroll
-            for (int t = 1; t <= BW; ++t) {
-                if (k - t < 0) continue;
-                if (t & 1) a = fmaf(-Lk(k * W + t), y[k - t], a);
-                else a2 = fmaf(-Lk(k * W + t), y[k - t], a2);
-            }
-            y[k] = (a + a2) * rl(dr, k);
-        }
-#pragma unroll
-        for (int k = NI - 1; k >= 0; --k) {
-            __builtin_amdgcn_sched_barrier(0);
-            float a = y[k], a2 = 0.f;
-#pragma unroll
-            for (int t = 1; t <= BW; ++t) {
-                if (k + t >= NI) continue;
-                if (t & 1) a = fmaf(-Lk((k + t) * W + t), y[k + t], a);
-                else a2 = fmaf(-Lk((k + t) * W + t), y[k + t], a2);
-            }
-            y[k] = (a + a2) * rl(dr, k);
-        }
-        if (j <= NI) {
-#pragma unroll
-            for (int i = 0; i < NI; ++i) kinv[i * KINV_P + j] = y[i];
-        }
-    }
     __syncthreads();
+    // interior coarse solution u_I = K^{-1} b = Z^T (Z b), in place of b
+    kinv_apply<NC>(kinv, b, part, b);
     RPHASE(2);
     for (int e = tid; e < NN; e += ROM_NT) {
         const int I = e % (NC + 1), J = e / (NC + 1);
-        u[e] = (I == 0 || I == NC) ? F[e] : kinv[(J * (NC - 1) + (I - 1)) * KINV_P + NI];
+        u[e] = (I == 0 || I == NC) ? F[e] : b[J * (NC - 1) + (I - 1)];
     }
     __syncthreads();
     if (d.uc) for (int e = tid; e < NN; e += ROM_NT) d.uc[(int64_t)s * NN + e] = u[e];
@@ -743,17 +711,16 @@ __global__ __launch_bounds__(ROM_NT) void rom_kernel_fast(gpi_rom_desc d, RomDim
     if (d.mode == GPI_ROM_FORWARD) return;
     __syncthreads();
     RPHASE(3);
-    // ---- adjoint lambda = K^{-1} (W^T dmu)_interior: thread i < NI takes row i (K^{-1} symmetric:
-    // kinv[i][j] is column i's entry j, read along j -- consecutive threads, consecutive banks)
-    if (tid < NI) {
-        float a = 0.f;
-#pragma unroll 9
-        for (int jj = 0; jj < NI; ++jj) {
-            const int J = jj / (NC - 1), I = jj - J * (NC - 1) + 1;
-            a = fmaf(kinv[jj * KINV_P + tid], (float)du[I + (NC + 1) * J], a);
-        }
-        const int J = tid / (NC - 1), I = tid - J * (NC - 1) + 1;
-        lam[I + (NC + 1) * J] = a;
+    // ---- adjoint lambda = K^{-1} (W^T dmu)_interior = Z^T (Z r)
+    for (int ii = tid; ii < NI; ii += ROM_NT) {
+        const int J = ii / (NC - 1), I = ii - J * (NC - 1) + 1;
+        b[ii] = (float)du[I + (NC + 1) * J];
+    }
+    __syncthreads();
+    kinv_apply<NC>(kinv, b, part, b);
+    for (int ii = tid; ii < NI; ii += ROM_NT) {
+        const int J = ii / (NC - 1), I = ii - J * (NC - 1) + 1;
+        lam[I + (NC + 1) * J] = b[ii];
     }
     __syncthreads();
     RPHASE(4);
@@ -775,7 +742,7 @@ __global__ __launch_bounds__(ROM_NT) void rom_kernel_fast(gpi_rom_desc d, RomDim
 template <int NC>
 size_t rom_fast_lds() {
     constexpr int W = NC, NI = (NC - 1) * (NC + 1), NN = (NC + 1) * (NC + 1), NT2 = 2 * NC * NC;
-    const size_t fl = ((NT2 + NI * W + 2 * NN + 2 * NI + NI * KINV_P + 1) & ~1);
+    const size_t fl = ((NT2 + NI * W + 2 * NN + 2 * NI + NI * KINV_P + 320 + 1) & ~1);
     return sizeof(float) * fl + sizeof(double) * (NN + ROM_NT / 64);
 }
 
@@ -942,11 +909,10 @@ extern "C" int gpi_rom(const gpi_rom_desc* d, void* stream) {
     static const bool slow = getenv("GPI_ROM_SLOW") && atoi(getenv("GPI_ROM_SLOW"));   // A/B: the r02 kernel
     if ((d->nc == 8 || d->nc == 4) && !slow) {
         const size_t lds = d->nc == 8 ? rom_fast_lds<8>() : rom_fast_lds<4>();
-        static const int chol_wave = getenv("GPI_ROM_CHOL") ? atoi(getenv("GPI_ROM_CHOL")) : 0;   // A/B only
         if (d->nc == 8)
-            hipLaunchKernelGGL(rom_kernel_fast<8>, dim3(d->n), dim3(ROM_NT), lds, (hipStream_t)stream, *d, D, chol_wave);
+            hipLaunchKernelGGL(rom_kernel_fast<8>, dim3(d->n), dim3(ROM_NT), lds, (hipStream_t)stream, *d, D);
         else
-            hipLaunchKernelGGL(rom_kernel_fast<4>, dim3(d->n), dim3(ROM_NT), lds, (hipStream_t)stream, *d, D, chol_wave);
+            hipLaunchKernelGGL(rom_kernel_fast<4>, dim3(d->n), dim3(ROM_NT), lds, (hipStream_t)stream, *d, D);
         GPI_CHECK_LAUNCH();
         return GPI_OK;
     }
