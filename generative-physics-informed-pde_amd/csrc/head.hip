@@ -34,44 +34,122 @@ __device__ __forceinline__ float block_sum128(float v, float* scratch) {
     return t;
 }
 
-// The weight reads are the latency chain of these kernels (one sample per workgroup, weights
-// from L2): each thread issues UL loads before their FMAs.
-constexpr int UL = 16;
+// The weight reads are the latency chain of these kernels (one sample per workgroup, weights from
+// L2): every dependent round trip costs ~0.5 us, so each thread issues a whole batch of weight loads
+// before its FMAs, batches are as wide as the registers allow (64 rows / columns), two matrices
+// that read the same input share one pass (mu and logsigma heads), and a transposed product
+// whose column count leaves threads idle splits its rows over thread groups.  A kernel that
+// prefetches every weight at entry was measured 2x slower (r03: fully unrolled, run-once code).
 
-// y[j] = b[j] + sum_k W[j*K + k] x[k]
-__device__ __forceinline__ void matvec(const float* __restrict__ W, const float* __restrict__ b, const float* x,
-                                       int J, int K, float* y) {
-    for (int j = threadIdx.x; j < J; j += HT) {
-        float a[4] = {b ? b[j] : 0.f, 0.f, 0.f, 0.f};
-        const float* w = W + (int64_t)j * K;
+// y0[j] = b0[j] + W0[j,:] . x for j < J0, then y1[j] = b1[j] + W1[j,:] . x for j < J1 (thread per row)
+__device__ __forceinline__ void matvec2(const float* __restrict__ W0, const float* __restrict__ b0, float* y0,
+                                        int J0, const float* __restrict__ W1, const float* __restrict__ b1,
+                                        float* y1, int J1, const float* x, int K) {
+    const bool vec = (K & 3) == 0 && ((reinterpret_cast<uintptr_t>(W0) | reinterpret_cast<uintptr_t>(W1)) & 15) == 0;
+    for (int j = threadIdx.x; j < J0 + J1; j += HT) {
+        const bool first = j < J0;
+        const int jr = first ? j : j - J0;
+        const float* bias = first ? b0 : b1;
+        const float* w = (first ? W0 : W1) + (int64_t)jr * K;
+        float a[4] = {bias ? bias[jr] : 0.f, 0.f, 0.f, 0.f};
         int k = 0;
-        for (; k + UL <= K; k += UL) {
-            float wv[UL];
+        if (vec) {
+            const float4* w4 = reinterpret_cast<const float4*>(w);
+            for (; k + 64 <= K; k += 64) {
+                float4 wv[16];
 #pragma unroll
-            for (int u = 0; u < UL; ++u) wv[u] = w[k + u];
+                for (int u = 0; u < 16; ++u) wv[u] = w4[(k >> 2) + u];
 #pragma unroll
-            for (int u = 0; u < UL; ++u) a[u & 3] = fmaf(wv[u], x[k + u], a[u & 3]);
+                for (int u = 0; u < 16; ++u) {
+                    a[0] = fmaf(wv[u].x, x[k + 4 * u], a[0]);
+                    a[1] = fmaf(wv[u].y, x[k + 4 * u + 1], a[1]);
+                    a[2] = fmaf(wv[u].z, x[k + 4 * u + 2], a[2]);
+                    a[3] = fmaf(wv[u].w, x[k + 4 * u + 3], a[3]);
+                }
+            }
+            for (; k + 16 <= K; k += 16) {
+                float4 wv[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) wv[u] = w4[(k >> 2) + u];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    a[0] = fmaf(wv[u].x, x[k + 4 * u], a[0]);
+                    a[1] = fmaf(wv[u].y, x[k + 4 * u + 1], a[1]);
+                    a[2] = fmaf(wv[u].z, x[k + 4 * u + 2], a[2]);
+                    a[3] = fmaf(wv[u].w, x[k + 4 * u + 3], a[3]);
+                }
+            }
         }
-        for (; k < K; ++k) a[0] = fmaf(w[k], x[k], a[0]);
-        y[j] = (a[0] + a[1]) + (a[2] + a[3]);
+        for (; k + 16 <= K; k += 16) {
+            float wv[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) wv[u] = w[k + u];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) a[u & 3] = fmaf(wv[u], x[k + u], a[u & 3]);
+        }
+        for (; k < K; ++k) a[k & 3] = fmaf(w[k], x[k], a[k & 3]);
+        (first ? y0 : y1)[jr] = (a[0] + a[1]) + (a[2] + a[3]);
     }
 }
 
-// y[k] (+)= sum_j W[j*K + k] d[j]
-__device__ __forceinline__ void matvec_t(const float* __restrict__ W, const float* d, int J, int K, float* y,
-                                         bool accumulate) {
-    for (int k = threadIdx.x; k < K; k += HT) {
-        float a[4] = {accumulate ? y[k] : 0.f, 0.f, 0.f, 0.f};
-        int j = 0;
-        for (; j + UL <= J; j += UL) {
-            float wv[UL];
+__device__ __forceinline__ void matvec(const float* __restrict__ W, const float* __restrict__ b, const float* x,
+                                       int J, int K, float* y) {
+    matvec2(W, b, y, J, W, b, y, 0, x, K);
+}
+
+// rows j0 <= j < j1 of W^T d into a[] (column k), batches of 32 loads in flight
+__device__ __forceinline__ void mt_rows(const float* __restrict__ W, const float* d, int K, int k, int j0, int j1,
+                                        float (&a)[4]) {
+    const float* w = W + (int64_t)j0 * K + k;
+    int j = j0;
+    for (; j + 32 <= j1; j += 32, w += (int64_t)32 * K) {
+        float wv[32];
 #pragma unroll
-            for (int u = 0; u < UL; ++u) wv[u] = W[(int64_t)(j + u) * K + k];
+        for (int u = 0; u < 32; ++u) wv[u] = w[(int64_t)u * K];
 #pragma unroll
-            for (int u = 0; u < UL; ++u) a[u & 3] = fmaf(wv[u], d[j + u], a[u & 3]);
+        for (int u = 0; u < 32; ++u) a[u & 3] = fmaf(wv[u], d[j + u], a[u & 3]);
+    }
+    for (; j + 8 <= j1; j += 8, w += (int64_t)8 * K) {
+        float wv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) wv[u] = w[(int64_t)u * K];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) a[u & 3] = fmaf(wv[u], d[j + u], a[u & 3]);
+    }
+    for (; j < j1; ++j, w += K) a[j & 3] = fmaf(*w, d[j], a[j & 3]);
+}
+
+// y[k] (+)= sum_j W0[j,k] d0[j] + sum_j W1[j,k] d1[j] (thread per column).  With K <= HT/2 the rows
+// are split over P = min(4, HT/K) thread groups whose partial sums meet in `part` (>= HT floats);
+// the call then holds a __syncthreads, so every thread of the workgroup must make it.
+__device__ __forceinline__ void matvec_t2(const float* __restrict__ W0, const float* d0, int J0,
+                                          const float* __restrict__ W1, const float* d1, int J1, int K, float* y,
+                                          bool accumulate, float* part) {
+    const int J = J0 + J1;
+    const int P = K <= HT / 2 ? min(4, HT / K) : 1;
+    if (P == 1) {
+        for (int k = threadIdx.x; k < K; k += HT) {
+            float a[4] = {accumulate ? y[k] : 0.f, 0.f, 0.f, 0.f};
+            mt_rows(W0, d0, K, k, 0, J0, a);
+            mt_rows(W1, d1, K, k, 0, J1, a);
+            y[k] = (a[0] + a[1]) + (a[2] + a[3]);
         }
-        for (; j < J; ++j) a[0] = fmaf(W[(int64_t)j * K + k], d[j], a[0]);
-        y[k] = (a[0] + a[1]) + (a[2] + a[3]);
+        return;
+    }
+    const int Jp = (((J + P - 1) / P) + 7) & ~7;       // rows per group, batch-aligned
+    const int p = threadIdx.x / K, k = threadIdx.x - p * K;
+    if (p < P) {
+        float a[4] = {0.f, 0.f, 0.f, 0.f};
+        const int j0 = p * Jp, j1 = min(J, j0 + Jp);
+        mt_rows(W0, d0, K, k, min(j0, J0), min(j1, J0), a);
+        mt_rows(W1, d1, K, k, max(j0, J0) - J0, max(j1, J0) - J0, a);
+        part[threadIdx.x] = (a[0] + a[1]) + (a[2] + a[3]);
+    }
+    __syncthreads();
+    if (threadIdx.x < K) {
+        float t = accumulate ? y[threadIdx.x] : 0.f;
+        for (int q = 0; q < P; ++q) t += part[q * K + threadIdx.x];
+        y[threadIdx.x] = t;
     }
 }
 
@@ -124,8 +202,7 @@ __global__ __launch_bounds__(HT) void head_fwd_kernel(gpi_head_desc d, const flo
                 v1[k] = fmaxf(v1[k], 0.f);
             }
             __syncthreads();
-            matvec(P + d.mu_w, P + d.mu_b, v1, dz, d.d_feat, v0);              // mu
-            matvec(P + d.ls_w, P + d.ls_b, v1, dz, d.d_feat, v3);              // logsigma
+            matvec2(P + d.mu_w, P + d.mu_b, v0, dz, P + d.ls_w, P + d.ls_b, v3, dz, v1, d.d_feat);   // mu, logsigma
             __syncthreads();
             for (int k = tid; k < dz; k += HT) {
                 ws[d.zmu + (int64_t)s * dz + k] = v0[k];
@@ -173,7 +250,7 @@ __global__ __launch_bounds__(HT) void head_fwd_kernel(gpi_head_desc d, const flo
     __syncthreads();
     if (d.flags & GPI_HEAD_LATENT) {
         float* lat = ws + d.lat + (int64_t)s * d.d_lat;
-        matvec(P + d.lat_w, P + d.lat_b, z, d.d_lat, dz, v1);       // UL weight loads in flight
+        matvec(P + d.lat_w, P + d.lat_b, z, d.d_lat, dz, v1);
         __syncthreads();
         for (int j = tid; j < d.d_lat; j += HT) lat[j] = v1[j];
     }
@@ -181,7 +258,7 @@ __global__ __launch_bounds__(HT) void head_fwd_kernel(gpi_head_desc d, const flo
         const bool lockx = g.flags & GPI_HEAD_LOCKX;             // uniform per workgroup
         float lx = 0.f, ent = 0.f;
         __syncthreads();
-        matvec(P + d.gp_w, P + d.gp_b, z, d.d_x, dz, v3);           // gp(z), UL weight loads in flight
+        matvec(P + d.gp_w, P + d.gp_b, z, d.d_x, dz, v3);           // gp(z)
         __syncthreads();
         for (int t = tid; t < d.d_x; t += HT) {
             const float a = v3[t];
@@ -214,6 +291,7 @@ __global__ __launch_bounds__(HT) void head_fwd_kernel(gpi_head_desc d, const flo
 __global__ __launch_bounds__(HT) void head_bwd_kernel(gpi_head_desc d, const float* __restrict__ P, float* ws,
                                                       double* gacc, int s_off) {
     __shared__ float v0[VMAX], v1[VMAX], v2[VMAX], v3[VMAX];
+    __shared__ float part[HT];
     const int s = blockIdx.x + s_off;
     const int tid = threadIdx.x;
     const bool enc = s < d.n_enc;
@@ -227,7 +305,7 @@ __global__ __launch_bounds__(HT) void head_bwd_kernel(gpi_head_desc d, const flo
         const float* gl = ws + d.glat + (int64_t)s * d.d_lat;
         for (int j = tid; j < d.d_lat; j += HT) v1[j] = gl[j];
         __syncthreads();
-        matvec_t(P + d.lat_w, v1, d.d_lat, dz, dz_, false);
+        matvec_t2(P + d.lat_w, v1, d.d_lat, P, v1, 0, dz, dz_, false, part);
     } else {
         for (int k = tid; k < dz; k += HT) dz_[k] = ws[d.gz + (int64_t)s * dz + k];
     }
@@ -258,7 +336,7 @@ __global__ __launch_bounds__(HT) void head_bwd_kernel(gpi_head_desc d, const flo
             gacc[g.qx_ls + pi] += (double)(dxs * expf(lsq) * ws[d.eps_x + qi] - g.lx_scale);
         }
         __syncthreads();
-        matvec_t(P + d.gp_w, v2, d.d_x, dz, dz_, true);
+        matvec_t2(P + d.gp_w, v2, d.d_x, P, v2, 0, dz, dz_, true, part);
         __syncthreads();
     }
 
@@ -295,9 +373,7 @@ __global__ __launch_bounds__(HT) void head_bwd_kernel(gpi_head_desc d, const flo
     __syncthreads();
     if (!(d.flags & GPI_HEAD_ENC)) return;
     // heads: dh = mu_w^T dmu + ls_w^T dls ; ReLU ; FC
-    matvec_t(P + d.mu_w, v1, dz, d.d_feat, v3, false);
-    __syncthreads();
-    matvec_t(P + d.ls_w, v2, dz, d.d_feat, v3, true);
+    matvec_t2(P + d.mu_w, v1, dz, P + d.ls_w, v2, dz, d.d_feat, v3, false, part);
     __syncthreads();
     for (int k = tid; k < d.d_feat; k += HT) {
         const float hp = ws[d.hpre + (int64_t)s * d.d_feat + k];
@@ -306,7 +382,7 @@ __global__ __launch_bounds__(HT) void head_bwd_kernel(gpi_head_desc d, const flo
         ws[d.dhpre + (int64_t)s * d.d_feat + k] = g;
     }
     __syncthreads();
-    matvec_t(P + d.fc_w, v3, d.d_feat, d.d_feat, v0, false);
+    matvec_t2(P + d.fc_w, v3, d.d_feat, P, v3, 0, d.d_feat, v0, false, part);
     __syncthreads();
     for (int k = tid; k < d.d_feat; k += HT) ws[d.gfeat + (int64_t)s * d.d_feat + k] = v0[k];
 }
