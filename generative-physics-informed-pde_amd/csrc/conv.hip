@@ -60,9 +60,16 @@ __device__ unsigned long long g_rt[4096 * 2];
     do {                                                                                             \
         if (threadIdx.x == 0) g_phase[(blockIdx.x & 4095) * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
+// slot 15 of g_phase: where the workgroup ran (HW_ID: cu [11:8], sh [12], se [15:13]; XCC_ID << 32)
 #define RTSTAMP(i)                                                                                 \
     do {                                                                                           \
-        if (threadIdx.x == 0) g_rt[(blockIdx.x & 4095) * 2 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+        if (threadIdx.x == 0) {                                                                    \
+            g_rt[(blockIdx.x & 4095) * 2 + (i)] = __builtin_amdgcn_s_memrealtime();                \
+            if ((i) == 0)                                                                          \
+                g_phase[(blockIdx.x & 4095) * 16 + 15] =                                           \
+                    (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) |                \
+                    ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32);        \
+        }                                                                                          \
     } while (0)
 #else
 #define PHASE(i) \
@@ -89,6 +96,8 @@ struct ConvGeom {
     int cg;         // forward, tiles of <= 128 pixels: input-channel groups computing partial sums in parallel
                     // (256 / pixels threads per pixel instead of one busy wave), summed through LDS
     int fuse;       // backward: the fused output-conv launch (forward + loss + backward, gpi_conv_loss_fused)
+    int lsum;       // backward (MFMA weight gradient): the four waves' partial slab rows summed in LDS at the
+                    // end into ONE row per tile (accumulators held in registers through the input gradient)
     int split;      // backward: 2 workgroups per tile, input gradient (blockIdx < nblocks) and weight gradient
                     // (the rest) in parallel on otherwise idle CUs (launches well under one round)
     int in_sq, in_sr, in_sc;   // 256 chunks of the input image = (planes, rows, chunks)
@@ -238,6 +247,7 @@ bool conv_geom(const gpi_conv_desc& d, const gpi_groups& g, ConvGeom& G, bool fw
     G.zreg = (!fwd && d.gout_mode == 0 && (int64_t)d.cout * G.gh * (G.PG / 4) <= (int64_t)ZREG * 256) ? 1 : 0;
     G.split = 0;   // decided by launch() from the LDS footprint
     G.fuse = fuse ? 1 : 0;
+    G.lsum = 0;     // decided by launch() / gpi_conv_blocks from the LDS footprint (lsum_op)
 #ifdef GPI_PHASE_TIMING
     static const int dbg = env_int("GPI_DBG_SKIP", 0);
     G.dbg = dbg;
@@ -1404,163 +1414,181 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
     // this wave's partial-slab row: [dW partial over the wave's output rows | dgamma | dbeta partials]
     // (vop: in LDS, summed below into the tile's one slab row)
     float* slab = vop ? mid + 512 + wv * rowlen : c.wpart + d.wpart_off + ((int64_t)tile * SLAB_ROWS + wv) * rowlen;
+    const bool lsum = !vop && G.lsum;   // (lsum_op: never with vwg; at most 2 x 2 accumulator blocks)
+    f32x4 hold[2][2];                   // lsum: this wave's weight-gradient blocks [mb][column block]
     // single-channel 7x7 / stride-2 input conv: weight gradient with the reduction over the tile's
     // output pixels (M = cout, N = the 49 taps in 4 column blocks, K = pixels), no zero-interleaved
     // stride-2 columns (the column-shift form below would compute ~6x the useful products here)
-    const bool vwg = K == 7 && S == 2 && !UP && d.cin == 1 && !has_gin && d.cout <= 16 && do_wgrad;
-    if constexpr (K == 7 && S == 2 && !UP) {
-        if (vwg && !SKIP(G, 1)) {
-            constexpr int PADC = K / 2, NB = (KK + 15) / 16;
-            const int tp = G.th * d.w_out;
-            const int co_a = min(l16, d.cout - 1);                  // A row (rows >= cout never stored)
-            int tap_off[NB];                                        // B column: tap (ky, kx) of this lane
-#pragma unroll
-            for (int nb = 0; nb < NB; ++nb) {
-                const int j = min(16 * nb + l16, KK - 1), ky = j / K, kx = j - ky * K;
-                tap_off[nb] = ky * G.P + kx - PADC;
-            }
-            f32x4 acc[NB];
-#pragma unroll
-            for (int nb = 0; nb < NB; ++nb) acc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
-            const float* gco = gl + co_a * gplane + (T.oy0 - gy0) * G.PG + HALO;
-            for (int ps = wv; 4 * ps < tp; ps += 4) {               // 4 output pixels per step, wave-strided
-                const int px = 4 * ps + kq;
-                const int ty = dq(px, G.d_wout), ox = px - ty * d.w_out;
-                const float a = gco[ty * G.PG + ox];
-                const float* xb = alb + (ty * S) * G.P + HALO + S * ox;
-                float bv[NB];
-#pragma unroll
-                for (int nb = 0; nb < NB; ++nb) bv[nb] = xb[tap_off[nb]];
-#pragma unroll
-                for (int nb = 0; nb < NB; ++nb) acc[nb] = mfma4(a, bv[nb], acc[nb]);
-            }
-            // each wave stores its own tile into its slab row (the slab reduction sums the rows)
-#pragma unroll
-            for (int nb = 0; nb < NB; ++nb) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int co2 = kq * 4 + r, j2 = 16 * nb + l16;
-                    if (co2 < d.cout && j2 < KK) slab[co2 * J + j2] = acc[nb][r];
+    // (vop: before the input gradient, its partial rows go to LDS; otherwise after it: the MFMA
+    // accumulators are then the last live values and, for lsum, go straight to the LDS row sum)
+    auto wgrad_phase = [&]() {
+        const bool vwg = K == 7 && S == 2 && !UP && d.cin == 1 && !has_gin && d.cout <= 16 && do_wgrad;
+        if constexpr (K == 7 && S == 2 && !UP) {
+            if (vwg && !SKIP(G, 1)) {
+                constexpr int PADC = K / 2, NB = (KK + 15) / 16;
+                const int tp = G.th * d.w_out;
+                const int co_a = min(l16, d.cout - 1);                  // A row (rows >= cout never stored)
+                int tap_off[NB];                                        // B column: tap (ky, kx) of this lane
+    #pragma unroll
+                for (int nb = 0; nb < NB; ++nb) {
+                    const int j = min(16 * nb + l16, KK - 1), ky = j / K, kx = j - ky * K;
+                    tap_off[nb] = ky * G.P + kx - PADC;
                 }
-            }
-        }
-    }
-    {
-        const int MI = d.cout * K, NJ = d.cin * K;
-        const int nmb = (SKIP(G, 1) || vwg || !do_wgrad) ? 0 : (MI + 15) >> 4, nnb = (NJ + 15) >> 4;
-        const int XW = UP ? d.w_out + K - 1 : S * (d.w_out - 1) + K;   // virtual input columns
-        const int nxs = (XW + 3) >> 2;
-        for (int mb = 0; mb < nmb; ++mb) {
-            const int i = 16 * mb + l16;
-            const int co = min(i / K, d.cout - 1), kx = i - (i / K) * K;
-            for (int nb0 = 0; nb0 < nnb; nb0 += 2) {
-                const bool two = nb0 + 1 < nnb;
-                int ci[2], ky[2];
-#pragma unroll
-                for (int u = 0; u < 2; ++u) {
-                    const int j = 16 * (nb0 + u) + l16;
-                    ci[u] = min(j / K, d.cin - 1);
-                    ky[u] = j - (j / K) * K;
+                f32x4 acc[NB];
+    #pragma unroll
+                for (int nb = 0; nb < NB; ++nb) acc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+                const float* gco = gl + co_a * gplane + (T.oy0 - gy0) * G.PG + HALO;
+                for (int ps = wv; 4 * ps < tp; ps += 4) {               // 4 output pixels per step, wave-strided
+                    const int px = 4 * ps + kq;
+                    const int ty = dq(px, G.d_wout), ox = px - ty * d.w_out;
+                    const float a = gco[ty * G.PG + ox];
+                    const float* xb = alb + (ty * S) * G.P + HALO + S * ox;
+                    float bv[NB];
+    #pragma unroll
+                    for (int nb = 0; nb < NB; ++nb) bv[nb] = xb[tap_off[nb]];
+    #pragma unroll
+                    for (int nb = 0; nb < NB; ++nb) acc[nb] = mfma4(a, bv[nb], acc[nb]);
                 }
-                // the second column block is a compile-time branch around the whole row loop, so the
-                // accumulators stay in the MFMA registers (a runtime branch inside the loop made the
-                // compiler copy them in and out of AGPRs around every MFMA)
-                f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-                auto rows = [&](auto two_c) {
-                    constexpr bool TWO = decltype(two_c)::value;
-                    for (int ty = wv; ty < G.th; ty += 4) {
-                        const float* grow = gl + (co * G.gh + (T.oy0 + ty - gy0)) * G.PG + HALO - kx;
-                        const float* brow[2];
-#pragma unroll
-                        for (int u = 0; u < 2; ++u) {
-                            const int ry = UP ? fdiv2(T.oy0 + ty - d.pad + ky[u]) - iy0 : ty * S + ky[u];
-                            brow[u] = alb + (ci[u] * G.rh + ry) * G.P + HALO;
-                        }
-                        // operands of four steps are read before their MFMAs (LDS read -> dependent
-                        // MFMA would serialise every step)
-                        if constexpr (UP != 0) {
-                            // nearest x2 upsampling: virtual columns 2p + pad and 2p + pad + 1 both read
-                            // input column p, so their gradient columns are summed first and the
-                            // reduction runs over the (half as many) input columns p
-                            const int plo = fdiv2(-d.pad), nps = (fdiv2(XW - 1 - d.pad) - plo + 4) >> 2;
-                            int ps = 0;
-                            for (; ps + 4 <= nps; ps += 4) {
-                                float a[4], b0[4], b1[4];
-#pragma unroll
-                                for (int u = 0; u < 4; ++u) {
-                                    const int pc = plo + 4 * (ps + u) + kq;
-                                    const int xv = 2 * pc + d.pad;
-                                    a[u] = grow[xv] + grow[xv + 1];
-                                    b0[u] = brow[0][pc];
-                                    if (TWO) b1[u] = brow[1][pc];
-                                }
-#pragma unroll
-                                for (int u = 0; u < 4; ++u) {
-                                    acc0 = mfma4(a[u], b0[u], acc0);
-                                    if (TWO) acc1 = mfma4(a[u], b1[u], acc1);
-                                }
-                            }
-                            for (; ps < nps; ++ps) {
-                                const int pc = plo + 4 * ps + kq;
-                                const int xv = 2 * pc + d.pad;
-                                const float a = grow[xv] + grow[xv + 1];
-                                acc0 = mfma4(a, brow[0][pc], acc0);
-                                if (TWO) acc1 = mfma4(a, brow[1][pc], acc1);
-                            }
-                        } else {
-                            auto a_at = [&](int xv) -> float {
-                                if (S == 2) {
-                                    const int t2 = xv - kx;
-                                    return (t2 & 1) ? 0.f : grow[kx + (t2 >> 1)];
-                                }
-                                return grow[xv];
-                            };
-                            int xs = 0;
-                            for (; xs + 4 <= nxs; xs += 4) {
-                                float a[4], b0[4], b1[4];
-#pragma unroll
-                                for (int u = 0; u < 4; ++u) {
-                                    const int xv = 4 * (xs + u) + kq;
-                                    a[u] = a_at(xv);
-                                    b0[u] = brow[0][xv - d.pad];
-                                    if (TWO) b1[u] = brow[1][xv - d.pad];
-                                }
-#pragma unroll
-                                for (int u = 0; u < 4; ++u) {
-                                    acc0 = mfma4(a[u], b0[u], acc0);
-                                    if (TWO) acc1 = mfma4(a[u], b1[u], acc1);
-                                }
-                            }
-                            for (; xs < nxs; ++xs) {
-                                const int xv = 4 * xs + kq;
-                                const float a = a_at(xv);
-                                acc0 = mfma4(a, brow[0][xv - d.pad], acc0);
-                                if (TWO) acc1 = mfma4(a, brow[1][xv - d.pad], acc1);
-                            }
-                        }
-                    }
-                };
-                if (two) rows(BoolC<true>{});
-                else rows(BoolC<false>{});
-                const f32x4 acc[2] = {acc0, acc1};
-                // each wave stores its partial tile into its own slab row (lane (kq, l16) holds rows
-                // 4 kq + r, column l16 of the 16 x 16 block); the slab reduction sums the rows
-#pragma unroll
-                for (int u = 0; u < 2; ++u) {
-                    if (u == 1 && !two) break;
-                    const int j2 = 16 * (nb0 + u) + l16;
-#pragma unroll
+                // each wave stores its own tile into its slab row (the slab reduction sums the rows)
+    #pragma unroll
+                for (int nb = 0; nb < NB; ++nb) {
+    #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        const int i2 = 16 * mb + 4 * kq + r;
-                        if (i2 < MI && j2 < NJ) {
-                            const int co2 = i2 / K, kx2 = i2 - co2 * K, ci2 = j2 / K, ky2 = j2 - ci2 * K;
-                            slab[co2 * J + ci2 * KK + ky2 * K + kx2] = acc[u][r];
+                        const int co2 = kq * 4 + r, j2 = 16 * nb + l16;
+                        if (co2 < d.cout && j2 < KK) slab[co2 * J + j2] = acc[nb][r];
+                    }
+                }
+            }
+        }
+        {
+            const int MI = d.cout * K, NJ = d.cin * K;
+            const int nmb = (SKIP(G, 1) || vwg || !do_wgrad) ? 0 : (MI + 15) >> 4, nnb = (NJ + 15) >> 4;
+            const int XW = UP ? d.w_out + K - 1 : S * (d.w_out - 1) + K;   // virtual input columns
+            const int nxs = (XW + 3) >> 2;
+            for (int mb = 0; mb < nmb; ++mb) {
+                const int i = 16 * mb + l16;
+                const int co = min(i / K, d.cout - 1), kx = i - (i / K) * K;
+                for (int nb0 = 0; nb0 < nnb; nb0 += 2) {
+                    const bool two = nb0 + 1 < nnb;
+                    int ci[2], ky[2];
+    #pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+                        const int j = 16 * (nb0 + u) + l16;
+                        ci[u] = min(j / K, d.cin - 1);
+                        ky[u] = j - (j / K) * K;
+                    }
+                    // the second column block is a compile-time branch around the whole row loop, so the
+                    // accumulators stay in the MFMA registers (a runtime branch inside the loop made the
+                    // compiler copy them in and out of AGPRs around every MFMA)
+                    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+                    auto rows = [&](auto two_c) {
+                        constexpr bool TWO = decltype(two_c)::value;
+                        for (int ty = wv; ty < G.th; ty += 4) {
+                            const float* grow = gl + (co * G.gh + (T.oy0 + ty - gy0)) * G.PG + HALO - kx;
+                            const float* brow[2];
+    #pragma unroll
+                            for (int u = 0; u < 2; ++u) {
+                                const int ry = UP ? fdiv2(T.oy0 + ty - d.pad + ky[u]) - iy0 : ty * S + ky[u];
+                                brow[u] = alb + (ci[u] * G.rh + ry) * G.P + HALO;
+                            }
+                            // operands of four steps are read before their MFMAs (LDS read -> dependent
+                            // MFMA would serialise every step)
+                            if constexpr (UP != 0) {
+                                // nearest x2 upsampling: virtual columns 2p + pad and 2p + pad + 1 both read
+                                // input column p, so their gradient columns are summed first and the
+                                // reduction runs over the (half as many) input columns p
+                                const int plo = fdiv2(-d.pad), nps = (fdiv2(XW - 1 - d.pad) - plo + 4) >> 2;
+                                int ps = 0;
+                                for (; ps + 4 <= nps; ps += 4) {
+                                    float a[4], b0[4], b1[4];
+    #pragma unroll
+                                    for (int u = 0; u < 4; ++u) {
+                                        const int pc = plo + 4 * (ps + u) + kq;
+                                        const int xv = 2 * pc + d.pad;
+                                        a[u] = grow[xv] + grow[xv + 1];
+                                        b0[u] = brow[0][pc];
+                                        if (TWO) b1[u] = brow[1][pc];
+                                    }
+    #pragma unroll
+                                    for (int u = 0; u < 4; ++u) {
+                                        acc0 = mfma4(a[u], b0[u], acc0);
+                                        if (TWO) acc1 = mfma4(a[u], b1[u], acc1);
+                                    }
+                                }
+                                for (; ps < nps; ++ps) {
+                                    const int pc = plo + 4 * ps + kq;
+                                    const int xv = 2 * pc + d.pad;
+                                    const float a = grow[xv] + grow[xv + 1];
+                                    acc0 = mfma4(a, brow[0][pc], acc0);
+                                    if (TWO) acc1 = mfma4(a, brow[1][pc], acc1);
+                                }
+                            } else {
+                                auto a_at = [&](int xv) -> float {
+                                    if (S == 2) {
+                                        const int t2 = xv - kx;
+                                        return (t2 & 1) ? 0.f : grow[kx + (t2 >> 1)];
+                                    }
+                                    return grow[xv];
+                                };
+                                int xs = 0;
+                                for (; xs + 4 <= nxs; xs += 4) {
+                                    float a[4], b0[4], b1[4];
+    #pragma unroll
+                                    for (int u = 0; u < 4; ++u) {
+                                        const int xv = 4 * (xs + u) + kq;
+                                        a[u] = a_at(xv);
+                                        b0[u] = brow[0][xv - d.pad];
+                                        if (TWO) b1[u] = brow[1][xv - d.pad];
+                                    }
+    #pragma unroll
+                                    for (int u = 0; u < 4; ++u) {
+                                        acc0 = mfma4(a[u], b0[u], acc0);
+                                        if (TWO) acc1 = mfma4(a[u], b1[u], acc1);
+                                    }
+                                }
+                                for (; xs < nxs; ++xs) {
+                                    const int xv = 4 * xs + kq;
+                                    const float a = a_at(xv);
+                                    acc0 = mfma4(a, brow[0][xv - d.pad], acc0);
+                                    if (TWO) acc1 = mfma4(a, brow[1][xv - d.pad], acc1);
+                                }
+                            }
+                        }
+                    };
+                    if (two) rows(BoolC<true>{});
+                    else rows(BoolC<false>{});
+                    const f32x4 acc[2] = {acc0, acc1};
+                    if (lsum) {
+                        // kept for the LDS sum at the end (mb < 2, nb0 == 0: lsum_op)
+                        if (mb == 0) {
+                            hold[0][0] = acc0;
+                            hold[0][1] = acc1;
+                        } else {
+                            hold[1][0] = acc0;
+                            hold[1][1] = acc1;
+                        }
+                        continue;
+                    }
+                    // each wave stores its partial tile into its own slab row (lane (kq, l16) holds rows
+                    // 4 kq + r, column l16 of the 16 x 16 block); the slab reduction sums the rows
+    #pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+                        if (u == 1 && !two) break;
+                        const int j2 = 16 * (nb0 + u) + l16;
+    #pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const int i2 = 16 * mb + 4 * kq + r;
+                            if (i2 < MI && j2 < NJ) {
+                                const int co2 = i2 / K, kx2 = i2 - co2 * K, ci2 = j2 / K, ky2 = j2 - ci2 * K;
+                                slab[co2 * J + ci2 * KK + ky2 * K + kx2] = acc[u][r];
+                            }
                         }
                     }
                 }
             }
         }
-    }
+    };
+    if (vop) wgrad_phase();
     PHASE(5);
 
     // ---- phase 4b: input gradient (MFMA) + BN backward of the input + S_in (+)= gamma * dbn
@@ -1778,7 +1806,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
         if (d.cin <= 2) vdg_rows(IntC<2>{});
         else vdg_rows(IntC<4>{});
     }
-    PHASE(6);
     if (d.in_bn && dg_role) {
         __syncthreads();          // red aliases the offset table the input-gradient loop read
         if (vdg) {
@@ -1804,7 +1831,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
             if (kq == 0) {
                 red[wv * 32 + l16] = sd;
                 red[128 + wv * 32 + l16] = sdx;
-                if (cok) {
+                if (cok && !lsum) {
                     slab[d.cout * J + l16] = sdx;             // dgamma partial of this wave
                     slab[d.cout * J + d.cin + l16] = sd;      // dbeta partial
                 }
@@ -1825,6 +1852,48 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
                 atomicAdd(&st->ssum, gm * s_d);
                 atomicAdd(&st->sxsum, gm * s_dx);
             }
+        }
+    }
+    if (!vop) wgrad_phase();
+    PHASE(6);
+    if (lsum) {
+        // the four waves' partial rows into LDS (the whole region after the header is dead by now; the
+        // barrier also orders the channel-sum scratch reads above), summed in a fixed order into the
+        // tile's one slab row.  Split launches: each role sums and stores its own columns.
+        __syncthreads();
+        const int MI = d.cout * K, NJ = d.cin * K;
+        const int nmb = (SKIP(G, 1) || !do_wgrad) ? 0 : (MI + 15) >> 4;
+        const bool two = NJ > 16;
+        float* lrow = wD + wv * rowlen;
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb) {
+            if (mb >= nmb) break;
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                if (u == 1 && !two) break;
+                const f32x4 a = hold[mb][u];
+                const int j2 = 16 * u + l16;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int i2 = 16 * mb + 4 * kq + r;
+                    if (i2 < MI && j2 < NJ) {
+                        const int co2 = i2 / K, kx2 = i2 - co2 * K, ci2 = j2 / K, ky2 = j2 - ci2 * K;
+                        lrow[co2 * J + ci2 * KK + ky2 * K + kx2] = a[r];
+                    }
+                }
+            }
+        }
+        if (d.in_bn && dg_role && kq == 0 && cok) {
+            lrow[d.cout * J + l16] = sdx;             // dgamma partial of this wave
+            lrow[d.cout * J + d.cin + l16] = sd;      // dbeta partial
+        }
+        __syncthreads();
+        const int c0 = (G.split && !do_wgrad) ? d.cout * J : 0;
+        const int c1 = (G.split && !dg_role) ? d.cout * J : rowlen;
+        float* srow = c.wpart + d.wpart_off + (int64_t)tile * rowlen;
+        for (int e = c0 + tid; e < c1; e += 256) {
+            const float* r = wD + e;
+            srow[e] = (r[0] + r[rowlen]) + (r[2 * rowlen] + r[3 * rowlen]);
         }
     }
     if (vop) {
@@ -1858,6 +1927,20 @@ size_t bwd_lds_floats(const gpi_conv_desc& d, int rh, int P, int gh, int PG, int
 
 size_t bwd_lds(const gpi_conv_desc& d, const ConvGeom& G) {
     return sizeof(float) * bwd_lds_floats(d, G.rh, G.P, G.gh, G.PG, G.zreg, G.fuse != 0);
+}
+
+// One slab row per tile for the MFMA backward (G.lsum): the weight-gradient accumulators fit the
+// kernel's 2 x 2 register blocks (cout K, cin K <= 32), not the single-channel stride-2 input conv's
+// own form, and the four partial rows fit the LDS after the header.  Off by default (GPI_LSUM=1 turns
+// it on): a quarter of the slab bytes, but the two extra barriers and the LDS pass cost more than the
+// stores and the smaller reductions save -- 0.6315 vs 0.6258 ms/step (r03, 3 x 600 replays per arm).
+bool lsum_op(const gpi_conv_desc& d, const ConvGeom& G) {
+    static const int on = env_int("GPI_LSUM", 0);
+    if (!on || vop_op(d) || G.fuse) return false;
+    if (d.k == 7 && d.stride == 2 && !d.upsample && d.cin == 1 && d.gin_off < 0 && d.cout <= 16) return false;
+    if (d.cout * d.k > 32 || d.cin * d.k > 32) return false;
+    const size_t avail = bwd_lds_floats(d, G.rh, G.P, G.gh, G.PG, G.zreg, false) - bwd_hdr(d.cin, d.cout);
+    return avail >= (size_t)4 * bwd_rowlen(d);
 }
 
 typedef void (*conv_kernel_t)(gpi_conv_desc, gpi_codec_ctx, ConvGeom);
@@ -1940,6 +2023,7 @@ int launch(const gpi_conv_desc& d, const gpi_codec_ctx& c, hipStream_t st, bool 
         zero = (const float*)p;
     }
     G.zero = zero;
+    if (!fwd) G.lsum = lsum_op(d, G) ? 1 : 0;
     const size_t lds = fwd ? fwd_lds(d, G, cp) : bwd_lds(d, G);
     if (lds > 160 * 1024) return GPI_ERR_UNSUPPORTED;
     if (!fwd && d.gin_off >= 0 && !fuse && !vop_op(d)) {
@@ -2080,7 +2164,8 @@ extern "C" int gpi_conv_blocks(const gpi_conv_desc* op, const gpi_groups* groups
     if (!op || !groups || !blocks) return GPI_ERR_ARG;
     ConvGeom G;
     if (!conv_geom(*op, *groups, G, false)) return GPI_ERR_UNSUPPORTED;   // backward tiling
-    *blocks = G.nblocks * (vop_op(*op) ? 1 : SLAB_ROWS);    // one slab row per wave (vop ops: per workgroup)
+    // one slab row per wave, or per workgroup (vop ops; lsum: the rows summed in LDS)
+    *blocks = G.nblocks * ((vop_op(*op) || lsum_op(*op, G)) ? 1 : SLAB_ROWS);
     return GPI_OK;
 }
 

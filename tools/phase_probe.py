@@ -4,9 +4,12 @@ usage: GPI_PHASE_TIMING=1 python tools/phase_probe.py [OP_SUBSTRING ...] [--fwd]
 Runs every matching operator of the C64 ELBO step once more after a warm step,
 reads the s_memtime stamps each workgroup wrote at its phase boundaries and
 prints mean cycles per phase, the mean workgroup lifetime, the kernel span on
-the 100 MHz real-time clock and the mean number of workgroups in flight.
+the 100 MHz real-time clock and the mean number of workgroups in flight, the entry / exit
+time distribution and, from the HW_ID / XCC_ID each workgroup records, the exit times by
+workgroups per CU and by XCD.
 Phases (backward): 0 entry | 1 bases | 2 loads landed + stats | 3 coefficients |
-4 activations | 5 weight gradient | 6 input gradient | 7 sums/atomics; inside phase 1:
+4 activations | 5 input gradient | 6 BN-backward sums + weight gradient | 7 slab row sums
+(vop ops, weight gradient first: 5 weight gradient | 6 input gradient); inside phase 1:
 12 weights issued | 13 gradient image issued | 14 BN operand image issued | 8 input image issued |
 9 epilogue operands issued | 10 stat loads issued | 11 stats summed.
 """
@@ -67,6 +70,35 @@ def main():
             print('%-44s %s blocks %5d  life %6.2f us  span %6.2f us  in-flight %5.1f' %
                   (op.name, 'fwd' if fwd else 'bwd', nb, life.mean(), span, inflight))
             print('    cycles/phase: ' + '  '.join('%d:%6.0f' % (k + 1, d[:, k].mean()) for k in used))
+            if os.environ.get('GPI_PROBE_RAW'):
+                base = p[:, 5]
+                print('    raw (cycles after stamp 5): ' + '  '.join('%d:%6.0f' % (k, (p[:, k] - base).mean())
+                                                                    for k in (12, 13, 14, 8, 9, 6, 7)))
+            t0 = r[:, 0].min()
+            ent = np.sort((r[:, 0] - t0) * 10.0 / 1e3)
+            ext = np.sort((r[:, 1] - t0) * 10.0 / 1e3)
+            q = lambda a, f: a[min(len(a) - 1, int(f * len(a)))]
+            print('    entry us p10/p50/p90/max %5.2f %5.2f %5.2f %5.2f   exit p10/p50/p90/max %5.2f %5.2f %5.2f %5.2f' %
+                  (q(ent, .1), q(ent, .5), q(ent, .9), ent[-1], q(ext, .1), q(ext, .5), q(ext, .9), ext[-1]))
+            hw = ph[:nb, 15].astype(np.uint64)
+            if (hw != 0).any():
+                hid = (hw & np.uint64(0xffffffff)).astype(np.int64)
+                xcc = ((hw >> np.uint64(32)) & np.uint64(0xf)).astype(np.int64)
+                cu = (hid >> 8) & 15
+                sh = (hid >> 12) & 1
+                se = (hid >> 13) & 7
+                key = ((xcc * 8 + se) * 2 + sh) * 16 + cu
+                ex = (r[:, 1] - t0) * 10.0 / 1e3
+                lf = (r[:, 1] - r[:, 0]) * 10.0 / 1e3
+                ukey, inv, cnt = np.unique(key, return_inverse=True, return_counts=True)
+                per = cnt[inv]            # workgroups that ran on this workgroup's CU
+                print('    CUs used %d; workgroups per CU: %s' %
+                      (len(ukey), ' '.join('%d:%d' % (k, (cnt == k).sum()) for k in np.unique(cnt))))
+                for k in np.unique(per):
+                    m = per == k
+                    print('      on CUs with %d wg: n %4d  life mean %5.2f  exit mean %5.2f max %5.2f' %
+                          (k, m.sum(), lf[m].mean(), ex[m].mean(), ex[m].max()))
+                print('    exit mean by XCC: ' + ' '.join('%d:%5.2f' % (x, ex[xcc == x].mean()) for x in np.unique(xcc)))
             sub = [1, 12, 13, 14, 8, 9, 10, 11, 2]     # phase-1 issue points (timing build, backward)
             if all((p[:, k] != 0).all() for k in sub):
                 print('    phase-1 split: ' + '  '.join('%d->%d:%6.0f' % (sub[k], sub[k + 1],
