@@ -496,8 +496,35 @@ class ElboEngine(object):
         False when the previous step's epilogue already cleared the accumulator / the statistics
         and term scratch (gpi_step_epilogue).  running: BN running-statistics update 'now' (end of
         the forward), 'defer' (on the side stream during backward) or None."""
-        lib = _lib()
         st = stream if stream is not None else L.stream_handle()
+        self.forward_a(st, zero_gacc, zero_scratch)
+        if self.roms:
+            # the ROM solve only feeds the head backward: run it on a side stream,
+            # concurrently with the decoder (fork here, join in backward / value).  The decoder
+            # is enqueued first so that, in a captured graph, the main chain is the fork's first
+            # branch and keeps its hardware queue (each cross-queue dependency costs ~10 us).
+            main = torch.cuda.current_stream()
+            self._side_stream()
+            self._ev_fork.record(main)
+            if self.rom_first:
+                self._launch_roms()
+        self.forward_b(st)
+        if self.roms and not self.rom_first:
+            self._launch_roms()
+        if running == 'now':
+            self.running.launch(st)
+        self._running_pending = running == 'defer'
+        if compute_value:
+            self._join()
+            return self.elbo_value()
+        return None
+
+    # The step's pieces, per stream, between its cross-stream dependencies (forward / backward
+    # compose them with events; FusedElboStep's segment capture records each as its own
+    # single-stream graph).
+    def forward_a(self, st, zero_gacc=True, zero_scratch=True):
+        """Main stream, up to the ROM fork: scratch / accumulator reset, encoder forward, head forward."""
+        lib = _lib()
         if zero_scratch:
             self.ws.zero_scratch()
         if zero_gacc:
@@ -511,29 +538,80 @@ class ElboEngine(object):
             self.ws.view(self.hb['zls'], self.B_u, self.dz).copy_(self.q_unsup._logsigma.detach())
         _run(lib.gpi_head_forward, C.byref(self.head), C.c_void_p(self.flat.P.data_ptr()),
              C.c_void_p(self.ws.t_ws.data_ptr()), st, what='head forward')
-        if self.roms:
-            # the ROM solve only feeds the head backward: run it on a side stream,
-            # concurrently with the decoder (fork here, join in backward / value).  The decoder
-            # is enqueued first so that, in a captured graph, the main chain is the fork's first
-            # branch and keeps its hardware queue (each cross-queue dependency costs ~10 us).
-            main = torch.cuda.current_stream()
-            self._side_stream()
-            self._ev_fork.record(main)
-            if self.rom_first:
-                self._launch_roms()
+
+    def forward_b(self, st):
+        """Main stream: decoder forward and its fused output conv (forward + loss + backward)."""
+        lib = _lib()
         self._codec_forward(self.dec_descs, 0, self.n_dec_sep, self.dctx, st, 'decoder forward')
         if self.n_dec_sep < len(self.dec_descs):
             _run(lib.gpi_conv_loss_fused, C.byref(self.dec_descs[self.n_dec_sep]), C.byref(self.dctx), st,
                  what='decoder output conv (forward + loss + backward)')
-        if self.roms and not self.rom_first:
-            self._launch_roms()
-        if running == 'now':
-            self.running.launch(st)
-        self._running_pending = running == 'defer'
-        if compute_value:
-            self._join()
-            return self.elbo_value()
-        return None
+
+    def rom_side(self, sst):
+        """Side stream: the ROM solves (after the head forward)."""
+        if self.side_pre is not None:
+            self.side_pre(sst)
+        for r in self.roms:
+            _run(_lib().gpi_rom, C.byref(r), sst, what='rom')
+
+    def backward_a(self, st, split):
+        """Main stream: decoder backward and the head backward (encoder samples only when split:
+        the variational samples' need the ROM adjoint and follow it on the side stream)."""
+        lib = _lib()
+        self._codec_backward(self.dec_descs, 0, self.n_dec_sep, self.dctx, st, 'decoder backward')
+        P_, W_, G_ = (C.c_void_p(self.flat.P.data_ptr()), C.c_void_p(self.ws.t_ws.data_ptr()),
+                      C.c_void_p(self.flat.gacc.data_ptr()))
+        if split:
+            hd = L.HeadDesc.from_buffer_copy(self.head)
+            hd.flags |= L.HEAD_PART_ENC
+            _run(lib.gpi_head_backward, C.byref(hd), P_, W_, G_, st, what='head backward (encoder samples)')
+        else:
+            _run(lib.gpi_head_backward, C.byref(self.head), P_, W_, G_, st, what='head backward')
+        if not self.armortized and self.B_u > 0:
+            # d/dmu, d/dlogsigma of q_z['unsupervised'] (written by the head for its first segment)
+            n = self.B_u * self.dz
+            for src, q in (('dzmu', self.q_unsup._mean), ('dzls', self.q_unsup._logsigma)):
+                o = self.flat.offset(q)
+                self.flat.gacc[o:o + n].add_(self.ws.view(self.hb[src], n).double())
+
+    def backward_b(self, st):
+        """Main stream: every encoder conv's backward but the input conv's (reverse order)."""
+        if self.ep is not None and len(self.enc_descs) > 1:
+            self._codec_backward(self.enc_descs, 1, len(self.enc_descs), self.ectx, st, 'encoder backward')
+
+    def backward_c(self, st, enc_split):
+        """Main stream: the input conv's backward (weight gradient only) and the encoder slab
+        reduction (its own slabs only when enc_split: the side stream reduces the rest)."""
+        if self.ep is None:
+            return
+        if self.bn_sync is not None and self.enc_descs[0].gout_mode == 0:
+            self._sync_stats(self.enc_descs[0].out_stat, self.enc_descs[0].cout, 2)
+        _run(_lib().gpi_conv_backward, C.byref(self.enc_descs[0]), C.byref(self.ectx), st, what='In_conv backward')
+        run_reduce(self.reduce_enc[:self.n_reduce_in] if enc_split else self.reduce_enc, self.ws, self.flat, st)
+
+    def backward_side_a(self, sst, split, side_extra=None):
+        """Side stream, after the decoder backward: the variational samples' head backward (split),
+        the decoder slab reduction, the deferred BN running statistics, the dense weight GEMM and
+        side_extra."""
+        lib = _lib()
+        if split:
+            hq = L.HeadDesc.from_buffer_copy(self.head)
+            hq.flags |= L.HEAD_PART_Q
+            _run(lib.gpi_head_backward, C.byref(hq), C.c_void_p(self.flat.P.data_ptr()),
+                 C.c_void_p(self.ws.t_ws.data_ptr()), C.c_void_p(self.flat.gacc.data_ptr()), sst,
+                 what='head backward (variational samples)')
+        run_reduce(self.reduce_dec, self.ws, self.flat, sst)
+        if self._running_pending:
+            self.running.launch(sst)
+            self._running_pending = False
+        _run(lib.gpi_outer_gemm, self.gemm_items, len(self.gemm_items), C.c_void_p(self.ws.t_ws.data_ptr()),
+             C.c_void_p(self.flat.gacc.data_ptr()), sst, what='outer gemm')
+        if side_extra is not None:
+            side_extra(sst)
+
+    def backward_side_b(self, sst):
+        """Side stream, after backward_b: the encoder slab reduction but the input conv's."""
+        run_reduce(self.reduce_enc[self.n_reduce_in:], self.ws, self.flat, sst)
 
     # ------------------------------------------------------------------ SyncBN (optional)
     def set_sync_bn(self, allreduce, world):
@@ -590,10 +668,7 @@ class ElboEngine(object):
 
     def _launch_roms(self):
         self._side.wait_event(self._ev_fork)
-        if self.side_pre is not None:
-            self.side_pre(C.c_void_p(self._side.cuda_stream))
-        for r in self.roms:
-            _run(_lib().gpi_rom, C.byref(r), C.c_void_p(self._side.cuda_stream), what='rom')
+        self.rom_side(C.c_void_p(self._side.cuda_stream))
         self._ev_join.record(self._side)
         self._pending_join = True
 
@@ -666,64 +741,34 @@ class ElboEngine(object):
         the side stream after the decoder's reductions, concurrently with the encoder backward (the
         fused step draws the next step's subset, noise and decoder dropout masks there; nothing it
         writes may be read by the encoder backward)."""
-        lib = _lib()
         st = stream if stream is not None else L.stream_handle()
-        self._codec_backward(self.dec_descs, 0, self.n_dec_sep, self.dctx, st, 'decoder backward')
-        P_, W_, G_ = (C.c_void_p(self.flat.P.data_ptr()), C.c_void_p(self.ws.t_ws.data_ptr()),
-                      C.c_void_p(self.flat.gacc.data_ptr()))
         main = torch.cuda.current_stream()
         side = self._side_stream()
         # With the ROM still pending on the side stream, only the encoder samples' head backward
         # runs on the main stream; the variational samples' (which need the ROM adjoint) follow
         # the ROM on the side stream, so the main chain never waits for the ROM.
         split = self._pending_join
-        if split:
-            hd = L.HeadDesc.from_buffer_copy(self.head)
-            hd.flags |= L.HEAD_PART_ENC
-            _run(lib.gpi_head_backward, C.byref(hd), P_, W_, G_, st, what='head backward (encoder samples)')
-        else:
-            _run(lib.gpi_head_backward, C.byref(self.head), P_, W_, G_, st, what='head backward')
-        if not self.armortized and self.B_u > 0:
-            # d/dmu, d/dlogsigma of q_z['unsupervised'] (written by the head for its first segment)
-            n = self.B_u * self.dz
-            for src, q in (('dzmu', self.q_unsup._mean), ('dzls', self.q_unsup._logsigma)):
-                o = self.flat.offset(q)
-                self.flat.gacc[o:o + n].add_(self.ws.view(self.hb[src], n).double())
+        self.backward_a(st, split)
         # the decoder's slab reduction and the dense weight gradients depend only on what is
         # done by now: run them on the side stream, concurrently with the encoder backward
         # (enqueued after it, so the encoder stays on the main chain's queue in a graph)
         self._ev_fork2.record(main)
         n_enc = len(self.enc_descs) if self.ep is not None else 0
+        enc_split = n_enc and self.enc_reduce == 'split'
         if n_enc:
-            # every encoder conv but the first (reverse order) ...
-            self._codec_backward(self.enc_descs, 1, n_enc, self.ectx, st, 'encoder backward')
-            enc_split = self.enc_reduce == 'split'
+            self.backward_b(st)
             if enc_split:
                 self._ev_enc.record(main)
-            # ... then the input conv (weight gradient only), whose slab reduction stays on the main
-            # stream while the side stream reduces the other encoder slabs concurrently
-            if self.bn_sync is not None and self.enc_descs[0].gout_mode == 0:
-                self._sync_stats(self.enc_descs[0].out_stat, self.enc_descs[0].cout, 2)
-            _run(lib.gpi_conv_backward, C.byref(self.enc_descs[0]), C.byref(self.ectx), st, what='In_conv backward')
-            run_reduce(self.reduce_enc[:self.n_reduce_in] if enc_split else self.reduce_enc, self.ws, self.flat, st)
+            self.backward_c(st, enc_split)
+        # (captured ahead of the encoder backward instead, the side branch took the launch stream
+        # and the main chain the pooled one: 0.7526 vs 0.6289 ms per step, r03)
         side.wait_event(self._ev_fork2)
-        sst = C.c_void_p(side.cuda_stream)
+        self.backward_side_a(C.c_void_p(side.cuda_stream), split, side_extra)
         if split:
-            hq = L.HeadDesc.from_buffer_copy(self.head)
-            hq.flags |= L.HEAD_PART_Q
-            _run(lib.gpi_head_backward, C.byref(hq), P_, W_, G_, sst, what='head backward (variational samples)')
             self._pending_join = False          # joined below with the rest of the side work
-        run_reduce(self.reduce_dec, self.ws, self.flat, sst)
-        if self._running_pending:
-            self.running.launch(sst)
-            self._running_pending = False
-        _run(lib.gpi_outer_gemm, self.gemm_items, len(self.gemm_items), C.c_void_p(self.ws.t_ws.data_ptr()),
-             C.c_void_p(self.flat.gacc.data_ptr()), sst, what='outer gemm')
-        if side_extra is not None:
-            side_extra(sst)
-        if n_enc and self.enc_reduce == 'split':
+        if enc_split:
             side.wait_event(self._ev_enc)
-            run_reduce(self.reduce_enc[self.n_reduce_in:], self.ws, self.flat, sst)
+            self.backward_side_b(C.c_void_p(side.cuda_stream))
         self._ev_join2.record(side)
         main.wait_event(self._ev_join2)
 

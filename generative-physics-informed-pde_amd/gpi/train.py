@@ -10,6 +10,7 @@ communicated.  Every launch is stream-ordered with no host synchronisation,
 so the whole step can be captured once into a HIP graph and replayed.
 """
 import ctypes as C
+import os
 
 import torch
 import torch.distributed as dist
@@ -94,6 +95,11 @@ class FusedElboStep(object):
         self.idx_next = torch.zeros_like(self.idx)
         # A/B switch (tools/critpath_probe.py): draw the next step's subset on the side stream ahead of the ROM
         self.subset_early = False
+        # captured form: 'single' (one graph spanning both streams) or 'segments' (single-stream
+        # graphs joined by events, _capture_segments: the host launches them ~4x faster, but each
+        # graph boundary leaves the GPU idle ~15 us: 0.673 vs 0.629 ms per step, r03);
+        # GPI_GRAPH_MODE overrides (A/B runs)
+        self.graph_mode = os.environ.get('GPI_GRAPH_MODE', 'single')
         my_idx = self.idx[self.rank * self.B_u:(self.rank + 1) * self.B_u] if self.B_u else None
         self.engine.bind(X_u=self.X_pool, u_index=my_idx, X_s=X_s, Y=Y, F=F)
         n_pool = self.X_pool.shape[0] if self.X_pool is not None else 0
@@ -225,9 +231,12 @@ class FusedElboStep(object):
         torch.cuda.synchronize()
         self.g_fb = torch.cuda.CUDAGraph()
         self.g_up = None
+        self.segs = None
         self.split_graph = self.distributed and not (self.graph_allreduce and
                                                       dist.get_backend(self.pg) == dist.Backend.NCCL)
-        if self.split_graph:
+        if not self.split_graph and self.graph_mode == 'segments':
+            self._capture_segments()
+        elif self.split_graph:
             with torch.cuda.graph(self.g_fb):
                 self.forward_backward()
             self.g_up = torch.cuda.CUDAGraph()
@@ -240,10 +249,89 @@ class FusedElboStep(object):
                 self.update()
         self.graph = True
 
+    def _capture_segments(self):
+        """The step as single-stream graphs, one per stretch of a stream between two cross-stream
+        dependencies, replayed with events between them (_replay_segments).  A HIP graph whose
+        nodes span two streams costs the host ~4-8 us per node to launch (tools/graph_launch_probe.py:
+        64 nodes 211-245 us on two streams vs 50-58 us on one); with the step's ~70 nodes in one
+        two-stream graph the host walk (~0.59 ms) paced the GPU and the side stream's kernels were
+        submitted late, so the step waited at the join for them."""
+        e = self.engine
+        side = e._side_stream()
+        rom = bool(e.roms)
+        early = self.subset_early and rom
+        e.side_pre = (lambda sst: self._launch_subset(sst, self.idx_next)) if early else None
+        n_enc = len(e.enc_descs) if e.ep is not None else 0
+        enc_split = bool(n_enc) and e.enc_reduce == 'split'
+
+        def cap(fn):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                fn(L.stream_handle())
+            return g
+
+        def m2(st):
+            e.forward_b(st)
+            e._running_pending = True            # running statistics deferred to the side stream
+            e.backward_a(st, rom)
+
+        def m5(st):
+            L.check(L.lib().gpi_step_epilogue(C.byref(self.epi), st), 'step epilogue')
+            self.allreduce()                     # RCCL: captured as a graph node
+            self.update(st)
+
+        noise = (lambda sst: self._launch_noise(sst, self.idx_next, codecs=('dec',), subset=not early))
+        segs = {'m1': cap(lambda st: e.forward_a(st, zero_gacc=False, zero_scratch=False))}
+        if rom:
+            segs['s1'] = cap(e.rom_side)
+        segs['m2'] = cap(m2)
+        segs['s2'] = cap(lambda st: e.backward_side_a(st, rom, noise))
+        if n_enc:
+            segs['m3'] = cap(e.backward_b)
+        if enc_split:
+            segs['s3'] = cap(e.backward_side_b)
+        if n_enc:
+            segs['m4'] = cap(lambda st: e.backward_c(st, enc_split))
+        segs['m5'] = cap(m5)
+        self.segs = segs
+        self._seg_ev = [torch.cuda.Event() for _ in range(4)]
+        self._seg_side = side
+
+    def _replay_segments(self):
+        g, ev, side = self.segs, self._seg_ev, self._seg_side
+        main = torch.cuda.current_stream()
+        g['m1'].replay()
+        if 's1' in g:
+            ev[0].record(main)
+            with torch.cuda.stream(side):
+                side.wait_event(ev[0])
+                g['s1'].replay()
+        g['m2'].replay()
+        ev[1].record(main)
+        with torch.cuda.stream(side):
+            side.wait_event(ev[1])
+            g['s2'].replay()
+        if 'm3' in g:
+            g['m3'].replay()
+        if 's3' in g:
+            ev[2].record(main)
+            with torch.cuda.stream(side):
+                side.wait_event(ev[2])
+                g['s3'].replay()
+        ev[3].record(side)
+        if 'm4' in g:
+            g['m4'].replay()
+        main.wait_event(ev[3])
+        g['m5'].replay()
+
     def step(self):
         self.sync_lr()
         if self.graph is None:
             return self.step_eager()
+        if self.segs is not None:
+            self._replay_segments()
+            self._mark_optimizer_step()
+            return
         self.g_fb.replay()
         if self.split_graph:
             self.allreduce()

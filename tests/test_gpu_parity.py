@@ -445,10 +445,12 @@ def test_fused_step_matches_module_path(device, independent_X):
     assert step.step_ctr.item() == 2
 
 
-def test_capture_leaves_training_state_untouched(device):
+@pytest.mark.parametrize('mode', ['single', 'segments'])
+def test_capture_leaves_training_state_untouched(device, mode):
     """FusedElboStep.capture() warms up on snapshots: parameters, Adam moments, step counter, Philox
     offset and the pre-drawn subset / noise are bit-identical afterwards, and the first replayed step
-    is the step an eager loop takes (same ELBO, same parameters after the update)."""
+    is the step an eager loop takes (same ELBO, same parameters after the update) -- in both captured
+    forms (one two-stream graph; single-stream segment graphs joined by events)."""
     import copy
     from gpi.train import FusedElboStep
     d = load('elbo_c32.npz')
@@ -457,6 +459,7 @@ def test_capture_leaves_training_state_untouched(device):
     Xu, Xs, Y, F = cuda(d['Xu']), cuda(d['Xs']), cuda(d['Y']), cuda(d['F'])
     eager = FusedElboStep(model_a, Xu, bs, Xs, Y, F, lr=1e-3, seed=3)
     graph = FusedElboStep(model_b, Xu, bs, Xs, Y, F, lr=1e-3, seed=3)
+    graph.graph_mode = mode
     before = [t.clone() for t in graph._mutable_state()]
     graph.capture()
     torch.cuda.synchronize()
@@ -469,6 +472,7 @@ def test_capture_leaves_training_state_untouched(device):
         assert abs(eager.elbo().item() - graph.elbo().item()) <= 1e-6 * abs(eager.elbo().item())
         torch.testing.assert_close(graph.flat.P, eager.flat.P, rtol=1e-6, atol=1e-7)
     assert graph.step_ctr.item() == eager.step_ctr.item() == 3
+    assert (graph.segs is not None) == (mode == 'segments')
 
 
 def test_lr_schedule_drives_fused_step(device):

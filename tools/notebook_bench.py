@@ -73,6 +73,39 @@ def main():
         iteration()
     torch.cuda.synchronize()
     t_it = (time.perf_counter() - t0) / iters
+    parts = {}
+    for name, fn in (('step', step.step), ('pe3', g_pe.replay)):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            fn()
+        torch.cuda.synchronize()
+        parts[name] = (time.perf_counter() - t0) / iters
+        # host enqueue alone: replays queued back to back, timed before the synchronize
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(50):
+            fn()
+        parts[name + '_host'] = (time.perf_counter() - t0) / 50
+        torch.cuda.synchronize()
+
+    # the ELBO step and the three PE iterations captured as ONE graph (one replay per iteration)
+    g_all = torch.cuda.CUDAGraph()
+    torch.cuda.synchronize()
+    with torch.cuda.graph(g_all):
+        step.forward_backward()
+        step.update()
+        for _ in range(N_PE):
+            pe.update()
+    for _ in range(20):
+        g_all.replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        step.sync_lr()
+        g_all.replay()
+    torch.cuda.synchronize()
+    parts['one_graph'] = (time.perf_counter() - t0) / iters
 
     # monitoring: Analysis.eval_all_y on the PE's q_z (components.py:494-524), every 1000 iterations
     def monitor():
@@ -92,7 +125,11 @@ def main():
            'published_source': 'example.ipynb:112 (unnamed CUDA GPU, PyTorch 1.1)',
            'vs_published': round(1.0 / t_total / PUBLISHED_IT_S, 2),
            'ms_per_iteration': round(t_total * 1e3, 4), 'ms_step_plus_pe': round(t_it * 1e3, 4),
-           'ms_monitoring_eval': round(t_mon * 1e3, 3), 'iterations': iters, 'n_gpus': 1, 'dtype': 'f32',
+           'ms_monitoring_eval': round(t_mon * 1e3, 3),
+           'ms_step_alone': round(parts['step'] * 1e3, 4), 'ms_pe3_alone': round(parts['pe3'] * 1e3, 4),
+           'ms_step_host_enqueue': round(parts['step_host'] * 1e3, 4),
+           'ms_one_graph_iteration': round(parts['one_graph'] * 1e3, 4),
+           'ms_pe3_host_enqueue': round(parts['pe3_host'] * 1e3, 4), 'iterations': iters, 'n_gpus': 1, 'dtype': 'f32',
            'data': 'synthetic', 'elbo_samples_per_s': round((B_u + N_s) / t_total, 1),
            'excluded': 'tensorboard writes, host-side monitoring prints'}
     print(json.dumps(res))
