@@ -100,6 +100,11 @@ struct ConvGeom {
                     // end into ONE row per tile (accumulators held in registers through the input gradient)
     int split;      // backward: 2 workgroups per tile, input gradient (blockIdx < nblocks) and weight gradient
                     // (the rest) in parallel on otherwise idle CUs (launches well under one round)
+    int xcd;        // XCD-aware block order: the blocks the dispatcher deals to one XCD (b, b + 8, ...) take
+                    // consecutive tiles (adjacent rows of one sample; with split, the two roles of a tile next
+                    // to each other), so the halo rows two tiles share are read from HBM once into that
+                    // XCD's L2 instead of once per XCD.  0: tile = blockIdx.x (xcd_mode)
+    int grid;       // launched workgroups (xcd remap)
     int in_sq, in_sr, in_sc;   // 256 chunks of the input image = (planes, rows, chunks)
     int g_sq, g_sr, g_sc;      // ... of the output-gradient image
     Div d_in4, d_P4, d_g4, d_PG4, d_cin, d_cout, d_win, d_tp, d_wout, d_w2;
@@ -248,6 +253,8 @@ bool conv_geom(const gpi_conv_desc& d, const gpi_groups& g, ConvGeom& G, bool fw
     G.split = 0;   // decided by launch() from the LDS footprint
     G.fuse = fuse ? 1 : 0;
     G.lsum = 0;     // decided by launch() / gpi_conv_blocks from the LDS footprint (lsum_op)
+    G.xcd = 0;      // set by launch() (xcd_mode)
+    G.grid = 0;     // set by launch()
 #ifdef GPI_PHASE_TIMING
     static const int dbg = env_int("GPI_DBG_SKIP", 0);
     G.dbg = dbg;
@@ -395,9 +402,11 @@ __device__ __forceinline__ gpi_stat* stat_slot(const gpi_codec_ctx& c, int64_t s
     return c.stats + ((int64_t)r * GPI_MAX_GROUPS + grp) * c.n_stats + stat;
 }
 
+// BN coefficients: every rounding spelled out (explicit FMAs, no compiler contraction choice), so a
+// host can reproduce the kernels' ReLU decisions bit for bit (tests/gpu_masks.py)
 __device__ __forceinline__ void mean_invstd(const double* s4, double n, float eps, float& mean, float& invstd) {
     const double m = s4[0] / n;
-    double var = s4[1] / n - m * m;
+    double var = fma(-m, m, s4[1] / n);
     if (var < 0.0) var = 0.0;
     mean = (float)m;
     invstd = (float)(1.0 / sqrt(var + (double)eps));
@@ -470,8 +479,18 @@ struct TileIdx {
     int b, oy0, grp, gsz;
 };
 
+// logical block of this workgroup: identity, or (G.xcd) the blocks of dispatcher XCD slot x = b % 8
+// numbered consecutively -- XCD x holds logical blocks [x q + min(x, r), ...) for grid = 8 q + r.
+// A bijection on [0, grid) for any grid; placement affects speed only, never the result.
+__device__ __forceinline__ int logical_block(const ConvGeom& G) {
+    const int b = blockIdx.x;
+    if (!G.xcd) return b;
+    const int q = G.grid >> 3, r = G.grid & 7, x = b & 7;
+    return x * q + min(x, r) + (b >> 3);
+}
+
 __device__ __forceinline__ TileIdx tile_of(const ConvGeom& G, const gpi_groups& g, int tile = -1) {
-    if (tile < 0) tile = blockIdx.x;
+    if (tile < 0) tile = logical_block(G);
     TileIdx t;
     t.b = tile / G.tiles;
     t.oy0 = (tile - t.b * G.tiles) * G.th;
@@ -654,7 +673,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NPX == 0 ? 
             float mean, inv;
             mean_invstd(gst + 4 * tid, (double)T.gsz * HWi, c.bn_eps, mean, inv);
             sc[tid] = gam * inv;
-            sh[tid] = bet - mean * gam * inv;
+            sh[tid] = fmaf(-(mean * gam), inv, bet);   // explicit FMA (bn_coefs): no contraction choice
         }
         __syncthreads();
         // ---- phase 3: BN + ReLU in LDS
@@ -1036,10 +1055,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
     const int64_t gin_off = pin(d.gin_off);
     // split launches: workgroups [0, nblocks) compute the input gradient (+ BN-backward sums, dgamma /
     // dbeta), [nblocks, 2 nblocks) the weight gradient of the same tiles
-    const bool wg_role = G.split && (int)blockIdx.x >= G.nblocks;
+    // (xcd order: logical blocks 2t / 2t + 1 are tile t's two roles, on one XCD)
+    const int lb = logical_block(G);
+    const bool wg_role = G.split && (G.xcd ? (lb & 1) != 0 : lb >= G.nblocks);
     const bool dg_role = !wg_role;
-    const bool do_wgrad = !G.split || wg_role;
-    const int tile = wg_role ? (int)blockIdx.x - G.nblocks : (int)blockIdx.x;
+    // wpart_off < 0: input gradient only (no weight / gamma / beta gradient, no slab row): callers that
+    // discard the shared-weight gradients (the PredictionEnsemble's decoder passes)
+    const bool wout = d.wpart_off >= 0;
+    const bool do_wgrad = (!G.split || wg_role) && wout;
+    const int tile = !G.split ? lb : (G.xcd ? lb >> 1 : (wg_role ? lb - G.nblocks : lb));
     const TileIdx T = tile_of(G, c.groups, tile);
     const int HWi = d.h_in * d.w_in, HWo = d.h_out * d.w_out;
     const float* ib = input_base(d, c, T.b);
@@ -1182,7 +1206,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
         i_inv[tid] = inv;
         i_gam[tid] = gam;
         i_sc[tid] = gam * inv;
-        i_sh[tid] = bet - mean * gam * inv;
+        i_sh[tid] = fmaf(-(mean * gam), inv, bet);
     }
     if (obn && tid >= 64 && tid < 64 + d.cout) {
         const int co = tid - 64;
@@ -1831,7 +1855,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
             if (kq == 0) {
                 red[wv * 32 + l16] = sd;
                 red[128 + wv * 32 + l16] = sdx;
-                if (cok && !lsum) {
+                if (cok && !lsum && wout) {
                     slab[d.cout * J + l16] = sdx;             // dgamma partial of this wave
                     slab[d.cout * J + d.cin + l16] = sd;      // dbeta partial
                 }
@@ -1889,7 +1913,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
         }
         __syncthreads();
         const int c0 = (G.split && !do_wgrad) ? d.cout * J : 0;
-        const int c1 = (G.split && !dg_role) ? d.cout * J : rowlen;
+        const int c1 = !wout ? 0 : ((G.split && !dg_role) ? d.cout * J : rowlen);
         float* srow = c.wpart + d.wpart_off + (int64_t)tile * rowlen;
         for (int e = c0 + tid; e < c1; e += 256) {
             const float* r = wD + e;
@@ -1900,7 +1924,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
         // the four waves' partial rows in a fixed order -> the tile's slab row
         __syncthreads();
         float* srow = c.wpart + d.wpart_off + (int64_t)tile * rowlen;
-        for (int e = tid; e < rowlen; e += 256) {
+        for (int e = tid; e < (wout ? rowlen : 0); e += 256) {
             const float* r = mid + 512 + e;
             srow[e] = (r[0] + r[rowlen]) + (r[2 * rowlen] + r[3 * rowlen]);
         }
@@ -2000,6 +2024,17 @@ bool aligned_ok(const gpi_conv_desc& d, const gpi_codec_ctx& c, bool fwd) {
     return true;
 }
 
+// XCD-aware block order per launch kind (ConvGeom::xcd), GPI_XCD_MODE bits: 1 forward, 2 backward,
+// 4 split backward, 8 the fused output conv.  With every kind on, the step's PMC traffic fell 547 ->
+// 505 MB (the fused output conv 1.24x -> 1.05x its algorithmic bytes, the 32/64-wide forwards ~1.15x ->
+// 1.03x) at unchanged forward and fused launch times, but several backward launches ran 0.6-2.2 us
+// slower (step 0.635 vs 0.625 ms, r03x).  Default 9 (forward + fused): 0.6233 / 0.6219 ms vs 0.6232 /
+// 0.6228 with the fused conv alone and 0.6277 / 0.6250 with the non-split backwards too (r03y).
+bool xcd_mode(bool fwd, bool fuse, bool split) {
+    static const int mode = env_int("GPI_XCD_MODE", 9);
+    return (mode & (fuse ? 8 : fwd ? 1 : split ? 4 : 2)) != 0;
+}
+
 int launch(const gpi_conv_desc& d, const gpi_codec_ctx& c, hipStream_t st, bool fwd, bool fuse = false) {
     ConvGeom G;
     if (!conv_geom(d, c.groups, G, fwd, fuse)) return GPI_ERR_UNSUPPORTED;
@@ -2032,9 +2067,11 @@ int launch(const gpi_conv_desc& d, const gpi_codec_ctx& c, hipStream_t st, bool 
         static const int split_env = env_int("GPI_BWD_SPLIT", 1);
         const int per_cu = std::min((int)(160000 / std::max<size_t>(lds, 1)), d.k == 5 ? 4 : 6);
         // split only well under one round: 2 x 576 workgroups measured slower than 576 (r02 A/B)
-        G.split = (split_env && 2 * G.nblocks <= std::min(per_cu, 4) * 256) ? 1 : 0;
+        G.split = (split_env && d.wpart_off >= 0 && 2 * G.nblocks <= std::min(per_cu, 4) * 256) ? 1 : 0;
     }
     const int grid = G.nblocks * (G.split ? 2 : 1);
+    G.grid = grid;
+    G.xcd = xcd_mode(fwd, fuse, G.split != 0) ? 1 : 0;
 #ifdef GPI_PHASE_TIMING
     static const int dbg_print = env_int("GPI_DBG_PRINT", 0);
     if (dbg_print)

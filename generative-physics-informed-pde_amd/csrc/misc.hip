@@ -39,6 +39,70 @@ __global__ __launch_bounds__(256) void step_epilogue_kernel(gpi_step_epilogue_de
     }
 }
 
+// torch.optim.Adam's element update (torch/optim/adam.py single-tensor path, no weight decay /
+// amsgrad / maximize), every rounding spelled out with explicit FMAs so that the separate Adam launch
+// and the fused epilogue + Adam launch compute bit-identical results:
+//   m.lerp_(g, 1 - beta1);  v.mul_(beta2).addcmul_(g, g, 1 - beta2);
+//   p -= (lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps)
+__device__ __forceinline__ void adam_element(float g, float& p, float& m, float& v, float beta1, float beta2,
+                                             float eps, float step_size, float bc2_sqrt) {
+    m = fmaf(1.f - beta1, g - m, m);
+    v = fmaf(1.f - beta2, g * g, v * beta2);
+    const float denom = sqrtf(v) / bc2_sqrt + eps;
+    p = fmaf(-step_size, m / denom, p);
+}
+
+// The step epilogue with Adam fused in (single-process steps: no all-reduce between the gradient
+// delivery and the update): element i's fp64 gradient -> grad[i] -> Adam on p[i], m[i], v[i], plus the
+// epilogue's scratch / subset / dropout duties.  The step counter and the RNG offset are read by every
+// workgroup (bias corrections, the dropout draw) and advanced once all of them have read them: by the
+// last workgroup to finish (arrival counter *done, reset by that workgroup for the next launch).
+__global__ __launch_bounds__(256) void step_epilogue_adam_kernel(gpi_step_epilogue_desc d, gpi_adam_desc a,
+                                                                 uint32_t* done) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t t = *a.step + 1;              // the step number after this step's increment
+    const uint64_t base = d.drop_offset ? *d.drop_offset : 0;
+    if (i < d.n) {
+        const float g = (float)d.gacc[i];
+        d.grad[i] = g;
+        d.gacc[i] = 0.0;
+        const float lr = *a.lr;
+        const double bc1 = 1.0 - pow((double)a.beta1, (double)t);
+        const double bc2 = 1.0 - pow((double)a.beta2, (double)t);
+        const float step_size = (float)((double)lr / bc1);
+        const float bc2_sqrt = (float)sqrt(bc2);
+        float p = a.p[i], m = a.m[i], v = a.v[i];
+        adam_element(g, p, m, v, a.beta1, a.beta2, a.eps, step_size, bc2_sqrt);
+        a.m[i] = m;
+        a.v[i] = v;
+        a.p[i] = p;
+    }
+    if (i < d.n_scratch) {
+        if (i < d.n_terms) d.terms_dst[i] = d.scratch[i];
+        d.scratch[i] = 0.0;
+    }
+    if (i < d.n_idx) d.idx_dst[i] = d.idx_src[i];
+    if (i * 4 < d.drop_n) {
+        const uint4_ r = philox(base + (uint64_t)i, d.drop_sub, d.drop_seed);
+        const float u[4] = {u01(r.x), u01(r.y), u01(r.z), u01(r.w)};
+        const float scale = 1.f / (1.f - d.drop_p);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (i * 4 + k < d.drop_n) d.drop_out[i * 4 + k] = u[k] < d.drop_p ? 0.f : scale;
+    }
+    // every thread's reads of *step / *drop_offset are complete (their values were consumed above), so
+    // a relaxed arrival suffices: the last arriver's writes come after every workgroup's reads
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t prev = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev == gridDim.x - 1) {
+            *const_cast<int64_t*>(a.step) = t;
+            if (a.rng_offset) *a.rng_offset += a.rng_advance;
+            __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
 // torch.optim.Adam single-tensor math (torch/optim/adam.py, defaults:
 // no weight decay, no amsgrad, maximize=False).
 __global__ __launch_bounds__(256) void adam_kernel(gpi_adam_desc d) {
@@ -48,16 +112,12 @@ __global__ __launch_bounds__(256) void adam_kernel(gpi_adam_desc d) {
     const double bc2 = 1.0 - pow((double)d.beta2, (double)t);
     const float step_size = (float)((double)lr / bc1);
     const float bc2_sqrt = (float)sqrt(bc2);
-    const float w = 1.f - d.beta1;
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < d.n; i += (int64_t)gridDim.x * 256) {
-        const float g = d.g[i];
-        float m = d.m[i];
-        m = m + w * (g - m);                                   // lerp_(grad, 1 - beta1)
-        float v = d.v[i] * d.beta2 + (1.f - d.beta2) * g * g;  // mul_(beta2).addcmul_(g, g, 1 - beta2)
+        float p = d.p[i], m = d.m[i], v = d.v[i];
+        adam_element(d.g[i], p, m, v, d.beta1, d.beta2, d.eps, step_size, bc2_sqrt);
         d.m[i] = m;
         d.v[i] = v;
-        const float denom = sqrtf(v) / bc2_sqrt + d.eps;
-        d.p[i] = d.p[i] - step_size * (m / denom);
+        d.p[i] = p;
     }
     if (d.rng_offset && blockIdx.x == 0 && threadIdx.x == 0) *d.rng_offset += d.rng_advance;
 }
@@ -91,36 +151,32 @@ __global__ __launch_bounds__(256) void dropout_mask_kernel(float* out, int64_t n
 
 __global__ void rng_advance_kernel(uint64_t* offset, uint64_t by) { *offset += by; }
 
-// random subset: sort (random key, index) pairs with a bitonic network in LDS
-__global__ __launch_bounds__(1024) void subset_kernel(int32_t* out, int32_t n, int32_t k, uint64_t seed,
-                                                      const uint64_t* offset, uint64_t sub, int32_t npow2) {
-    extern __shared__ __attribute__((aligned(16))) unsigned long long keys[];
+// random subset: the first k of the n indices ordered by (Philox key, index) -- a uniformly random
+// k-subset in random order.  Each element's position is its rank, the number of (key, index) pairs
+// below its own, counted in parallel: every workgroup draws all n keys into LDS and ranks EPB
+// elements, TPE = 256 / EPB threads per element over strided slices of the keys, partial counts
+// summed across the TPE lanes.  Same result as sorting the pairs (ranks of distinct pairs are
+// distinct), without the sort's log^2 n dependent barrier steps in one workgroup (15 us at n = 1024).
+__global__ __launch_bounds__(256) void subset_rank_kernel(int32_t* out, int32_t n, int32_t k, uint64_t seed,
+                                                          const uint64_t* offset, uint64_t sub, int32_t epb) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t hk[];
     const uint64_t base = offset ? *offset : 0;
-    for (int i = threadIdx.x; i < npow2; i += 1024) {
-        unsigned long long key;
-        if (i < n) {
-            const uint4_ r = philox(base + (uint64_t)i, sub, seed);
-            key = ((unsigned long long)r.x << 32) | (unsigned)i;
-        } else {
-            key = ~0ull;
-        }
-        keys[i] = key;
-    }
+    for (int j = threadIdx.x; j < n; j += 256) hk[j] = philox(base + (uint64_t)j, sub, seed).x;
     __syncthreads();
-    for (int size = 2; size <= npow2; size <<= 1) {
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            for (int i = threadIdx.x; i < npow2; i += 1024) {
-                const int j = i ^ stride;
-                if (j > i) {
-                    const bool up = (i & size) == 0;
-                    const unsigned long long a = keys[i], b = keys[j];
-                    if ((a > b) == up) { keys[i] = b; keys[j] = a; }
-                }
-            }
-            __syncthreads();
+    const int tpe = 256 / epb;
+    const int e = threadIdx.x / tpe, part = threadIdx.x - e * tpe;
+    const int i = blockIdx.x * epb + e;
+    int cnt = 0;
+    if (i < n) {
+        const uint32_t ki = hk[i];
+        for (int j = part; j < n; j += tpe) {
+            const uint32_t kj = hk[j];
+            cnt += (kj < ki || (kj == ki && j < i)) ? 1 : 0;
         }
     }
-    for (int i = threadIdx.x; i < k; i += 1024) out[i] = (int32_t)(keys[i] & 0xffffffffu);
+    // tpe consecutive lanes (a power of two <= 64 within one wave) hold one element's partial counts
+    for (int m = 1; m < tpe; m <<= 1) cnt += __shfl_xor(cnt, m, 64);
+    if (i < n && part == 0 && cnt < k) out[cnt] = i;
 }
 
 }  // namespace
@@ -177,6 +233,30 @@ extern "C" int gpi_step_epilogue(const gpi_step_epilogue_desc* d, void* stream) 
     return GPI_OK;
 }
 
+extern "C" int gpi_step_epilogue_adam(const gpi_step_epilogue_desc* d, const gpi_adam_desc* a, uint32_t* done,
+                                      void* stream) {
+    if (!d || !a || !done || d->n < 0 || d->n_scratch < 0 || d->n_idx < 0 || d->n_terms < 0 || d->n_terms > d->n_scratch)
+        return GPI_ERR_ARG;
+    if (!d->gacc || !d->grad || (d->n_scratch && !d->scratch) || (d->n_terms && !d->terms_dst) ||
+        (d->n_idx && (!d->idx_src || !d->idx_dst)))
+        return GPI_ERR_ARG;
+    if (d->drop_n < 0 || (d->drop_n && (!d->drop_out || !(d->drop_p >= 0.f && d->drop_p < 1.f)))) return GPI_ERR_ARG;
+    // the fused form owns the counter (Adam's) and always zeroes the accumulator; the update covers
+    // exactly the gradient's elements
+    if (d->flags != GPI_FINALIZE_ZERO || d->step || !a->p || !a->g || !a->m || !a->v || !a->lr || !a->step ||
+        a->n != d->n || a->g != d->grad || (d->drop_n && d->drop_offset && a->rng_offset &&
+                                              d->drop_offset != a->rng_offset))
+        return GPI_ERR_ARG;
+    int64_t m = d->n > d->n_scratch ? d->n : d->n_scratch;
+    if (d->n_idx > m) m = d->n_idx;
+    if ((d->drop_n + 3) / 4 > m) m = (d->drop_n + 3) / 4;
+    const int64_t nb = m > 0 ? (m + 255) / 256 : 1;
+    if (nb > 0x7fffffff) return GPI_ERR_ARG;
+    hipLaunchKernelGGL(step_epilogue_adam_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, *d, *a, done);
+    GPI_CHECK_LAUNCH();
+    return GPI_OK;
+}
+
 extern "C" int gpi_adam(const gpi_adam_desc* d, void* stream) {
     if (!d || !d->p || !d->g || !d->m || !d->v || !d->lr || !d->step || d->n < 0) return GPI_ERR_ARG;
     if (d->n == 0) return GPI_OK;
@@ -218,16 +298,15 @@ extern "C" int gpi_rng_advance(uint64_t* offset, uint64_t by, void* stream) {
 extern "C" int gpi_random_subset(int32_t* out, int32_t n, int32_t k, uint64_t seed, const uint64_t* offset,
                                  uint64_t sub, void* stream) {
     if (!out || n <= 0 || k < 0 || k > n || n > 16384) return GPI_ERR_ARG;
-    int32_t np2 = 1;
-    while (np2 < n) np2 <<= 1;
-    const size_t lds = sizeof(unsigned long long) * np2;
-    if (lds > 64 * 1024) {
-        if (hipFuncSetAttribute((const void*)subset_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
-            hipSuccess)
-            return GPI_ERR_LAUNCH;
-    }
-    hipLaunchKernelGGL(subset_kernel, dim3(1), dim3(1024), lds, (hipStream_t)stream, out, n, k, seed, offset, sub,
-                       np2);
+    if (k == 0) return GPI_OK;
+    // elements per workgroup: about n / 256 (>= 4, <= 64, a power of two): enough workgroups to
+    // spread the n^2 comparisons, few enough that the n key draws per workgroup stay cheap
+    int32_t epb = 4;                      // >= 4: an element's 256 / epb lanes stay inside one wave
+    while (epb < 64 && epb * 256 < n) epb <<= 1;
+    const size_t lds = sizeof(uint32_t) * n;
+    if (lds > 64 * 1024) return GPI_ERR_ARG;
+    hipLaunchKernelGGL(subset_rank_kernel, dim3((unsigned)((n + epb - 1) / epb)), dim3(256), lds, (hipStream_t)stream,
+                       out, n, k, seed, offset, sub, epb);
     GPI_CHECK_LAUNCH();
     return GPI_OK;
 }

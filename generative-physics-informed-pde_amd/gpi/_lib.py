@@ -198,6 +198,7 @@ SIGNATURES = {
     'gpi_grad_finalize': (C.c_int, [vp, vp, i64, C.c_int, vp, vp]),
     'gpi_adam': (C.c_int, [C.POINTER(AdamDesc), vp]),
     'gpi_step_epilogue': (C.c_int, [C.POINTER(StepEpilogueDesc), vp]),
+    'gpi_step_epilogue_adam': (C.c_int, [C.POINTER(StepEpilogueDesc), C.POINTER(AdamDesc), vp, vp]),
     'gpi_fom_workspace': (i64, [i32]),
     'gpi_fom_solve': (C.c_int, [C.POINTER(FomDesc), vp]),
     'gpi_random_field': (C.c_int, [C.POINTER(RandomFieldDesc), vp]),

@@ -202,10 +202,15 @@ class ElboEngine(object):
     from the VO posterior); vo_holdoff keeps only its logL_x - KL part (generative.py:349-364)."""
 
     def __init__(self, model, B_u, N_s, normalize=False, N_vo=0, vo_holdoff=False, q_unsup=None,
-                 running_modules=None):
+                 running_modules=None, shared_grads=True):
         """q_unsup: q_z['unsupervised'] for the non-armortized unsupervised term (no encoder,
         GenerativeModel.elbo_unsupervised generative.py:515-544): its rows replace the encoder
-        heads; the term's KL is the reference's KLD of q_z['supervised'] (sic, :525)."""
+        heads; the term's KL is the reference's KLD of q_z['supervised'] (sic, :525).
+        shared_grads=False: gradients of the per-sample variational rows only -- the codec backward
+        computes input gradients without weight / BN-affine gradients (no slab rows, no slab
+        reductions) and the dense weight GEMM is skipped (the PredictionEnsemble, whose Adam updates
+        its q_z rows only while the reference discards the decoder gradients it also forms)."""
+        self.shared_grads = bool(shared_grads)
         self.model = model
         self.q_unsup = q_unsup
         self.armortized = q_unsup is None
@@ -252,6 +257,9 @@ class ElboEngine(object):
         # the loss epilogue consumes (mu, logsigma) in registers: nobody reads the output image (9.4 MB of
         # writes per step at C64)
         self.dec_descs[len(self.dec_descs) - 1].out_off = -1
+        if not self.shared_grads:
+            for d in self.dec_descs:
+                d.wpart_off = -1          # input gradients only
         # the output conv's forward and backward run as ONE launch at the end of the forward
         # (gpi_conv_loss_fused: the loss gradient stays in LDS); GPI_FUSE_OUT=0 keeps them apart (A/B only)
         self.n_dec_sep = len(self.dec_descs) - (1 if os.environ.get('GPI_FUSE_OUT', '1') != '0' else 0)
@@ -366,6 +374,8 @@ class ElboEngine(object):
             gemm(hb['dzmu'], hb['hpre'], self.B_u, dz, d_feat, dz, d_feat, h.mu_w, h.mu_b, 1)
             gemm(hb['dzls'], hb['hpre'], self.B_u, dz, d_feat, dz, d_feat, h.ls_w, h.ls_b, 1)
             gemm(hb['dhpre'], h.feat, self.B_u, d_feat, d_feat, d_feat, d_feat, h.fc_w, h.fc_b)
+        if not self.shared_grads:
+            gi = []
         self.gemm_items = (L.GemmItem * len(gi))(*gi)
         # ---- ROM (one launch per labeled / VO term; both on the side stream)
         def rom_desc(row0, n, scale, slot):
@@ -405,7 +415,7 @@ class ElboEngine(object):
             self.rom_vo.Y = ws.fptr(hb['y_vo']).value
             self.roms.append(self.rom_vo)
         # the ROMs' d/dlogsigma_y rows are reduced with the decoder slabs (after the ROMs on the side stream)
-        self.reduce_dec = self.reduce_dec + self.rom_reduce
+        self.reduce_dec = (self.reduce_dec if self.shared_grads else []) + self.rom_reduce
         self.reduce_items = self.reduce_enc + self.reduce_dec
         self._fixed = (self.B_u, self.N_s, self.N_vo)
         self._side = None
@@ -604,8 +614,9 @@ class ElboEngine(object):
         if self._running_pending:
             self.running.launch(sst)
             self._running_pending = False
-        _run(lib.gpi_outer_gemm, self.gemm_items, len(self.gemm_items), C.c_void_p(self.ws.t_ws.data_ptr()),
-             C.c_void_p(self.flat.gacc.data_ptr()), sst, what='outer gemm')
+        if len(self.gemm_items):
+            _run(lib.gpi_outer_gemm, self.gemm_items, len(self.gemm_items), C.c_void_p(self.ws.t_ws.data_ptr()),
+                 C.c_void_p(self.flat.gacc.data_ptr()), sst, what='outer gemm')
         if side_extra is not None:
             side_extra(sst)
 

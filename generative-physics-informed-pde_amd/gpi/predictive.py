@@ -7,7 +7,9 @@ PredictionEnsembleEngine -- PredictionEnsemble.update (components.py:365-388), t
     private flat buffer: [shadow copy of the decoder weights | the ensemble's q_z]; the
     shadow is refreshed from the model with one device copy per update, and Adam
     (gpi_adam) updates the q_z rows only.  The decoder weight gradients the reference
-    leaves in f.*.grad (cleared by the trainer's next zero_grad) are not delivered.
+    leaves in f.*.grad (cleared by the trainer's next zero_grad) are not delivered -- nor computed:
+    the codec backward runs input gradients only (no weight-gradient phases, slab rows or slab
+    reductions, no dense weight GEMM).
 
 predictive_y -- Analysis.sample_predictive_y for every sample at once
     (components.py:472-478,493-524): q_z draws -> gp mean (+ exp(logsigma_X) noise)
@@ -17,6 +19,7 @@ predictive_y -- Analysis.sample_predictive_y for every sample at once
 """
 import copy
 import ctypes as C
+import os
 
 import torch
 
@@ -113,7 +116,10 @@ class PredictionEnsembleEngine(object):
         em = _EngineModel(self.shadow, model.gp, model.g, q_z, self.flat, getattr(model, 'config', {}))
         # the PE's decoder calls are the model's decoder's in the reference (components.py:371): its BN
         # running statistics are model.f's
-        self.engine = ElboEngine(em, 0, 0, N_vo=self.N, vo_holdoff=True, running_modules={'dec': model.f})
+        # q_z rows' gradients only (the decoder weight gradients the reference forms here are discarded);
+        # GPI_PE_SHARED_GRADS=1 computes them anyway (A/B and the parity test's reference form)
+        self.engine = ElboEngine(em, 0, 0, N_vo=self.N, vo_holdoff=True, running_modules={'dec': model.f},
+                                 shared_grads=os.environ.get('GPI_PE_SHARED_GRADS', '0') == '1')
         self.engine.bind(X_vo=self.X)
         self.m = torch.zeros(self.q_n, dtype=torch.float32, device=dev)
         self.v = torch.zeros_like(self.m)

@@ -130,6 +130,12 @@ class FusedElboStep(object):
             self.epi.drop_seed = self.seed
             self.epi.drop_offset = self.rng_off.data_ptr()
             self.epi.drop_sub = 4
+        # single-process steps: the epilogue and Adam in one launch (gpi_step_epilogue_adam; nothing
+        # runs between the gradient delivery and the update); GPI_FUSED_ADAM=0 keeps two launches
+        self.fuse_adam = not self.distributed and os.environ.get('GPI_FUSED_ADAM', '1') != '0'
+        self.epi_adam = L.StepEpilogueDesc.from_buffer_copy(self.epi)
+        self.epi_adam.step = None                  # Adam's counter: incremented once by the fused launch
+        self.done_ctr = torch.zeros(1, dtype=torch.int32, device=dev)
         self.graph = None
         # the first step's noise; every step then draws the next step's during its backward
         self._launch_noise(L.stream_handle(), self.idx, sub0=100)
@@ -157,6 +163,11 @@ class FusedElboStep(object):
             L.check(lib.gpi_randn(L.ptr(ex), ex.numel(), self.seed, L.ptr(self.rng_off), sub0 + 3, st), 'randn x')
 
     def forward_backward(self, stream=None):
+        """One step without the parameter update (gradient in flat.G and the ELBO terms delivered;
+        update() then applies Adam)."""
+        self._forward_backward(stream, epilogue=True)
+
+    def _forward_backward(self, stream=None, epilogue=True):
         """One step without the parameter update.  The step's noise and subset were drawn by the
         previous step (off the critical path); the next step's are drawn on the side stream once
         the head backward has consumed this step's; the epilogue (gradient finalisation, scratch
@@ -170,7 +181,8 @@ class FusedElboStep(object):
         # encoder's masks by the epilogue below (the encoder backward reads this step's)
         self.engine.backward(st, side_extra=lambda sst: self._launch_noise(sst, self.idx_next, codecs=('dec',),
                                                                            subset=not early))
-        L.check(L.lib().gpi_step_epilogue(C.byref(self.epi), st), 'step epilogue')
+        if epilogue:                  # (else: launched by update(fused=True), with Adam)
+            L.check(L.lib().gpi_step_epilogue(C.byref(self.epi), st), 'step epilogue')
 
     def allreduce(self):
         if self.distributed:
@@ -183,9 +195,15 @@ class FusedElboStep(object):
             self.lr.fill_(lr)
             self._lr_host = lr
 
-    def update(self, stream=None):
+    def update(self, stream=None, fused=False):
+        """Adam (+ RNG offset advance).  fused: the step epilogue and Adam in one launch -- after
+        _forward_backward(epilogue=False), single-process steps only."""
         st = stream if stream is not None else L.stream_handle()
-        L.check(L.lib().gpi_adam(C.byref(self.adam), st), 'adam (+ rng offset advance)')
+        if fused:
+            L.check(L.lib().gpi_step_epilogue_adam(C.byref(self.epi_adam), C.byref(self.adam),
+                                                   L.ptr(self.done_ctr), st), 'step epilogue + adam')
+        else:
+            L.check(L.lib().gpi_adam(C.byref(self.adam), st), 'adam (+ rng offset advance)')
 
     def _mark_optimizer_step(self):
         """Tell torch LR schedulers that an optimizer step happened (their hook wraps
@@ -194,9 +212,10 @@ class FusedElboStep(object):
         self.optimizer._opt_called = True
 
     def step_eager(self):
-        self.forward_backward()
+        fused = self.fuse_adam
+        self._forward_backward(epilogue=not fused)
         self.allreduce()
-        self.update()
+        self.update(fused=fused)
         self._mark_optimizer_step()
 
     # ------------------------------------------------------------------
@@ -205,7 +224,7 @@ class FusedElboStep(object):
         subsets, accumulators, gradient, the workspace (incl. the pre-drawn noise) and the term /
         statistics scratch."""
         ws = self.engine.ws
-        return [self.flat.P, self.m, self.v, self.step_ctr, self.rng_off, self.idx, self.idx_next,
+        return [self.flat.P, self.m, self.v, self.step_ctr, self.rng_off, self.idx, self.idx_next, self.done_ctr,
                 self.flat.gacc, self.flat.G, ws.t_ws, ws.t_scr, ws.t_parts, ws.t_flag, self.last_terms] + \
             self.engine.running.buffers
 
@@ -243,10 +262,11 @@ class FusedElboStep(object):
             with torch.cuda.graph(self.g_up):
                 self.update()
         else:
+            fused = self.fuse_adam
             with torch.cuda.graph(self.g_fb):
-                self.forward_backward()
+                self._forward_backward(epilogue=not fused)
                 self.allreduce()        # RCCL: captured as a graph node
-                self.update()
+                self.update(fused=fused)
         self.graph = True
 
     def _capture_segments(self):
@@ -276,9 +296,11 @@ class FusedElboStep(object):
             e.backward_a(st, rom)
 
         def m5(st):
-            L.check(L.lib().gpi_step_epilogue(C.byref(self.epi), st), 'step epilogue')
+            fused = self.fuse_adam
+            if not fused:
+                L.check(L.lib().gpi_step_epilogue(C.byref(self.epi), st), 'step epilogue')
             self.allreduce()                     # RCCL: captured as a graph node
-            self.update(st)
+            self.update(st, fused=fused)
 
         noise = (lambda sst: self._launch_noise(sst, self.idx_next, codecs=('dec',), subset=not early))
         segs = {'m1': cap(lambda st: e.forward_a(st, zero_gacc=False, zero_scratch=False))}

@@ -531,6 +531,12 @@ typedef struct gpi_step_epilogue_desc {
 } gpi_step_epilogue_desc;
 int gpi_step_epilogue(const gpi_step_epilogue_desc* d, void* stream);
 int gpi_adam(const gpi_adam_desc* d, void* stream);
+/* gpi_step_epilogue followed by gpi_adam in ONE launch (single-process steps: nothing runs between the
+ * gradient delivery and the update).  Requires d->flags == GPI_FINALIZE_ZERO, d->step == NULL (Adam's
+ * a->step is the counter: read by every workgroup, incremented once), a->g == d->grad, a->n == d->n,
+ * and a shared RNG offset (d->drop_offset == a->rng_offset when both are set).  done: a device
+ * uint32 arrival counter, zero before the first call (the launch leaves it zero). */
+int gpi_step_epilogue_adam(const gpi_step_epilogue_desc* d, const gpi_adam_desc* a, uint32_t* done, void* stream);
 
 /* Device Philox4x32-10 normals: out[i] = N(0,1) for counter (*offset + i);
  * offset is a device uint64 advanced by gpi_rng_advance (graph-replay safe). */

@@ -1,9 +1,13 @@
 """The ReLU branch decisions of the native fp32 kernels, read back from an ElboEngine's workspace
-after its forward: for every BatchNorm+ReLU the consumer conv applies on load, mask = (x * sc + sh
-> 0) with x the stored raw fp32 input and (sc, sh) the kernels' fp32 coefficients from the fp64
-batch sums (conv.hip mean_invstd / phase 2); for the encoder's FC ReLU, the stored pre-activation
-(head.hip hpre).  Test infrastructure: fed to the fp64 oracle (oracle/codec.py masks) so that
-activations within rounding of 0 take the same branch on both sides."""
+after its forward: for every BatchNorm+ReLU the consumer conv applies on load, mask =
+(fmaf(x, sc, sh) > 0) with x the stored raw fp32 input and (sc, sh) the kernels' fp32 coefficients
+from the fp64 batch sums, reproduced bit for bit (replica summation order and explicit FMAs,
+conv.hip stat_finish / mean_invstd / phase 2), so a near-tie pixel takes the kernels' branch
+exactly; for the encoder's FC ReLU, the stored pre-activation (head.hip hpre).  Test
+infrastructure: fed to the fp64 oracle (oracle/codec.py masks) so that activations within rounding
+of 0 take the same branch on both sides."""
+from fractions import Fraction
+
 import numpy as np
 import torch
 
@@ -11,16 +15,53 @@ from gpi import _lib as L
 from gpi.engine import N_TERMS
 
 
+def _round_f32(q):
+    """The float32 nearest to the Fraction q (ties to even): one rounding, as fmaf's."""
+    f = np.float32(float(q))
+    best = f
+    for c in (np.nextafter(f, np.float32(-np.inf)), np.nextafter(f, np.float32(np.inf))):
+        dc, db = abs(Fraction(float(c)) - q), abs(Fraction(float(best)) - q)
+        if dc < db or (dc == db and (int(np.float32(c).view(np.int32)) & 1) == 0):
+            best = c
+    return np.float32(best)
+
+
+def replica_sums(stats_r):
+    """conv.hip stat_finish: the GPI_REPLICAS fp64 records [R, ..., 4] of a channel summed in the
+    kernels' order -- per half h (replicas 8h..8h+7) the even and the odd replicas separately, the
+    two halves added last."""
+    R = stats_r.shape[0]
+    assert R == 16
+    halves = []
+    for h in range(2):
+        s0 = np.zeros(stats_r.shape[1:])
+        s1 = np.zeros(stats_r.shape[1:])
+        for r in range(0, 8, 2):
+            s0 = s0 + stats_r[8 * h + r]
+            s1 = s1 + stats_r[8 * h + r + 1]
+        halves.append(s0 + s1)
+    return halves[0] + halves[1]
+
+
 def _coefs(stats, gamma, beta, n, eps=1e-5):
-    """conv.hip mean_invstd + phase 2, in the kernels' precisions."""
-    m = stats[:, 0] / n
-    var = np.maximum(stats[:, 1] / n - m * m, 0.0)
-    mean = m.astype(np.float32)
-    inv = (1.0 / np.sqrt(var + np.float64(np.float32(eps)))).astype(np.float32)
-    g = gamma.astype(np.float32)
-    b = beta.astype(np.float32)
-    sc = g * inv
-    sh = b - (mean * g) * inv
+    """conv.hip mean_invstd + phase 2, every rounding as the kernels do it: mean = fl32(s/n),
+    var = fma(-m, m, s2/n) in fp64, inv = fl32(1 / sqrt(var + eps)), sc = fl32(gamma inv),
+    sh = fmaf(-fl32(mean gamma), inv, beta)."""
+    C = stats.shape[0]
+    sc = np.empty(C, np.float32)
+    sh = np.empty(C, np.float32)
+    e = np.float64(np.float32(eps))
+    for c in range(C):
+        m = np.float64(stats[c, 0]) / np.float64(n)
+        s2n = np.float64(stats[c, 1]) / np.float64(n)
+        var = float(Fraction(float(s2n)) - Fraction(float(m)) * Fraction(float(m)))   # one fp64 rounding
+        var = max(var, 0.0)
+        mean = np.float32(m)
+        inv = np.float32(np.float64(1.0) / np.sqrt(np.float64(var) + e))
+        g, b = np.float32(gamma[c]), np.float32(beta[c])
+        sc[c] = np.float32(g * inv)
+        p = np.float32(np.float64(mean) * np.float64(g))                                 # exact product, one rounding
+        sh[c] = _round_f32(Fraction(float(b)) - Fraction(float(p)) * Fraction(float(inv)))
     return sc.astype(np.float64), sh.astype(np.float64)
 
 
@@ -37,6 +78,8 @@ def _program_masks(prog, ws_np, stats, P, rows, group, n_group):
         st = stats[group, d.in_stat:d.in_stat + op.cin]
         sc, sh = _coefs(st, P[d.gamma_off:d.gamma_off + op.cin], P[d.beta_off:d.beta_off + op.cin],
                         float(n_group) * src.H * src.W)
+        # fmaf(x, sc, sh) > 0: the fp64 product of two fp32 values is exact and one fp64 addition
+        # keeps the sign of the exact sum (the kernels' single fp32 rounding keeps it too)
         y = x.astype(np.float64) * sc[None, :, None, None] + sh[None, :, None, None]
         out[op.bn] = torch.tensor(y > 0)
         del B_all
@@ -53,7 +96,7 @@ def engine_relu_masks(engine):
     R, G = L.GPI_REPLICAS, L.GPI_MAX_GROUPS
     scr = ws.t_scr.cpu().numpy()
     o = N_TERMS * R
-    stats = scr[o:o + R * G * ws.n_stats * 4].reshape(R, G, ws.n_stats, 4).sum(0)
+    stats = replica_sums(scr[o:o + R * G * ws.n_stats * 4].reshape(R, G, ws.n_stats, 4))
     masks = {}
     if engine.ep is not None and engine.B_u > 0:
         estats = stats      # the encoder context's statistics live in the same arena, group 0

@@ -332,6 +332,19 @@ def test_device_rng(device):
     assert len(set(v.tolist())) == 256 and v.min() >= 0 and v.max() < 2048
 
 
+@pytest.mark.parametrize('n,k,off', [(1, 1, 0), (7, 3, 5), (1000, 256, 17), (1024, 256, 0), (2048, 2048, 3),
+                                      (16384, 16384, 1 << 40), (16384, 64, 9)])
+def test_random_subset_exact(device, n, k, off):
+    """gpi_random_subset (parallel ranks) = the (Philox key, index) order of the numpy restatement,
+    bit for bit, including ties and the maximum pool."""
+    from gpi import _lib as L
+    from philox_ref import random_subset
+    o = torch.tensor([off], dtype=torch.int64, device='cuda')
+    idx = torch.full((k,), -1, dtype=torch.int32, device='cuda')
+    L.check(L.lib().gpi_random_subset(L.ptr(idx), n, k, 1234567, L.ptr(o), 11, L.stream_handle()), 'subset')
+    assert np.array_equal(idx.cpu().numpy(), random_subset(n, k, 1234567, off, 11))
+
+
 # ---------------------------------------------------------------- larger grids (BASELINE configs 4 / 5)
 def _codec_case(imsize, blocks, B, seed, dz=64, growth=4, f0=6):
     """Per-tensor relative gradient errors (and forward errors) of the native encoder / decoder vs
@@ -473,6 +486,34 @@ def test_capture_leaves_training_state_untouched(device, mode):
         torch.testing.assert_close(graph.flat.P, eager.flat.P, rtol=1e-6, atol=1e-7)
     assert graph.step_ctr.item() == eager.step_ctr.item() == 3
     assert (graph.segs is not None) == (mode == 'segments')
+
+
+def test_fused_epilogue_adam_matches_two_launches(device):
+    """gpi_step_epilogue_adam (epilogue + Adam in one launch, the single-process default) leaves
+    exactly what gpi_step_epilogue followed by gpi_adam leave -- parameters, Adam moments, gradient,
+    step counter, Philox offset, terms, subsets and dropout masks, bit for bit, over four captured
+    steps (the step is deterministic: its fp64 sums of fp32 terms are exact in any order; both launches
+    share the explicit-FMA element update) -- and the arrival counter is back at zero after every launch."""
+    import copy
+    from gpi.train import FusedElboStep
+    d = load('elbo_c32.npz')
+    model_a, bs = build_golden_model(d)
+    model_b = copy.deepcopy(model_a)
+    Xu, Xs, Y, F = cuda(d['Xu']), cuda(d['Xs']), cuda(d['Y']), cuda(d['F'])
+    two = FusedElboStep(model_a, Xu, bs, Xs, Y, F, lr=1e-3, seed=3)
+    one = FusedElboStep(model_b, Xu, bs, Xs, Y, F, lr=1e-3, seed=3)
+    two.fuse_adam = False
+    assert one.fuse_adam
+    two.capture()
+    one.capture()
+    for _ in range(4):
+        two.step()
+        one.step()
+    torch.cuda.synchronize()
+    for a, b in zip(two._mutable_state(), one._mutable_state()):
+        assert torch.equal(a, b)
+    assert one.step_ctr.item() == 4 and one.done_ctr.item() == 0
+    assert one.rng_off.item() == 4 * one.rng_span
 
 
 def test_lr_schedule_drives_fused_step(device):

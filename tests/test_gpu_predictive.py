@@ -83,6 +83,27 @@ def test_prediction_ensemble_update(device):
     assert rel(pe.q_z.logsigma.detach().cpu(), d['pe_logsigma']) < 1e-4
 
 
+def test_prediction_ensemble_input_gradient_only(device, monkeypatch):
+    """The PredictionEnsemble's codec backward without weight gradients (the default: no slab rows,
+    reductions or dense weight GEMM) moves q_z exactly as the full backward does, and leaves the
+    model's decoder untouched."""
+    from bottleneck.components import PredictionEnsemble
+    from lamp.optimization import LearningScheduleWrapper
+    d = load('pe_analysis_c32.npz')
+    out = {}
+    for flag in ('1', '0'):
+        monkeypatch.setenv('GPI_PE_SHARED_GRADS', flag)
+        model, ds = build(d)
+        before = [p.detach().clone() for p in model.f.parameters()]
+        pe = PredictionEnsemble(model, ds, LearningScheduleWrapper.Dummy(), lr=1e-2, writer=_Writer())
+        pe.update(numIter=3, record=True, step=0, eps=[cuda(e) for e in d['pe_eps']])
+        torch.cuda.synchronize()
+        assert all(torch.equal(a, b.detach()) for a, b in zip(before, model.f.parameters()))
+        out[flag] = (pe.q_z.mean.detach().clone(), pe.q_z.logsigma.detach().clone(), dict(pe.writer.d))
+    assert torch.equal(out['1'][0], out['0'][0]) and torch.equal(out['1'][1], out['0'][1])
+    assert out['1'][2] == out['0'][2]
+
+
 def test_analysis_eval_all_y(device):
     from bottleneck.components import Analysis, VariationalApproximation
     d = load('pe_analysis_c32.npz')
