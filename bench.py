@@ -42,7 +42,7 @@ HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 # HBM traffic per launch of the heaviest operators, from two separate rocprofv3 PMC
 # passes (FETCH_SIZE, WRITE_SIZE) over tools/kprobe.py: tools/profile_round.sh +
 # tools/pmc_traffic.py.  Used for roofline.traffic when the dominant operator is listed.
-TRAFFIC_JSON = os.path.join(ROOT, 'profiles', 'r03_traffic.json')
+TRAFFIC_JSON = os.path.join(ROOT, 'profiles', 'r03z_traffic.json')
 
 CONFIGS = {
     # name: (factory, B_u, N_s, pool, field params (mean, std, corrlength))
