@@ -39,6 +39,8 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+F32_PEAK_TFS = 157.3       # MI355X fp32 peak, vector (v_pk_fma_f32) = matrix (v_mfma_f32_16x16x4_f32) (same table)
+RIDGE_FLOP_PER_B = F32_PEAK_TFS * 1e12 / (HBM_PEAK_GBS * 1e9)   # 19.7 flop/B
 # HBM traffic per launch of the heaviest operators, from two separate rocprofv3 PMC
 # passes (FETCH_SIZE, WRITE_SIZE) over tools/kprobe.py: tools/profile_round.sh +
 # tools/pmc_traffic.py.  Used for roofline.traffic when the dominant operator is listed.
@@ -126,6 +128,20 @@ def conv_bytes(d, B, fwd, fused=False):
     return 4.0 * b
 
 
+def conv_flops(d, B, kind):
+    """Algorithmic fp32 FLOPs of one conv launch: M = B * H_out * W_out * cout * cin * K^2 multiply-adds
+    per pass (every (output pixel, tap, input channel, output channel) product once; the upsampling
+    convs' taps run on the upsampled image), 2 flops each; forward one pass, backward the weight
+    gradient plus the input gradient when there is one, the fused output conv all three (its halo-row
+    forward recompute and the loss epilogue's few flops per pixel are not counted)."""
+    m = float(B) * d.h_out * d.w_out * d.cout * d.cin * d.k * d.k
+    if kind == 'fwd':
+        return 2.0 * m
+    if kind == 'fused':
+        return 6.0 * m
+    return 2.0 * m * (2 if d.gin_off >= 0 else 1)
+
+
 def step_conv_launches(e):
     """The codec launches of one ELBO step of engine e, in step order per program:
     [(name, kind, entry point, desc, ctx, batch)] with kind 'fwd' / 'bwd', or 'fused' for the
@@ -152,7 +168,7 @@ def launch_bytes(kind, d, B):
 
 def profile_kernels(step, reps=20):
     """Per-launch device time of every codec operator, measured with HIP events on
-    the stream the kernels run on; returns [(name, ms, bytes)].  The reps launches of an
+    the stream the kernels run on; returns [(name, ms, bytes, flops)].  The reps launches of an
     operator are captured into one HIP graph and timed as two replays of it: back to back on
     the device, so a slow host (eager launches through ctypes cost about as much as the
     smallest kernels) cannot stretch the measured time."""
@@ -177,7 +193,7 @@ def profile_kernels(step, reps=20):
         g.replay()
         t1.record()
         torch.cuda.synchronize()
-        out.append((name, t0.elapsed_time(t1) / (2 * reps), launch_bytes(kind, d, B)))
+        out.append((name, t0.elapsed_time(t1) / (2 * reps), launch_bytes(kind, d, B), conv_flops(d, B, kind)))
         del g
     return out
 
@@ -458,9 +474,12 @@ def main():
         log('per-operator profile done')
         if args.kprof:
             with open(args.kprof, 'w') as fh:
-                json.dump([dict(op=n, ms=m, bytes=b, gbs=b / (m * 1e-3) / 1e9) for n, m, b in prof], fh, indent=1)
-        name, ms, byts = max(prof, key=lambda t: t[1])
+                json.dump([dict(op=n, ms=m, bytes=b, gbs=b / (m * 1e-3) / 1e9, flops=f, tfs=f / (m * 1e-3) / 1e12)
+                           for n, m, b, f in prof], fh, indent=1)
+        name, ms, byts, flops = max(prof, key=lambda t: t[1])
         ach = byts / (ms * 1e-3) / 1e9
+        ach_tf = flops / (ms * 1e-3) / 1e12
+        ai = flops / byts
         traffic = None
         traffic_note = 'no PMC traffic file'
         if os.path.exists(TRAFFIC_JSON):
@@ -473,9 +492,16 @@ def main():
                 traffic = round(t['traffic_bytes']) if t else None
                 traffic_note = '%s (PMC FETCH_SIZE / WRITE_SIZE passes)' % os.path.basename(TRAFFIC_JSON)
         step_ach = sbytes / (ms_step * 1e-3) / 1e9
-        roof = dict(bound='hbm', achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit='GB/s',
-                    frac=round(ach / HBM_PEAK_GBS, 4), traffic=traffic, traffic_source=traffic_note, kernel=name,
-                    kernel_ms=round(ms, 5), bytes_per_launch=byts,
+        # the dominant launch's bound by its arithmetic intensity: above the fp32 ridge (19.7 flop/B) it is
+        # compute-bound (the fused 5x5 output conv: 30 flop/B), priced against the fp32 peak; below it
+        # the HBM roofline.  Both figures are recorded.
+        hbm = dict(achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit='GB/s', frac=round(ach / HBM_PEAK_GBS, 4))
+        cmp_ = dict(achieved=round(ach_tf, 2), peak=F32_PEAK_TFS, unit='TFLOP/s', frac=round(ach_tf / F32_PEAK_TFS, 4))
+        main = cmp_ if ai >= RIDGE_FLOP_PER_B else hbm
+        roof = dict(bound='mfma' if ai >= RIDGE_FLOP_PER_B else 'hbm', achieved=main['achieved'], peak=main['peak'],
+                    unit=main['unit'], frac=main['frac'], traffic=traffic, traffic_source=traffic_note, kernel=name,
+                    kernel_ms=round(ms, 5), bytes_per_launch=byts, flops_per_launch=flops,
+                    arithmetic_intensity=round(ai, 2), ridge=round(RIDGE_FLOP_PER_B, 2), hbm=hbm, compute=cmp_,
                     codec_ms_sum=round(sum(t[1] for t in prof), 4),
                     step=dict(bytes=sbytes, achieved=round(step_ach, 1), frac=round(step_ach / HBM_PEAK_GBS, 4),
                               **sparts))

@@ -22,7 +22,7 @@ def main():
     torch.cuda.synchronize()
     prof = bench.profile_kernels(step, reps=50)
     with open(sys.argv[1], 'w') as fh:
-        json.dump([dict(op=n, ms=ms, bytes=b) for n, ms, b in prof], fh, indent=1)
+        json.dump([dict(op=n, ms=ms, bytes=b, flops=f) for n, ms, b, f in prof], fh, indent=1)
 
 
 if __name__ == '__main__':
