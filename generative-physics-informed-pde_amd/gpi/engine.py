@@ -432,6 +432,10 @@ class ElboEngine(object):
         self.enc_reduce = 'split'
         # ROM launches enqueued before the decoder forward (capture order) instead of after it
         self.rom_first = False
+        # where the fused step's ROM forks to the side stream: after the head forward ('forward') or
+        # with the backward's side work ('backward'; GPI_ROM_AT)
+        self.rom_at = os.environ.get('GPI_ROM_AT', 'forward')
+        self._rom_deferred = False
         # callable(side stream handle) launched on the side stream ahead of the ROM (fused step)
         self.side_pre = None
         # SyncBN (set_sync_bn): None = replica-BN, per-rank batch statistics
@@ -508,7 +512,11 @@ class ElboEngine(object):
         the forward), 'defer' (on the side stream during backward) or None."""
         st = stream if stream is not None else L.stream_handle()
         self.forward_a(st, zero_gacc, zero_scratch)
-        if self.roms:
+        # rom_at 'backward': the ROM follows the backward's fork on the side stream (ahead of the
+        # variational samples' head backward that needs it) -- one cross-stream dependency less per
+        # step; only when the value is not read right after the forward
+        self._rom_deferred = bool(self.roms) and self.rom_at == 'backward' and not compute_value
+        if self.roms and not self._rom_deferred:
             # the ROM solve only feeds the head backward: run it on a side stream,
             # concurrently with the decoder (fork here, join in backward / value).  The decoder
             # is enqueued first so that, in a captured graph, the main chain is the fork's first
@@ -519,7 +527,7 @@ class ElboEngine(object):
             if self.rom_first:
                 self._launch_roms()
         self.forward_b(st)
-        if self.roms and not self.rom_first:
+        if self.roms and not self.rom_first and not self._rom_deferred:
             self._launch_roms()
         if running == 'now':
             self.running.launch(st)
@@ -604,6 +612,9 @@ class ElboEngine(object):
         the decoder slab reduction, the deferred BN running statistics, the dense weight GEMM and
         side_extra."""
         lib = _lib()
+        if self._rom_deferred:
+            self.rom_side(sst)
+            self._rom_deferred = False
         if split:
             hq = L.HeadDesc.from_buffer_copy(self.head)
             hq.flags |= L.HEAD_PART_Q
@@ -758,7 +769,7 @@ class ElboEngine(object):
         # With the ROM still pending on the side stream, only the encoder samples' head backward
         # runs on the main stream; the variational samples' (which need the ROM adjoint) follow
         # the ROM on the side stream, so the main chain never waits for the ROM.
-        split = self._pending_join
+        split = self._pending_join or self._rom_deferred
         self.backward_a(st, split)
         # the decoder's slab reduction and the dense weight gradients depend only on what is
         # done by now: run them on the side stream, concurrently with the encoder backward
