@@ -96,6 +96,8 @@ struct ConvGeom {
     int cg;         // forward, tiles of <= 128 pixels: input-channel groups computing partial sums in parallel
                     // (256 / pixels threads per pixel instead of one busy wave), summed through LDS
     int fuse;       // backward: the fused output-conv launch (forward + loss + backward, gpi_conv_loss_fused)
+    int vsum;       // backward, single-channel stride-2 input conv (weight gradient only, vwg): the four waves'
+                    // partial slab rows summed in LDS into one row per tile (vsum_op)
     int lsum;       // backward (MFMA weight gradient): the four waves' partial slab rows summed in LDS at the
                     // end into ONE row per tile (accumulators held in registers through the input gradient)
     int split;      // backward: 2 workgroups per tile, input gradient (blockIdx < nblocks) and weight gradient
@@ -253,6 +255,7 @@ bool conv_geom(const gpi_conv_desc& d, const gpi_groups& g, ConvGeom& G, bool fw
     G.split = 0;   // decided by launch() from the LDS footprint
     G.fuse = fuse ? 1 : 0;
     G.lsum = 0;     // decided by launch() / gpi_conv_blocks from the LDS footprint (lsum_op)
+    G.vsum = 0;     // decided by launch() / gpi_conv_blocks (vsum_op)
     G.xcd = 0;      // set by launch() (xcd_mode)
     G.grid = 0;     // set by launch()
 #ifdef GPI_PHASE_TIMING
@@ -1473,13 +1476,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
     #pragma unroll
                     for (int nb = 0; nb < NB; ++nb) acc[nb] = mfma4(a, bv[nb], acc[nb]);
                 }
-                // each wave stores its own tile into its slab row (the slab reduction sums the rows)
+                // G.vsum: the four waves' tiles summed in LDS (the gradient image, dead after the loop)
+                // into ONE slab row per tile -- a quarter of the slab bytes the reduction reads, on the
+                // step's critical path at its end; otherwise each wave stores its own row
+                float* const wrow = G.vsum ? gl + wv * rowlen : slab;
+                if (G.vsum) __syncthreads();        // every wave is done reading gl
     #pragma unroll
                 for (int nb = 0; nb < NB; ++nb) {
     #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         const int co2 = kq * 4 + r, j2 = 16 * nb + l16;
-                        if (co2 < d.cout && j2 < KK) slab[co2 * J + j2] = acc[nb][r];
+                        if (co2 < d.cout && j2 < KK) wrow[co2 * J + j2] = acc[nb][r];
+                    }
+                }
+                if (G.vsum) {
+                    __syncthreads();
+                    float* srow = c.wpart + d.wpart_off + (int64_t)tile * rowlen;
+                    for (int e = tid; e < d.cout * J; e += 256) {
+                        const float* r = gl + e;
+                        srow[e] = (r[0] + r[rowlen]) + (r[2 * rowlen] + r[3 * rowlen]);
                     }
                 }
             }
@@ -1967,6 +1982,14 @@ bool lsum_op(const gpi_conv_desc& d, const ConvGeom& G) {
     return avail >= (size_t)4 * bwd_rowlen(d);
 }
 
+// One slab row per tile for the single-channel 7x7 stride-2 input conv's weight gradient (the kernel's
+// vwg form): the four waves' rows summed in LDS over the dead gradient image, when it holds them.
+bool vsum_op(const gpi_conv_desc& d, const ConvGeom& G) {
+    static const int on = env_int("GPI_VSUM", 1);
+    if (!on || !(d.k == 7 && d.stride == 2 && !d.upsample && d.cin == 1 && d.gin_off < 0 && d.cout <= 16)) return false;
+    return (size_t)img_floats(d.cout, G.gh, G.PG) >= (size_t)4 * bwd_rowlen(d);
+}
+
 typedef void (*conv_kernel_t)(gpi_conv_desc, gpi_codec_ctx, ConvGeom);
 
 template <int K, int S, int UP, int NPX>
@@ -2059,6 +2082,7 @@ int launch(const gpi_conv_desc& d, const gpi_codec_ctx& c, hipStream_t st, bool 
     }
     G.zero = zero;
     if (!fwd) G.lsum = lsum_op(d, G) ? 1 : 0;
+    if (!fwd) G.vsum = vsum_op(d, G) ? 1 : 0;
     const size_t lds = fwd ? fwd_lds(d, G, cp) : bwd_lds(d, G);
     if (lds > 160 * 1024) return GPI_ERR_UNSUPPORTED;
     if (!fwd && d.gin_off >= 0 && !fuse && !vop_op(d)) {
@@ -2202,7 +2226,7 @@ extern "C" int gpi_conv_blocks(const gpi_conv_desc* op, const gpi_groups* groups
     ConvGeom G;
     if (!conv_geom(*op, *groups, G, false)) return GPI_ERR_UNSUPPORTED;   // backward tiling
     // one slab row per wave, or per workgroup (vop ops; lsum: the rows summed in LDS)
-    *blocks = G.nblocks * ((vop_op(*op) || lsum_op(*op, G)) ? 1 : SLAB_ROWS);
+    *blocks = G.nblocks * ((vop_op(*op) || lsum_op(*op, G) || vsum_op(*op, G)) ? 1 : SLAB_ROWS);
     return GPI_OK;
 }
 

@@ -429,11 +429,14 @@ class ElboEngine(object):
         # encoder slab reduction: all on the main stream after the input conv's backward ('main'), or
         # split ('split': the input conv's slabs on the main stream, the rest on the side stream
         # concurrently with the input conv's backward)
-        self.enc_reduce = 'split'
+        self.enc_reduce = os.environ.get('GPI_ENC_REDUCE', 'split')
         # ROM launches enqueued before the decoder forward (capture order) instead of after it
         self.rom_first = False
         # where the fused step's ROM forks to the side stream: after the head forward ('forward') or
         # with the backward's side work ('backward'; GPI_ROM_AT)
+        # (A/Bs within the boxes' +-1 % noise: 'backward' 0.6308 / 0.6286 vs 0.6370 / 0.6332 ms on one box,
+        # 0.6277 / 0.6274 / 0.6316 / 0.6342 / 0.6485 vs 'forward' 0.6240 / 0.6255 / 0.6303 / 0.6255 / 0.6336 on
+        # two others, r03: kept 'forward')
         self.rom_at = os.environ.get('GPI_ROM_AT', 'forward')
         self._rom_deferred = False
         # callable(side stream handle) launched on the side stream ahead of the ROM (fused step)
