@@ -264,7 +264,7 @@ class PredictionEnsemble(object):
         (a list of numIter [N, d_z] tensors)."""
         e = self._native()
         for n in range(numIter):
-            elbo, logL, KLD = e.update(eps=eps[n] if eps is not None else None)
+            elbo, logL, KLD = e.update(eps=eps[n] if eps is not None else None, sync=n == 0)
             if n == numIter - 1:
                 if record and self.writer is not None:
                     self.writer.add_scalar('PredictionEnsemble/elbo', elbo.item(), global_step=step)

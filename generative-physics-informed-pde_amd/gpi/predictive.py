@@ -136,6 +136,10 @@ class PredictionEnsembleEngine(object):
         self.adam.rng_offset = self.rng_off.data_ptr()
         dp = self.engine.dp
         self.adam.rng_advance = max((self.N * self.engine.dz + 3) // 4 + 1, (dp.drop_numel + 3) // 4 + 1)
+        # gradient delivery of the q rows (fp64 accumulator -> G, accumulator zeroed) fused with their Adam
+        self.epi = L.StepEpilogueDesc(gacc=self.flat.gacc.data_ptr() + 8 * self.q_off, grad=G.data_ptr() + 4 * self.q_off,
+                                      n=self.q_n, flags=L.FINALIZE_ZERO)
+        self.done_ctr = torch.zeros(1, dtype=torch.int32, device=dev)
 
     def _sync_decoder(self):
         src_flat = getattr(self.model.f, '_gpi_flat', None)
@@ -161,10 +165,13 @@ class PredictionEnsembleEngine(object):
             self.lr.fill_(lr)
             self._lr_host = lr
 
-    def update(self, eps=None):
-        """One PredictionEnsemble iteration; returns (elbo, logL, KLD) device scalars (no host sync)."""
+    def update(self, eps=None, sync=True):
+        """One PredictionEnsemble iteration; returns (elbo, logL, KLD) device scalars (no host sync).
+        sync=False skips refreshing the shadow decoder (the model has not changed since the last
+        update: the later iterations of one PredictionEnsemble.update(numIter) call)."""
         lib, st = L.lib(), L.stream_handle()
-        self._sync_decoder()
+        if sync:
+            self._sync_decoder()
         self._sync_lr()
         ez = self.engine.eps_z()
         if eps is not None:
@@ -178,6 +185,11 @@ class PredictionEnsembleEngine(object):
         from .engine import T_LX0, T_KL_Q2
         logL, kld = t[T_LX0].float(), t[T_KL_Q2].float()
         self.engine.backward(st)
-        self.engine.finalize(self.flat.G, step=self.step_ctr, stream=st, zero_acc=True)
-        L.check(lib.gpi_adam(C.byref(self.adam), st), 'pe adam')
+        if self.engine.shared_grads:
+            self.engine.finalize(self.flat.G, step=self.step_ctr, stream=st, zero_acc=True)
+            L.check(lib.gpi_adam(C.byref(self.adam), st), 'pe adam')
+        else:
+            # only the q rows carry gradients: their delivery and Adam in one launch
+            L.check(lib.gpi_step_epilogue_adam(C.byref(self.epi), C.byref(self.adam), L.ptr(self.done_ctr), st),
+                    'pe gradient + adam')
         return logL - kld, logL, kld

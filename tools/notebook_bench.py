@@ -58,8 +58,8 @@ def main():
     torch.cuda.current_stream().wait_stream(s)
     torch.cuda.synchronize()
     with torch.cuda.graph(g_pe):
-        for _ in range(N_PE):
-            pe.update()
+        for i in range(N_PE):
+            pe.update(sync=i == 0)
 
     def iteration():
         step.step()
@@ -95,8 +95,8 @@ def main():
     with torch.cuda.graph(g_all):
         step.forward_backward()
         step.update()
-        for _ in range(N_PE):
-            pe.update()
+        for i in range(N_PE):
+            pe.update(sync=i == 0)
     for _ in range(20):
         g_all.replay()
     torch.cuda.synchronize()

@@ -97,8 +97,8 @@ def main():
     torch.cuda.synchronize()
     g_pe = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g_pe):
-        for _ in range(3):
-            pe.update()
+        for i in range(3):
+            pe.update(sync=i == 0)
     torch.cuda.synchronize()
     t_setup = time.perf_counter() - t_setup
 
