@@ -97,7 +97,10 @@ class _EngineModel(object):
 
 class PredictionEnsembleEngine(object):
 
-    def __init__(self, model, q_z, X, lr_source, betas=(0.9, 0.999), eps=1e-8):
+    def __init__(self, model, q_z, X, lr_source, betas=(0.9, 0.999), eps=1e-8, running_stage=False):
+        """running_stage: the decoder calls' BN running statistics go to the shadow decoder's buffers
+        (zeroed: an EMA staging area that ConcurrentPredictionEnsemble folds into model.f) instead of
+        straight into model.f's."""
         L.require_device(X)
         self.model = model
         self.q_z = q_z
@@ -118,7 +121,13 @@ class PredictionEnsembleEngine(object):
         # running statistics are model.f's
         # q_z rows' gradients only (the decoder weight gradients the reference forms here are discarded);
         # GPI_PE_SHARED_GRADS=1 computes them anyway (A/B and the parity test's reference form)
-        self.engine = ElboEngine(em, 0, 0, N_vo=self.N, vo_holdoff=True, running_modules={'dec': model.f},
+        self.running_stage = bool(running_stage)
+        if self.running_stage:
+            with torch.no_grad():
+                for b in self.shadow.buffers():
+                    b.zero_()
+        self.engine = ElboEngine(em, 0, 0, N_vo=self.N, vo_holdoff=True,
+                                 running_modules={'dec': self.shadow if self.running_stage else model.f},
                                  shared_grads=os.environ.get('GPI_PE_SHARED_GRADS', '0') == '1')
         self.engine.bind(X_vo=self.X)
         self.m = torch.zeros(self.q_n, dtype=torch.float32, device=dev)
@@ -160,19 +169,22 @@ class PredictionEnsembleEngine(object):
         return out
 
     def _sync_lr(self):
-        lr = float(self._lr_source())
+        self._set_lr(float(self._lr_source()))
+
+    def _set_lr(self, lr):
         if lr != self._lr_host:
             self.lr.fill_(lr)
             self._lr_host = lr
 
-    def update(self, eps=None, sync=True):
+    def update(self, eps=None, sync=True, sync_lr=True):
         """One PredictionEnsemble iteration; returns (elbo, logL, KLD) device scalars (no host sync).
         sync=False skips refreshing the shadow decoder (the model has not changed since the last
         update: the later iterations of one PredictionEnsemble.update(numIter) call)."""
         lib, st = L.lib(), L.stream_handle()
         if sync:
             self._sync_decoder()
-        self._sync_lr()
+        if sync_lr:
+            self._sync_lr()
         ez = self.engine.eps_z()
         if eps is not None:
             ez.copy_(eps)
@@ -193,3 +205,127 @@ class PredictionEnsembleEngine(object):
             L.check(lib.gpi_step_epilogue_adam(C.byref(self.epi), C.byref(self.adam), L.ptr(self.done_ctr), st),
                     'pe gradient + adam')
         return logL - kld, logL, kld
+
+
+class ConcurrentPredictionEnsemble(object):
+    """The notebook loop's PredictionEnsemble.update(numIter) (training.py:419) on its own stream,
+    concurrently with the NEXT training step.
+
+    The reference's iteration n runs training step n (theta_n -> theta_{n+1}) and then the PE group
+    PE(n): numIter iterations on theta_{n+1}.  The PE reads the decoder only through its shadow copy
+    and writes only its own q_z rows; step n+1 reads theta_{n+1} and writes theta_{n+2} in its final
+    Adam.  So once the shadow holds theta_{n+1}, PE(n) and step n+1 are independent:
+
+        for n: cpe.before_step(); step.step(); cpe.after_step(); [cpe.catch_up(); monitor]; schedulers
+        cpe.catch_up()
+
+    before_step() (main stream) waits for the PE group in flight and folds its BN running statistics
+    into model.f, refreshes the shadow with the current parameters when a PE group is owed and records
+    an event; after_step() replays that group (PE(n-1), on theta_n) on the side stream behind the event,
+    concurrently with the step just enqueued.  catch_up() runs every owed group on the main stream
+    (before reading q_z: the reference's monitoring at iteration n follows PE(n)).  Parameters and q_z
+    take exactly the sequential schedule's values (the same launches on the same inputs); the PE's
+    learning rate is the one the reference's PE(n) sees (read at after_step of iteration n, before that
+    iteration's scheduler steps).  The BN running buffers of model.f (never read by the training
+    computation: the reference has no eval mode) receive each PE group's exponential-average updates
+    one training step later than in the reference: the PE's calls update a zeroed staging copy (the
+    shadow's buffers), folded in as running = (1 - m)^k running + staged, num_batches_tracked += k."""
+
+    def __init__(self, engine, n_iter=3, momentum=0.1):
+        if not engine.running_stage:
+            raise ValueError('ConcurrentPredictionEnsemble needs PredictionEnsembleEngine(running_stage=True)')
+        self.e = engine
+        self.n_iter = int(n_iter)
+        self.momentum = float(momentum)
+        self.stream = torch.cuda.Stream()
+        self.ev_a, self.ev_b = torch.cuda.Event(), torch.cuda.Event()
+        stage = dict(engine.shadow.named_buffers())
+        dst = dict(engine.model.f.named_buffers())
+        names = [n for n in stage if n.endswith('running_mean') or n.endswith('running_var')]
+        self._fl_dst = [dst[n] for n in names]
+        self._fl_stage = [stage[n] for n in names]
+        nb = [n for n in stage if n.endswith('num_batches_tracked')]
+        self._nb_dst = [dst[n] for n in nb]
+        self._nb_stage = [stage[n] for n in nb]
+        self.graph = None
+        self.in_flight = False       # a PE group launched on the side stream, not yet waited for
+        self.steps = 0               # training steps enqueued
+        self.groups = 0              # PE groups enqueued: PE(j) for j < groups
+        self._launch = False
+        self._lr_next = None         # learning rate of the next owed group (host value)
+
+    def _group(self):
+        for i in range(self.n_iter):
+            self.e.update(sync=False, sync_lr=False)
+
+    def capture(self):
+        """The group captured as a HIP graph (after one warm-up group on the side stream; the PE state
+        it changes is restored).  Call before training starts."""
+        e = self.e
+        state = [e.flat.P, e.m, e.v, e.step_ctr, e.rng_off] + self._fl_stage + self._nb_stage
+        torch.cuda.synchronize()
+        saved = [t.clone() for t in state]
+        with torch.cuda.stream(self.stream):
+            self._group()
+        torch.cuda.synchronize()
+        for t, v in zip(state, saved):
+            t.copy_(v)
+        torch.cuda.synchronize()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self._group()
+        torch.cuda.synchronize()
+
+    def _fold(self):
+        if self._fl_dst:
+            torch._foreach_mul_(self._fl_dst, (1.0 - self.momentum) ** self.n_iter)
+            torch._foreach_add_(self._fl_dst, self._fl_stage)
+            torch._foreach_zero_(self._fl_stage)
+        if self._nb_dst:
+            torch._foreach_add_(self._nb_dst, self._nb_stage)
+            torch._foreach_zero_(self._nb_stage)
+
+    def _wait(self):
+        if self.in_flight:
+            torch.cuda.current_stream().wait_event(self.ev_b)
+            self._fold()
+            self.in_flight = False
+
+    def _refresh(self):
+        self.e._sync_decoder()
+        if self._lr_next is not None:
+            self.e._set_lr(self._lr_next)
+
+    def before_step(self):
+        self._wait()
+        self._launch = self.groups < self.steps
+        if self._launch:
+            self._refresh()
+            self.ev_a.record(torch.cuda.current_stream())
+
+    def after_step(self):
+        self.steps += 1
+        if self._launch:
+            self.stream.wait_event(self.ev_a)
+            with torch.cuda.stream(self.stream):
+                if self.graph is not None:
+                    self.graph.replay()
+                else:
+                    self._group()
+            self.ev_b.record(self.stream)
+            self.in_flight = True
+            self.groups += 1
+            self._launch = False
+        self._lr_next = float(self.e._lr_source())
+
+    def catch_up(self):
+        """Main stream: every owed PE group done (and folded): q_z is the reference's after PE(steps-1)."""
+        self._wait()
+        while self.groups < self.steps:
+            self._refresh()
+            if self.graph is not None:
+                self.graph.replay()
+            else:
+                self._group()
+            self._fold()
+            self.groups += 1

@@ -116,3 +116,55 @@ def test_analysis_eval_all_y(device):
     assert abs(logscore - float(d['logscore'])) <= 1e-4 * abs(float(d['logscore']))
     assert abs(r2 - float(d['r2'])) <= 1e-4 * abs(float(d['r2']))
     assert abs(relerr - float(d['relerr'])) <= 1e-4 * abs(float(d['relerr']))
+
+
+@pytest.mark.parametrize('captured', [False, True])
+def test_concurrent_prediction_ensemble_matches_sequential(device, tmp_path, captured):
+    """ConcurrentPredictionEnsemble (the PE group of iteration n on a second stream, concurrently with
+    training step n+1) leaves the model parameters and the PE's q_z exactly as the sequential
+    schedule (step n, then the PE group on theta_{n+1}; training.py:417-419) does over five iterations,
+    eager and as HIP graphs; the BN running buffers get the same number of updates (their EMA order
+    differs by one step, documented)."""
+    import sys
+    sys.path.insert(0, __file__.rsplit('/', 1)[0])
+    from test_gpu_training import _setup
+    from gpi.train import FusedElboStep
+    from gpi.predictive import PredictionEnsembleEngine, ConcurrentPredictionEnsemble
+    from bottleneck.components import VariationalApproximation
+    out = {}
+    for conc in (False, True):
+        model, val = _setup(tmp_path / ('c' if conc else 's'), seed=0)
+        ds_u, ds_s = model._datasets['unsupervised'], model._datasets['supervised']
+        step = FusedElboStep(model, ds_u.get('X'), 32, ds_s.get('X'), ds_s.get('Y'), ds_s.get('F_ROM_BC'),
+                             lr=1e-2, seed=3)
+        Xv = val.get('X').contiguous().float()
+        q = VariationalApproximation(model.dim_latent, Xv.shape[0], Xv).to('cuda')
+        torch.manual_seed(9)
+        pe = PredictionEnsembleEngine(model, q, Xv, lambda: 1e-2, running_stage=conc)
+        if captured:
+            step.capture()
+        if conc:
+            cpe = ConcurrentPredictionEnsemble(pe, 3)
+            if captured:
+                cpe.capture()
+            for _ in range(5):
+                cpe.before_step()
+                step.step()
+                cpe.after_step()
+            cpe.catch_up()
+        else:
+            for _ in range(5):
+                step.step()
+                for i in range(3):
+                    pe.update(sync=i == 0)
+        torch.cuda.synchronize()
+        out[conc] = (step.flat.P.clone(), pe.flat.P[pe.q_off:].clone(),
+                     {n: b.clone() for n, b in model.f.named_buffers()})
+    assert torch.equal(out[False][0], out[True][0])
+    assert torch.equal(out[False][1], out[True][1])
+    for n, b in out[False][2].items():
+        c = out[True][2][n]
+        if n.endswith('num_batches_tracked'):
+            assert torch.equal(b, c), n
+        else:
+            assert torch.isfinite(c).all() and (c - b).abs().max() <= 0.25 * b.abs().max() + 0.05, n

@@ -56,7 +56,7 @@ def main():
     from utils.data import DataSet
     from lamp.optimization import LearningScheduleWrapper
     from gpi.train import FusedElboStep
-    from gpi.predictive import PredictionEnsembleEngine, predictive_y, predictive_scores
+    from gpi.predictive import PredictionEnsembleEngine, ConcurrentPredictionEnsemble, predictive_y, predictive_scores
     from bottleneck.components import VariationalApproximation
 
     t_setup = time.perf_counter()
@@ -86,20 +86,13 @@ def main():
     q_val = VariationalApproximation(model.dim_latent, N_val, Xv).to(dev)
     pe_lr = _LrHandle(1e-2)
     sw.register_optimizer(pe_lr, 'validation')                                       # components.py:337
-    pe = PredictionEnsembleEngine(model, q_val, Xv, lambda: pe_lr.param_groups[0]['lr'])
-    pe._sync_lr()           # outside the graph: replays then read the device learning rate as it is
+    pe = PredictionEnsembleEngine(model, q_val, Xv, lambda: pe_lr.param_groups[0]['lr'], running_stage=True)
+    pe._sync_lr()
     step.capture()
-    s = torch.cuda.Stream()
-    s.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(s):
-        pe.update()         # allocator / kernel warm-up (one real PE iteration)
-    torch.cuda.current_stream().wait_stream(s)
-    torch.cuda.synchronize()
-    g_pe = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g_pe):
-        for i in range(3):
-            pe.update(sync=i == 0)
-    torch.cuda.synchronize()
+    # the PE group of iteration n-1 runs concurrently with training step n (same parameters and q_z as
+    # the sequential loop; gpi.predictive.ConcurrentPredictionEnsemble)
+    cpe = ConcurrentPredictionEnsemble(pe, 3)
+    cpe.capture()
     t_setup = time.perf_counter() - t_setup
 
     def monitor(n_mc):
@@ -110,9 +103,11 @@ def main():
     history = []
     t0 = time.perf_counter()
     for n in range(iters):
+        cpe.before_step()
         step.step()
-        g_pe.replay()
+        cpe.after_step()
         if n % 1000 == 0 and n > 0:                               # training.py:421-428
+            cpe.catch_up()                                        # PE(n) done: the reference's order
             m = monitor(64)
             m.update(iteration=n, elbo=float(step.elbo().item()), lr=step.optimizer.param_groups[0]['lr'])
             history.append(m)
@@ -121,15 +116,16 @@ def main():
         sw.step('training')                                       # training.py:452
         sw.step('validation')                                     # components.py:385, once per update(3)
         step.sync_lr()
-        pe._sync_lr()
+    cpe.catch_up()
     torch.cuda.synchronize()
     t_train = time.perf_counter() - t0
     # final: 250 rounds of 3 PE updates, then eval_all_y with 1024 MC samples (training.py:457-460)
     t1 = time.perf_counter()
     for _ in range(250):
-        g_pe.replay()
-        sw.step('validation')
         pe._sync_lr()
+        cpe.graph.replay()
+        cpe._fold()
+        sw.step('validation')
     final = monitor(1024)
     torch.cuda.synchronize()
     t_final = time.perf_counter() - t1
