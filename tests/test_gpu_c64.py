@@ -354,3 +354,73 @@ def test_fused_step_scaleup_grids(device, ident, n, Nu, bs, Ns):
     errs = {k: tensor_rel(G[off[k]:off[k] + st[k].numel()].cpu().numpy().reshape(st[k].shape), st[k].grad.numpy())
             for k in st}
     print(check_grads(errs, tol_all=5e-5, frac_tight=1.0))
+
+
+@pytest.mark.parametrize('tag', ['c32', 'c64'])
+def test_codec_module_path_vs_oracle(device, tag):
+    """The standalone CNNEncoder / CNNDecoder module path (Encoder.py:191-196, Decoder.py:288-305 on
+    the native codec) on the reference fixture's weights and inputs vs the fp64 oracle codec with the
+    kernels' ReLU decisions (tests/gpu_masks.py, bit-exact coefficient arithmetic): forward 1e-5 and
+    every gradient tensor 5e-5 per-tensor relative (max|d| / max|ref|, no floor), mask audit -- the
+    tie-aware form of test_encoder_forward_backward / test_decoder_forward_backward (which compare
+    with the reference's own fp32 run)."""
+    import sys
+    sys.path.insert(0, __file__.rsplit('/', 1)[0])
+    from test_gpu_parity import _codec
+    from gpu_masks import _program_masks, replica_sums
+    from gpi import _lib as L
+    from gpi.engine import N_TERMS
+    d, enc, dec = _codec(tag)
+    imsize, dz, latent, growth, f_enc, f_dec = [int(v) for v in d['cfg'][:6]]
+    blocks = [int(v) for v in d['cfg'][6:]]
+
+    def engine_masks(e, B):
+        torch.cuda.synchronize()
+        ws = e.ws
+        R, G = L.GPI_REPLICAS, L.GPI_MAX_GROUPS
+        scr = ws.t_scr.cpu().numpy()
+        o = N_TERMS * R
+        stats = replica_sums(scr[o:o + R * G * ws.n_stats * 4].reshape(R, G, ws.n_stats, 4))
+        return _program_masks(e.p, ws.t_ws.cpu().numpy(), stats, e.flat.P.detach().cpu().numpy(),
+                              slice(0, B), 0, B), ws
+
+    # ---- encoder
+    X = cuda(d['X'])
+    mu, ls = enc(X)
+    e = next(iter(enc._gpi_engines.values()))
+    masks, ws = engine_masks(e, X.shape[0])
+    hp = ws.t_ws.cpu().numpy()[e.hb['hpre']:e.hb['hpre'] + X.shape[0] * e.p.d_feat]
+    masks['features.FC'] = torch.tensor(hp.reshape(X.shape[0], -1) > 0)
+    (torch.sum(mu * cuda(d['enc_wm'])) + torch.sum(ls * cuda(d['enc_ws']))).backward()
+    pe = {k[4:]: torch.tensor(v, dtype=torch.float64).requires_grad_(True) for k, v in d.items()
+          if k.startswith('enc.') and not k.startswith('enc.grad.') and 'running' not in k and 'num_batches' not in k}
+    ocodec.MASK_AUDIT.clear()
+    mu_o, ls_o = ocodec.encoder_forward(pe, torch.tensor(d['X'], dtype=torch.float64), imsize, blocks, growth, f_enc,
+                                        masks=masks)
+    (torch.sum(mu_o * torch.tensor(d['enc_wm'], dtype=torch.float64)) +
+     torch.sum(ls_o * torch.tensor(d['enc_ws'], dtype=torch.float64))).backward()
+    check_mask_audit(max_frac=1e-4)
+    assert tensor_rel(mu.detach().cpu().numpy(), mu_o.detach().numpy()) < 1e-5
+    assert tensor_rel(ls.detach().cpu().numpy(), ls_o.detach().numpy()) < 1e-5
+    errs = {k: tensor_rel(p.grad.cpu().numpy(), pe[k].grad.numpy()) for k, p in enc.named_parameters()}
+    bad = {k: v for k, v in errs.items() if not v < 5e-5}
+    assert not bad, bad
+    # ---- decoder
+    Z = cuda(d['Z']).requires_grad_(True)
+    mx, lsx = dec(Z)
+    e = next(iter(dec._gpi_engines.values()))
+    masks, _ = engine_masks(e, Z.shape[0])
+    (torch.sum(mx * cuda(d['dec_vm'])) + torch.sum(lsx * cuda(d['dec_vs']))).backward()
+    pd = {k[4:]: torch.tensor(v, dtype=torch.float64).requires_grad_(True) for k, v in d.items()
+          if k.startswith('dec.') and not k.startswith('dec.grad.') and 'running' not in k and 'num_batches' not in k}
+    Zo = torch.tensor(d['Z'], dtype=torch.float64).requires_grad_(True)
+    mx_o, lsx_o = ocodec.decoder_forward(pd, Zo, latent, blocks, growth, f_dec, masks=masks)
+    (torch.sum(mx_o * torch.tensor(d['dec_vm'], dtype=torch.float64)) +
+     torch.sum(lsx_o * torch.tensor(d['dec_vs'], dtype=torch.float64))).backward()
+    check_mask_audit(max_frac=1e-4)
+    assert tensor_rel(mx.detach().cpu().numpy(), mx_o.detach().numpy()) < 1e-5
+    assert tensor_rel(lsx.detach().cpu().numpy(), lsx_o.detach().numpy()) < 1e-5
+    errs = {k: tensor_rel(p.grad.cpu().numpy(), pd[k].grad.numpy()) for k, p in dec.named_parameters()}
+    errs['Z'] = tensor_rel(Z.grad.cpu().numpy(), Zo.grad.numpy())
+    bad = {k: v for k, v in errs.items() if not v < 5e-5}
+    assert not bad, bad
