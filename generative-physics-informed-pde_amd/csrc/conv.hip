@@ -1000,6 +1000,17 @@ __host__ __device__ inline int vop_mid_floats(int gh, int w_out, int rowlen, boo
 #ifndef GPI_FUSE_WAVES
 #define GPI_FUSE_WAVES 5
 #endif
+// fused output conv forward: which of the K weight-pair taps come by broadcast LDS read (one ds_read_b64 of
+// the (co 0, co 1) pair) instead of two v_readlane (GPI_FUSE_WLDS = how many; the odd taps first).  The
+// launch: 30.29 / 30.52 us with every pair by readlane, 29.63 / 29.55 with 4 of 5 by LDS, 29.40 / 29.44 with
+// all 5 (r03 A/B): the forward phase was VALU-issue bound, the LDS pipe has room for the broadcast reads
+#ifndef GPI_FUSE_WLDS
+#define GPI_FUSE_WLDS 5
+#endif
+__host__ __device__ constexpr bool fuse_wlds(int ky) {
+    return GPI_FUSE_WLDS <= 0 ? false : (GPI_FUSE_WLDS >= 5 ? true : (ky & 1 ? (ky / 2) < GPI_FUSE_WLDS : (ky / 2) < GPI_FUSE_WLDS - 2));
+}
+
 template <int K, int S, int UP, bool FUSE = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (FUSE ? GPI_FUSE_WAVES : 4) : 6))) void conv_bwd_kernel(gpi_conv_desc d, gpi_codec_ctx c, ConvGeom G) {
     touch_kernargs<CONV_KARG_BYTES>();
@@ -1353,10 +1364,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
         // RPF vertically adjacent pixels of one column per thread: items (column, row group) fill the
         // 256 lanes exactly on 64-wide planes (20 rows = 4 groups x 64 columns with 16-row tiles).  Per
         // (ci, kx) the column's RPF + K - 1 input values are read once (lanes on consecutive columns: one
-        // 256-B LDS row per read, no bank conflicts) and serve the RPF x K taps.  The weights: lane l
-        // holds WF[64 j + l] in wr[j] (one LDS read each), a tap's (co 0, co 1) pair is taken by two
-        // v_readlane into SGPRs -- VALU work instead of 50 broadcast LDS reads per item (the phase was
-        // LDS-bound: r03c 15.6 k cycles per workgroup)
+        // 256-B LDS row per read, no bank conflicts) and serve the RPF x K taps.  The weights: a tap's
+        // (co 0, co 1) pair by one broadcast ds_read_b64 (fuse_wlds, the default for every tap) or, for
+        // taps left to the VALU, by two v_readlane from wr[] (lane l holds WF[64 j + l])
         const int nrg = (G.gh + RPF - 1) / RPF, nitem = nrg * d.w_out;
         auto fwd_items = [&](auto ci_c) {
             constexpr int CIN = decltype(ci_c)::value;
@@ -1390,9 +1400,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
 #pragma unroll
                         for (int ky = 0; ky < K; ++ky) {
                             const int i = ((ci * K + kx) * K + ky) * 2;
-                            w[ky][0] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wr[i >> 6]), i & 63));
-                            w[ky][1] = __int_as_float(
-                                __builtin_amdgcn_readlane(__float_as_int(wr[(i + 1) >> 6]), (i + 1) & 63));
+                            if (fuse_wlds(ky)) {
+                                // (co 0, co 1) pair by one broadcast LDS read: the LDS pipe takes part of
+                                // the weight traffic off the VALU (GPI_FUSE_WLDS taps of K)
+                                w[ky] = *reinterpret_cast<const f32x2*>(mid + 256 + i);
+                            } else {
+                                w[ky][0] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wr[i >> 6]), i & 63));
+                                w[ky][1] = __int_as_float(
+                                    __builtin_amdgcn_readlane(__float_as_int(wr[(i + 1) >> 6]), (i + 1) & 63));
+                            }
                         }
                         // input row j0 + r feeds pixel p through tap ky = r - p
 #pragma unroll
