@@ -1007,6 +1007,10 @@ __host__ __device__ inline int vop_mid_floats(int gh, int w_out, int rowlen, boo
 #ifndef GPI_FUSE_WLDS
 #define GPI_FUSE_WLDS 5
 #endif
+// the VALU input gradient (vop ops): weight channel pairs by broadcast LDS read (1) or v_readlane (0)
+#ifndef GPI_VDG_WLDS
+#define GPI_VDG_WLDS 1
+#endif
 __host__ __device__ constexpr bool fuse_wlds(int ky) {
     return GPI_FUSE_WLDS <= 0 ? false : (GPI_FUSE_WLDS >= 5 ? true : (ky & 1 ? (ky / 2) < GPI_FUSE_WLDS : (ky / 2) < GPI_FUSE_WLDS - 2));
 }
@@ -1809,9 +1813,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
     #pragma unroll
                             for (int h = 0; h < CH; ++h) {
                                 const int i = ((co * K + ky) * K + kx) * CI + 2 * h;
-                                w[h][0] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wb[i >> 6]), i & 63));
-                                w[h][1] = __int_as_float(
-                                    __builtin_amdgcn_readlane(__float_as_int(wb[(i + 1) >> 6]), (i + 1) & 63));
+                                if (GPI_VDG_WLDS) {
+                                    // the channel pair by one broadcast LDS read (as the fused forward's weights)
+                                    w[h] = *reinterpret_cast<const f32x2*>(mid + i);
+                                } else {
+                                    w[h][0] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wb[i >> 6]), i & 63));
+                                    w[h][1] = __int_as_float(
+                                        __builtin_amdgcn_readlane(__float_as_int(wb[(i + 1) >> 6]), (i + 1) & 63));
+                                }
                             }
     #pragma unroll
                             for (int q = 0; q < Q; ++q) {
