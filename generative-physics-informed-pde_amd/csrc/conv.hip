@@ -84,6 +84,11 @@ __host__ __device__ inline int fdiv2(int x) { return x >= 0 ? x / 2 : -((-x + 1)
 __host__ __device__ inline int cdiv2(int x) { return -fdiv2(-x); }
 __host__ __device__ inline int pad256(int n) { return (n + 255) & ~255; }
 
+// forward (one pixel per thread): the per-channel weight offset forced into a VGPR (1) or left to the compiler (0)
+#ifndef GPI_FWD_WVGPR
+#define GPI_FWD_WVGPR 1
+#endif
+
 // Tile geometry: tile t of sample b covers output rows [t*th, (t+1)*th), all columns.
 struct ConvGeom {
     int th, tiles, nblocks;
@@ -853,7 +858,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NPX == 0 ? 
                 const int plane = G.rh * G.P;
                 for (int ci = grp; ci < d.cin; ci += cg) {
                     const float* tci = img + ci * plane;
-                    const float* wci = wT + ci * KK * CP;
+                    // the weight offset held in a VGPR: the uniform LDS reads then take one VGPR base with
+                    // immediate offsets (as an SGPR address every read needed its own v_mov of the address)
+                    int wofs = pad256(FWD_HDR) + ci * KK * CP;      // wT = smem + pad256(FWD_HDR)
+                    if (GPI_FWD_WVGPR) asm volatile("" : "+v"(wofs));
+                    const float* wci = smem + wofs;
     #pragma unroll
                     for (int ky = 0; ky < K; ++ky) {
                         const int ry = UP ? (fdiv2(oy - d.pad + ky) - iy0) : (ty * S + ky);
