@@ -44,7 +44,7 @@ RIDGE_FLOP_PER_B = F32_PEAK_TFS * 1e12 / (HBM_PEAK_GBS * 1e9)   # 19.7 flop/B
 # HBM traffic per launch of the heaviest operators, from two separate rocprofv3 PMC
 # passes (FETCH_SIZE, WRITE_SIZE) over tools/kprobe.py: tools/profile_round.sh +
 # tools/pmc_traffic.py.  Used for roofline.traffic when the dominant operator is listed.
-TRAFFIC_JSON = os.path.join(ROOT, 'profiles', 'r03g_traffic.json')
+TRAFFIC_JSON = os.path.join(ROOT, 'profiles', 'r03h_traffic.json')
 
 CONFIGS = {
     # name: (factory, B_u, N_s, pool, field params (mean, std, corrlength))

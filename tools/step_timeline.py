@@ -30,6 +30,11 @@ def main():
         busy_end = max(busy_end, e)
     print('window %.1f us, busy %.1f us, idle %.1f us, %d kernels' % ((t1 - t0) / 1e3, busy / 1e3,
                                                                      (t1 - t0 - busy) / 1e3, len(win)))
+    # every traced step (the window above is one of them; traced steps run longer than untraced ones)
+    w = sorted((b - a) / 1e3 for a, b in zip(ends, ends[1:]))
+    if w:
+        print('all %d traced step windows: min %.1f us, median %.1f us, max %.1f us'
+              % (len(w), w[0], w[len(w) // 2], w[-1]))
 
 
 if __name__ == '__main__':
