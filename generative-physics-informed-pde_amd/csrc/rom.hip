@@ -196,6 +196,9 @@ __device__ __forceinline__ void interp(int i, int j, int r, int nc, int& n00, in
 #endif
 constexpr int ROM_NT = GPI_ROM_NT;   // threads per sample
 constexpr int ROM_U = 8;         // fine nodes per batch of global loads
+#ifndef GPI_ROM_FAST_NT_DEFAULT
+#define GPI_ROM_FAST_NT_DEFAULT 512
+#endif
 
 __global__ __launch_bounds__(ROM_NT) void rom_kernel(gpi_rom_desc d, RomDims D) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -482,40 +485,51 @@ __device__ __forceinline__ void chol_inv_wave(const float* __restrict__ L, float
     }
 }
 
-// out[i] = (Z^T (Z v))_i = (K^{-1} v)_i for i < NI (v, out in LDS; out may alias v; part: 4 x 64 floats of
-// scratch).  All ROM_NT = 256 threads call it: wave p sums the terms k = p (mod 4) of every row i = lane
-// (fully unrolled, conflict-free: bank (i + k) mod 64), the four partial sums meet in LDS; three barriers.
-template <int NC>
+// out[i] = (Z^T (Z v))_i = (K^{-1} v)_i for i < NI (v, out in LDS; out may alias v; part: NW x 64 + 64
+// floats of scratch).  All NT = 64 NW threads call it: wave p sums the terms k = p (mod NW) of every row
+// i = lane (fully unrolled, conflict-free: bank (i + k) mod 64), the NW partial sums meet in LDS (pairwise,
+// in a fixed order); three barriers.
+template <int NW>
+__device__ __forceinline__ float part_sum(const float* part, int i) {
+    if constexpr (NW == 4) return (part[i] + part[64 + i]) + (part[128 + i] + part[192 + i]);
+    else return part_sum<NW / 2>(part, i) + part_sum<NW / 2>(part + 64 * (NW / 2), i);
+}
+
+template <int NC, int NT>
 __device__ __forceinline__ void kinv_apply(const float* __restrict__ z, const float* v, float* part, float* out) {
-    constexpr int NI = (NC - 1) * (NC + 1), NM = (NI + 3) / 4;
+    constexpr int NW = NT / 64, NI = (NC - 1) * (NC + 1), NM = (NI + NW - 1) / NW;
     const int i = threadIdx.x & 63, p = threadIdx.x >> 6;
     float a = 0.f;
 #pragma unroll
     for (int m = 0; m < NM; ++m) {            // (Z v)_i = sum_{k <= i} Z[i][k] v_k
-        const int k = 4 * m + p;
+        const int k = NW * m + p;
         if (k < NI) a = fmaf((k <= i && i < NI) ? z[i * KINV_P + k] : 0.f, v[k], a);
     }
     part[p * 64 + i] = a;
     __syncthreads();
-    float* w = part + 256;                    // (Z v), 64 floats
-    if (threadIdx.x < 64) w[i] = (part[i] + part[64 + i]) + (part[128 + i] + part[192 + i]);
+    float* w = part + 64 * NW;                // (Z v), 64 floats
+    if (threadIdx.x < 64) w[i] = part_sum<NW>(part, i);
     __syncthreads();
     a = 0.f;
 #pragma unroll
     for (int m = 0; m < NM; ++m) {            // (Z^T w)_i = sum_{k >= i} Z[k][i] w_k
-        const int k = 4 * m + p;
+        const int k = NW * m + p;
         if (k < NI) a = fmaf((k >= i && i < NI) ? z[k * KINV_P + i] : 0.f, w[k], a);
     }
     part[p * 64 + i] = a;
     __syncthreads();
-    if (threadIdx.x < NI) out[i] = (part[i] + part[64 + i]) + (part[128 + i] + part[192 + i]);
+    if (threadIdx.x < NI) out[i] = part_sum<NW>(part, i);
     __syncthreads();
 }
 
-template <int NC>
-__global__ __launch_bounds__(ROM_NT) void rom_kernel_fast(gpi_rom_desc d, RomDims D) {
+// NT threads per sample (256 / 512 / 1024): SUB = NT / 64 threads share one coarse square of the
+// prolongation (nc = 8: 64 squares; nc = 4 uses 16 of them), so a wider workgroup has more waves in flight
+// over the 4095 fine nodes; the factorisation stays in wave 0.
+template <int NC, int NT>
+__global__ __launch_bounds__(NT) void rom_kernel_fast(gpi_rom_desc d, RomDims D) {
     constexpr int W = NC, BW = NC - 1, NI = (NC - 1) * (NC + 1), NN = (NC + 1) * (NC + 1), NT2 = 2 * NC * NC;
-    constexpr int PF = 3 * ROM_U;            // prefetched fine nodes per thread (a square holds <= (r+1) r)
+    constexpr int SUB = NT / 64, NW = NT / 64;
+    constexpr int PF = (SUB >= 8 ? 1 : 3) * ROM_U;   // prefetched fine nodes per thread (a square holds <= (r+1) r)
     extern __shared__ __attribute__((aligned(16))) float sm[];
     float* kp = sm;                   // [NT2] kappa
     float* L = kp + NT2;              // [NI * W]
@@ -524,9 +538,9 @@ __global__ __launch_bounds__(ROM_NT) void rom_kernel_fast(gpi_rom_desc d, RomDim
     float* lam = b + NI;              // [NN]
     float* dinv = lam + NN;           // [NI]
     float* kinv = dinv + NI;          // [NI][KINV_P]: Z = L^{-1}
-    float* part = kinv + NI * KINV_P; // [320] kinv_apply scratch
-    double* du = (double*)(sm + ((NT2 + NI * W + 2 * NN + 2 * NI + NI * KINV_P + 320 + 1) & ~1));   // [NN]
-    double* lred = du + NN;           // [ROM_NT / 64]
+    float* part = kinv + NI * KINV_P; // [64 NW + 64] kinv_apply scratch
+    double* du = (double*)(sm + ((NT2 + NI * W + 2 * NN + 2 * NI + NI * KINV_P + 64 * NW + 64 + 1) & ~1));   // [NN]
+    double* lred = du + NN;           // [NW]
     const int s = blockIdx.x;
     const int tid = threadIdx.x;
     const float* x = d.x + (int64_t)s * d.x_stride;
@@ -535,7 +549,7 @@ __global__ __launch_bounds__(ROM_NT) void rom_kernel_fast(gpi_rom_desc d, RomDim
     RPHASE(0);
 
     // ---- entry: every global read in flight (kappa, F, and this thread's first PF fine nodes)
-    const int q0 = tid >> 2, sub = tid & 3;
+    const int q0 = tid / SUB, sub = tid & (SUB - 1);
     float ypf[PF], lpf[PF];
     {
         const bool okq = q0 < NC * NC && d.mode == GPI_ROM_LOGLIK;
@@ -546,7 +560,7 @@ __global__ __launch_bounds__(ROM_NT) void rom_kernel_fast(gpi_rom_desc d, RomDim
         const uint32_t mcol = (ncol > 1 ? (uint32_t)(((1ull << 32) + ncol - 1) / ncol) : 0u);   // e / ncol = umulhi(e, mcol), e < 2^16
 #pragma unroll
         for (int k = 0; k < PF; ++k) {
-            const int e = sub + 4 * k;
+            const int e = sub + SUB * k;
             const bool ok = okq && e < total;
             const int jj = ok ? (mcol ? (int)__umulhi((uint32_t)e, mcol) : e) : 0, ii = ok ? e - jj * ncol : 0;
             const int pp = (J * r + jj) * (nf - 1) + (i0 + ii - 1);
@@ -555,19 +569,19 @@ __global__ __launch_bounds__(ROM_NT) void rom_kernel_fast(gpi_rom_desc d, RomDim
         }
     }
     bool bad = false;
-    for (int t = tid; t < NT2; t += ROM_NT) {
+    for (int t = tid; t < NT2; t += NT) {
         const float kv = d.input_kappa ? x[t] : expf(x[t]) + 1e-8f;
         bad |= !(kv > 1e-12f);
         kp[t] = kv;
     }
     if (bad && d.flag) atomicOr(d.flag, 1);
-    for (int e = tid; e < NN; e += ROM_NT) {
+    for (int e = tid; e < NN; e += NT) {
         du[e] = (d.mode == GPI_ROM_BACKWARD && d.duc) ? (double)d.duc[(int64_t)s * NN + e] : 0.0;
         lam[e] = 0.f;
     }
     __syncthreads();
     // ---- assemble the interior system (banded lower) + rhs
-    for (int ii = tid; ii < NI; ii += ROM_NT) {
+    for (int ii = tid; ii < NI; ii += NT) {
         const int J = ii / (NC - 1), I = ii - J * (NC - 1) + 1;
         const int p = I + (NC + 1) * J;
         const float chl = c_h(kp, NC, I - 1, J), chr = c_h(kp, NC, I, J);
@@ -596,21 +610,21 @@ __global__ __launch_bounds__(ROM_NT) void rom_kernel_fast(gpi_rom_desc d, RomDim
     RPHASE(6);
     __syncthreads();
     // interior coarse solution u_I = K^{-1} b = Z^T (Z b), in place of b
-    kinv_apply<NC>(kinv, b, part, b);
+    kinv_apply<NC, NT>(kinv, b, part, b);
     RPHASE(2);
-    for (int e = tid; e < NN; e += ROM_NT) {
+    for (int e = tid; e < NN; e += NT) {
         const int I = e % (NC + 1), J = e / (NC + 1);
         u[e] = (I == 0 || I == NC) ? F[e] : b[J * (NC - 1) + (I - 1)];
     }
     __syncthreads();
-    if (d.uc) for (int e = tid; e < NN; e += ROM_NT) d.uc[(int64_t)s * NN + e] = u[e];
+    if (d.uc) for (int e = tid; e < NN; e += NT) d.uc[(int64_t)s * NN + e] = u[e];
 
     // ---- prolongation (+ log-likelihood, + W^T of the output gradient), as rom_kernel; the first
     // PF nodes of every thread's square from the entry prefetch
     const float rinv = 1.f / (float)r;
     float Lsum = 0.f;
     const bool want_g = d.mode == GPI_ROM_LOGLIK || (d.mode == GPI_ROM_BACKWARD && d.dmu);
-    for (int qb = 0; qb < NC * NC; qb += ROM_NT / 4) {
+    for (int qb = 0; qb < NC * NC; qb += NT / SUB) {
         const int q = qb + q0;
         float acc[4] = {0.f, 0.f, 0.f, 0.f};
         int v0 = 0;
@@ -622,14 +636,14 @@ __global__ __launch_bounds__(ROM_NT) void rom_kernel_fast(gpi_rom_desc d, RomDim
             const int rows = J == NC - 1 ? r + 1 : r;
             const int ncol = i1 - i0 + 1, total = rows * ncol;
             const uint32_t mcol = (ncol > 1 ? (uint32_t)(((1ull << 32) + ncol - 1) / ncol) : 0u);
-            for (int e0 = sub; e0 < total; e0 += 4 * ROM_U) {
-                const int bi = (e0 - sub) / (4 * ROM_U);
+            for (int e0 = sub; e0 < total; e0 += SUB * ROM_U) {
+                const int bi = (e0 - sub) / (SUB * ROM_U);
                 const bool pre = qb == 0 && bi < PF / ROM_U;
                 int pp[ROM_U];
                 float yv[ROM_U], lv[ROM_U], gv[ROM_U];
 #pragma unroll
                 for (int k = 0; k < ROM_U; ++k) {
-                    const int e = min(e0 + 4 * k, total - 1);
+                    const int e = min(e0 + SUB * k, total - 1);
                     const int jj = (mcol ? (int)__umulhi((uint32_t)e, mcol) : e), ii = e - jj * ncol;
                     pp[k] = (J * r + jj) * (nf - 1) + (i0 + ii - 1);
                 }
@@ -637,8 +651,13 @@ __global__ __launch_bounds__(ROM_NT) void rom_kernel_fast(gpi_rom_desc d, RomDim
                     if (pre) {
 #pragma unroll
                         for (int k = 0; k < ROM_U; ++k) {
-                            yv[k] = bi == 0 ? ypf[k] : (bi == 1 ? ypf[ROM_U + k] : ypf[2 * ROM_U + k]);
-                            lv[k] = bi == 0 ? lpf[k] : (bi == 1 ? lpf[ROM_U + k] : lpf[2 * ROM_U + k]);
+                            if constexpr (PF == ROM_U) {
+                                yv[k] = ypf[k];
+                                lv[k] = lpf[k];
+                            } else {
+                                yv[k] = bi == 0 ? ypf[k] : (bi == 1 ? ypf[ROM_U + k] : ypf[2 * ROM_U + k]);
+                                lv[k] = bi == 0 ? lpf[k] : (bi == 1 ? lpf[ROM_U + k] : lpf[2 * ROM_U + k]);
+                            }
                         }
                     } else {
 #pragma unroll
@@ -653,7 +672,7 @@ __global__ __launch_bounds__(ROM_NT) void rom_kernel_fast(gpi_rom_desc d, RomDim
                 }
 #pragma unroll
                 for (int k = 0; k < ROM_U; ++k) {
-                    const int e = e0 + 4 * k;
+                    const int e = e0 + SUB * k;
                     if (e >= total) break;
                     const int jj = (mcol ? (int)__umulhi((uint32_t)e, mcol) : e), ii = e - jj * ncol;
                     const float xi = (float)(i0 + ii - I * r) * rinv, eta = (float)jj * rinv;
@@ -684,10 +703,9 @@ __global__ __launch_bounds__(ROM_NT) void rom_kernel_fast(gpi_rom_desc d, RomDim
         }
         if (want_g) {
 #pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                acc[c] += __shfl_xor(acc[c], 1, 64);
-                acc[c] += __shfl_xor(acc[c], 2, 64);
-            }
+            for (int c = 0; c < 4; ++c)
+#pragma unroll
+                for (int o = 1; o < SUB; o <<= 1) acc[c] += __shfl_xor(acc[c], o, 64);
             if (q < NC * NC && sub == 0) {
                 atomicAdd(&du[v0], (double)acc[0]);
                 atomicAdd(&du[v0 + 1], (double)acc[1]);
@@ -704,7 +722,7 @@ __global__ __launch_bounds__(ROM_NT) void rom_kernel_fast(gpi_rom_desc d, RomDim
         if (tid == 0 && d.loss_acc) {
             double t = lred[0];
 #pragma unroll
-            for (int w = 1; w < ROM_NT / 64; ++w) t += lred[w];
+            for (int w = 1; w < NW; ++w) t += lred[w];
             atomicAdd(d.loss_acc + blockIdx.x % GPI_REPLICAS, t);
         }
     }
@@ -712,20 +730,20 @@ __global__ __launch_bounds__(ROM_NT) void rom_kernel_fast(gpi_rom_desc d, RomDim
     __syncthreads();
     RPHASE(3);
     // ---- adjoint lambda = K^{-1} (W^T dmu)_interior = Z^T (Z r)
-    for (int ii = tid; ii < NI; ii += ROM_NT) {
+    for (int ii = tid; ii < NI; ii += NT) {
         const int J = ii / (NC - 1), I = ii - J * (NC - 1) + 1;
         b[ii] = (float)du[I + (NC + 1) * J];
     }
     __syncthreads();
-    kinv_apply<NC>(kinv, b, part, b);
-    for (int ii = tid; ii < NI; ii += ROM_NT) {
+    kinv_apply<NC, NT>(kinv, b, part, b);
+    for (int ii = tid; ii < NI; ii += NT) {
         const int J = ii / (NC - 1), I = ii - J * (NC - 1) + 1;
         lam[I + (NC + 1) * J] = b[ii];
     }
     __syncthreads();
     RPHASE(4);
     // ---- dJ/dx per coarse triangle
-    for (int t = tid; t < NT2; t += ROM_NT) {
+    for (int t = tid; t < NT2; t += NT) {
         const int q = t >> 1, ul = t & 1;
         const int I = q % NC, J = q / NC;
         const int v0 = I + (NC + 1) * J, v1 = v0 + 1, v2 = v0 + (NC + 1), v3 = v2 + 1;
@@ -739,11 +757,11 @@ __global__ __launch_bounds__(ROM_NT) void rom_kernel_fast(gpi_rom_desc d, RomDim
     RPHASE(5);
 }
 
-template <int NC>
+template <int NC, int NT>
 size_t rom_fast_lds() {
-    constexpr int W = NC, NI = (NC - 1) * (NC + 1), NN = (NC + 1) * (NC + 1), NT2 = 2 * NC * NC;
-    const size_t fl = ((NT2 + NI * W + 2 * NN + 2 * NI + NI * KINV_P + 320 + 1) & ~1);
-    return sizeof(float) * fl + sizeof(double) * (NN + ROM_NT / 64);
+    constexpr int W = NC, NI = (NC - 1) * (NC + 1), NN = (NC + 1) * (NC + 1), NT2 = 2 * NC * NC, NW = NT / 64;
+    const size_t fl = ((NT2 + NI * W + 2 * NN + 2 * NI + NI * KINV_P + 64 * NW + 64 + 1) & ~1);
+    return sizeof(float) * fl + sizeof(double) * (NN + NW);
 }
 
 // Coarse solutions only (FORWARD without mu_y: the VO MC predictive, N_vo x N_mc samples), nc = 4 / 8:
@@ -908,11 +926,18 @@ extern "C" int gpi_rom(const gpi_rom_desc* d, void* stream) {
     }
     static const bool slow = getenv("GPI_ROM_SLOW") && atoi(getenv("GPI_ROM_SLOW"));   // A/B: the r02 kernel
     if ((d->nc == 8 || d->nc == 4) && !slow) {
-        const size_t lds = d->nc == 8 ? rom_fast_lds<8>() : rom_fast_lds<4>();
-        if (d->nc == 8)
-            hipLaunchKernelGGL(rom_kernel_fast<8>, dim3(d->n), dim3(ROM_NT), lds, (hipStream_t)stream, *d, D);
+        // nc = 8: the workgroup width (GPI_ROM_FAST_NT = 256 / 512 / 1024; r03 A/B in DESIGN.md)
+        static const int fnt = getenv("GPI_ROM_FAST_NT") ? atoi(getenv("GPI_ROM_FAST_NT")) : GPI_ROM_FAST_NT_DEFAULT;
+        const size_t lds_8_1024 = rom_fast_lds<8, 1024>(), lds_8_512 = rom_fast_lds<8, 512>();
+        const size_t lds_8_256 = rom_fast_lds<8, 256>(), lds_4_256 = rom_fast_lds<4, 256>();
+        if (d->nc == 8 && fnt == 1024)
+            hipLaunchKernelGGL((rom_kernel_fast<8, 1024>), dim3(d->n), dim3(1024), lds_8_1024, (hipStream_t)stream, *d, D);
+        else if (d->nc == 8 && fnt == 512)
+            hipLaunchKernelGGL((rom_kernel_fast<8, 512>), dim3(d->n), dim3(512), lds_8_512, (hipStream_t)stream, *d, D);
+        else if (d->nc == 8)
+            hipLaunchKernelGGL((rom_kernel_fast<8, 256>), dim3(d->n), dim3(256), lds_8_256, (hipStream_t)stream, *d, D);
         else
-            hipLaunchKernelGGL(rom_kernel_fast<4>, dim3(d->n), dim3(ROM_NT), lds, (hipStream_t)stream, *d, D);
+            hipLaunchKernelGGL((rom_kernel_fast<4, 256>), dim3(d->n), dim3(256), lds_4_256, (hipStream_t)stream, *d, D);
         GPI_CHECK_LAUNCH();
         return GPI_OK;
     }
