@@ -272,6 +272,9 @@ class PredictionEnsemble(object):
                     self.writer.add_scalar('PredictionEnsemble/KLD', KLD.item(), global_step=step)
                     self.writer.add_scalar('PredictionEnsemble/AvgLatentStddev',
                                            torch.mean(torch.exp(self._q_z.logsigma)), global_step=step)
+                # the native engine did this optimizer's steps: tell torch's scheduler hook (as
+                # FusedElboStep does), so it does not warn of a scheduler step before any optimizer step
+                self._optimizer._opt_called = True
                 self._scheduler_wrapper.step('validation', None, None, None, elbo)
         return elbo
 

@@ -46,7 +46,7 @@ class _Writer(object):
         self.d = {}
 
     def add_scalar(self, k, v, global_step=None):
-        self.d[k] = float(v)
+        self.d[k] = float(v.detach()) if hasattr(v, "detach") else float(v)
 
 
 def build(d):

@@ -10,6 +10,7 @@ FOM labels on the GPU), torch Adam over model.parameters(), LearningScheduleWrap
 PredictionEnsemble; then the same with the fused graph-captured step.  The ELBO must rise (the
 objective is maximised): mean of the last 10 steps above the mean of the first 10, all finite."""
 import math
+import warnings
 
 import numpy as np
 import pytest
@@ -49,14 +50,18 @@ def test_trainer_loop_module_path(device, tmp_path):
     sw.register_optimizer(opt, 'training')
     pe = PredictionEnsemble(model, val, sw, lr=1e-2)
     elbos = []
-    for n in range(N_STEPS):
-        opt.zero_grad()
-        elbo = model.elbo(step=n, armortized_bs=32)
-        (-elbo).backward()
-        opt.step()
-        pe.update(3, step=n)
-        sw.step('training', metric=elbo)
-        elbos.append(elbo.item())
+    with warnings.catch_warnings():
+        # the PredictionEnsemble's native q_z update reports its optimizer step to torch's scheduler
+        # hook (no "lr_scheduler.step() before optimizer.step()" warning for the 'validation' schedule)
+        warnings.filterwarnings('error', message='.*lr_scheduler.step.*')
+        for n in range(N_STEPS):
+            opt.zero_grad()
+            elbo = model.elbo(step=n, armortized_bs=32)
+            (-elbo).backward()
+            opt.step()
+            pe.update(3, step=n)
+            sw.step('training', metric=elbo)
+            elbos.append(elbo.item())
     assert all(math.isfinite(e) for e in elbos)
     assert np.mean(elbos[-10:]) > np.mean(elbos[:10]), elbos
     assert opt.param_groups[0]['lr'] == pytest.approx(1e-3, rel=1e-6)     # two milestones x sqrt(0.1)
@@ -77,7 +82,6 @@ def test_trainer_loop_fused_step(device, tmp_path):
     sw.register_optimizer(step.optimizer, 'training')
     step.capture()
     elbos = []
-    import warnings
     with warnings.catch_warnings():
         # the fused step reports its optimizer step to torch's scheduler hook (no "lr_scheduler.step()
         # before optimizer.step()" warning)
