@@ -489,8 +489,12 @@ def main():
                 traffic_note = 'PMC traffic file measured on other conv.hip code: dropped'
             else:
                 t = tj['ops'].get(name)
-                traffic = round(t['traffic_bytes']) if t else None
-                traffic_note = '%s (PMC FETCH_SIZE / WRITE_SIZE passes)' % os.path.basename(TRAFFIC_JSON)
+                if t and abs(t.get('algorithmic_bytes', -1) - byts) > 0.5:
+                    # the file's entry is this operator at another shape (e.g. the c64 record on a c128 run)
+                    traffic_note = 'PMC traffic file measured on another workload shape: dropped'
+                else:
+                    traffic = round(t['traffic_bytes']) if t else None
+                    traffic_note = '%s (PMC FETCH_SIZE / WRITE_SIZE passes)' % os.path.basename(TRAFFIC_JSON)
         step_ach = sbytes / (ms_step * 1e-3) / 1e9
         # the dominant launch's bound by its arithmetic intensity: above the fp32 ridge (19.7 flop/B) it is
         # compute-bound (the fused 5x5 output conv: 30 flop/B), priced against the fp32 peak; below it
