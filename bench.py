@@ -44,7 +44,19 @@ RIDGE_FLOP_PER_B = F32_PEAK_TFS * 1e12 / (HBM_PEAK_GBS * 1e9)   # 19.7 flop/B
 # HBM traffic per launch of the heaviest operators, from two separate rocprofv3 PMC
 # passes (FETCH_SIZE, WRITE_SIZE) over tools/kprobe.py: tools/profile_round.sh +
 # tools/pmc_traffic.py.  Used for roofline.traffic when the dominant operator is listed.
-TRAFFIC_JSON = os.path.join(ROOT, 'profiles', 'r03h_traffic.json')
+# One file per bench configuration (the entry for an operator is used only when it was measured on this
+# conv.hip / common.h and at this run's algorithmic bytes, i.e. the same shape).
+TRAFFIC_FILES = {'c64': ['r04_traffic.json', 'r03h_traffic.json'], 'c128': ['r04_traffic_c128.json'],
+                 'c256': ['r04_traffic_c256.json'], 'c32': ['r04_traffic_c32.json']}
+
+
+def traffic_json(config):
+    """The newest existing PMC traffic file of a bench configuration (or None)."""
+    for f in TRAFFIC_FILES.get(config, []):
+        p = os.path.join(ROOT, 'profiles', f)
+        if os.path.exists(p):
+            return p
+    return None
 
 CONFIGS = {
     # name: (factory, B_u, N_s, pool, field params (mean, std, corrlength))
@@ -481,20 +493,23 @@ def main():
         ach_tf = flops / (ms * 1e-3) / 1e12
         ai = flops / byts
         traffic = None
-        traffic_note = 'no PMC traffic file'
-        if os.path.exists(TRAFFIC_JSON):
-            with open(TRAFFIC_JSON) as fh:
+        traffic_note = 'no PMC traffic file for %s' % args.config
+        tjp = traffic_json(args.config)
+        if tjp is not None:
+            with open(tjp) as fh:
                 tj = json.load(fh)
             if tj.get('conv_hip_sha1') != conv_source_sha():
-                traffic_note = 'PMC traffic file measured on other conv.hip code: dropped'
+                traffic_note = '%s measured on other conv.hip code: dropped' % os.path.basename(tjp)
             else:
                 t = tj['ops'].get(name)
-                if t and abs(t.get('algorithmic_bytes', -1) - byts) > 0.5:
+                if t is None:
+                    traffic_note = '%s has no entry for %s' % (os.path.basename(tjp), name)
+                elif abs(t.get('algorithmic_bytes', -1) - byts) > 0.5:
                     # the file's entry is this operator at another shape (e.g. the c64 record on a c128 run)
-                    traffic_note = 'PMC traffic file measured on another workload shape: dropped'
+                    traffic_note = '%s measured on another workload shape: dropped' % os.path.basename(tjp)
                 else:
-                    traffic = round(t['traffic_bytes']) if t else None
-                    traffic_note = '%s (PMC FETCH_SIZE / WRITE_SIZE passes)' % os.path.basename(TRAFFIC_JSON)
+                    traffic = round(t['traffic_bytes'])
+                    traffic_note = '%s (PMC FETCH_SIZE / WRITE_SIZE passes)' % os.path.basename(tjp)
         step_ach = sbytes / (ms_step * 1e-3) / 1e9
         # the dominant launch's bound by its arithmetic intensity: above the fp32 ridge (19.7 flop/B) it is
         # compute-bound (the fused 5x5 output conv: 30 flop/B), priced against the fp32 peak; below it
@@ -502,7 +517,12 @@ def main():
         hbm = dict(achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit='GB/s', frac=round(ach / HBM_PEAK_GBS, 4))
         cmp_ = dict(achieved=round(ach_tf, 2), peak=F32_PEAK_TFS, unit='TFLOP/s', frac=round(ach_tf / F32_PEAK_TFS, 4))
         main = cmp_ if ai >= RIDGE_FLOP_PER_B else hbm
-        roof = dict(bound='mfma' if ai >= RIDGE_FLOP_PER_B else 'hbm', achieved=main['achieved'], peak=main['peak'],
+        # bound: the contract's roofline name ('mfma' = the compute roofline, priced at the fp32 peak, which
+        # the packed-VALU v_pk_fma_f32 and the fp32 MFMA share); limiter: what actually issues the flops
+        roof = dict(bound='mfma' if ai >= RIDGE_FLOP_PER_B else 'hbm',
+                    limiter=('fp32 compute (VALU v_pk_fma_f32 forward / input gradient, MFMA weight gradient)'
+                             if ai >= RIDGE_FLOP_PER_B else 'HBM bandwidth'),
+                    achieved=main['achieved'], peak=main['peak'],
                     unit=main['unit'], frac=main['frac'], traffic=traffic, traffic_source=traffic_note, kernel=name,
                     kernel_ms=round(ms, 5), bytes_per_launch=byts, flops_per_launch=flops,
                     arithmetic_intensity=round(ai, 2), ridge=round(RIDGE_FLOP_PER_B, 2), hbm=hbm, compute=cmp_,

@@ -179,6 +179,85 @@ __global__ __launch_bounds__(256) void subset_rank_kernel(int32_t* out, int32_t 
     if (i < n && part == 0 && cnt < k) out[cnt] = i;
 }
 
+// Any pool size (gpi_random_subset_ws): the same order -- the first k of the n indices by (Philox key,
+// index) -- without all n keys in one workgroup's LDS.  The keys are uniform 32-bit values, so a
+// histogram of their top 16 bits finds the bin b* where the count of smaller-or-equal keys first reaches
+// k; every key whose top bits are <= b* is a candidate (about k + n / 65536 of them), every other key
+// is larger than all candidates, so the first k pairs in the global order are the first k among the
+// candidates, ranked as above.  Five small launches: zero, histogram, scan (b*), compact, rank.
+constexpr int SUB_BINS = 1 << 16;
+
+__global__ __launch_bounds__(256) void subset_zero_kernel(uint32_t* w, int32_t nwords) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < nwords) w[i] = 0u;
+}
+
+__global__ __launch_bounds__(256) void subset_hist_kernel(uint32_t* hist, int32_t n, uint64_t seed,
+                                                          const uint64_t* offset, uint64_t sub) {
+    const int j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= n) return;
+    const uint64_t base = offset ? *offset : 0;
+    atomicAdd(&hist[philox(base + (uint64_t)j, sub, seed).x >> 16], 1u);
+}
+
+// one workgroup of 1024 threads, thread t owning bins [64 t, 64 t + 64): ctl[0] = b*, ctl[1] = 0
+__global__ __launch_bounds__(1024) void subset_scan_kernel(const uint32_t* hist, uint32_t* ctl, int32_t k) {
+    __shared__ uint32_t part[1024];
+    const int t = threadIdx.x;
+    uint32_t s = 0;
+    for (int b = 0; b < 64; ++b) s += hist[64 * t + b];
+    part[t] = s;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {      // inclusive Hillis-Steele scan
+        const uint32_t v = t >= o ? part[t - o] : 0u;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    const uint32_t ex = part[t] - s;
+    if (ex < (uint32_t)k && (uint32_t)k <= part[t]) {
+        uint32_t c = ex;
+        for (int b = 0; b < 64; ++b) {
+            c += hist[64 * t + b];
+            if (c >= (uint32_t)k) {
+                ctl[0] = (uint32_t)(64 * t + b);
+                break;
+            }
+        }
+    }
+    if (t == 0) ctl[1] = 0u;
+}
+
+__global__ __launch_bounds__(256) void subset_compact_kernel(uint2* cand, uint32_t* ctl, int32_t n, uint64_t seed,
+                                                             const uint64_t* offset, uint64_t sub) {
+    const int j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= n) return;
+    const uint64_t base = offset ? *offset : 0;
+    const uint32_t key = philox(base + (uint64_t)j, sub, seed).x;
+    if ((key >> 16) <= ctl[0]) {
+        const uint32_t slot = atomicAdd(&ctl[1], 1u);
+        cand[slot] = make_uint2(key, (uint32_t)j);
+    }
+}
+
+// one wave per candidate (grid-stride over the waves): its rank among all C candidates
+__global__ __launch_bounds__(256) void subset_cand_rank_kernel(int32_t* out, const uint2* cand, const uint32_t* ctl,
+                                                               int32_t k) {
+    const int C = (int)ctl[1];
+    const int lane = threadIdx.x & 63;
+    const int nw = gridDim.x * 4;
+    for (int w = blockIdx.x * 4 + (threadIdx.x >> 6); w < C; w += nw) {
+        const uint2 me = cand[w];
+        int cnt = 0;
+        for (int j = lane; j < C; j += 64) {
+            const uint2 o = cand[j];
+            cnt += (o.x < me.x || (o.x == me.x && o.y < me.y)) ? 1 : 0;
+        }
+        for (int m = 32; m > 0; m >>= 1) cnt += __shfl_xor(cnt, m, 64);
+        if (lane == 0 && cnt < k) out[cnt] = (int32_t)me.y;
+    }
+}
+
 }  // namespace
 
 extern "C" int gpi_version(void) { return 1; }
@@ -291,6 +370,37 @@ extern "C" int gpi_dropout_masks(float* out, int64_t n, float p, uint64_t seed, 
 extern "C" int gpi_rng_advance(uint64_t* offset, uint64_t by, void* stream) {
     if (!offset) return GPI_ERR_ARG;
     hipLaunchKernelGGL(rng_advance_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, offset, by);
+    GPI_CHECK_LAUNCH();
+    return GPI_OK;
+}
+
+extern "C" int gpi_random_subset_workspace(int32_t n, int64_t* bytes) {
+    if (n <= 0 || !bytes) return GPI_ERR_ARG;
+    *bytes = (int64_t)sizeof(uint32_t) * (SUB_BINS + 64) + (int64_t)sizeof(uint2) * n;
+    return GPI_OK;
+}
+
+extern "C" int gpi_random_subset(int32_t* out, int32_t n, int32_t k, uint64_t seed, const uint64_t* offset,
+                                 uint64_t sub, void* stream);
+
+extern "C" int gpi_random_subset_ws(int32_t* out, int32_t n, int32_t k, uint64_t seed, const uint64_t* offset,
+                                    uint64_t sub, void* workspace, int64_t ws_bytes, void* stream) {
+    if (!out || n <= 0 || k < 0 || k > n) return GPI_ERR_ARG;
+    if (k == 0) return GPI_OK;
+    if (n <= 16384) return gpi_random_subset(out, n, k, seed, offset, sub, stream);
+    int64_t need = 0;
+    gpi_random_subset_workspace(n, &need);
+    if (!workspace || ws_bytes < need || ((uintptr_t)workspace & 15)) return GPI_ERR_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    uint32_t* hist = (uint32_t*)workspace;
+    uint32_t* ctl = hist + SUB_BINS;
+    uint2* cand = (uint2*)(ctl + 64);
+    const unsigned gn = (unsigned)((n + 255) / 256);
+    hipLaunchKernelGGL(subset_zero_kernel, dim3((SUB_BINS + 64 + 255) / 256), dim3(256), 0, st, hist, SUB_BINS + 64);
+    hipLaunchKernelGGL(subset_hist_kernel, dim3(gn), dim3(256), 0, st, hist, n, seed, offset, sub);
+    hipLaunchKernelGGL(subset_scan_kernel, dim3(1), dim3(1024), 0, st, hist, ctl, k);
+    hipLaunchKernelGGL(subset_compact_kernel, dim3(gn), dim3(256), 0, st, cand, ctl, n, seed, offset, sub);
+    hipLaunchKernelGGL(subset_cand_rank_kernel, dim3(512), dim3(256), 0, st, out, cand, ctl, k);
     GPI_CHECK_LAUNCH();
     return GPI_OK;
 }

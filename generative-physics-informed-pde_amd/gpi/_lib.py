@@ -206,6 +206,8 @@ SIGNATURES = {
     'gpi_dropout_masks': (C.c_int, [vp, i64, f32, u64, vp, u64, vp]),
     'gpi_rng_advance': (C.c_int, [vp, u64, vp]),
     'gpi_random_subset': (C.c_int, [vp, i32, i32, u64, vp, u64, vp]),
+    'gpi_random_subset_workspace': (C.c_int, [i32, C.POINTER(i64)]),
+    'gpi_random_subset_ws': (C.c_int, [vp, i32, i32, u64, vp, u64, vp, i64, vp]),
     'gpi_vo_rows': (C.c_int, [i32, i32, i32]),
     'gpi_vo_query': (C.c_int, [C.POINTER(VoQueryDesc), vp]),
     'gpi_vo_moments': (C.c_int, [C.POINTER(VoMomentsDesc), vp]),

@@ -606,7 +606,7 @@ class ElboEngine(object):
         if self.ep is None:
             return
         if self.bn_sync is not None and self.enc_descs[0].gout_mode == 0:
-            self._sync_stats(self.enc_descs[0].out_stat, self.enc_descs[0].cout, 2)
+            self._sync_stats(self.enc_descs[0].out_stat, self.enc_descs[0].cout, 2, 'enc')
         _run(_lib().gpi_conv_backward, C.byref(self.enc_descs[0]), C.byref(self.ectx), st, what='In_conv backward')
         run_reduce(self.reduce_enc[:self.n_reduce_in] if enc_split else self.reduce_enc, self.ws, self.flat, st)
 
@@ -645,11 +645,33 @@ class ElboEngine(object):
         over its one process's batch (codec.py:164-173 in train mode).  allreduce(t): in-place SUM
         over the ranks.  After each producing conv the fp64 channel sums {sum x, sum x^2} of its output
         are all-reduced (forward), and before each conv whose output feeds a BN the BN-backward sums
-        {sum S, sum S x-hat} of that output (backward) -- once per channel and phase.  The sums are
-        divided by the world size: the kernels divide by their per-rank count, so equal per-rank
-        batches give the global means.  The codec launches then go one by one (host hook between
-        them); running_var's Bessel factor keeps the per-rank count (N/(N-1) for N = per-rank
-        samples x pixels, >= 16384 here: a <1e-4 relative difference in the running buffer only)."""
+        {sum S, sum S x-hat} of that output (backward) -- once per channel and phase.  The kernels
+        divide a sum by their own per-rank count n_r of the codec call's BN group, so the all-reduced
+        sum is scaled by n_r / N (N = the group's count over all ranks, all-reduced once here): the
+        global means for any per-rank batch sizes.  Every rank must run the same BN groups (a term
+        with samples on some ranks only is refused).  The codec launches then go one by one (host
+        hook between them); running_var's Bessel factor keeps the per-rank count (N/(N-1) for
+        N = per-rank samples x pixels, >= 16384 here: a <1e-4 relative difference in the running
+        buffer only)."""
+        # per-group sample counts: the encoder call (group 0), then the decoder's groups in order, and
+        # the term presence flags (B_u, N_s, N_vo > 0), all summed over the ranks in ONE collective
+        enc_n = [self.B_u if self.ep is not None else 0]
+        local = enc_n + list(self.dec_sizes) + [0] * (L.GPI_MAX_GROUPS - len(self.dec_sizes))
+        present = [float(n > 0) for n in (self.B_u, self.N_s, self.N_vo)]
+        t = torch.tensor([float(n) for n in local] + present, dtype=torch.float64, device=self.flat.P.device)
+        allreduce(t)
+        tot = t.cpu().tolist()
+        if any(abs(p * world - s) > 0.5 for p, s in zip(present, tot[len(local):])):
+            raise ValueError('SyncBN: every rank must run the same ELBO terms (B_u / N_s / N_vo > 0 on all or '
+                             'none of the ranks); got %s of %d ranks' % (tot[len(local):], world))
+        fac = [(n / g if g > 0 else 0.0) for n, g in zip(local, tot[:len(local)])]
+        dev = self.flat.P.device
+        # scale per (program, group): [GPI_MAX_GROUPS] for the encoder's and the decoder's stat slots
+        self.bn_scale = {'enc': torch.tensor([fac[0]] + [0.0] * (L.GPI_MAX_GROUPS - 1), dtype=torch.float64,
+                                             device=dev).view(-1, 1, 1),
+                         'dec': torch.tensor(fac[1:1 + L.GPI_MAX_GROUPS], dtype=torch.float64,
+                                             device=dev).view(-1, 1, 1)}
+        self.bn_global_counts = {'enc': tot[0], 'dec': tot[1:1 + len(self.dec_sizes)]}
         self.bn_sync = allreduce
         self.bn_world = int(world)
 
@@ -658,13 +680,18 @@ class ElboEngine(object):
         o = N_TERMS * R
         return self.ws.t_scr[o:o + R * G * self.ws.n_stats * 4].view(R, G, self.ws.n_stats, 4)
 
-    def _sync_stats(self, stat0, n, f0):
+    def _sync_stats(self, stat0, n, f0, kind):
+        """All-reduce the replica-folded sums of stat slots [stat0, stat0 + n), fields f0, f0 + 1, scaled
+        per BN group by n_rank / N_global (set_sync_bn), back into replica 0."""
         v = self._stats_view()
         sub = v[:, :, stat0:stat0 + n, f0:f0 + 2].sum(0)        # replicas folded: [groups, n, 2]
         self.bn_sync(sub)
-        sub.div_(self.bn_world)
+        sub.mul_(self.bn_scale[kind])
         v[:, :, stat0:stat0 + n, f0:f0 + 2] = 0.0
         v[0, :, stat0:stat0 + n, f0:f0 + 2] = sub
+
+    def _codec_kind(self, descs):
+        return 'enc' if self.ep is not None and descs is self.enc_descs else 'dec'
 
     def _codec_forward(self, descs, i0, i1, ctx, st, what):
         lib = _lib()
@@ -672,11 +699,12 @@ class ElboEngine(object):
             ptr = C.cast(C.byref(descs, i0 * C.sizeof(L.ConvDesc)), C.POINTER(L.ConvDesc))
             _run(lib.gpi_codec_forward, ptr, i1 - i0, C.byref(ctx), st, what=what)
             return
+        kind = self._codec_kind(descs)
         for i in range(i0, i1):
             d = descs[i]
             _run(lib.gpi_conv_forward, C.byref(d), C.byref(ctx), st, what=what)
             if d.epilogue == L.EPI_STORE_STATS and d.out_stat >= 0:
-                self._sync_stats(d.out_stat, d.cout, 0)
+                self._sync_stats(d.out_stat, d.cout, 0, kind)
 
     def _codec_backward(self, descs, i0, i1, ctx, st, what):
         """descs[i1 - 1] down to descs[i0] (gpi_codec_backward's order)."""
@@ -685,10 +713,11 @@ class ElboEngine(object):
             ptr = C.cast(C.byref(descs, i0 * C.sizeof(L.ConvDesc)), C.POINTER(L.ConvDesc))
             _run(lib.gpi_codec_backward, ptr, i1 - i0, C.byref(ctx), st, what=what)
             return
+        kind = self._codec_kind(descs)
         for i in range(i1 - 1, i0 - 1, -1):
             d = descs[i]
             if d.gout_mode == 0:          # its output feeds a BN: that BN's backward sums are complete
-                self._sync_stats(d.out_stat, d.cout, 2)
+                self._sync_stats(d.out_stat, d.cout, 2, kind)
             _run(lib.gpi_conv_backward, C.byref(d), C.byref(ctx), st, what=what)
 
     def _launch_roms(self):
@@ -710,8 +739,17 @@ class ElboEngine(object):
             torch.cuda.current_stream().wait_event(self._ev_join)
             self._pending_join = False
 
+    def _check_rom_written(self):
+        if self._rom_deferred:
+            # GPI_ROM_AT=backward with compute_value=False: the ROM (and its log-likelihood terms) runs
+            # with the backward's side work, so the terms are not written until backward() is enqueued
+            raise RuntimeError('ElboEngine: the ROM log-likelihood is deferred to the backward '
+                               '(rom_at="backward"); read the ELBO terms after backward()')
+
     def elbo_value(self, terms=None):
         """0-d ELBO from the term accumulators (or from a saved copy ``terms`` [N_TERMS * R])."""
+        if terms is None:
+            self._check_rom_written()
         t = self.ws.terms if terms is None else terms.view(N_TERMS, R).sum(1)
         su, ss, sv = self.su, self.ss, self.sv
         val = t.new_zeros(())
@@ -733,6 +771,7 @@ class ElboEngine(object):
 
     def terms(self):
         """Dictionary of the individual ELBO terms (host sync)."""
+        self._check_rom_written()
         t = self.ws.terms.cpu()
         out = {}
         gi = 0

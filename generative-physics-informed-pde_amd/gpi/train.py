@@ -64,8 +64,10 @@ class FusedElboStep(object):
             raise ValueError('FusedElboStep: world > 1 needs an explicit subset_seed shared by all ranks')
         self.engine = ElboEngine(model, self.B_u, self.N_s, normalize=normalize)
         # SyncBN: every codec call's BN statistics over the union of the ranks' batches (ElboEngine.set_sync_bn);
-        # default replica-BN (per-rank batch statistics, no collective in the codec)
-        self.sync_bn = bool(sync_bn) and bool(distributed) and self.world > 1
+        # default replica-BN (per-rank batch statistics, no collective in the codec).  Any distributed world
+        # size, 1 included: a one-rank NCCL job runs (and captures) the same per-conv collectives as the
+        # 8-GPU one (tools/dist_capture_probe.py --sync-bn)
+        self.sync_bn = bool(sync_bn) and bool(distributed)
         if self.sync_bn:
             pg = process_group
             self.engine.set_sync_bn(lambda t: dist.all_reduce(t, op=dist.ReduceOp.SUM, group=pg), self.world)
@@ -106,6 +108,11 @@ class FusedElboStep(object):
         if self.B_u and self.n_sub > n_pool:
             raise ValueError('the pool (%d) is smaller than the global armortized batch (%d)' % (n_pool, self.n_sub))
         self.n_pool = n_pool
+        self._subset_ws = None
+        if self.B_u and n_pool > 16384:
+            nb = C.c_int64(0)
+            L.check(L.lib().gpi_random_subset_workspace(n_pool, C.byref(nb)), 'random subset workspace')
+            self._subset_ws = torch.zeros(nb.value, dtype=torch.uint8, device=dev)
         drop_span = max([(p.drop_numel + 3) // 4 + 1 for p in (self.engine.ep, self.engine.dp)
                          if p is not None and p.drop_numel] or [0])
         self.rng_span = max(n_pool, (self.engine.B * self.engine.dz + 3) // 4 + 1,
@@ -142,9 +149,15 @@ class FusedElboStep(object):
 
     # ------------------------------------------------------------------
     def _launch_subset(self, st, idx, sub0=0):
-        if self.B_u:
+        if not self.B_u:
+            return
+        if self._subset_ws is None:       # pools up to 16384: one launch, the keys in LDS
             L.check(L.lib().gpi_random_subset(L.ptr(idx), self.n_pool, self.n_sub, self.subset_seed,
                                               L.ptr(self.rng_off), sub0 + 1, st), 'random subset')
+        else:                             # any pool (the reference's randperm(N) has no cap)
+            L.check(L.lib().gpi_random_subset_ws(L.ptr(idx), self.n_pool, self.n_sub, self.subset_seed,
+                                                 L.ptr(self.rng_off), sub0 + 1, L.ptr(self._subset_ws),
+                                                 self._subset_ws.numel(), st), 'random subset')
 
     def _launch_noise(self, st, idx, sub0=0, codecs=('enc', 'dec'), subset=True):
         """Random subset into ``idx`` and the reparametrisation noise into the engine's eps

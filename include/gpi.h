@@ -548,6 +548,14 @@ int gpi_dropout_masks(float* out, int64_t n, float p, uint64_t seed, const uint6
                       void* stream);
 /* Uniform random subset (randperm(n)[:k] semantics, utils/data.py:444). */
 int gpi_random_subset(int32_t* out, int32_t n, int32_t k, uint64_t seed, const uint64_t* offset, uint64_t sub, void* stream);
+/* The same subset for ANY pool size n (torch.randperm(N)[:k] of utils/data.py:441-445 accepts any N;
+ * gpi_random_subset keeps all n keys in one workgroup's LDS and refuses n > 16384): a 16-bit
+ * histogram of the keys selects the candidates that can be among the first k, which are then ranked.
+ * Bit-identical order to gpi_random_subset.  workspace: caller-owned device memory of at least
+ * gpi_random_subset_workspace(n) bytes, 16-byte aligned (no state kept between calls). */
+int gpi_random_subset_workspace(int32_t n, int64_t* bytes);
+int gpi_random_subset_ws(int32_t* out, int32_t n, int32_t k, uint64_t seed, const uint64_t* offset, uint64_t sub,
+                         void* workspace, int64_t ws_bytes, void* stream);
 
 /* ---- FOM data generation (setup side; reference utils/data.py:72-103 DataLoader.assemble ->
  * physics/LinearElliptic.py:85-101 solve, one PETSc LU per sample).  Batched Jacobi-preconditioned

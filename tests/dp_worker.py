@@ -21,6 +21,81 @@ import torch.distributed as dist  # noqa: E402
 
 B_U = 4          # per rank (global 8 of the fixture's pool of 16)
 NS_RANK = 2      # labeled samples per rank (fixture: 4)
+# BASELINE config 3's per-rank shape (C64 highres, droprate 0.2): B_u = 256 unlabeled of a shared pool of
+# 1024 per rank + N_s = 32 rank-owned labeled samples
+C64_BU, C64_NS, C64_POOL = 256, 32, 1024
+
+
+def c64_data(world, rank):
+    """Synthetic config-3 inputs: the shared unlabeled pool (same on every rank) and rank `rank`'s
+    labeled fields, targets and ROM boundary forces (tests/test_gpu_dist.py regenerates them)."""
+    n, nc = 64, 8
+    rng = np.random.default_rng(7)
+    Xu = rng.normal(0.3, 0.6, (C64_POOL * world, n, n)).astype(np.float32)
+    rr = np.random.default_rng(100 + rank)
+    Xs = rr.normal(0.3, 0.6, (C64_NS, n, n)).astype(np.float32)
+    Y = rr.normal(0.0, 0.3, (C64_NS, (n + 1) * (n - 1))).astype(np.float32)
+    F = np.zeros((C64_NS, (nc + 1) ** 2), dtype=np.float32)
+    bnodes = [e for e in range((nc + 1) ** 2) if e % (nc + 1) in (0, nc)]
+    F[:, bnodes] = rr.uniform(-0.5, 0.5, (C64_NS, len(bnodes)))
+    return Xu, Xs, Y, F
+
+
+def run_c64_sync(out):
+    """One SyncBN step of the NATIVE FusedElboStep at config 3's per-rank shape; records the inputs it
+    drew, the kernels' ReLU decisions (for the fp64 union-batch oracle), the local and all-reduced
+    gradients and the ELBO."""
+    import ctypes as C
+    from factories.model import ModelFactory
+    from gpi.train import FusedElboStep
+    from gpi import _lib as L
+    from gpu_masks import engine_relu_masks
+    from test_gpu_c64 import _DS
+    rank, world = int(os.environ['RANK']), int(os.environ['WORLD_SIZE'])
+    torch.cuda.set_device(0)
+    dist.init_process_group('gloo')
+    torch.manual_seed(0)                    # identical shared parameters (and q rows) on every rank
+    fac = ModelFactory.FromIdentifier('highres')
+    fac.set('device', 'cuda')
+    physics_, model, _, encoder, _, _ = fac.setup()
+    model.encoder = encoder.cuda()
+    Xu, Xs, Y, F = c64_data(world, rank)
+    cu = lambda a: torch.tensor(a, device='cuda')
+    model.register_datasets({'supervised': _DS(X=cu(Xs), Y=cu(Y), F_ROM_BC=cu(F)),
+                             'unsupervised': _DS(perm=None, X=cu(Xu))}, None,
+                            create_unsupervised_variational_approximation=False)
+    model.cuda()
+    step = FusedElboStep(model, cu(Xu), C64_BU, cu(Xs), cu(Y), cu(F), lr=1e-3, seed=50 + rank, subset_seed=9,
+                         distributed=True, rank=rank, world=world, sync_bn=True)
+    assert step.sync_bn and step.engine.bn_sync is not None
+    e = step.engine
+    rec = dict(idx=step.idx.cpu().numpy(), eps_z=e.eps_z().cpu().numpy(), eps_x=e.eps_x().cpu().numpy(),
+               P0=step.flat.P.cpu().numpy())
+    for key, dd in e.dropout_views().items():
+        for nm, v in dd.items():
+            rec['drop.%s.%s' % (key, nm)] = v.cpu().numpy()
+    step._forward_backward(epilogue=False)
+    masks = engine_relu_masks(e)            # before the epilogue clears the statistics
+    for call, mm in masks.items():
+        for nm, m in mm.items():
+            rec['mask.%s.%s' % (call, nm)] = m.numpy()
+    L.check(L.lib().gpi_step_epilogue(C.byref(step.epi), L.stream_handle()), 'step epilogue')
+    torch.cuda.synchronize()
+    rec['G_local'] = step.flat.G.cpu().numpy()
+    step.allreduce()
+    torch.cuda.synchronize()
+    rec['G_red'] = step.flat.G.cpu().numpy()
+    rec['n_shared'] = np.int64(step.flat.n_shared)
+    rec['elbo'] = np.float64(step.elbo().item())
+    names = [k for k, _ in model.named_parameters()]
+    rec['names'] = np.array(names)
+    rec['offsets'] = np.array([step.flat.name_offsets[k] for k in names])
+    for k, p in model.named_parameters():
+        rec['shape.' + k] = np.array(p.shape, dtype=np.int64)
+    rec['counts'] = np.array(e.bn_global_counts['dec'] + [e.bn_global_counts['enc']])
+    np.savez(os.path.join(out, 'rank%d.npz' % rank), **rec)
+    dist.barrier()
+    dist.destroy_process_group()
 
 
 def shard_model(d, rank, B_u=B_U, ns=NS_RANK):
@@ -80,4 +155,7 @@ def main(out, mode='replica'):
 
 
 if __name__ == '__main__':
-    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else 'replica')
+    if len(sys.argv) > 2 and sys.argv[2] == 'c64sync':
+        run_c64_sync(sys.argv[1])
+    else:
+        main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else 'replica')

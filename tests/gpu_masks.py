@@ -115,3 +115,21 @@ def engine_relu_masks(engine):
         r0 = engine.B_u + engine.N_s
         masks['dec_v'] = _program_masks(engine.dp, ws_np, stats, P, slice(r0, r0 + engine.N_vo), g, engine.N_vo)
     return masks
+
+
+def codec_engine_masks(e, B):
+    """The ReLU decisions of a standalone EncoderEngine / DecoderEngine (CNNEncoder / CNNDecoder module
+    path) after its forward: {BN layer: mask} over the B samples (one BN group), plus the encoder FC's
+    ('features.FC') for an encoder engine."""
+    torch.cuda.synchronize()
+    ws = e.ws
+    R, G = L.GPI_REPLICAS, L.GPI_MAX_GROUPS
+    scr = ws.t_scr.cpu().numpy()
+    o = N_TERMS * R
+    stats = replica_sums(scr[o:o + R * G * ws.n_stats * 4].reshape(R, G, ws.n_stats, 4))
+    ws_np = ws.t_ws.cpu().numpy()
+    masks = _program_masks(e.p, ws_np, stats, e.flat.P.detach().cpu().numpy(), slice(0, B), 0, B)
+    if 'hpre' in getattr(e, 'hb', {}) and e.p.kind == 'encoder':
+        hp = ws_np[e.hb['hpre']:e.hb['hpre'] + B * e.p.d_feat]
+        masks['features.FC'] = torch.tensor(hp.reshape(B, -1) > 0)
+    return masks

@@ -82,3 +82,11 @@ def test_fom_workspace_host_query(lib):
     assert L.gpi_fom_solve(C.byref(d), None) != 0
     r = lib.RandomFieldDesc()
     assert L.gpi_random_field(C.byref(r), None) != 0
+
+
+def test_random_subset_workspace_host_query(lib):
+    L = lib.lib()
+    nb = C.c_int64(0)
+    assert L.gpi_random_subset_workspace(1 << 20, C.byref(nb)) == 0
+    assert nb.value == 4 * ((1 << 16) + 64) + 8 * (1 << 20)
+    assert L.gpi_random_subset_workspace(0, C.byref(nb)) != 0

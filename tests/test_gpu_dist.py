@@ -154,3 +154,104 @@ def test_rccl_allreduce_captured_in_step_graph(device):
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert 'max |dP| = 0.000e+00' in r.stdout, r.stdout[-2000:]
+
+
+def test_rccl_sync_bn_captured_in_step_graph(device):
+    """SyncBN over RCCL inside the captured step (world size 1 on this box; the 8-GPU node runs the
+    same graph across ranks): the per-conv collectives of the BN batch sums (26 at C32, 46 at C64) are graph nodes, the
+    replays equal eager SyncBN steps bit for bit, and at one rank SyncBN agrees with replica-BN to
+    rounding."""
+    env = dict(os.environ)
+    env['PYTHONUNBUFFERED'] = '1'
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node=1',
+           '--master-addr=127.0.0.1', '--master-port=%d' % _free_port(),
+           os.path.join(os.path.dirname(HERE), 'tools', 'dist_capture_probe.py'), '--sync-bn']
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert 'max |dP| = 0.000e+00' in r.stdout, r.stdout[-2000:]
+    n = int(r.stdout.split('SyncBN (')[1].split()[0])
+    assert n >= 20, r.stdout[-2000:]          # C32 codec: 26 (C64: 46)
+    assert 'SyncBN vs replica-BN' in r.stdout, r.stdout[-2000:]
+
+
+def test_dp_config3_shape_sync_bn_vs_union_oracle(device, tmp_path):
+    """BASELINE config 3's global-batch semantics through the real DP code: 4 gloo ranks, each running
+    the NATIVE FusedElboStep with SyncBN at config 3's per-rank shape (C64 highres, B_u = 256 of a shared
+    pool + N_s = 32 rank-owned labeled samples, Dropout2d 0.2), against the fp64 oracle of ONE process
+    on the union batch (B_u = 1024, N_s = 128: train-mode BN over the whole codec call,
+    codec.py:164-173) on the ranks' own subsets, noise and dropout scales, with the kernels' ReLU
+    decisions (tests/gpu_masks.py).  The ranks' ELBOs sum to the union ELBO within 1e-5; the
+    all-reduced shared gradient and each rank's q rows match the union gradient at 5e-5 per tensor."""
+    from dp_worker import C64_BU, C64_NS, c64_data
+    from elbo_ref import oracle_elbo
+    from test_gpu_c64 import check_mask_audit
+    from oracle import codec as ocodec
+    world = 4
+    env = dict(os.environ)
+    env['PYTHONUNBUFFERED'] = '1'
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node=%d' % world,
+           '--master-addr=127.0.0.1', '--master-port=%d' % _free_port(), os.path.join(HERE, 'dp_worker.py'),
+           str(tmp_path), 'c64sync']
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    rk = [dict(np.load(str(tmp_path / ('rank%d.npz' % i)))) for i in range(world)]
+    idx = rk[0]['idx']
+    assert all(np.array_equal(x['idx'], idx) for x in rk)
+    assert len(set(idx[:world * C64_BU].tolist())) == world * C64_BU
+    # every BN group's global count: world x the per-rank batch
+    assert list(rk[0]['counts']) == [world * C64_BU, world * C64_NS, world * C64_BU]
+    ns = int(rk[0]['n_shared'])
+    Xu, _, _, _ = c64_data(world, 0)
+    data = [c64_data(world, j)[1:] for j in range(world)]
+    cat = lambda parts: np.concatenate(parts, 0)
+    Xs, Y, F = [cat([dd[i] for dd in data]) for i in range(3)]
+    eps_enc = cat([x['eps_z'][:C64_BU] for x in rk])
+    eps_qz = cat([x['eps_z'][C64_BU:] for x in rk])
+    eps_qX = cat([x['eps_x'] for x in rk])
+    drops = {'enc': {}, 'dec': {}}
+    masks = {'enc': {}, 'dec_u': {}, 'dec_s': {}}
+    for k in rk[0]:
+        if k.startswith('drop.enc.'):
+            drops['enc'][k[9:]] = torch.tensor(cat([x[k] for x in rk]), dtype=torch.float64)
+        elif k.startswith('drop.dec.'):        # union decoder rows: every rank's unlabeled, then labeled
+            drops['dec'][k[9:]] = torch.tensor(cat([x[k][:C64_BU] for x in rk] + [x[k][C64_BU:] for x in rk]),
+                                               dtype=torch.float64)
+        elif k.startswith('mask.'):
+            call, nm = k[5:].split('.', 1)
+            masks[call][nm] = torch.tensor(cat([x[k] for x in rk]))
+    assert drops['enc'] and drops['dec'] and masks['enc'] and masks['dec_u'] and masks['dec_s']
+    names = list(rk[0]['names'])
+    st = {}
+    for i, k in enumerate(names):
+        shp = tuple(int(v) for v in rk[0]['shape.' + k])
+        nel = int(np.prod(shp))
+        if k.startswith(('q_z.', 'q_X.')):       # rank-owned rows: the union's rows in rank order
+            a = cat([x['P0'][int(x['offsets'][i]):int(x['offsets'][i]) + nel].reshape(shp) for x in rk])
+        else:
+            o = int(rk[0]['offsets'][i])
+            a = rk[0]['P0'][o:o + nel].reshape(shp)
+        st[k] = torch.tensor(a, dtype=torch.float64, requires_grad=True)
+    ocodec.MASK_AUDIT.clear()
+    val = oracle_elbo(st, Xu[idx[:world * C64_BU]], Xs, Y, F, eps_enc, eps_qz, eps_qX, 8, 8, masks=masks,
+                      drops=drops)
+    check_mask_audit()
+    (-val).backward()
+    tot = sum(float(x['elbo']) for x in rk)
+    assert abs(tot - val.item()) <= 1e-5 * abs(val.item()), (tot, val.item())
+    errs = {}
+    for i, k in enumerate(names):
+        g = st[k].grad.numpy().ravel()
+        if k.startswith(('q_z.', 'q_X.')):
+            part = g.size // world
+            for j, x in enumerate(rk):
+                o = int(x['offsets'][i])
+                errs['%s[rank%d]' % (k, j)] = tensor_rel(x['G_red'][o:o + part], g[j * part:(j + 1) * part])
+        else:
+            o = int(rk[0]['offsets'][i])
+            assert o + g.size <= ns
+            errs[k] = tensor_rel(rk[0]['G_red'][o:o + g.size], g)
+            for x in rk[1:]:
+                assert np.array_equal(x['G_red'][o:o + g.size], rk[0]['G_red'][o:o + g.size]), k
+    bad = {k: v for k, v in errs.items() if not v < 5e-5}
+    assert not bad, (bad, sorted(errs.items(), key=lambda kv: -kv[1])[:8])
+

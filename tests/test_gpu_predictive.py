@@ -168,3 +168,45 @@ def test_concurrent_prediction_ensemble_matches_sequential(device, tmp_path, cap
             assert torch.equal(b, c), n
         else:
             assert torch.isfinite(c).all() and (c - b).abs().max() <= 0.25 * b.abs().max() + 0.05, n
+
+
+def test_pe_running_stage_fold_exact(device):
+    """ConcurrentPredictionEnsemble's BN running-statistics fold, pinned exactly: one PE
+    group of 3 iterations with running_stage=True (the calls' EMA updates go to the zeroed staging
+    buffers of the shadow decoder), folded as running = (1 - m)^3 running + staged, equals the same
+    group run with running_stage=False (every call updates model.f's buffers directly) to fp32 rounding
+    (2e-6 relative); num_batches_tracked equal, staging buffers zeroed by the fold, q_z identical.  A
+    wrong decay exponent or momentum, or a missed zeroing, moves the buffers by >= 1e-2 relative."""
+    from gpi.predictive import PredictionEnsembleEngine, ConcurrentPredictionEnsemble
+    from bottleneck.components import VariationalApproximation
+    d = load('pe_analysis_c32.npz')
+    out = {}
+    for stage in (False, True):
+        model, ds = build(d)
+        n, nc, dz, Nval, Nmc, iters = [int(v) for v in d['cfg']]
+        q = VariationalApproximation(dz, Nval, ds.get('X')).to('cuda')
+        q.init(cuda(d['q_mean']), cuda(d['q_logsigma']))
+        before = {k: b.clone() for k, b in model.f.named_buffers()}
+        torch.manual_seed(9)
+        pe = PredictionEnsembleEngine(model, q, ds.get('X').contiguous().float(), lambda: 1e-2, running_stage=stage)
+        for i in range(3):
+            pe.update(sync=i == 0)
+        if stage:
+            cpe = ConcurrentPredictionEnsemble(pe, 3)
+            cpe._fold()
+            for b in cpe._fl_stage + cpe._nb_stage:
+                assert not b.any()
+        torch.cuda.synchronize()
+        out[stage] = ({k: b.clone() for k, b in model.f.named_buffers()}, pe.flat.P[pe.q_off:].clone(), before)
+    direct, staged = out[False][0], out[True][0]
+    assert torch.equal(out[False][1], out[True][1])
+    moved = 0
+    for k, b in direct.items():
+        c = staged[k]
+        if k.endswith('num_batches_tracked'):
+            assert torch.equal(b, c) and int(b) == int(out[False][2][k]) + 3, k
+            continue
+        err = ((c - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
+        assert err < 2e-6, (k, err)
+        moved += int(not torch.equal(b, out[False][2][k]))
+    assert moved > 0

@@ -1,6 +1,9 @@
 """RCCL all-reduce captured in the fused step's graph: run with torch.distributed.run (nccl), compare
 graph replays with eager steps of an identical copy (same seeds) -- parameters after 3 steps.
-usage: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 tools/dist_capture_probe.py"""
+--sync-bn: SyncBN (every BN layer's batch sums all-reduced conv by conv, ~46 collectives per step) captured
+into the step graph as well; the replays must equal the eager SyncBN steps bit for bit, and at world size 1
+the SyncBN step must also agree with the replica-BN step to rounding (the same batch statistics).
+usage: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 tools/dist_capture_probe.py [--sync-bn]"""
 import copy
 import os
 import sys
@@ -23,18 +26,43 @@ def main():
     ma, bs = build_golden_model(d)
     mb = copy.deepcopy(ma)
     args = (cuda(d['Xu']), bs // world, cuda(d['Xs']), cuda(d['Y']), cuda(d['F']))
-    kw = dict(lr=1e-3, seed=5 + rank, subset_seed=1, distributed=True, rank=rank, world=world)
+    sync = '--sync-bn' in sys.argv
+    mc = copy.deepcopy(ma) if sync and world == 1 else None
+    kw = dict(lr=1e-3, seed=5 + rank, subset_seed=1, distributed=True, rank=rank, world=world, sync_bn=sync)
     eager = FusedElboStep(ma, *args, **kw)
     graph = FusedElboStep(mb, *args, **kw)
+    assert eager.sync_bn == sync and graph.sync_bn == sync
+    assert (graph.engine.bn_sync is not None) == sync
+    n_coll = [0]
+    if sync:     # count the codec's collectives of one captured step
+        inner = graph.engine.bn_sync
+
+        def counted(t):
+            n_coll[0] += 1
+            inner(t)
+        graph.engine.bn_sync = counted
     graph.capture()
     assert not graph.split_graph
+    n_per_step = n_coll[0] // 3          # two warm-up steps + the captured one
     for _ in range(3):
         eager.step_eager()
         graph.step()
     torch.cuda.synchronize()
     err = (graph.flat.P - eager.flat.P).abs().max().item()
-    print('rank %d world %d: graph-captured all-reduce vs eager, max |dP| = %.3e' % (rank, world, err), flush=True)
+    what = 'SyncBN (%d codec collectives per step) + ' % n_per_step if sync else ''
+    print('rank %d world %d: graph-captured %sall-reduce vs eager, max |dP| = %.3e' % (rank, world, what, err),
+          flush=True)
     assert err < 1e-6
+    if mc is not None:
+        # one rank: SyncBN's statistics are the replica-BN ones (folded into replica 0, other order)
+        ref = FusedElboStep(mc, *args, **dict(kw, sync_bn=False))
+        for _ in range(3):
+            ref.step_eager()
+        torch.cuda.synchronize()
+        dr = ((graph.flat.P - ref.flat.P).abs().max() / ref.flat.P.abs().max()).item()
+        print('rank %d world 1: SyncBN vs replica-BN after 3 steps, max |dP| / max |P| = %.3e' % (rank, dr),
+              flush=True)
+        assert dr < 1e-5
     dist.barrier()
     dist.destroy_process_group()
 
