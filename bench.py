@@ -164,11 +164,13 @@ def step_conv_launches(e):
     fns = {'fwd': lib.gpi_conv_forward, 'bwd': lib.gpi_conv_backward, 'fused': lib.gpi_conv_loss_fused}
     progs = []
     if e.ep is not None:
-        progs.append((e.ep, e.enc_descs, e.ectx, e.B_u, len(e.enc_descs)))
-    progs.append((e.dp, e.dec_descs, e.dctx, e.B, e.n_dec_sep))
+        progs.append((e.ep, e.enc_descs, e.ectx, e.B_u, len(e.enc_descs), 0, e.n_enc_conv))
+    progs.append((e.dp, e.dec_descs, e.dctx, e.B, e.n_dec_sep, e.dec0, len(e.dec_descs)))
     out = []
-    for prog, descs, ctx, B, n_sep in progs:
+    for prog, descs, ctx, B, n_sep, i0, i1 in progs:
         for i, op in enumerate(prog.ops):
+            if i < i0 or i >= i1:          # folded into the head launches (gpi_head_fold)
+                continue
             for kind in (('fused',) if i >= n_sep else ('fwd', 'bwd')):
                 out.append(('%s.%s' % (op.name, kind), kind, fns[kind], descs[i], ctx, B))
     return out

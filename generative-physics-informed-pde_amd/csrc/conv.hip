@@ -112,6 +112,8 @@ struct ConvGeom {
                     // to each other), so the halo rows two tiles share are read from HBM once into that
                     // XCD's L2 instead of once per XCD.  0: tile = blockIdx.x (xcd_mode)
     int grid;       // launched workgroups (xcd remap)
+    uint32_t* sig;             // cross-stream hand-off (gpi_*_sig): workgroup 0 stores *sig_epoch + 1 at entry,
+    const int64_t* sig_epoch;  // i.e. once every earlier kernel of the stream has completed (gpi_stream_signal)
     int in_sq, in_sr, in_sc;   // 256 chunks of the input image = (planes, rows, chunks)
     int g_sq, g_sr, g_sc;      // ... of the output-gradient image
     Div d_in4, d_P4, d_g4, d_PG4, d_cin, d_cout, d_win, d_tp, d_wout, d_w2;
@@ -263,6 +265,8 @@ bool conv_geom(const gpi_conv_desc& d, const gpi_groups& g, ConvGeom& G, bool fw
     G.vsum = 0;     // decided by launch() / gpi_conv_blocks (vsum_op)
     G.xcd = 0;      // set by launch() (xcd_mode)
     G.grid = 0;     // set by launch()
+    G.sig = nullptr;
+    G.sig_epoch = nullptr;
 #ifdef GPI_PHASE_TIMING
     static const int dbg = env_int("GPI_DBG_SKIP", 0);
     G.dbg = dbg;
@@ -471,6 +475,13 @@ __device__ __forceinline__ void touch_kernargs() {
 }
 constexpr int CONV_KARG_BYTES = (int)(sizeof(gpi_conv_desc) + sizeof(gpi_codec_ctx) + sizeof(ConvGeom) + 16);
 
+// the launch's hand-off signal (G.sig): one write-through store by workgroup 0 at entry -- the kernels
+// before this one on its stream have completed and released their writes by the time it starts
+__device__ __forceinline__ void entry_signal(const ConvGeom& G) {
+    if (G.sig && blockIdx.x == 0 && threadIdx.x == 0)
+        __hip_atomic_store(G.sig, (uint32_t)(*G.sig_epoch + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Global-address-space views of (pinned, hence generic) pointers: ordinary loads and
 // stores through them stay global_load / global_store.  A flat access could alias LDS,
 // so the compiler would drain every outstanding LDS-DMA (vmcnt(0)) in front of it.
@@ -623,6 +634,7 @@ template <int K, int S, int UP, int CP, int NPX>
 // (the channel-group instantiation NPX == 0 runs one workgroup per CU: no occupancy target)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NPX == 0 ? 1 : 5))) void conv_fwd_kernel(gpi_conv_desc d, gpi_codec_ctx c, ConvGeom G) {
     touch_kernargs<CONV_KARG_BYTES>();
+    entry_signal(G);
     if (SKIP(G, 16)) return;
     constexpr int KK = K * K;
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -1027,6 +1039,7 @@ __host__ __device__ constexpr bool fuse_wlds(int ky) {
 template <int K, int S, int UP, bool FUSE = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (FUSE ? GPI_FUSE_WAVES : 4) : 6))) void conv_bwd_kernel(gpi_conv_desc d, gpi_codec_ctx c, ConvGeom G) {
     touch_kernargs<CONV_KARG_BYTES>();
+    entry_signal(G);
     if (SKIP(G, 16)) return;
     constexpr int KK = K * K;
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -2092,9 +2105,13 @@ bool xcd_mode(bool fwd, bool fuse, bool split) {
     return (mode & (fuse ? 8 : fwd ? 1 : split ? 4 : 2)) != 0;
 }
 
-int launch(const gpi_conv_desc& d, const gpi_codec_ctx& c, hipStream_t st, bool fwd, bool fuse = false) {
+int launch(const gpi_conv_desc& d, const gpi_codec_ctx& c, hipStream_t st, bool fwd, bool fuse = false,
+           uint32_t* sig = nullptr, const int64_t* sig_epoch = nullptr) {
     ConvGeom G;
     if (!conv_geom(d, c.groups, G, fwd, fuse)) return GPI_ERR_UNSUPPORTED;
+    if (sig && !sig_epoch) return GPI_ERR_ARG;
+    G.sig = sig;
+    G.sig_epoch = sig_epoch;
     if (fuse && (fwd || d.k != 5 || d.stride != 1 || d.upsample || d.cout != 2 || d.cin > 4 || d.drop_off >= 0 ||
                  d.gout_mode != 1 || d.gin_off < 0 ||
                  (d.epilogue != GPI_EPI_GAUSS_LOSS && d.epilogue != GPI_EPI_GAUSS_EXP_LOSS)))
@@ -2294,22 +2311,44 @@ extern "C" int gpi_conv_loss_fused(const gpi_conv_desc* op, const gpi_codec_ctx*
     return launch(*op, *ctx, (hipStream_t)stream, false, true);
 }
 
-extern "C" int gpi_codec_forward(const gpi_conv_desc* ops, int n_ops, const gpi_codec_ctx* ctx, void* stream) {
+extern "C" int gpi_conv_forward_sig(const gpi_conv_desc* op, const gpi_codec_ctx* ctx, uint32_t* flag,
+                                    const int64_t* epoch, void* stream) {
+    if (!op || !ctx) return GPI_ERR_ARG;
+    return launch(*op, *ctx, (hipStream_t)stream, true, false, flag, epoch);
+}
+
+extern "C" int gpi_conv_backward_sig(const gpi_conv_desc* op, const gpi_codec_ctx* ctx, uint32_t* flag,
+                                     const int64_t* epoch, void* stream) {
+    if (!op || !ctx) return GPI_ERR_ARG;
+    return launch(*op, *ctx, (hipStream_t)stream, false, false, flag, epoch);
+}
+
+extern "C" int gpi_codec_forward_sig(const gpi_conv_desc* ops, int n_ops, const gpi_codec_ctx* ctx, uint32_t* flag,
+                                     const int64_t* epoch, void* stream) {
     if (!ops || !ctx || n_ops < 0) return GPI_ERR_ARG;
     for (int i = 0; i < n_ops; ++i) {
-        int r = launch(ops[i], *ctx, (hipStream_t)stream, true);
+        int r = launch(ops[i], *ctx, (hipStream_t)stream, true, false, i == 0 ? flag : nullptr, epoch);
         if (r != GPI_OK) return r;
     }
     return GPI_OK;
 }
 
-extern "C" int gpi_codec_backward(const gpi_conv_desc* ops, int n_ops, const gpi_codec_ctx* ctx, void* stream) {
+extern "C" int gpi_codec_backward_sig(const gpi_conv_desc* ops, int n_ops, const gpi_codec_ctx* ctx, uint32_t* flag,
+                                      const int64_t* epoch, void* stream) {
     if (!ops || !ctx || n_ops < 0) return GPI_ERR_ARG;
     for (int i = n_ops - 1; i >= 0; --i) {
-        int r = launch(ops[i], *ctx, (hipStream_t)stream, false);
+        int r = launch(ops[i], *ctx, (hipStream_t)stream, false, false, i == n_ops - 1 ? flag : nullptr, epoch);
         if (r != GPI_OK) return r;
     }
     return GPI_OK;
+}
+
+extern "C" int gpi_codec_forward(const gpi_conv_desc* ops, int n_ops, const gpi_codec_ctx* ctx, void* stream) {
+    return gpi_codec_forward_sig(ops, n_ops, ctx, nullptr, nullptr, stream);
+}
+
+extern "C" int gpi_codec_backward(const gpi_conv_desc* ops, int n_ops, const gpi_codec_ctx* ctx, void* stream) {
+    return gpi_codec_backward_sig(ops, n_ops, ctx, nullptr, nullptr, stream);
 }
 
 extern "C" int gpi_wgrad_reduce(const gpi_reduce_item* items, int n_items, const float* wpart, double* gacc,

@@ -57,8 +57,11 @@ __device__ __forceinline__ void adam_element(float g, float& p, float& m, float&
 // epilogue's scratch / subset / dropout duties.  The step counter and the RNG offset are read by every
 // workgroup (bias corrections, the dropout draw) and advanced once all of them have read them: by the
 // last workgroup to finish (arrival counter *done, reset by that workgroup for the next launch).
+__device__ __forceinline__ void epilogue_wait(const uint32_t* flag, const int64_t* epoch, uint32_t* err);
+
 __global__ __launch_bounds__(256) void step_epilogue_adam_kernel(gpi_step_epilogue_desc d, gpi_adam_desc a,
                                                                  uint32_t* done) {
+    if (d.wait_flag) epilogue_wait(d.wait_flag, a.step, d.wait_err);
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const int64_t t = *a.step + 1;              // the step number after this step's increment
     const uint64_t base = d.drop_offset ? *d.drop_offset : 0;
@@ -258,7 +261,65 @@ __global__ __launch_bounds__(256) void subset_cand_rank_kernel(int32_t* out, con
     }
 }
 
+// Cross-stream hand-off by a device flag (gpi_stream_signal / gpi_stream_wait).  The signal kernel runs
+// after every earlier kernel of its stream has completed and released its writes (the queue's kernel
+// boundary), so one write-through store of the step's tag publishes them; the waiter spins on that word
+// with sc1 loads and exits, and the stream's next kernel starts with the usual acquire.  The tag is the
+// step counter + 1 (the counter changes only in the step's final epilogue, after every hand-off of the
+// step), so a flag left from the previous step never matches.  Every spin is bounded: on a timeout the
+// waiter sets *err and returns (the results are then garbage, the host reads the flag, nothing hangs).
+constexpr int WAIT_SPIN_MAX = 1 << 24;
+
+// every workgroup: one lane polls the flag (relaxed sc1 loads), then ONE agent acquire so that the
+// workgroup's later plain loads see what the signalling stream wrote, then the workgroup barrier
+__device__ __forceinline__ void epilogue_wait(const uint32_t* flag, const int64_t* epoch, uint32_t* err) {
+    if (threadIdx.x == 0) {
+        const uint32_t want = (uint32_t)(*epoch + 1);
+        for (int i = 0; __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want; ++i) {
+            __builtin_amdgcn_s_sleep(2);
+            if (i > WAIT_SPIN_MAX) {
+                if (err) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+}
+
+__global__ void stream_signal_kernel(uint32_t* flag, const int64_t* epoch) {
+    if (threadIdx.x == 0)
+        __hip_atomic_store(flag, (uint32_t)(*epoch + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ void stream_wait_kernel(const uint32_t* flag, const int64_t* epoch, uint32_t* err) {
+    if (threadIdx.x != 0) return;
+    const uint32_t want = (uint32_t)(*epoch + 1);
+    for (int i = 0; __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want; ++i) {
+        __builtin_amdgcn_s_sleep(2);
+        if (i > WAIT_SPIN_MAX) {
+            if (err) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+    }
+}
+
 }  // namespace
+
+extern "C" int gpi_stream_signal(uint32_t* flag, const int64_t* epoch, void* stream) {
+    if (!flag || !epoch) return GPI_ERR_ARG;
+    hipLaunchKernelGGL(stream_signal_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, flag, epoch);
+    GPI_CHECK_LAUNCH();
+    return GPI_OK;
+}
+
+extern "C" int gpi_stream_wait(const uint32_t* flag, const int64_t* epoch, uint32_t* err, void* stream) {
+    if (!flag || !epoch) return GPI_ERR_ARG;
+    hipLaunchKernelGGL(stream_wait_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, flag, epoch, err);
+    GPI_CHECK_LAUNCH();
+    return GPI_OK;
+}
 
 extern "C" int gpi_version(void) { return 1; }
 
@@ -271,7 +332,7 @@ extern "C" int gpi_struct_sizes(int64_t* out, int n) {
                          (int64_t)sizeof(gpi_vo_precision_desc), (int64_t)sizeof(gpi_gp_sample_desc),
                          (int64_t)sizeof(gpi_vo_galerkin_desc), (int64_t)sizeof(gpi_step_epilogue_desc),
                          (int64_t)sizeof(gpi_fom_desc), (int64_t)sizeof(gpi_random_field_desc),
-                         (int64_t)sizeof(gpi_vo_sparse)};
+                         (int64_t)sizeof(gpi_vo_sparse), (int64_t)sizeof(gpi_head_fold)};
     const int k = (int)(sizeof(s) / sizeof(s[0]));
     if (!out || n < k) return GPI_ERR_ARG;
     for (int i = 0; i < k; ++i) out[i] = s[i];

@@ -159,7 +159,7 @@ class StepEpilogueDesc(C.Structure):
     _fields_ = [('gacc', vp), ('grad', vp), ('n', i64), ('flags', i32), ('n_terms', i32), ('step', vp),
                 ('scratch', vp), ('n_scratch', i64), ('terms_dst', vp), ('idx_src', vp), ('idx_dst', vp),
                 ('n_idx', i64), ('drop_out', vp), ('drop_n', i64), ('drop_p', f32), ('_pad2', i32),
-                ('drop_seed', u64), ('drop_offset', vp), ('drop_sub', u64)]
+                ('drop_seed', u64), ('drop_offset', vp), ('drop_sub', u64), ('wait_flag', vp), ('wait_err', vp)]
 
 
 class FomDesc(C.Structure):
@@ -172,9 +172,14 @@ class RandomFieldDesc(C.Structure):
                 ('ly', vp), ('lxt', vp), ('scale', vp), ('gamma', vp), ('seed', u64), ('sub', u64), ('work', vp), ('x', vp)]
 
 
+class HeadFold(C.Structure):
+    _fields_ = [('has_feat', i32), ('has_lat', i32), ('feat', ConvDesc), ('lat', ConvDesc), ('enc_ctx', CodecCtx),
+                ('dec_ctx', CodecCtx)]
+
+
 STRUCTS = [Stat, Groups, ConvDesc, CodecCtx, ReduceItem, HeadDesc, GemmItem, RomDesc, ResidualDesc, AdamDesc,
            VoQueryDesc, VoMomentsDesc, VoConditionDesc, VoPrecisionDesc, GpSampleDesc,
-           VoGalerkinDesc, StepEpilogueDesc, FomDesc, RandomFieldDesc, VoSparse]
+           VoGalerkinDesc, StepEpilogueDesc, FomDesc, RandomFieldDesc, VoSparse, HeadFold]
 
 # name -> (restype, argtypes)
 SIGNATURES = {
@@ -189,9 +194,15 @@ SIGNATURES = {
     'gpi_conv_backward': (C.c_int, [C.POINTER(ConvDesc), C.POINTER(CodecCtx), vp]),
     'gpi_codec_forward': (C.c_int, [C.POINTER(ConvDesc), C.c_int, C.POINTER(CodecCtx), vp]),
     'gpi_codec_backward': (C.c_int, [C.POINTER(ConvDesc), C.c_int, C.POINTER(CodecCtx), vp]),
+    'gpi_conv_forward_sig': (C.c_int, [C.POINTER(ConvDesc), C.POINTER(CodecCtx), vp, vp, vp]),
+    'gpi_conv_backward_sig': (C.c_int, [C.POINTER(ConvDesc), C.POINTER(CodecCtx), vp, vp, vp]),
+    'gpi_codec_forward_sig': (C.c_int, [C.POINTER(ConvDesc), C.c_int, C.POINTER(CodecCtx), vp, vp, vp]),
+    'gpi_codec_backward_sig': (C.c_int, [C.POINTER(ConvDesc), C.c_int, C.POINTER(CodecCtx), vp, vp, vp]),
     'gpi_wgrad_reduce': (C.c_int, [C.POINTER(ReduceItem), C.c_int, vp, vp, vp]),
     'gpi_head_forward': (C.c_int, [C.POINTER(HeadDesc), vp, vp, vp]),
     'gpi_head_backward': (C.c_int, [C.POINTER(HeadDesc), vp, vp, vp, vp]),
+    'gpi_head_forward_folded': (C.c_int, [C.POINTER(HeadDesc), C.POINTER(HeadFold), vp, vp, vp]),
+    'gpi_head_backward_folded': (C.c_int, [C.POINTER(HeadDesc), C.POINTER(HeadFold), vp, vp, vp, vp]),
     'gpi_outer_gemm': (C.c_int, [C.POINTER(GemmItem), C.c_int, vp, vp, vp]),
     'gpi_rom': (C.c_int, [C.POINTER(RomDesc), vp]),
     'gpi_cgr_residual': (C.c_int, [C.POINTER(ResidualDesc), vp]),
@@ -205,6 +216,8 @@ SIGNATURES = {
     'gpi_randn': (C.c_int, [vp, i64, u64, vp, u64, vp]),
     'gpi_dropout_masks': (C.c_int, [vp, i64, f32, u64, vp, u64, vp]),
     'gpi_rng_advance': (C.c_int, [vp, u64, vp]),
+    'gpi_stream_signal': (C.c_int, [vp, vp, vp]),
+    'gpi_stream_wait': (C.c_int, [vp, vp, vp, vp]),
     'gpi_random_subset': (C.c_int, [vp, i32, i32, u64, vp, u64, vp]),
     'gpi_random_subset_workspace': (C.c_int, [i32, C.POINTER(i64)]),
     'gpi_random_subset_ws': (C.c_int, [vp, i32, i32, u64, vp, u64, vp, i64, vp]),

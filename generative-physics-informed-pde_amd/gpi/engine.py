@@ -235,14 +235,20 @@ class ElboEngine(object):
         offD = lambda n: flat.offset(dec.get_parameter(n))
         dz = dec.dim_latent
         self.dz = dz
+        # the encoder's last conv and the decoder's first one run inside the head launches (gpi_head_fold:
+        # four launches less per step); GPI_HEAD_FOLD=0 keeps them as conv launches (A/B)
+        fold = os.environ.get('GPI_HEAD_FOLD', '1') != '0'
         # ---- encoder program
         if self.B_u > 0 and self.armortized:
             ec = enc.native_config()
             self.ep = encoder_program(**ec)
-            self.enc_descs = self.ep.layout(self.B_u, ws.ws, ws.stats, ws.parts, groups_struct([self.B_u]), offE)
+            self.fold_feat = fold and self.ep.foldable_feat()
+            self.enc_descs = self.ep.layout(self.B_u, ws.ws, ws.stats, ws.parts, groups_struct([self.B_u]), offE,
+                                            per_sample_ops=(self.ep.ops[-1].name,) if self.fold_feat else ())
             d_feat = self.ep.d_feat
         else:
             self.ep = None
+            self.fold_feat = False
             d_feat = 1
         # ---- decoder program (groups: unsup, sup, vo)
         dc = dec.native_config()
@@ -250,10 +256,15 @@ class ElboEngine(object):
         # exponentiated field's (reconstruct_log_eff_property = False)
         log_field = getattr(model, 'config', {}).get('reconstruct_log_eff_property', True)
         self.dp = decoder_program(final_epilogue=L.EPI_GAUSS_LOSS if log_field else L.EPI_GAUSS_EXP_LOSS, **dc)
+        self.fold_lat = fold and self.dp.foldable_lat()
         self.dec_sizes = [n for n in (self.B_u, self.N_s, self.N_vo) if n > 0]
         self.g_sup = (1 if self.B_u > 0 else 0) if self.N_s > 0 else None
         self.g_vo = ((self.B_u > 0) + (self.N_s > 0)) if self.N_vo > 0 else None
-        self.dec_descs = self.dp.layout(self.B, ws.ws, ws.stats, ws.parts, groups_struct(self.dec_sizes), offD)
+        self.dec_descs = self.dp.layout(self.B, ws.ws, ws.stats, ws.parts, groups_struct(self.dec_sizes), offD,
+                                        per_sample_ops=(self.dp.ops[0].name,) if self.fold_lat else ())
+        # codec launch ranges: the encoder's ops [0, n_enc_conv), the decoder's [dec0, ...)
+        self.n_enc_conv = (len(self.enc_descs) - (1 if self.fold_feat else 0)) if self.ep is not None else 0
+        self.dec0 = 1 if self.fold_lat else 0
         # the loss epilogue consumes (mu, logsigma) in registers: nobody reads the output image (9.4 MB of
         # writes per step at C64)
         self.dec_descs[len(self.dec_descs) - 1].out_off = -1
@@ -439,13 +450,75 @@ class ElboEngine(object):
         # two others, r03: kept 'forward')
         self.rom_at = os.environ.get('GPI_ROM_AT', 'forward')
         self._rom_deferred = False
+        self._pending_sig = None       # hand-off flag the next main-stream codec call signals
         # callable(side stream handle) launched on the side stream ahead of the ROM (fused step)
         self.side_pre = None
         # SyncBN (set_sync_bn): None = replica-BN, per-rank batch statistics
         self.bn_sync = None
         self.bn_world = 1
+        # cross-stream hand-offs: graph events (None) or device flags (set_flag_handoff)
+        self.handoff = None
+        self._rejoin_pending = False
 
     # ------------------------------------------------------------------
+    def set_flag_handoff(self, flags, epoch, err=None):
+        """Hand the side stream its work by device flags (gpi_stream_signal / gpi_stream_wait) instead of
+        event edges between the streams: flags = int32 device tensor (>= 4 words), epoch = the step
+        counter (int64 device tensor, constant within a step), err = an int32 word the waits set on a
+        timeout.  The side stream forks from the main stream once at the start of the forward; after
+        the step's last kernel the caller joins it back with rejoin() (stream-capture legality: the
+        events there sit at the graph's end, not between kernels of the main chain)."""
+        self.handoff = (flags, epoch, err)
+
+    def _signal(self, k, st):
+        f, e, _ = self.handoff
+        _run(_lib().gpi_stream_signal, C.c_void_p(f.data_ptr() + 4 * k), C.c_void_p(e.data_ptr()), st,
+             what='stream signal')
+
+    def _sig_args(self, k):
+        """(flag, epoch) pointers of hand-off flag k for the *_sig launches (signal folded into a conv)."""
+        f, e, _ = self.handoff
+        return C.c_void_p(f.data_ptr() + 4 * k), C.c_void_p(e.data_ptr())
+
+    def _wait(self, k, st):
+        f, e, err = self.handoff
+        _run(_lib().gpi_stream_wait, C.c_void_p(f.data_ptr() + 4 * k), C.c_void_p(e.data_ptr()),
+             C.c_void_p(err.data_ptr()) if err is not None else None, st, what='stream wait')
+
+    def rejoin(self):
+        """Main stream waits for the side stream's end (flag hand-off mode; a no-op otherwise)."""
+        if self._rejoin_pending:
+            torch.cuda.current_stream().wait_event(self._ev_join2)
+            self._rejoin_pending = False
+
+    def head_fold(self):
+        """gpi_head_fold of the folded convs (or None): their descriptors and program contexts."""
+        if not (self.fold_feat or self.fold_lat):
+            return None
+        f = L.HeadFold()
+        f.has_feat, f.has_lat = int(self.fold_feat), int(self.fold_lat)
+        if self.fold_feat:
+            f.feat = self.enc_descs[len(self.enc_descs) - 1]
+            f.enc_ctx = self.ectx
+        if self.fold_lat:
+            f.lat = self.dec_descs[0]
+            f.dec_ctx = self.dctx
+        return f
+
+    def _head_forward(self, st):
+        f = self.head_fold()
+        _run(_lib().gpi_head_forward_folded, C.byref(self.head), C.byref(f) if f is not None else None,
+             C.c_void_p(self.flat.P.data_ptr()), C.c_void_p(self.ws.t_ws.data_ptr()), st, what='head forward')
+        if self.bn_sync is not None and self.fold_lat:       # the folded decoder conv's output statistics
+            d = self.dec_descs[0]
+            self._sync_stats(d.out_stat, d.cout, 0, 'dec')
+
+    def _head_backward(self, hd, st):
+        f = self.head_fold()
+        _run(_lib().gpi_head_backward_folded, C.byref(hd), C.byref(f) if f is not None else None,
+             C.c_void_p(self.flat.P.data_ptr()), C.c_void_p(self.ws.t_ws.data_ptr()),
+             C.c_void_p(self.flat.gacc.data_ptr()), st, what='head backward')
+
     def eps_z(self):
         return self.ws.view(self.hb['eps_z'], self.B, self.dz)
 
@@ -514,6 +587,12 @@ class ElboEngine(object):
         and term scratch (gpi_step_epilogue).  running: BN running-statistics update 'now' (end of
         the forward), 'defer' (on the side stream during backward) or None."""
         st = stream if stream is not None else L.stream_handle()
+        if self.handoff is not None:
+            # the side stream's one fork of the step, before any of its kernels: its flag waits then
+            # follow this step's signals only (never the previous step's)
+            self._side_stream()
+            self._ev_start.record(torch.cuda.current_stream())
+            self._side.wait_event(self._ev_start)
         self.forward_a(st, zero_gacc, zero_scratch)
         # rom_at 'backward': the ROM follows the backward's fork on the side stream (ahead of the
         # variational samples' head backward that needs it) -- one cross-stream dependency less per
@@ -526,7 +605,10 @@ class ElboEngine(object):
             # branch and keeps its hardware queue (each cross-queue dependency costs ~10 us).
             main = torch.cuda.current_stream()
             self._side_stream()
-            self._ev_fork.record(main)
+            if self.handoff is not None:
+                self._pending_sig = 0          # folded into forward_b's first decoder conv
+            else:
+                self._ev_fork.record(main)
             if self.rom_first:
                 self._launch_roms()
         self.forward_b(st)
@@ -551,19 +633,20 @@ class ElboEngine(object):
         if zero_gacc:
             self.flat.gacc.zero_()
         if self.ep is not None:
-            self._codec_forward(self.enc_descs, 0, len(self.enc_descs), self.ectx, st, 'encoder forward')
+            self._codec_forward(self.enc_descs, 0, self.n_enc_conv, self.ectx, st, 'encoder forward')
         if not self.armortized and self.B_u > 0:
             # q_z['unsupervised'] rows as the "encoder" outputs of the head's first segment
             # (torch copies on the current stream, which the launches use)
             self.ws.view(self.hb['zmu'], self.B_u, self.dz).copy_(self.q_unsup._mean.detach())
             self.ws.view(self.hb['zls'], self.B_u, self.dz).copy_(self.q_unsup._logsigma.detach())
-        _run(lib.gpi_head_forward, C.byref(self.head), C.c_void_p(self.flat.P.data_ptr()),
-             C.c_void_p(self.ws.t_ws.data_ptr()), st, what='head forward')
+        assert lib is not None
+        self._head_forward(st)
 
     def forward_b(self, st):
         """Main stream: decoder forward and its fused output conv (forward + loss + backward)."""
         lib = _lib()
-        self._codec_forward(self.dec_descs, 0, self.n_dec_sep, self.dctx, st, 'decoder forward')
+        sig, self._pending_sig = self._pending_sig, None
+        self._codec_forward(self.dec_descs, self.dec0, self.n_dec_sep, self.dctx, st, 'decoder forward', sig=sig)
         if self.n_dec_sep < len(self.dec_descs):
             _run(lib.gpi_conv_loss_fused, C.byref(self.dec_descs[self.n_dec_sep]), C.byref(self.dctx), st,
                  what='decoder output conv (forward + loss + backward)')
@@ -578,16 +661,16 @@ class ElboEngine(object):
     def backward_a(self, st, split):
         """Main stream: decoder backward and the head backward (encoder samples only when split:
         the variational samples' need the ROM adjoint and follow it on the side stream)."""
-        lib = _lib()
-        self._codec_backward(self.dec_descs, 0, self.n_dec_sep, self.dctx, st, 'decoder backward')
-        P_, W_, G_ = (C.c_void_p(self.flat.P.data_ptr()), C.c_void_p(self.ws.t_ws.data_ptr()),
-                      C.c_void_p(self.flat.gacc.data_ptr()))
+        self._codec_backward(self.dec_descs, self.dec0, self.n_dec_sep, self.dctx, st, 'decoder backward')
+        if self.bn_sync is not None and self.fold_lat:       # the folded decoder conv's BN-backward sums
+            d = self.dec_descs[0]
+            self._sync_stats(d.out_stat, d.cout, 2, 'dec')
         if split:
             hd = L.HeadDesc.from_buffer_copy(self.head)
             hd.flags |= L.HEAD_PART_ENC
-            _run(lib.gpi_head_backward, C.byref(hd), P_, W_, G_, st, what='head backward (encoder samples)')
+            self._head_backward(hd, st)
         else:
-            _run(lib.gpi_head_backward, C.byref(self.head), P_, W_, G_, st, what='head backward')
+            self._head_backward(self.head, st)
         if not self.armortized and self.B_u > 0:
             # d/dmu, d/dlogsigma of q_z['unsupervised'] (written by the head for its first segment)
             n = self.B_u * self.dz
@@ -595,19 +678,28 @@ class ElboEngine(object):
                 o = self.flat.offset(q)
                 self.flat.gacc[o:o + n].add_(self.ws.view(self.hb[src], n).double())
 
-    def backward_b(self, st):
-        """Main stream: every encoder conv's backward but the input conv's (reverse order)."""
-        if self.ep is not None and len(self.enc_descs) > 1:
-            self._codec_backward(self.enc_descs, 1, len(self.enc_descs), self.ectx, st, 'encoder backward')
+    def backward_b(self, st, sig=None):
+        """Main stream: every encoder conv's backward but the input conv's (reverse order); sig: hand-off
+        flag its first launch signals."""
+        if self.ep is not None and self.n_enc_conv > 1:
+            self._codec_backward(self.enc_descs, 1, self.n_enc_conv, self.ectx, st, 'encoder backward', sig=sig)
+        elif sig is not None:
+            self._signal(sig, st)
 
-    def backward_c(self, st, enc_split):
+    def backward_c(self, st, enc_split, sig=None):
         """Main stream: the input conv's backward (weight gradient only) and the encoder slab
-        reduction (its own slabs only when enc_split: the side stream reduces the rest)."""
+        reduction (its own slabs only when enc_split: the side stream reduces the rest); sig: hand-off
+        flag the input conv's launch signals."""
         if self.ep is None:
             return
         if self.bn_sync is not None and self.enc_descs[0].gout_mode == 0:
             self._sync_stats(self.enc_descs[0].out_stat, self.enc_descs[0].cout, 2, 'enc')
-        _run(_lib().gpi_conv_backward, C.byref(self.enc_descs[0]), C.byref(self.ectx), st, what='In_conv backward')
+        if sig is not None:
+            _run(_lib().gpi_conv_backward_sig, C.byref(self.enc_descs[0]), C.byref(self.ectx), *self._sig_args(sig),
+                 st, what='In_conv backward')
+        else:
+            _run(_lib().gpi_conv_backward, C.byref(self.enc_descs[0]), C.byref(self.ectx), st,
+                 what='In_conv backward')
         run_reduce(self.reduce_enc[:self.n_reduce_in] if enc_split else self.reduce_enc, self.ws, self.flat, st)
 
     def backward_side_a(self, sst, split, side_extra=None):
@@ -621,9 +713,7 @@ class ElboEngine(object):
         if split:
             hq = L.HeadDesc.from_buffer_copy(self.head)
             hq.flags |= L.HEAD_PART_Q
-            _run(lib.gpi_head_backward, C.byref(hq), C.c_void_p(self.flat.P.data_ptr()),
-                 C.c_void_p(self.ws.t_ws.data_ptr()), C.c_void_p(self.flat.gacc.data_ptr()), sst,
-                 what='head backward (variational samples)')
+            self._head_backward(hq, sst)
         run_reduce(self.reduce_dec, self.ws, self.flat, sst)
         if self._running_pending:
             self.running.launch(sst)
@@ -693,35 +783,52 @@ class ElboEngine(object):
     def _codec_kind(self, descs):
         return 'enc' if self.ep is not None and descs is self.enc_descs else 'dec'
 
-    def _codec_forward(self, descs, i0, i1, ctx, st, what):
+    def _codec_forward(self, descs, i0, i1, ctx, st, what, sig=None):
+        """descs[i0] .. descs[i1 - 1]; sig: hand-off flag the first launch signals (gpi_codec_forward_sig)."""
         lib = _lib()
+        sa = self._sig_args(sig) if sig is not None else (None, None)
+        if i1 <= i0:
+            if sig is not None:
+                self._signal(sig, st)
+            return
         if self.bn_sync is None:
             ptr = C.cast(C.byref(descs, i0 * C.sizeof(L.ConvDesc)), C.POINTER(L.ConvDesc))
-            _run(lib.gpi_codec_forward, ptr, i1 - i0, C.byref(ctx), st, what=what)
+            _run(lib.gpi_codec_forward_sig, ptr, i1 - i0, C.byref(ctx), *sa, st, what=what)
             return
         kind = self._codec_kind(descs)
         for i in range(i0, i1):
             d = descs[i]
-            _run(lib.gpi_conv_forward, C.byref(d), C.byref(ctx), st, what=what)
+            _run(lib.gpi_conv_forward_sig, C.byref(d), C.byref(ctx), *(sa if i == i0 else (None, None)), st,
+                 what=what)
             if d.epilogue == L.EPI_STORE_STATS and d.out_stat >= 0:
                 self._sync_stats(d.out_stat, d.cout, 0, kind)
 
-    def _codec_backward(self, descs, i0, i1, ctx, st, what):
-        """descs[i1 - 1] down to descs[i0] (gpi_codec_backward's order)."""
+    def _codec_backward(self, descs, i0, i1, ctx, st, what, sig=None):
+        """descs[i1 - 1] down to descs[i0] (gpi_codec_backward's order); sig: hand-off flag the first
+        launch signals."""
         lib = _lib()
+        sa = self._sig_args(sig) if sig is not None else (None, None)
+        if i1 <= i0:
+            if sig is not None:
+                self._signal(sig, st)
+            return
         if self.bn_sync is None:
             ptr = C.cast(C.byref(descs, i0 * C.sizeof(L.ConvDesc)), C.POINTER(L.ConvDesc))
-            _run(lib.gpi_codec_backward, ptr, i1 - i0, C.byref(ctx), st, what=what)
+            _run(lib.gpi_codec_backward_sig, ptr, i1 - i0, C.byref(ctx), *sa, st, what=what)
             return
         kind = self._codec_kind(descs)
         for i in range(i1 - 1, i0 - 1, -1):
             d = descs[i]
             if d.gout_mode == 0:          # its output feeds a BN: that BN's backward sums are complete
                 self._sync_stats(d.out_stat, d.cout, 2, kind)
-            _run(lib.gpi_conv_backward, C.byref(d), C.byref(ctx), st, what=what)
+            _run(lib.gpi_conv_backward_sig, C.byref(d), C.byref(ctx), *(sa if i == i1 - 1 else (None, None)), st,
+                 what=what)
 
     def _launch_roms(self):
-        self._side.wait_event(self._ev_fork)
+        if self.handoff is not None:
+            self._wait(0, C.c_void_p(self._side.cuda_stream))
+        else:
+            self._side.wait_event(self._ev_fork)
         self.rom_side(C.c_void_p(self._side.cuda_stream))
         self._ev_join.record(self._side)
         self._pending_join = True
@@ -732,6 +839,7 @@ class ElboEngine(object):
             self._ev_fork, self._ev_join = torch.cuda.Event(), torch.cuda.Event()
             self._ev_fork2, self._ev_join2 = torch.cuda.Event(), torch.cuda.Event()
             self._ev_enc = torch.cuda.Event()
+            self._ev_start = torch.cuda.Event()
         return self._side
 
     def _join(self):
@@ -800,11 +908,13 @@ class ElboEngine(object):
                     out['vo_entropy'] = float(t[T_ENT2]) + self.N_vo * ENT_CONST
         return out
 
-    def backward(self, stream=None, side_extra=None):
+    def backward(self, stream=None, side_extra=None, main_wait=True):
         """Gradients of -ELBO into flat.gacc (fp64).  side_extra(side_stream_handle) is launched on
         the side stream after the decoder's reductions, concurrently with the encoder backward (the
         fused step draws the next step's subset, noise and decoder dropout masks there; nothing it
-        writes may be read by the encoder backward)."""
+        writes may be read by the encoder backward).  main_wait=False (flag hand-off only): the main
+        stream does not wait for the side stream's end here -- the caller's next launch does
+        (gpi_step_epilogue_adam wait_flag)."""
         st = stream if stream is not None else L.stream_handle()
         main = torch.cuda.current_stream()
         side = self._side_stream()
@@ -812,29 +922,52 @@ class ElboEngine(object):
         # runs on the main stream; the variational samples' (which need the ROM adjoint) follow
         # the ROM on the side stream, so the main chain never waits for the ROM.
         split = self._pending_join or self._rom_deferred
+        flags = self.handoff is not None
+        sst = C.c_void_p(side.cuda_stream)
         self.backward_a(st, split)
         # the decoder's slab reduction and the dense weight gradients depend only on what is
         # done by now: run them on the side stream, concurrently with the encoder backward
         # (enqueued after it, so the encoder stays on the main chain's queue in a graph)
-        self._ev_fork2.record(main)
+        if not flags:
+            self._ev_fork2.record(main)
         n_enc = len(self.enc_descs) if self.ep is not None else 0
         enc_split = n_enc and self.enc_reduce == 'split'
         if n_enc:
-            self.backward_b(st)
-            if enc_split:
+            # flags: the encoder backward's first conv signals flag 1 (the head backward is done), the
+            # input conv's backward flag 2 (the rest of the encoder backward is done)
+            self.backward_b(st, sig=1 if flags else None)
+            if enc_split and not flags:
                 self._ev_enc.record(main)
-            self.backward_c(st, enc_split)
+            self.backward_c(st, enc_split, sig=2 if (flags and enc_split) else None)
+        elif flags:
+            self._signal(1, st)
         # (captured ahead of the encoder backward instead, the side branch took the launch stream
         # and the main chain the pooled one: 0.7526 vs 0.6289 ms per step, r03)
-        side.wait_event(self._ev_fork2)
-        self.backward_side_a(C.c_void_p(side.cuda_stream), split, side_extra)
+        if flags:
+            self._wait(1, sst)
+        else:
+            side.wait_event(self._ev_fork2)
+        self.backward_side_a(sst, split, side_extra)
         if split:
             self._pending_join = False          # joined below with the rest of the side work
         if enc_split:
-            side.wait_event(self._ev_enc)
-            self.backward_side_b(C.c_void_p(side.cuda_stream))
-        self._ev_join2.record(side)
-        main.wait_event(self._ev_join2)
+            if flags:
+                self._wait(2, sst)
+            else:
+                side.wait_event(self._ev_enc)
+            self.backward_side_b(sst)
+        if flags:
+            # the side's end by flag on the main chain (a wait launch, or folded into the caller's
+            # epilogue: main_wait False); the event join (capture legality) after the step's last
+            # kernel: rejoin()
+            self._signal(3, sst)
+            if main_wait:
+                self._wait(3, st)
+            self._ev_join2.record(side)
+            self._rejoin_pending = True
+        else:
+            self._ev_join2.record(side)
+            main.wait_event(self._ev_join2)
 
     def finalize(self, out, accumulate=False, step=None, stream=None, zero_acc=False):
         st = stream if stream is not None else L.stream_handle()

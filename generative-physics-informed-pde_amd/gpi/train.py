@@ -143,6 +143,16 @@ class FusedElboStep(object):
         self.epi_adam = L.StepEpilogueDesc.from_buffer_copy(self.epi)
         self.epi_adam.step = None                  # Adam's counter: incremented once by the fused launch
         self.done_ctr = torch.zeros(1, dtype=torch.int32, device=dev)
+        # side-stream hand-offs by device flags (gpi_stream_signal / gpi_stream_wait) instead of graph
+        # events between the streams; GPI_HANDOFF=events keeps the events (A/B)
+        self.handoff_flags = torch.zeros(8, dtype=torch.int32, device=dev)   # [0..3] flags, [4] wait timeout
+        self.handoff = os.environ.get('GPI_HANDOFF', 'flags') if self.graph_mode == 'single' else 'events'
+        if self.handoff == 'flags':
+            self.engine.set_flag_handoff(self.handoff_flags[:4], self.step_ctr, self.handoff_flags[4:5])
+            if self.fuse_adam:
+                # the join with the side stream's last reduction inside the fused epilogue + Adam launch
+                self.epi_adam.wait_flag = self.handoff_flags.data_ptr() + 4 * 3
+                self.epi_adam.wait_err = self.handoff_flags.data_ptr() + 4 * 4
         self.graph = None
         # the first step's noise; every step then draws the next step's during its backward
         self._launch_noise(L.stream_handle(), self.idx, sub0=100)
@@ -179,6 +189,7 @@ class FusedElboStep(object):
         """One step without the parameter update (gradient in flat.G and the ELBO terms delivered;
         update() then applies Adam)."""
         self._forward_backward(stream, epilogue=True)
+        self.engine.rejoin()
 
     def _forward_backward(self, stream=None, epilogue=True):
         """One step without the parameter update.  The step's noise and subset were drawn by the
@@ -192,8 +203,11 @@ class FusedElboStep(object):
         self.engine.forward(st, compute_value=False, zero_gacc=False, zero_scratch=False, running='defer')
         # next step's subset / noise / decoder masks concurrently with the encoder backward; the
         # encoder's masks by the epilogue below (the encoder backward reads this step's)
+        # the fused epilogue + Adam launch (update(fused=True)) waits for the side stream itself; every
+        # other continuation needs the main stream to wait here
         self.engine.backward(st, side_extra=lambda sst: self._launch_noise(sst, self.idx_next, codecs=('dec',),
-                                                                           subset=not early))
+                                                                           subset=not early),
+                             main_wait=epilogue or not self.fuse_adam)
         if epilogue:                  # (else: launched by update(fused=True), with Adam)
             L.check(L.lib().gpi_step_epilogue(C.byref(self.epi), st), 'step epilogue')
 
@@ -229,7 +243,13 @@ class FusedElboStep(object):
         self._forward_backward(epilogue=not fused)
         self.allreduce()
         self.update(fused=fused)
+        self.engine.rejoin()
         self._mark_optimizer_step()
+
+    def check_handoff(self):
+        """Raise if a side-stream flag wait timed out (host sync; results of that step are invalid)."""
+        if int(self.handoff_flags[4].item()) != 0:
+            raise RuntimeError('FusedElboStep: a cross-stream flag wait timed out (gpi_stream_wait)')
 
     # ------------------------------------------------------------------
     def _mutable_state(self):
@@ -238,6 +258,7 @@ class FusedElboStep(object):
         statistics scratch."""
         ws = self.engine.ws
         return [self.flat.P, self.m, self.v, self.step_ctr, self.rng_off, self.idx, self.idx_next, self.done_ctr,
+                self.handoff_flags,
                 self.flat.gacc, self.flat.G, ws.t_ws, ws.t_scr, ws.t_parts, ws.t_flag, self.last_terms] + \
             self.engine.running.buffers
 
@@ -271,6 +292,7 @@ class FusedElboStep(object):
         elif self.split_graph:
             with torch.cuda.graph(self.g_fb):
                 self.forward_backward()
+                self.engine.rejoin()
             self.g_up = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.g_up):
                 self.update()
@@ -280,6 +302,7 @@ class FusedElboStep(object):
                 self._forward_backward(epilogue=not fused)
                 self.allreduce()        # RCCL: captured as a graph node
                 self.update(fused=fused)
+                self.engine.rejoin()
         self.graph = True
 
     def _capture_segments(self):
@@ -290,6 +313,9 @@ class FusedElboStep(object):
         two-stream graph the host walk (~0.59 ms) paced the GPU and the side stream's kernels were
         submitted late, so the step waited at the join for them."""
         e = self.engine
+        e.handoff = None                     # the segments are joined by events between the graphs
+        self.epi_adam.wait_flag = None
+        self.epi_adam.wait_err = None
         side = e._side_stream()
         rom = bool(e.roms)
         early = self.subset_early and rom

@@ -512,6 +512,35 @@ def test_capture_leaves_training_state_untouched(device, mode):
     assert (graph.segs is not None) == (mode == 'segments')
 
 
+def test_flag_handoff_matches_event_handoff(device, monkeypatch):
+    """The captured step with its side-stream hand-offs as device flags (gpi_stream_signal /
+    gpi_stream_wait, the default) leaves exactly what the same step with graph events between the
+    streams leaves: parameters, Adam moments, ELBO terms and step counter bit for bit over four
+    replays, and no flag wait timed out."""
+    import copy
+    from gpi.train import FusedElboStep
+    d = load('elbo_c32.npz')
+    model_a, bs = build_golden_model(d)
+    model_b = copy.deepcopy(model_a)
+    Xu, Xs, Y, F = cuda(d['Xu']), cuda(d['Xs']), cuda(d['Y']), cuda(d['F'])
+    monkeypatch.setenv('GPI_HANDOFF', 'events')
+    ev = FusedElboStep(model_a, Xu, bs, Xs, Y, F, lr=1e-3, seed=3)
+    monkeypatch.setenv('GPI_HANDOFF', 'flags')
+    fl = FusedElboStep(model_b, Xu, bs, Xs, Y, F, lr=1e-3, seed=3)
+    assert ev.engine.handoff is None and fl.engine.handoff is not None
+    ev.capture()
+    fl.capture()
+    for _ in range(4):
+        ev.step()
+        fl.step()
+    torch.cuda.synchronize()
+    fl.check_handoff()
+    for a, b in ((ev.flat.P, fl.flat.P), (ev.m, fl.m), (ev.v, fl.v), (ev.last_terms, fl.last_terms),
+                 (ev.step_ctr, fl.step_ctr)):
+        assert torch.equal(a, b)
+    assert int(fl.handoff_flags[0].item()) == 4        # the tag of the last step (counter 3, + 1)
+
+
 def test_fused_epilogue_adam_matches_two_launches(device):
     """gpi_step_epilogue_adam (epilogue + Adam in one launch, the single-process default) leaves
     exactly what gpi_step_epilogue followed by gpi_adam leave -- parameters, Adam moments, gradient,
