@@ -169,7 +169,7 @@ def step_conv_launches(e):
     out = []
     for prog, descs, ctx, B, n_sep, i0, i1 in progs:
         for i, op in enumerate(prog.ops):
-            if i < i0 or i >= i1:          # folded into the head launches (gpi_head_fold)
+            if i < i0 or i >= i1:          # not launched as a conv by the engine
                 continue
             for kind in (('fused',) if i >= n_sep else ('fwd', 'bwd')):
                 out.append(('%s.%s' % (op.name, kind), kind, fns[kind], descs[i], ctx, B))

@@ -112,8 +112,8 @@ struct ConvGeom {
                     // to each other), so the halo rows two tiles share are read from HBM once into that
                     // XCD's L2 instead of once per XCD.  0: tile = blockIdx.x (xcd_mode)
     int grid;       // launched workgroups (xcd remap)
-    uint32_t* sig;             // cross-stream hand-off (gpi_*_sig): workgroup 0 stores *sig_epoch + 1 at entry,
-    const int64_t* sig_epoch;  // i.e. once every earlier kernel of the stream has completed (gpi_stream_signal)
+    uint32_t* sig;             // cross-stream hand-off (gpi_*_sig): workgroup 0 increments *sig at entry, i.e.
+    const int64_t* sig_epoch;  // once every earlier kernel of the stream has completed (gpi_stream_signal)
     int in_sq, in_sr, in_sc;   // 256 chunks of the input image = (planes, rows, chunks)
     int g_sq, g_sr, g_sc;      // ... of the output-gradient image
     Div d_in4, d_P4, d_g4, d_PG4, d_cin, d_cout, d_win, d_tp, d_wout, d_w2;
@@ -475,11 +475,12 @@ __device__ __forceinline__ void touch_kernargs() {
 }
 constexpr int CONV_KARG_BYTES = (int)(sizeof(gpi_conv_desc) + sizeof(gpi_codec_ctx) + sizeof(ConvGeom) + 16);
 
-// the launch's hand-off signal (G.sig): one write-through store by workgroup 0 at entry -- the kernels
-// before this one on its stream have completed and released their writes by the time it starts
+// the launch's hand-off signal (G.sig): one relaxed agent-scope atomic increment by workgroup 0 at entry,
+// fire and forget -- the kernels before this one on its stream have completed and released their writes
+// by the time it starts (the counter protocol of gpi_stream_signal)
 __device__ __forceinline__ void entry_signal(const ConvGeom& G) {
     if (G.sig && blockIdx.x == 0 && threadIdx.x == 0)
-        __hip_atomic_store(G.sig, (uint32_t)(*G.sig_epoch + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(G.sig, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Global-address-space views of (pinned, hence generic) pointers: ordinary loads and

@@ -179,289 +179,9 @@ __device__ __forceinline__ QSeg qseg(const gpi_head_desc& d, int q) {
     return g;
 }
 
-// ------------------------------------------------------------------ folded codec convolutions
-// (gpi_head_forward_folded / gpi_head_backward_folded: the encoder's last conv and the decoder's first
-// one computed by the head's per-sample workgroup; same arithmetic as conv.hip's kernels)
-constexpr int FOLD_CIN = 16, FOLD_COUT = 8, FOLD_HW = 8;      // planes of at most 8 x 8
-constexpr int FOLD_PAD_IMG = FOLD_CIN * (FOLD_HW + 2) * (FOLD_HW + 2);   // padded input image
-constexpr int FOLD_W = FOLD_COUT * FOLD_CIN * 9;
-constexpr int FOLD_OUT = FOLD_COUT * FOLD_HW * FOLD_HW;
-constexpr int FOLD_IN = FOLD_CIN * FOLD_HW * FOLD_HW;
-
-struct FoldLds {
-    float img[FOLD_PAD_IMG];     // padded activation (feat) / latent image (lat), later the dY image
-    float w[FOLD_W];             // weights [cout][cin][3][3]
-    float o[FOLD_OUT];           // outputs / gradients [cout][HWo] or [cin][HWi]
-    float o2[2 * FOLD_IN];       // input-gradient channel-sum operands: dbn | dbn x-hat
-    float sc[FOLD_CIN], sh[FOLD_CIN], gam[FOLD_CIN], mean[FOLD_CIN], inv[FOLD_CIN];
-    float oc[4 * FOLD_COUT];     // output BN-backward coefficients: mean, inv, mS, mSx
-    float ds[FOLD_COUT];         // Dropout2d scales of the output channels
-};
-
-// the GPI_REPLICAS records of field f of (group grp, stat st), summed in conv.hip stat_finish's order
-// (per half the even and the odd replicas, then the halves), which tests/gpu_masks.py reproduces
-__device__ __forceinline__ double fold_stat(const gpi_codec_ctx& c, int grp, int64_t st, int f) {
-    const int64_t rs = (int64_t)GPI_MAX_GROUPS * c.n_stats * 4;          // doubles per replica
-    const double* p = &c.stats[(int64_t)grp * c.n_stats + st].sum + f;
-    double h[2];
-#pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
-        double s0 = 0.0, s1 = 0.0;
-#pragma unroll
-        for (int r = 0; r < 8; r += 2) {
-            s0 += p[(8 * hh + r) * rs];
-            s1 += p[(8 * hh + r + 1) * rs];
-        }
-        h[hh] = s0 + s1;
-    }
-    return h[0] + h[1];
-}
-
-// conv.hip mean_invstd: every rounding spelled out
-__device__ __forceinline__ void fold_mean_invstd(double s, double s2, double n, float eps, float& mean, float& inv) {
-    const double m = s / n;
-    double var = fma(-m, m, s2 / n);
-    if (var < 0.0) var = 0.0;
-    mean = (float)m;
-    inv = (float)(1.0 / sqrt(var + (double)eps));
-}
-
-__device__ __forceinline__ int fold_group(const gpi_codec_ctx& c, int s, int& gsz) {
-    const int g = group_of(c.groups, s);
-    gsz = karg_sel(c.groups.start, g + 1) - karg_sel(c.groups.start, g);
-    return g;
-}
-
-// weights [cout][cin][9] of c into F.w; the input BN coefficients (gamma, beta, batch statistics of
-// the sample's group) into F.sc / F.sh / F.gam / F.mean / F.inv (threads < cin)
-__device__ __forceinline__ void fold_stage_params(const gpi_conv_desc& c, const gpi_codec_ctx& x, const float* P,
-                                                  FoldLds& F, int s) {
-    const int tid = threadIdx.x;
-    const int nw = c.cout * c.cin * 9;
-    for (int e = tid; e < nw; e += HT) F.w[e] = P[c.w_off + e];
-    if (c.in_bn && tid < c.cin) {
-        int gsz;
-        const int g = fold_group(x, s, gsz);
-        const double s1 = fold_stat(x, g, c.in_stat + tid, 0), s2 = fold_stat(x, g, c.in_stat + tid, 1);
-        float mean, inv;
-        fold_mean_invstd(s1, s2, (double)gsz * c.h_in * c.w_in, x.bn_eps, mean, inv);
-        const float gam = P[c.gamma_off + tid], bet = P[c.beta_off + tid];
-        F.gam[tid] = gam;
-        F.mean[tid] = mean;
-        F.inv[tid] = inv;
-        F.sc[tid] = gam * inv;
-        F.sh[tid] = fmaf(-(mean * gam), inv, bet);
-    }
-    if (tid >= 64 && tid < 64 + c.cout)
-        F.ds[tid - 64] = c.drop_off >= 0 ? x.ws[c.drop_off + (int64_t)s * c.cout + (tid - 64)] : 1.f;
-}
-
-// Plane geometry of a folded conv: power-of-two sides (host-checked), so every pixel decomposition is a
-// shift; the stride is a template parameter (no runtime division anywhere in these loops).
-struct FoldGeom {
-    int lwi, lhwi, lwo, lhwo, Wp, Hp, PP;      // log2 widths / plane sizes, padded pitch / rows / plane
-};
-
-__device__ __forceinline__ int ilog2(int v) { return 31 - __clz(v); }
-
-__device__ __forceinline__ FoldGeom fold_geom(const gpi_conv_desc& c) {
-    FoldGeom g;
-    g.lwi = ilog2(c.w_in);
-    g.lhwi = ilog2(c.h_in * c.w_in);
-    g.lwo = ilog2(c.w_out);
-    g.lhwo = ilog2(c.h_out * c.w_out);
-    g.Wp = c.w_in + 2;
-    g.Hp = c.h_in + 2;
-    g.PP = g.Hp * g.Wp;
-    return g;
-}
-
-// the padded input image of sample s: BN + ReLU of the raw input (in_bn) or the raw input itself;
-// src: the raw input in the program's layout (or, src_lds, already in LDS as [cin][HWi]).  The zero
-// border is written by the first pass; callers sync before reading.
-__device__ __forceinline__ void fold_input_image(const gpi_conv_desc& c, const float* ws, FoldLds& F, int s,
-                                                 const float* src_lds) {
-    const FoldGeom G = fold_geom(c);
-    const int HWi = 1 << G.lhwi;
-    for (int e = threadIdx.x; e < c.cin * G.PP; e += HT) F.img[e] = 0.f;
-    __syncthreads();
-    for (int e = threadIdx.x; e < c.cin * HWi; e += HT) {
-        const int ci = e >> G.lhwi, p = e & (HWi - 1), y = p >> G.lwi, x = p & (c.w_in - 1);
-        float v = src_lds ? src_lds[e] : ws[c.in_off + ((int64_t)s * c.in_ctot + c.in_c0) * HWi + e];
-        if (c.in_bn) v = fmaxf(fmaf(v, F.sc[ci], F.sh[ci]), 0.f);
-        F.img[ci * G.PP + (y + 1) * G.Wp + x + 1] = v;
-    }
-}
-
-// forward of the folded conv for sample s: F.o[co * HWo + p] = dropout(conv(img)); stored to the
-// output buffer; with a stats epilogue the per-channel fp32 sums go to the group's replica record
-template <int S>
-__device__ __forceinline__ void fold_forward_s(const gpi_conv_desc& c, const gpi_codec_ctx& x, FoldLds& F, int s,
-                                               float* out_copy) {
-    const int tid = threadIdx.x;
-    const FoldGeom G = fold_geom(c);
-    const int HWo = 1 << G.lhwo;
-    for (int e = tid; e < c.cout * HWo; e += HT) {
-        const int co = e >> G.lhwo, p = e & (HWo - 1), oy = p >> G.lwo, ox = p & (c.w_out - 1);
-        float acc = 0.f;
-        const float* im0 = F.img + (oy * S) * G.Wp + ox * S;
-        const float* w0 = F.w + co * c.cin * 9;
-        for (int ci = 0; ci < c.cin; ++ci) {
-            const float* im = im0 + ci * G.PP;
-            const float* w = w0 + ci * 9;
-#pragma unroll
-            for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-                for (int kx = 0; kx < 3; ++kx) acc = fmaf(w[ky * 3 + kx], im[ky * G.Wp + kx], acc);
-        }
-        acc *= F.ds[co];
-        F.o[e] = acc;
-        if (out_copy) out_copy[e] = acc;
-        x.ws[c.out_off + ((int64_t)s * c.out_ctot + c.out_c0) * HWo + e] = acc;
-    }
-    if (c.epilogue != GPI_EPI_STORE_STATS || c.out_stat < 0) return;
-    __syncthreads();
-    // per channel: 16 lanes sum its pixels, fold by shuffles, one fp64 atomic per (channel, field)
-    int gsz;
-    const int g = fold_group(x, s, gsz);
-    for (int co = tid >> 4; co < c.cout; co += HT / 16) {
-        const int part = tid & 15;
-        float a = 0.f, b = 0.f;
-        for (int p = part; p < HWo; p += 16) {
-            const float v = F.o[co * HWo + p];
-            a += v;
-            b += v * v;
-        }
-#pragma unroll
-        for (int m = 8; m > 0; m >>= 1) {
-            a += __shfl_xor(a, m, 64);
-            b += __shfl_xor(b, m, 64);
-        }
-        if (part == 0) {
-            gpi_stat* st = x.stats + ((int64_t)(blockIdx.x % GPI_REPLICAS) * GPI_MAX_GROUPS + g) * x.n_stats +
-                           c.out_stat + co;
-            atomicAdd(&st->sum, (double)a);
-            atomicAdd(&st->sumsq, (double)b);
-        }
-    }
-}
-
-__device__ __forceinline__ void fold_forward(const gpi_conv_desc& c, const gpi_codec_ctx& x, FoldLds& F, int s,
-                                             float* out_copy) {
-    if (c.stride == 2) fold_forward_s<2>(c, x, F, s, out_copy);
-    else fold_forward_s<1>(c, x, F, s, out_copy);
-}
-
-// backward of the folded conv for sample s, given its output gradient dY in F.o ([cout][HWo], already
-// BN-backward'ed and dropout-scaled) and the padded input image in F.img (the activation): weight
-// gradient slab row s, input gradient (ReLU mask, S_in (+)= gamma dbn) to gin and to gin_copy
-// ([cin][HWi], may be nullptr), dgamma / dbeta partials and the input's BN-backward sums
-template <int S>
-__device__ __forceinline__ void fold_backward_s(const gpi_conv_desc& c, const gpi_codec_ctx& x, FoldLds& F, int s,
-                                                float* gin_copy) {
-    const int tid = threadIdx.x;
-    const FoldGeom G = fold_geom(c);
-    const int HWi = 1 << G.lhwi, HWo = 1 << G.lhwo;
-    const int J = c.cin * 9, rowlen = c.cout * J + (c.in_bn ? 2 * c.cin : 0);
-    float* slab = c.wpart_off >= 0 ? x.wpart + c.wpart_off + (int64_t)s * rowlen : nullptr;
-    // weight gradient: dW[co][ci][ky][kx] = sum_p dY[co][p] img[ci][oy S + ky][ox S + kx]; item (ci, tap)
-    // of every output channel per thread (the division by 9 is by a constant)
-    if (slab) {
-        for (int r = tid; r < J; r += HT) {
-            const int ci = r / 9, t = r - 9 * ci, ky = t / 3, kx = t - 3 * ky;
-            const float* im = F.img + ci * G.PP + ky * G.Wp + kx;
-            for (int co = 0; co < c.cout; ++co) {
-                const float* g = F.o + co * HWo;
-                float a0 = 0.f, a1 = 0.f;
-                for (int p = 0; p < HWo; p += 2) {
-                    const int oy = p >> G.lwo, ox = p & (c.w_out - 1);
-                    a0 = fmaf(g[p], im[(oy * S) * G.Wp + ox * S], a0);
-                    a1 = fmaf(g[p + 1], im[(oy * S) * G.Wp + (ox + 1) * S], a1);
-                }
-                slab[co * J + r] = a0 + a1;
-            }
-        }
-    }
-    if (c.gin_off < 0) return;
-    // input gradient: pixel (iy, ix) receives output (oy, ox) through tap (ky, kx) iff
-    // oy S - 1 + ky = iy and ox S - 1 + kx = ix
-    for (int e = tid; e < c.cin * HWi; e += HT) {
-        const int ci = e >> G.lhwi, p = e & (HWi - 1), iy = p >> G.lwi, ix = p & (c.w_in - 1);
-        float a = 0.f;
-        for (int co = 0; co < c.cout; ++co) {
-            const float* w = F.w + (co * c.cin + ci) * 9;
-            const float* g = F.o + co * HWo;
-#pragma unroll
-            for (int ky = 0; ky < 3; ++ky) {
-                const int ty = iy + 1 - ky;
-                if (ty < 0 || (S == 2 && (ty & 1))) continue;
-                const int oy = S == 2 ? ty >> 1 : ty;
-                if (oy >= c.h_out) continue;
-#pragma unroll
-                for (int kx = 0; kx < 3; ++kx) {
-                    const int tx = ix + 1 - kx;
-                    if (tx < 0 || (S == 2 && (tx & 1))) continue;
-                    const int ox = S == 2 ? tx >> 1 : tx;
-                    if (ox >= c.w_out) continue;
-                    a = fmaf(w[ky * 3 + kx], g[(oy << G.lwo) + ox], a);
-                }
-            }
-        }
-        float* gp = x.ws + c.gin_off + ((int64_t)s * c.in_ctot + c.in_c0) * HWi + e;
-        const float prev = c.gin_accumulate ? *gp : 0.f;
-        if (c.in_bn) {
-            const float av = F.img[ci * G.PP + (iy + 1) * G.Wp + ix + 1];
-            const float dbn = av > 0.f ? a : 0.f;
-            const float lbet = F.sh[ci] + F.mean[ci] * F.sc[ci];       // conv.hip: beta from the coefficients
-            F.o2[e] = dbn;
-            F.o2[FOLD_IN + e] = dbn * ((av - lbet) * (1.f / F.gam[ci]));
-            *gp = prev + F.gam[ci] * dbn;
-        } else {
-            *gp = prev + a;
-            if (gin_copy) gin_copy[e] = a;
-        }
-    }
-    if (!c.in_bn) return;
-    __syncthreads();
-    int gsz;
-    const int g = fold_group(x, s, gsz);
-    for (int ci = tid >> 4; ci < c.cin; ci += HT / 16) {
-        const int part = tid & 15;
-        float sd = 0.f, sdx = 0.f;
-        for (int p = part; p < HWi; p += 16) {
-            sd += F.o2[ci * HWi + p];
-            sdx += F.o2[FOLD_IN + ci * HWi + p];
-        }
-#pragma unroll
-        for (int m = 8; m > 0; m >>= 1) {
-            sd += __shfl_xor(sd, m, 64);
-            sdx += __shfl_xor(sdx, m, 64);
-        }
-        if (part == 0) {
-            if (slab) {
-                slab[c.cout * J + ci] = sdx;                 // dgamma partial
-                slab[c.cout * J + c.cin + ci] = sd;          // dbeta partial
-            }
-            gpi_stat* st = x.stats + ((int64_t)(blockIdx.x % GPI_REPLICAS) * GPI_MAX_GROUPS + g) * x.n_stats +
-                           c.in_stat + ci;
-            const double gm = F.gam[ci];
-            atomicAdd(&st->ssum, gm * (double)sd);
-            atomicAdd(&st->sxsum, gm * (double)sdx);
-        }
-    }
-}
-
-__device__ __forceinline__ void fold_backward(const gpi_conv_desc& c, const gpi_codec_ctx& x, FoldLds& F, int s,
-                                              float* gin_copy) {
-    if (c.stride == 2) fold_backward_s<2>(c, x, F, s, gin_copy);
-    else fold_backward_s<1>(c, x, F, s, gin_copy);
-}
-
-__global__ __launch_bounds__(HT) void head_fwd_kernel(gpi_head_desc d, const float* __restrict__ P, float* ws,
-                                                      gpi_head_fold Fd) {
+__global__ __launch_bounds__(HT) void head_fwd_kernel(gpi_head_desc d, const float* __restrict__ P, float* ws) {
     __shared__ float v0[VMAX], v1[VMAX], v2[VMAX], v3[VMAX];
     __shared__ float scratch[4];
-    __shared__ FoldLds FL;
     const int s = blockIdx.x;
     const int tid = threadIdx.x;
     const bool enc = s < d.n_enc;
@@ -472,17 +192,8 @@ __global__ __launch_bounds__(HT) void head_fwd_kernel(gpi_head_desc d, const flo
 
     if (enc) {
         if (d.flags & GPI_HEAD_ENC) {
-            if (Fd.has_feat) {
-                // the encoder's last conv: its (dropout-scaled) output is this sample's feature row
-                fold_stage_params(Fd.feat, Fd.enc_ctx, P, FL, s);
-                __syncthreads();
-                fold_input_image(Fd.feat, ws, FL, s, nullptr);
-                __syncthreads();
-                fold_forward(Fd.feat, Fd.enc_ctx, FL, s, v0);
-            } else {
-                const float* f = ws + d.feat + (int64_t)s * d.d_feat;
-                for (int k = tid; k < d.d_feat; k += HT) v0[k] = f[k];
-            }
+            const float* f = ws + d.feat + (int64_t)s * d.d_feat;
+            for (int k = tid; k < d.d_feat; k += HT) v0[k] = f[k];
             __syncthreads();
             matvec(P + d.fc_w, P + d.fc_b, v0, d.d_feat, d.d_feat, v1);
             __syncthreads();
@@ -542,14 +253,6 @@ __global__ __launch_bounds__(HT) void head_fwd_kernel(gpi_head_desc d, const flo
         matvec(P + d.lat_w, P + d.lat_b, z, d.d_lat, dz, v1);
         __syncthreads();
         for (int j = tid; j < d.d_lat; j += HT) lat[j] = v1[j];
-        if (Fd.has_lat) {
-            // the decoder's first conv on the latent image (its output and batch sums)
-            fold_stage_params(Fd.lat, Fd.dec_ctx, P, FL, s);
-            __syncthreads();
-            fold_input_image(Fd.lat, ws, FL, s, v1);
-            __syncthreads();
-            fold_forward(Fd.lat, Fd.dec_ctx, FL, s, nullptr);
-        }
     }
     if (!enc && (g.flags & GPI_HEAD_GP)) {
         const bool lockx = g.flags & GPI_HEAD_LOCKX;             // uniform per workgroup
@@ -586,10 +289,9 @@ __global__ __launch_bounds__(HT) void head_fwd_kernel(gpi_head_desc d, const flo
 }
 
 __global__ __launch_bounds__(HT) void head_bwd_kernel(gpi_head_desc d, const float* __restrict__ P, float* ws,
-                                                      double* gacc, int s_off, gpi_head_fold Fd) {
+                                                      double* gacc, int s_off) {
     __shared__ float v0[VMAX], v1[VMAX], v2[VMAX], v3[VMAX];
     __shared__ float part[HT];
-    __shared__ FoldLds FA, FB;           // the decoder's first conv, the encoder's last conv
     const int s = blockIdx.x + s_off;
     const int tid = threadIdx.x;
     const bool enc = s < d.n_enc;
@@ -597,53 +299,11 @@ __global__ __launch_bounds__(HT) void head_bwd_kernel(gpi_head_desc d, const flo
     const QSeg g = qseg(d, q);
     const int dz = d.d_z;
     float* dz_ = v0;   // dJ/dz
-    const bool feat = enc && Fd.has_feat && (d.flags & GPI_HEAD_ENC);
-
-    // the folded convs' parameters, input BN coefficients and batch statistics first: their loads are in
-    // flight together (the encoder conv's are consumed at the end)
-    if (feat) fold_stage_params(Fd.feat, Fd.enc_ctx, P, FB, s);
-    if (Fd.has_lat && (d.flags & GPI_HEAD_LATENT)) {
-        const gpi_conv_desc& c = Fd.lat;
-        fold_stage_params(c, Fd.dec_ctx, P, FA, s);
-        if (tid >= 32 && tid < 32 + c.cout) {          // the output's BN-backward coefficients
-            const int co = tid - 32;
-            int gsz;
-            const int gr = fold_group(Fd.dec_ctx, s, gsz);
-            const double n = (double)gsz * c.h_out * c.w_out;
-            const int64_t st = c.out_stat + co;
-            float mean, inv;
-            fold_mean_invstd(fold_stat(Fd.dec_ctx, gr, st, 0), fold_stat(Fd.dec_ctx, gr, st, 1), n, Fd.dec_ctx.bn_eps,
-                             mean, inv);
-            FA.oc[4 * co] = mean;
-            FA.oc[4 * co + 1] = inv;
-            FA.oc[4 * co + 2] = (float)(fold_stat(Fd.dec_ctx, gr, st, 2) / n);
-            FA.oc[4 * co + 3] = (float)(fold_stat(Fd.dec_ctx, gr, st, 3) / n);
-        }
-    }
-    __syncthreads();
-    if (feat) fold_input_image(Fd.feat, ws, FB, s, nullptr);
 
     // latent map: dz = lat_w^T glat
     if (d.flags & GPI_HEAD_LATENT) {
-        if (Fd.has_lat) {
-            // the decoder's first conv backward: dY = BN-backward of its output's S, weight-gradient
-            // slab row, input gradient = the latent image gradient (stored at glat, and into v1)
-            const gpi_conv_desc& c = Fd.lat;
-            fold_input_image(c, ws, FA, s, nullptr);
-            const int HWo = c.h_out * c.w_out;
-            for (int e = tid; e < c.cout * HWo; e += HT) {
-                const int co = e / HWo, p = e - co * HWo;
-                const int64_t o = ((int64_t)s * c.out_ctot + c.out_c0 + co) * HWo + p;
-                const float zv = ws[c.out_off + o], sv = ws[c.gout_off + o];
-                const float* oc = FA.oc + 4 * co;
-                FA.o[e] = FA.ds[co] * ((sv - oc[2] - ((zv - oc[0]) * oc[1]) * oc[3]) * oc[1]);
-            }
-            __syncthreads();
-            fold_backward(c, Fd.dec_ctx, FA, s, v1);
-        } else {
-            const float* gl = ws + d.glat + (int64_t)s * d.d_lat;
-            for (int j = tid; j < d.d_lat; j += HT) v1[j] = gl[j];
-        }
+        const float* gl = ws + d.glat + (int64_t)s * d.d_lat;
+        for (int j = tid; j < d.d_lat; j += HT) v1[j] = gl[j];
         __syncthreads();
         matvec_t2(P + d.lat_w, v1, d.d_lat, P, v1, 0, dz, dz_, false, part);
     } else {
@@ -724,14 +384,6 @@ __global__ __launch_bounds__(HT) void head_bwd_kernel(gpi_head_desc d, const flo
     __syncthreads();
     matvec_t2(P + d.fc_w, v3, d.d_feat, P, v3, 0, d.d_feat, v0, false, part);
     __syncthreads();
-    if (feat) {
-        // the encoder's last conv backward on its (direct, dropout-scaled) output gradient
-        const int HWo = Fd.feat.h_out * Fd.feat.w_out;
-        for (int e = tid; e < d.d_feat; e += HT) FB.o[e] = v0[e] * FB.ds[e / HWo];
-        __syncthreads();
-        fold_backward(Fd.feat, Fd.enc_ctx, FB, s, nullptr);
-        return;
-    }
     for (int k = tid; k < d.d_feat; k += HT) ws[d.gfeat + (int64_t)s * d.d_feat + k] = v0[k];
 }
 
@@ -785,36 +437,6 @@ __global__ __launch_bounds__(256) void outer_gemm_kernel(GemmArgs a, const float
     }
 }
 
-// the folded convs' shapes (gpi.h gpi_head_fold) and their wiring to the head's buffers
-bool pow2(int v) { return v >= 2 && (v & (v - 1)) == 0; }
-
-bool fold_conv_ok(const gpi_conv_desc& c) {
-    return c.k == 3 && c.pad == 1 && (c.stride == 1 || c.stride == 2) && !c.upsample && c.cin >= 1 &&
-           pow2(c.w_in) && pow2(c.h_in) && pow2(c.w_out) && pow2(c.h_out) &&
-           c.cin <= FOLD_CIN && c.cout >= 1 && c.cout <= FOLD_COUT && c.h_in <= FOLD_HW && c.w_in <= FOLD_HW &&
-           c.h_out * c.stride == c.h_in && c.w_out * c.stride == c.w_in && c.in_off >= 0;
-}
-
-bool fold_ok(const gpi_head_desc* d, const gpi_head_fold* f) {
-    if (!f) return true;
-    if (f->has_feat) {
-        const gpi_conv_desc& c = f->feat;
-        if (!fold_conv_ok(c) || !c.in_bn || c.gout_mode != 1 || c.epilogue != GPI_EPI_STORE || c.out_off != d->feat ||
-            c.out_c0 != 0 || c.out_ctot != c.cout || c.cout * c.h_out * c.w_out != d->d_feat || !f->enc_ctx.stats ||
-            !f->enc_ctx.ws || !(d->flags & GPI_HEAD_ENC))
-            return false;
-    }
-    if (f->has_lat) {
-        const gpi_conv_desc& c = f->lat;
-        if (!fold_conv_ok(c) || c.in_bn || c.stride != 1 || c.gout_mode != 0 || c.epilogue != GPI_EPI_STORE_STATS ||
-            c.out_stat < 0 || c.in_off != d->lat || c.in_c0 != 0 || c.in_ctot != c.cin ||
-            c.cin * c.h_in * c.w_in != d->d_lat || (c.gin_off >= 0 && (c.gin_off != d->glat || c.gin_accumulate)) ||
-            !f->dec_ctx.stats || !f->dec_ctx.ws || !(d->flags & GPI_HEAD_LATENT))
-            return false;
-    }
-    return true;
-}
-
 bool head_ok(const gpi_head_desc* d) {
     return d && d->d_z > 0 && d->d_z <= VMAX && d->d_feat <= VMAX && d->d_lat <= VMAX && d->d_x <= VMAX &&
            d->n_enc >= 0 && d->n_q >= 0 && d->n_q2 >= 0 && (d->n_enc + d->n_q + d->n_q2) > 0 && d->terms &&
@@ -823,41 +445,24 @@ bool head_ok(const gpi_head_desc* d) {
 
 }  // namespace
 
-extern "C" int gpi_head_forward_folded(const gpi_head_desc* d, const gpi_head_fold* f, const float* params, float* ws,
-                                       void* stream) {
-    if (!head_ok(d) || !params || !ws) return GPI_ERR_ARG;
-    if (!fold_ok(d, f)) return GPI_ERR_UNSUPPORTED;
-    gpi_head_fold F{};
-    if (f) F = *f;
-    hipLaunchKernelGGL(head_fwd_kernel, dim3(d->n_enc + d->n_q + d->n_q2), dim3(HT), 0, (hipStream_t)stream, *d, params, ws,
-                       F);
-    GPI_CHECK_LAUNCH();
-    return GPI_OK;
-}
-
 extern "C" int gpi_head_forward(const gpi_head_desc* d, const float* params, float* ws, void* stream) {
-    return gpi_head_forward_folded(d, nullptr, params, ws, stream);
-}
-
-extern "C" int gpi_head_backward_folded(const gpi_head_desc* d, const gpi_head_fold* f, const float* params, float* ws,
-                                        double* gacc, void* stream) {
-    if (!head_ok(d) || !params || !ws || !gacc) return GPI_ERR_ARG;
-    if (!fold_ok(d, f)) return GPI_ERR_UNSUPPORTED;
-    const bool pe = d->flags & GPI_HEAD_PART_ENC, pq = d->flags & GPI_HEAD_PART_Q;
-    if (pe && pq) return GPI_ERR_ARG;
-    const int nq = d->n_q + d->n_q2;
-    const int nb = pe ? d->n_enc : (pq ? nq : d->n_enc + nq), s_off = pq ? d->n_enc : 0;
-    if (nb == 0) return GPI_OK;
-    gpi_head_fold F{};
-    if (f) F = *f;
-    hipLaunchKernelGGL(head_bwd_kernel, dim3(nb), dim3(HT), 0, (hipStream_t)stream, *d, params, ws, gacc, s_off, F);
+    if (!head_ok(d) || !params || !ws) return GPI_ERR_ARG;
+    hipLaunchKernelGGL(head_fwd_kernel, dim3(d->n_enc + d->n_q + d->n_q2), dim3(HT), 0, (hipStream_t)stream, *d, params, ws);
     GPI_CHECK_LAUNCH();
     return GPI_OK;
 }
 
 extern "C" int gpi_head_backward(const gpi_head_desc* d, const float* params, float* ws, double* gacc,
                                  void* stream) {
-    return gpi_head_backward_folded(d, nullptr, params, ws, gacc, stream);
+    if (!head_ok(d) || !params || !ws || !gacc) return GPI_ERR_ARG;
+    const bool pe = d->flags & GPI_HEAD_PART_ENC, pq = d->flags & GPI_HEAD_PART_Q;
+    if (pe && pq) return GPI_ERR_ARG;
+    const int nq = d->n_q + d->n_q2;
+    const int nb = pe ? d->n_enc : (pq ? nq : d->n_enc + nq), s_off = pq ? d->n_enc : 0;
+    if (nb == 0) return GPI_OK;
+    hipLaunchKernelGGL(head_bwd_kernel, dim3(nb), dim3(HT), 0, (hipStream_t)stream, *d, params, ws, gacc, s_off);
+    GPI_CHECK_LAUNCH();
+    return GPI_OK;
 }
 
 extern "C" int gpi_outer_gemm(const gpi_gemm_item* items, int n_items, const float* ws, double* gacc,

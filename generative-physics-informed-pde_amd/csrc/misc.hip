@@ -261,21 +261,26 @@ __global__ __launch_bounds__(256) void subset_cand_rank_kernel(int32_t* out, con
     }
 }
 
-// Cross-stream hand-off by a device flag (gpi_stream_signal / gpi_stream_wait).  The signal kernel runs
+// Cross-stream hand-off by a device counter (gpi_stream_signal / gpi_stream_wait).  The signal kernel runs
 // after every earlier kernel of its stream has completed and released its writes (the queue's kernel
-// boundary), so one write-through store of the step's tag publishes them; the waiter spins on that word
-// with sc1 loads and exits, and the stream's next kernel starts with the usual acquire.  The tag is the
-// step counter + 1 (the counter changes only in the step's final epilogue, after every hand-off of the
-// step), so a flag left from the previous step never matches.  Every spin is bounded: on a timeout the
-// waiter sets *err and returns (the results are then garbage, the host reads the flag, nothing hangs).
+// boundary), so one relaxed agent-scope increment publishes them (no load, fire and forget); the waiter
+// spins on that word with sc1 loads until it reaches the step's count and exits, and the stream's next
+// kernel starts with the usual acquire.  Every step signals each flag exactly once, so the count after
+// step t's signal is t + 1 with t = the step counter, which changes only in the step's final epilogue,
+// after every hand-off of the step.  Every spin is bounded: on a timeout the waiter sets *err and
+// returns (the results are then garbage, the host reads the flag, nothing hangs).
 constexpr int WAIT_SPIN_MAX = 1 << 24;
 
 // every workgroup: one lane polls the flag (relaxed sc1 loads), then ONE agent acquire so that the
 // workgroup's later plain loads see what the signalling stream wrote, then the workgroup barrier
+__device__ __forceinline__ bool count_reached(const uint32_t* flag, uint32_t want) {
+    return (int32_t)(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - want) >= 0;
+}
+
 __device__ __forceinline__ void epilogue_wait(const uint32_t* flag, const int64_t* epoch, uint32_t* err) {
     if (threadIdx.x == 0) {
         const uint32_t want = (uint32_t)(*epoch + 1);
-        for (int i = 0; __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want; ++i) {
+        for (int i = 0; !count_reached(flag, want); ++i) {
             __builtin_amdgcn_s_sleep(2);
             if (i > WAIT_SPIN_MAX) {
                 if (err) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -288,15 +293,14 @@ __device__ __forceinline__ void epilogue_wait(const uint32_t* flag, const int64_
     __syncthreads();
 }
 
-__global__ void stream_signal_kernel(uint32_t* flag, const int64_t* epoch) {
-    if (threadIdx.x == 0)
-        __hip_atomic_store(flag, (uint32_t)(*epoch + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__global__ void stream_signal_kernel(uint32_t* flag) {
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __global__ void stream_wait_kernel(const uint32_t* flag, const int64_t* epoch, uint32_t* err) {
     if (threadIdx.x != 0) return;
     const uint32_t want = (uint32_t)(*epoch + 1);
-    for (int i = 0; __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want; ++i) {
+    for (int i = 0; !count_reached(flag, want); ++i) {
         __builtin_amdgcn_s_sleep(2);
         if (i > WAIT_SPIN_MAX) {
             if (err) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -309,7 +313,7 @@ __global__ void stream_wait_kernel(const uint32_t* flag, const int64_t* epoch, u
 
 extern "C" int gpi_stream_signal(uint32_t* flag, const int64_t* epoch, void* stream) {
     if (!flag || !epoch) return GPI_ERR_ARG;
-    hipLaunchKernelGGL(stream_signal_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, flag, epoch);
+    hipLaunchKernelGGL(stream_signal_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, flag);
     GPI_CHECK_LAUNCH();
     return GPI_OK;
 }
@@ -332,7 +336,7 @@ extern "C" int gpi_struct_sizes(int64_t* out, int n) {
                          (int64_t)sizeof(gpi_vo_precision_desc), (int64_t)sizeof(gpi_gp_sample_desc),
                          (int64_t)sizeof(gpi_vo_galerkin_desc), (int64_t)sizeof(gpi_step_epilogue_desc),
                          (int64_t)sizeof(gpi_fom_desc), (int64_t)sizeof(gpi_random_field_desc),
-                         (int64_t)sizeof(gpi_vo_sparse), (int64_t)sizeof(gpi_head_fold)};
+                         (int64_t)sizeof(gpi_vo_sparse)};
     const int k = (int)(sizeof(s) / sizeof(s[0]));
     if (!out || n < k) return GPI_ERR_ARG;
     for (int i = 0; i < k; ++i) out[i] = s[i];

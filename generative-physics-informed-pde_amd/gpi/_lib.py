@@ -172,14 +172,9 @@ class RandomFieldDesc(C.Structure):
                 ('ly', vp), ('lxt', vp), ('scale', vp), ('gamma', vp), ('seed', u64), ('sub', u64), ('work', vp), ('x', vp)]
 
 
-class HeadFold(C.Structure):
-    _fields_ = [('has_feat', i32), ('has_lat', i32), ('feat', ConvDesc), ('lat', ConvDesc), ('enc_ctx', CodecCtx),
-                ('dec_ctx', CodecCtx)]
-
-
 STRUCTS = [Stat, Groups, ConvDesc, CodecCtx, ReduceItem, HeadDesc, GemmItem, RomDesc, ResidualDesc, AdamDesc,
            VoQueryDesc, VoMomentsDesc, VoConditionDesc, VoPrecisionDesc, GpSampleDesc,
-           VoGalerkinDesc, StepEpilogueDesc, FomDesc, RandomFieldDesc, VoSparse, HeadFold]
+           VoGalerkinDesc, StepEpilogueDesc, FomDesc, RandomFieldDesc, VoSparse]
 
 # name -> (restype, argtypes)
 SIGNATURES = {
@@ -201,8 +196,6 @@ SIGNATURES = {
     'gpi_wgrad_reduce': (C.c_int, [C.POINTER(ReduceItem), C.c_int, vp, vp, vp]),
     'gpi_head_forward': (C.c_int, [C.POINTER(HeadDesc), vp, vp, vp]),
     'gpi_head_backward': (C.c_int, [C.POINTER(HeadDesc), vp, vp, vp, vp]),
-    'gpi_head_forward_folded': (C.c_int, [C.POINTER(HeadDesc), C.POINTER(HeadFold), vp, vp, vp]),
-    'gpi_head_backward_folded': (C.c_int, [C.POINTER(HeadDesc), C.POINTER(HeadFold), vp, vp, vp, vp]),
     'gpi_outer_gemm': (C.c_int, [C.POINTER(GemmItem), C.c_int, vp, vp, vp]),
     'gpi_rom': (C.c_int, [C.POINTER(RomDesc), vp]),
     'gpi_cgr_residual': (C.c_int, [C.POINTER(ResidualDesc), vp]),

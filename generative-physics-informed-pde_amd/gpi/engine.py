@@ -235,20 +235,14 @@ class ElboEngine(object):
         offD = lambda n: flat.offset(dec.get_parameter(n))
         dz = dec.dim_latent
         self.dz = dz
-        # the encoder's last conv and the decoder's first one run inside the head launches (gpi_head_fold:
-        # four launches less per step); GPI_HEAD_FOLD=0 keeps them as conv launches (A/B)
-        fold = os.environ.get('GPI_HEAD_FOLD', '1') != '0'
         # ---- encoder program
         if self.B_u > 0 and self.armortized:
             ec = enc.native_config()
             self.ep = encoder_program(**ec)
-            self.fold_feat = fold and self.ep.foldable_feat()
-            self.enc_descs = self.ep.layout(self.B_u, ws.ws, ws.stats, ws.parts, groups_struct([self.B_u]), offE,
-                                            per_sample_ops=(self.ep.ops[-1].name,) if self.fold_feat else ())
+            self.enc_descs = self.ep.layout(self.B_u, ws.ws, ws.stats, ws.parts, groups_struct([self.B_u]), offE)
             d_feat = self.ep.d_feat
         else:
             self.ep = None
-            self.fold_feat = False
             d_feat = 1
         # ---- decoder program (groups: unsup, sup, vo)
         dc = dec.native_config()
@@ -256,15 +250,13 @@ class ElboEngine(object):
         # exponentiated field's (reconstruct_log_eff_property = False)
         log_field = getattr(model, 'config', {}).get('reconstruct_log_eff_property', True)
         self.dp = decoder_program(final_epilogue=L.EPI_GAUSS_LOSS if log_field else L.EPI_GAUSS_EXP_LOSS, **dc)
-        self.fold_lat = fold and self.dp.foldable_lat()
         self.dec_sizes = [n for n in (self.B_u, self.N_s, self.N_vo) if n > 0]
         self.g_sup = (1 if self.B_u > 0 else 0) if self.N_s > 0 else None
         self.g_vo = ((self.B_u > 0) + (self.N_s > 0)) if self.N_vo > 0 else None
-        self.dec_descs = self.dp.layout(self.B, ws.ws, ws.stats, ws.parts, groups_struct(self.dec_sizes), offD,
-                                        per_sample_ops=(self.dp.ops[0].name,) if self.fold_lat else ())
+        self.dec_descs = self.dp.layout(self.B, ws.ws, ws.stats, ws.parts, groups_struct(self.dec_sizes), offD)
         # codec launch ranges: the encoder's ops [0, n_enc_conv), the decoder's [dec0, ...)
-        self.n_enc_conv = (len(self.enc_descs) - (1 if self.fold_feat else 0)) if self.ep is not None else 0
-        self.dec0 = 1 if self.fold_lat else 0
+        self.n_enc_conv = len(self.enc_descs) if self.ep is not None else 0
+        self.dec0 = 0
         # the loss epilogue consumes (mu, logsigma) in registers: nobody reads the output image (9.4 MB of
         # writes per step at C64)
         self.dec_descs[len(self.dec_descs) - 1].out_off = -1
@@ -491,33 +483,13 @@ class ElboEngine(object):
             torch.cuda.current_stream().wait_event(self._ev_join2)
             self._rejoin_pending = False
 
-    def head_fold(self):
-        """gpi_head_fold of the folded convs (or None): their descriptors and program contexts."""
-        if not (self.fold_feat or self.fold_lat):
-            return None
-        f = L.HeadFold()
-        f.has_feat, f.has_lat = int(self.fold_feat), int(self.fold_lat)
-        if self.fold_feat:
-            f.feat = self.enc_descs[len(self.enc_descs) - 1]
-            f.enc_ctx = self.ectx
-        if self.fold_lat:
-            f.lat = self.dec_descs[0]
-            f.dec_ctx = self.dctx
-        return f
-
     def _head_forward(self, st):
-        f = self.head_fold()
-        _run(_lib().gpi_head_forward_folded, C.byref(self.head), C.byref(f) if f is not None else None,
-             C.c_void_p(self.flat.P.data_ptr()), C.c_void_p(self.ws.t_ws.data_ptr()), st, what='head forward')
-        if self.bn_sync is not None and self.fold_lat:       # the folded decoder conv's output statistics
-            d = self.dec_descs[0]
-            self._sync_stats(d.out_stat, d.cout, 0, 'dec')
+        _run(_lib().gpi_head_forward, C.byref(self.head), C.c_void_p(self.flat.P.data_ptr()),
+             C.c_void_p(self.ws.t_ws.data_ptr()), st, what='head forward')
 
     def _head_backward(self, hd, st):
-        f = self.head_fold()
-        _run(_lib().gpi_head_backward_folded, C.byref(hd), C.byref(f) if f is not None else None,
-             C.c_void_p(self.flat.P.data_ptr()), C.c_void_p(self.ws.t_ws.data_ptr()),
-             C.c_void_p(self.flat.gacc.data_ptr()), st, what='head backward')
+        _run(_lib().gpi_head_backward, C.byref(hd), C.c_void_p(self.flat.P.data_ptr()),
+             C.c_void_p(self.ws.t_ws.data_ptr()), C.c_void_p(self.flat.gacc.data_ptr()), st, what='head backward')
 
     def eps_z(self):
         return self.ws.view(self.hb['eps_z'], self.B, self.dz)
@@ -662,9 +634,6 @@ class ElboEngine(object):
         """Main stream: decoder backward and the head backward (encoder samples only when split:
         the variational samples' need the ROM adjoint and follow it on the side stream)."""
         self._codec_backward(self.dec_descs, self.dec0, self.n_dec_sep, self.dctx, st, 'decoder backward')
-        if self.bn_sync is not None and self.fold_lat:       # the folded decoder conv's BN-backward sums
-            d = self.dec_descs[0]
-            self._sync_stats(d.out_stat, d.cout, 2, 'dec')
         if split:
             hd = L.HeadDesc.from_buffer_copy(self.head)
             hd.flags |= L.HEAD_PART_ENC

@@ -96,10 +96,8 @@ class CodecProgram(object):
         return op
 
     # ------------------------------------------------------------ lowering
-    def layout(self, B, ws, stats, parts, groups, param_offset, grad=True, per_sample_ops=()):
-        """Assign workspace / stat / partial-slab offsets for batch B.  per_sample_ops: names of ops
-        computed per sample by another launch (the head's folded convs, gpi_head_fold) -- one
-        weight-gradient slab row per sample instead of the conv kernels' tiling."""
+    def layout(self, B, ws, stats, parts, groups, param_offset, grad=True):
+        """Assign workspace / stat / partial-slab offsets for batch B."""
         for b in self.buffers:
             if b.external:
                 continue
@@ -159,7 +157,7 @@ class CodecProgram(object):
                 d.gin_off = -1
             nb = C.c_int32(0)
             L.check(L.lib().gpi_conv_blocks(C.byref(d), C.byref(groups), C.byref(nb)), 'gpi_conv_blocks(%s)' % op.name)
-            op.blocks = B if op.name in per_sample_ops else nb.value
+            op.blocks = nb.value
             op.numel = op.cout * op.cin * op.k * op.k
             op.rowlen = op.numel + (2 * op.cin if op.bn is not None else 0)
             d.wpart_off = parts.alloc(op.blocks * op.rowlen) if grad else -1
@@ -194,24 +192,6 @@ class CodecProgram(object):
                     item(base + op.numel, g, op.cin, op.rowlen, op.blocks)
                     item(base + op.numel + op.cin, b, op.cin, op.rowlen, op.blocks)
         return items
-
-    def foldable_feat(self):
-        """The encoder's last conv can run inside the head launches (gpi_head_fold.feat): a 3x3 / pad 1
-        conv without upsampling on a plane of at most 8 x 8, BN on its input, its output the
-        program's output (the FC input, no BN after it)."""
-        op = self.ops[-1]
-        return (self.kind == 'encoder' and op.dst is self.output and op.k == 3 and op.pad == 1 and not op.upsample
-                and op.bn is not None and not op.dst.bn_consumed and op.cin <= 16 and op.cout <= 8
-                and op.src.H <= 8 and op.src.W <= 8 and op.epilogue is None)
-
-    def foldable_lat(self):
-        """The decoder's first conv can run inside the head launches (gpi_head_fold.lat): a 3x3 / pad 1 /
-        stride 1 conv on the latent-map image (no BN on its input, at most 8 x 8), its output
-        BN-consumed."""
-        op = self.ops[0]
-        return (self.kind == 'decoder' and op.src is self.input and op.k == 3 and op.pad == 1 and op.stride == 1
-                and not op.upsample and op.bn is None and op.dst.bn_consumed and op.cin <= 16 and op.cout <= 8
-                and op.src.H <= 8 and op.src.W <= 8 and op.epilogue is None)
 
     def reduce_counts(self, param_offset):
         """Number of reduce_items() entries each op contributes, in op order."""

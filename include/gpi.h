@@ -464,9 +464,9 @@ int gpi_conv_loss_fused(const gpi_conv_desc* op, const gpi_codec_ctx* ctx, void*
 int gpi_codec_forward(const gpi_conv_desc* ops, int n_ops, const gpi_codec_ctx* ctx, void* stream);
 int gpi_codec_backward(const gpi_conv_desc* ops, int n_ops, const gpi_codec_ctx* ctx, void* stream);
 /* The same launches with a cross-stream hand-off signal folded into the FIRST kernel launched (ops[0]
- * forward, ops[n_ops-1] backward): its workgroup 0 stores (*epoch + 1) into *flag at entry, which is
- * what gpi_stream_signal on this stream right before the call would store (see gpi_stream_wait), without
- * a launch of its own.  flag NULL: no signal. */
+ * forward, ops[n_ops-1] backward): its workgroup 0 increments *flag at entry, which is what
+ * gpi_stream_signal on this stream right before the call would do (see gpi_stream_wait), without a
+ * launch of its own.  flag NULL: no signal (epoch: the wait's counter, checked non-NULL). */
 int gpi_conv_forward_sig(const gpi_conv_desc* op, const gpi_codec_ctx* ctx, uint32_t* flag, const int64_t* epoch,
                          void* stream);
 int gpi_conv_backward_sig(const gpi_conv_desc* op, const gpi_codec_ctx* ctx, uint32_t* flag, const int64_t* epoch,
@@ -480,30 +480,6 @@ int gpi_wgrad_reduce(const gpi_reduce_item* items, int n_items, const float* wpa
 int gpi_head_forward(const gpi_head_desc* d, const float* params, float* ws, void* stream);
 int gpi_head_backward(const gpi_head_desc* d, const float* params, float* ws, double* gacc, void* stream);
 
-/* The codec convolutions next to the dense head, run inside the head launches (one workgroup per
- * sample; no launch of their own): `feat` = the encoder's last conv, whose raw output IS the FC input
- * (no BatchNorm between: Encoder.py:175-182, the TransDown of the last encoder block,
- * codec.py:221-228), and `lat` = the decoder's first conv, whose input is the latent-map image
- * (Decoder.py:213,293-294: conv0 of the features Sequential).  Each is that conv's descriptor of the
- * codec program (the same buffers, statistics slots and Dropout2d scales) with its program's context.
- * Forward: feat's output (= the head's feature rows) from its BN + ReLU'd input, lat's output and its
- * per-channel fp64 sums from the latent image.  Backward: lat's BN-backward (its output's batch sums
- * are complete once its consumers ran), weight-gradient slab row and input gradient (= the latent
- * image gradient, stored at d->glat), and feat's weight-gradient / dgamma / dbeta slab row, input
- * gradient into its input's S buffer and BN-backward sums -- exactly what gpi_conv_forward /
- * gpi_conv_backward of those descriptors compute, except that the slab rows are one per SAMPLE
- * (wpart_off row s; the caller reduces B rows).  Supported: 3x3 kernels, pad 1, stride 1 or 2
- * without upsampling, at most 16 input and 8 output channels on planes of at most 16 x 16; feat with
- * an input BN and a direct output gradient, lat without. */
-typedef struct gpi_head_fold {
-    int32_t has_feat, has_lat;
-    gpi_conv_desc feat, lat;
-    gpi_codec_ctx enc_ctx, dec_ctx;
-} gpi_head_fold;
-int gpi_head_forward_folded(const gpi_head_desc* d, const gpi_head_fold* f, const float* params, float* ws,
-                            void* stream);
-int gpi_head_backward_folded(const gpi_head_desc* d, const gpi_head_fold* f, const float* params, float* ws,
-                             double* gacc, void* stream);
 int gpi_outer_gemm(const gpi_gemm_item* items, int n_items, const float* ws, double* gacc, void* stream);
 
 int gpi_rom(const gpi_rom_desc* d, void* stream);
@@ -566,7 +542,7 @@ typedef struct gpi_step_epilogue_desc {
     const uint64_t* drop_offset;
     uint64_t drop_sub;
     /* optional cross-stream wait folded into the epilogue (gpi_step_epilogue_adam only): every
-     * workgroup waits until *wait_flag == *step + 1 (the Adam step counter; see gpi_stream_wait) and
+     * workgroup waits until *wait_flag >= *step + 1 (the Adam step counter; see gpi_stream_wait) and
      * acquires before it reads the gradient accumulator -- the join with another stream's final
      * reductions without a wait launch; a timeout sets *wait_err.  NULL: no wait. */
     const uint32_t* wait_flag;
@@ -581,14 +557,15 @@ int gpi_adam(const gpi_adam_desc* d, void* stream);
  * uint32 arrival counter, zero before the first call (the launch leaves it zero). */
 int gpi_step_epilogue_adam(const gpi_step_epilogue_desc* d, const gpi_adam_desc* a, uint32_t* done, void* stream);
 
-/* Cross-stream hand-off by a device flag instead of an event edge between two streams (in a captured
- * step each such edge costs the waiting hardware queue ~5 us of idle; a flag hand-off costs a kernel
- * boundary on the signalling stream): gpi_stream_signal stores (*epoch + 1) into *flag once every
- * earlier kernel of its stream has completed; gpi_stream_wait, launched on another stream, returns once
- * *flag == *epoch + 1, so the kernels after it see everything the signalling stream wrote before the
- * signal.  epoch: a device counter that does not change between the signal and the wait (the training
- * step counter).  A wait that does not see its signal within ~1 s sets *err (if not NULL) and returns.
- * Both are single-workgroup kernels; safe inside stream capture. */
+/* Cross-stream hand-off by a device counter instead of an event edge between two streams (in a captured
+ * step each such edge costs the waiting hardware queue ~5 us of idle): gpi_stream_signal increments
+ * *flag once every earlier kernel of its stream has completed; gpi_stream_wait, launched on another
+ * stream, returns once *flag >= *epoch + 1, so the kernels after it see everything the signalling
+ * stream wrote before the signal.  Protocol: one signal per flag per step, epoch = the step counter
+ * (a device counter that advances only after the step's last hand-off), flags and counter saved /
+ * restored together.  A wait that does not see its signal within ~1 s sets *err (if not NULL) and
+ * returns.  Both are single-workgroup kernels; safe inside stream capture.  The *_sig launches below
+ * fold the signal into a conv launch. */
 int gpi_stream_signal(uint32_t* flag, const int64_t* epoch, void* stream);
 int gpi_stream_wait(const uint32_t* flag, const int64_t* epoch, uint32_t* err, void* stream);
 

@@ -432,3 +432,4 @@ def test_codec_module_path_vs_oracle(device, tag):
     errs['Z'] = tensor_rel(Z.grad.cpu().numpy(), Zo.grad.numpy())
     bad = {k: v for k, v in errs.items() if not v < 5e-5}
     assert not bad, bad
+
