@@ -309,7 +309,26 @@ __global__ void stream_wait_kernel(const uint32_t* flag, const int64_t* epoch, u
     }
 }
 
+__global__ void stream_wait_ge_kernel(const int64_t* a, const int64_t* b, uint32_t* err) {
+    if (threadIdx.x != 0) return;
+    const int64_t want = __hip_atomic_load(b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int i = 0; __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want; ++i) {
+        __builtin_amdgcn_s_sleep(2);
+        if (i > WAIT_SPIN_MAX) {
+            if (err) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+    }
+}
+
 }  // namespace
+
+extern "C" int gpi_stream_wait_ge(const int64_t* a, const int64_t* b, uint32_t* err, void* stream) {
+    if (!a || !b) return GPI_ERR_ARG;
+    hipLaunchKernelGGL(stream_wait_ge_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, a, b, err);
+    GPI_CHECK_LAUNCH();
+    return GPI_OK;
+}
 
 extern "C" int gpi_stream_signal(uint32_t* flag, const int64_t* epoch, void* stream) {
     if (!flag || !epoch) return GPI_ERR_ARG;

@@ -211,6 +211,7 @@ SIGNATURES = {
     'gpi_rng_advance': (C.c_int, [vp, u64, vp]),
     'gpi_stream_signal': (C.c_int, [vp, vp, vp]),
     'gpi_stream_wait': (C.c_int, [vp, vp, vp, vp]),
+    'gpi_stream_wait_ge': (C.c_int, [vp, vp, vp, vp]),
     'gpi_random_subset': (C.c_int, [vp, i32, i32, u64, vp, u64, vp]),
     'gpi_random_subset_workspace': (C.c_int, [i32, C.POINTER(i64)]),
     'gpi_random_subset_ws': (C.c_int, [vp, i32, i32, u64, vp, u64, vp, i64, vp]),

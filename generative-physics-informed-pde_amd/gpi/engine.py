@@ -450,17 +450,23 @@ class ElboEngine(object):
         self.bn_world = 1
         # cross-stream hand-offs: graph events (None) or device flags (set_flag_handoff)
         self.handoff = None
+        self.side_done = None
         self._rejoin_pending = False
 
     # ------------------------------------------------------------------
-    def set_flag_handoff(self, flags, epoch, err=None):
+    def set_flag_handoff(self, flags, epoch, err=None, side_done=None):
         """Hand the side stream its work by device flags (gpi_stream_signal / gpi_stream_wait) instead of
         event edges between the streams: flags = int32 device tensor (>= 4 words), epoch = the step
         counter (int64 device tensor, constant within a step), err = an int32 word the waits set on a
         timeout.  The side stream forks from the main stream once at the start of the forward; after
         the step's last kernel the caller joins it back with rejoin() (stream-capture legality: the
-        events there sit at the graph's end, not between kernels of the main chain)."""
+        events there sit at the graph's end, not between kernels of the main chain).
+        side_done (int64 device counter): the streams are not joined by events at all -- the side
+        stream's step starts with a wait until the step counter has reached side_done (the main stream's
+        previous step has ended) and ends by incrementing it, so each stream can be captured as a
+        graph of its own (FusedElboStep graph_mode 'streams')."""
         self.handoff = (flags, epoch, err)
+        self.side_done = side_done
 
     def _signal(self, k, st):
         f, e, _ = self.handoff
@@ -561,10 +567,16 @@ class ElboEngine(object):
         st = stream if stream is not None else L.stream_handle()
         if self.handoff is not None:
             # the side stream's one fork of the step, before any of its kernels: its flag waits then
-            # follow this step's signals only (never the previous step's)
+            # follow this step's signals only (never the previous step's); side_done: by the step counter
             self._side_stream()
-            self._ev_start.record(torch.cuda.current_stream())
-            self._side.wait_event(self._ev_start)
+            if self.side_done is not None:
+                _, e, err = self.handoff
+                _run(_lib().gpi_stream_wait_ge, C.c_void_p(e.data_ptr()), C.c_void_p(self.side_done.data_ptr()),
+                     C.c_void_p(err.data_ptr()) if err is not None else None, C.c_void_p(self._side.cuda_stream),
+                     what='side step gate')
+            else:
+                self._ev_start.record(torch.cuda.current_stream())
+                self._side.wait_event(self._ev_start)
         self.forward_a(st, zero_gacc, zero_scratch)
         # rom_at 'backward': the ROM follows the backward's fork on the side stream (ahead of the
         # variational samples' head backward that needs it) -- one cross-stream dependency less per
@@ -932,8 +944,11 @@ class ElboEngine(object):
             self._signal(3, sst)
             if main_wait:
                 self._wait(3, st)
-            self._ev_join2.record(side)
-            self._rejoin_pending = True
+            if self.side_done is not None:
+                _run(_lib().gpi_rng_advance, C.c_void_p(self.side_done.data_ptr()), 1, sst, what='side step done')
+            else:
+                self._ev_join2.record(side)
+                self._rejoin_pending = True
         else:
             self._ev_join2.record(side)
             main.wait_event(self._ev_join2)

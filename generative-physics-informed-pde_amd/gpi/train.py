@@ -146,9 +146,16 @@ class FusedElboStep(object):
         # side-stream hand-offs by device flags (gpi_stream_signal / gpi_stream_wait) instead of graph
         # events between the streams; GPI_HANDOFF=events keeps the events (A/B)
         self.handoff_flags = torch.zeros(8, dtype=torch.int32, device=dev)   # [0..3] flags, [4] wait timeout
-        self.handoff = os.environ.get('GPI_HANDOFF', 'flags') if self.graph_mode == 'single' else 'events'
+        self.handoff = os.environ.get('GPI_HANDOFF', 'flags') if self.graph_mode in ('single', 'streams') \
+            else 'events'
+        if self.graph_mode == 'streams' and self.handoff != 'flags':
+            self.graph_mode = 'single'
+        # 'streams': the side stream is gated per step by this counter (no event between the streams), so
+        # each stream's part of the step is captured as a graph of its own
+        self.side_done = torch.zeros(1, dtype=torch.int64, device=dev)
         if self.handoff == 'flags':
-            self.engine.set_flag_handoff(self.handoff_flags[:4], self.step_ctr, self.handoff_flags[4:5])
+            self.engine.set_flag_handoff(self.handoff_flags[:4], self.step_ctr, self.handoff_flags[4:5],
+                                         side_done=self.side_done if self.graph_mode == 'streams' else None)
             if self.fuse_adam:
                 # the join with the side stream's last reduction inside the fused epilogue + Adam launch
                 self.epi_adam.wait_flag = self.handoff_flags.data_ptr() + 4 * 3
@@ -258,7 +265,7 @@ class FusedElboStep(object):
         statistics scratch."""
         ws = self.engine.ws
         return [self.flat.P, self.m, self.v, self.step_ctr, self.rng_off, self.idx, self.idx_next, self.done_ctr,
-                self.handoff_flags,
+                self.handoff_flags, self.side_done,
                 self.flat.gacc, self.flat.G, ws.t_ws, ws.t_scr, ws.t_parts, ws.t_flag, self.last_terms] + \
             self.engine.running.buffers
 
@@ -284,11 +291,14 @@ class FusedElboStep(object):
         torch.cuda.synchronize()
         self.g_fb = torch.cuda.CUDAGraph()
         self.g_up = None
+        self.g_side = None
         self.segs = None
         self.split_graph = self.distributed and not (self.graph_allreduce and
                                                       dist.get_backend(self.pg) == dist.Backend.NCCL)
         if not self.split_graph and self.graph_mode == 'segments':
             self._capture_segments()
+        elif not self.split_graph and self.graph_mode == 'streams':
+            self._capture_streams()
         elif self.split_graph:
             with torch.cuda.graph(self.g_fb):
                 self.forward_backward()
@@ -304,6 +314,33 @@ class FusedElboStep(object):
                 self.update(fused=fused)
                 self.engine.rejoin()
         self.graph = True
+
+    def _capture_streams(self):
+        """The step as TWO graphs, one per stream, captured at once: the main stream's (encoder, head,
+        decoder, their backward, the epilogue + Adam) and the side stream's (ROM, the variational samples'
+        head backward, the slab reductions, the next step's noise), ordered only by the device counters
+        of the flag hand-offs and the side stream's step gate -- no graph edge between the streams."""
+        fused = self.fuse_adam
+        side = self.engine._side_stream()
+        cap = torch.cuda.Stream()
+        cap.wait_stream(torch.cuda.current_stream())
+        side.wait_stream(torch.cuda.current_stream())
+        self.g_side = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(side):
+            self.g_side.capture_begin(capture_error_mode='relaxed')
+        try:
+            with torch.cuda.stream(cap):
+                self.g_fb.capture_begin(capture_error_mode='relaxed')
+                try:
+                    self._forward_backward(epilogue=not fused)
+                    self.allreduce()        # RCCL: captured as a graph node
+                    self.update(fused=fused)
+                finally:
+                    self.g_fb.capture_end()
+        finally:
+            with torch.cuda.stream(side):
+                self.g_side.capture_end()
+        torch.cuda.current_stream().wait_stream(cap)
 
     def _capture_segments(self):
         """The step as single-stream graphs, one per stretch of a stream between two cross-stream
@@ -391,6 +428,12 @@ class FusedElboStep(object):
             return self.step_eager()
         if self.segs is not None:
             self._replay_segments()
+            self._mark_optimizer_step()
+            return
+        if self.g_side is not None:
+            self.g_fb.replay()
+            with torch.cuda.stream(self.engine._side):
+                self.g_side.replay()
             self._mark_optimizer_step()
             return
         self.g_fb.replay()

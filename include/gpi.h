@@ -568,6 +568,10 @@ int gpi_step_epilogue_adam(const gpi_step_epilogue_desc* d, const gpi_adam_desc*
  * fold the signal into a conv launch. */
 int gpi_stream_signal(uint32_t* flag, const int64_t* epoch, void* stream);
 int gpi_stream_wait(const uint32_t* flag, const int64_t* epoch, uint32_t* err, void* stream);
+/* Waits until the device counter *a reaches *b (read once at entry): a stream's step gate on another
+ * stream's step counter (the side stream of a step waits for the main stream's previous step to have
+ * ended); timeout as gpi_stream_wait. */
+int gpi_stream_wait_ge(const int64_t* a, const int64_t* b, uint32_t* err, void* stream);
 
 /* Device Philox4x32-10 normals: out[i] = N(0,1) for counter (*offset + i);
  * offset is a device uint64 advanced by gpi_rng_advance (graph-replay safe). */

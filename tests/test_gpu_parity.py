@@ -482,7 +482,7 @@ def test_fused_step_matches_module_path(device, independent_X):
     assert step.step_ctr.item() == 2
 
 
-@pytest.mark.parametrize('mode', ['single', 'segments'])
+@pytest.mark.parametrize('mode', ['single', 'segments', 'streams'])
 def test_capture_leaves_training_state_untouched(device, mode):
     """FusedElboStep.capture() warms up on snapshots: parameters, Adam moments, step counter, Philox
     offset and the pre-drawn subset / noise are bit-identical afterwards, and the first replayed step
@@ -495,8 +495,13 @@ def test_capture_leaves_training_state_untouched(device, mode):
     model_b = copy.deepcopy(model_a)
     Xu, Xs, Y, F = cuda(d['Xu']), cuda(d['Xs']), cuda(d['Y']), cuda(d['F'])
     eager = FusedElboStep(model_a, Xu, bs, Xs, Y, F, lr=1e-3, seed=3)
-    graph = FusedElboStep(model_b, Xu, bs, Xs, Y, F, lr=1e-3, seed=3)
-    graph.graph_mode = mode
+    import os as _os
+    _os.environ['GPI_GRAPH_MODE'] = mode     # read by the constructor ('streams' sets the side step gate)
+    try:
+        graph = FusedElboStep(model_b, Xu, bs, Xs, Y, F, lr=1e-3, seed=3)
+    finally:
+        del _os.environ['GPI_GRAPH_MODE']
+    assert graph.graph_mode == mode
     before = [t.clone() for t in graph._mutable_state()]
     graph.capture()
     torch.cuda.synchronize()
@@ -510,6 +515,10 @@ def test_capture_leaves_training_state_untouched(device, mode):
         torch.testing.assert_close(graph.flat.P, eager.flat.P, rtol=1e-6, atol=1e-7)
     assert graph.step_ctr.item() == eager.step_ctr.item() == 3
     assert (graph.segs is not None) == (mode == 'segments')
+    assert (graph.g_side is not None) == (mode == 'streams')
+    if mode == 'streams':
+        graph.check_handoff()
+        assert graph.side_done.item() == 3
 
 
 def test_flag_handoff_matches_event_handoff(device, monkeypatch):

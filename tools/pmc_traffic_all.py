@@ -25,7 +25,7 @@ def main():
     total = sum(x['launches'] for x in m['launches'])
     fe, wr = conv_rows(fdir, 'FETCH_SIZE')[-total:], conv_rows(wdir, 'WRITE_SIZE')[-total:]
     assert len(fe) == total and len(wr) == total, (len(fe), len(wr), total)
-    res = dict(conv_hip_sha1=m['conv_hip_sha1'],
+    res = dict(conv_hip_sha1=m['conv_hip_sha1'], config=m.get('config', 'c64'),
                rule='(2*FETCH_SIZE + WRITE_SIZE) * 1024 bytes per dispatch; separate --pmc passes over '
                     'tools/pmc_all.py; mean over each operator\'s launches', ops={})
     k = 0
