@@ -191,6 +191,8 @@ SIGNATURES = {
     'gpi_codec_backward': (C.c_int, [C.POINTER(ConvDesc), C.c_int, C.POINTER(CodecCtx), vp]),
     'gpi_conv_forward_sig': (C.c_int, [C.POINTER(ConvDesc), C.POINTER(CodecCtx), vp, vp, vp]),
     'gpi_conv_backward_sig': (C.c_int, [C.POINTER(ConvDesc), C.POINTER(CodecCtx), vp, vp, vp]),
+    'gpi_conv_backward_reduce': (C.c_int, [C.POINTER(ConvDesc), C.POINTER(CodecCtx), vp, vp, vp, vp]),
+    'gpi_conv_backward_reduce_counters': (C.c_int, [C.POINTER(ConvDesc), C.POINTER(Groups), C.POINTER(i32)]),
     'gpi_codec_forward_sig': (C.c_int, [C.POINTER(ConvDesc), C.c_int, C.POINTER(CodecCtx), vp, vp, vp]),
     'gpi_codec_backward_sig': (C.c_int, [C.POINTER(ConvDesc), C.c_int, C.POINTER(CodecCtx), vp, vp, vp]),
     'gpi_wgrad_reduce': (C.c_int, [C.POINTER(ReduceItem), C.c_int, vp, vp, vp]),

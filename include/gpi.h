@@ -471,6 +471,17 @@ int gpi_conv_forward_sig(const gpi_conv_desc* op, const gpi_codec_ctx* ctx, uint
                          void* stream);
 int gpi_conv_backward_sig(const gpi_conv_desc* op, const gpi_codec_ctx* ctx, uint32_t* flag, const int64_t* epoch,
                           void* stream);
+/* gpi_conv_backward_sig with the launch's weight-gradient slab reduction folded in: ctx->gacc[op->w_off + i]
+ * += the sum of the launch's slab rows (what gpi_wgrad_reduce over them would add), so no reduction
+ * launch follows it.  Only for the single-channel 7x7 stride-2 input conv's weight-gradient-only
+ * backward (Encoder.py:147-149 In_conv; no input BN, wpart_off >= 0): GPI_ERR_UNSUPPORTED otherwise.
+ * counters: gpi_conv_backward_reduce_counters() zeroed uint32 words (device memory, persistent), which
+ * the launch leaves zero.  flag / epoch as gpi_conv_backward_sig (flag NULL: no signal).  The slab rows
+ * are still written (wpart). */
+int gpi_conv_backward_reduce(const gpi_conv_desc* op, const gpi_codec_ctx* ctx, uint32_t* counters, uint32_t* flag,
+                             const int64_t* epoch, void* stream);
+/* Counter words gpi_conv_backward_reduce needs for op at this batch (host only, no device work). */
+int gpi_conv_backward_reduce_counters(const gpi_conv_desc* op, const gpi_groups* groups, int32_t* n);
 int gpi_codec_forward_sig(const gpi_conv_desc* ops, int n_ops, const gpi_codec_ctx* ctx, uint32_t* flag,
                           const int64_t* epoch, void* stream);
 int gpi_codec_backward_sig(const gpi_conv_desc* ops, int n_ops, const gpi_codec_ctx* ctx, uint32_t* flag,
