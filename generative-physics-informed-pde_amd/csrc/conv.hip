@@ -114,8 +114,6 @@ struct ConvGeom {
     int grid;       // launched workgroups (xcd remap)
     uint32_t* sig;             // cross-stream hand-off (gpi_*_sig): workgroup 0 increments *sig at entry, i.e.
     const int64_t* sig_epoch;  // once every earlier kernel of the stream has completed (gpi_stream_signal)
-    uint32_t* red_ctr;         // vsum ops (gpi_conv_backward_reduce): arrival counters of RED_GROUP-tile groups;
-                               // the last workgroup of a group sums the group's slab rows into ctx.gacc
     int in_sq, in_sr, in_sc;   // 256 chunks of the input image = (planes, rows, chunks)
     int g_sq, g_sr, g_sc;      // ... of the output-gradient image
     Div d_in4, d_P4, d_g4, d_PG4, d_cin, d_cout, d_win, d_tp, d_wout, d_w2;
@@ -265,7 +263,6 @@ bool conv_geom(const gpi_conv_desc& d, const gpi_groups& g, ConvGeom& G, bool fw
     G.fuse = fuse ? 1 : 0;
     G.lsum = 0;     // decided by launch() / gpi_conv_blocks from the LDS footprint (lsum_op)
     G.vsum = 0;     // decided by launch() / gpi_conv_blocks (vsum_op)
-    G.red_ctr = nullptr;
     G.xcd = 0;      // set by launch() (xcd_mode)
     G.grid = 0;     // set by launch()
     G.sig = nullptr;
@@ -1040,55 +1037,6 @@ __host__ __device__ constexpr bool fuse_wlds(int ky) {
     return GPI_FUSE_WLDS <= 0 ? false : (GPI_FUSE_WLDS >= 5 ? true : (ky & 1 ? (ky / 2) < GPI_FUSE_WLDS : (ky / 2) < GPI_FUSE_WLDS - 2));
 }
 
-// In-launch slab reduction (G.red_ctr, vsum ops): the tiles form groups of RED_GROUP consecutive tiles;
-// every workgroup has stored its tile's slab row write-through (sc1) and fences it, one thread counts the
-// workgroup in, and the group's LAST arriver (which resets the counter for the next launch) sums the
-// group's rows -- in row order, read with sc1 loads, since the other rows come from other XCDs -- and
-// adds each sum to gacc with one fp64 atomic: the launch leaves the weight gradient where the separate
-// slab reduction (wgrad_reduce) would have put it, and the step's tail loses that launch.
-constexpr int RED_GROUP = 32;
-
-__device__ __forceinline__ float ld_sc1(const float* p) {
-    return __hip_atomic_load((const __attribute__((address_space(1))) float*)p, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ __forceinline__ void fold_slab_rows(uint32_t* ctr, int nblocks, const float* slab, double* gacc, int tile,
-                                               int rowlen, int numel, int* lds_flag) {
-    const int tid = threadIdx.x;
-    const int grp = tile / RED_GROUP, t0 = grp * RED_GROUP, n = min(RED_GROUP, nblocks - t0);
-    // no release fence: its L2 write-back (buffer_wbl2), once per workgroup, made the launch 4x longer and
-    // stalled the concurrent side-stream kernels (r04f trace: 67.9 vs 16.8 us).  The row stores are
-    // write-through (sc1), so their completion (vmcnt) is what makes them visible to another XCD.
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();                      // every thread's row stores are out, every LDS read of the sums done
-    if (tid == 0) {
-        const uint32_t old = __hip_atomic_fetch_add(ctr + grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int last = old == (uint32_t)(n - 1);
-        if (last) __hip_atomic_store(ctr + grp, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *lds_flag = last;
-    }
-    __syncthreads();
-    if (!*lds_flag) return;
-    // (no acquire fence either -- its L2 invalidate would hit every workgroup still running on this XCD:
-    // the rows are read with sc1 loads, which do not take them from this XCD's L2)
-    const float* rows = slab + (int64_t)t0 * rowlen;
-    for (int e = tid; e < numel; e += 256) {
-        const float* p = rows + e;
-        float acc = 0.f;
-        int r = 0;
-        for (; r + 8 <= n; r += 8) {
-            float v[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = ld_sc1(p + (int64_t)(r + u) * rowlen);
-#pragma unroll
-            for (int u = 0; u < 8; ++u) acc += v[u];
-        }
-        for (; r < n; ++r) acc += ld_sc1(p + (int64_t)r * rowlen);
-        atomicAdd(gacc + e, (double)acc);
-    }
-}
-
 template <int K, int S, int UP, bool FUSE = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (FUSE ? GPI_FUSE_WAVES : 4) : 6))) void conv_bwd_kernel(gpi_conv_desc d, gpi_codec_ctx c, ConvGeom G) {
     touch_kernargs<CONV_KARG_BYTES>();
@@ -1589,13 +1537,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
                     float* srow = c.wpart + d.wpart_off + (int64_t)tile * rowlen;
                     for (int e = tid; e < d.cout * J; e += 256) {
                         const float* r = gl + e;
-                        const float v = (r[0] + r[rowlen]) + (r[2 * rowlen] + r[3 * rowlen]);
-                        if (G.red_ctr) st1(srow + e, v);     // write-through: read back by another XCD below
-                        else srow[e] = v;
+                        srow[e] = (r[0] + r[rowlen]) + (r[2 * rowlen] + r[3 * rowlen]);
                     }
-                    if (G.red_ctr)
-                        fold_slab_rows(G.red_ctr, G.nblocks, c.wpart + d.wpart_off, c.gacc + d.w_off, tile, rowlen,
-                                       d.cout * J, (int*)gl);
                 }
             }
         }
@@ -2079,8 +2022,11 @@ size_t bwd_lds(const gpi_conv_desc& d, const ConvGeom& G) {
 // it on): a quarter of the slab bytes, but the two extra barriers and the LDS pass cost more than the
 // stores and the smaller reductions save -- 0.6315 vs 0.6258 ms/step (r03, 3 x 600 replays per arm).
 bool lsum_op(const gpi_conv_desc& d, const ConvGeom& G) {
+    // GPI_LSUM=2 / 3: only on output planes of <= 16 x 16 / <= 8 x 8 pixels, where the four slab rows per
+    // tile are as many bytes as the launch's own operands (PMC: TransDown3.conv2.bwd 3.0x its algorithmic bytes)
     static const int on = env_int("GPI_LSUM", 0);
     if (!on || vop_op(d) || G.fuse) return false;
+    if ((on == 2 && d.h_out * d.w_out > 256) || (on == 3 && d.h_out * d.w_out > 64)) return false;
     if (d.k == 7 && d.stride == 2 && !d.upsample && d.cin == 1 && d.gin_off < 0 && d.cout <= 16) return false;
     if (d.cout * d.k > 32 || d.cin * d.k > 32) return false;
     const size_t avail = bwd_lds_floats(d, G.rh, G.P, G.gh, G.PG, G.zreg, false) - bwd_hdr(d.cin, d.cout);
@@ -2164,16 +2110,12 @@ bool xcd_mode(bool fwd, bool fuse, bool split) {
 }
 
 int launch(const gpi_conv_desc& d, const gpi_codec_ctx& c, hipStream_t st, bool fwd, bool fuse = false,
-           uint32_t* sig = nullptr, const int64_t* sig_epoch = nullptr, uint32_t* red_ctr = nullptr) {
+           uint32_t* sig = nullptr, const int64_t* sig_epoch = nullptr) {
     ConvGeom G;
     if (!conv_geom(d, c.groups, G, fwd, fuse)) return GPI_ERR_UNSUPPORTED;
     if (sig && !sig_epoch) return GPI_ERR_ARG;
     G.sig = sig;
     G.sig_epoch = sig_epoch;
-    G.red_ctr = red_ctr;
-    // the in-launch reduction: vsum ops only (one slab row per tile, the weight gradient only)
-    if (red_ctr && (fwd || fuse || !vsum_op(d, G) || d.wpart_off < 0 || d.in_bn || !c.gacc))
-        return GPI_ERR_UNSUPPORTED;
     if (fuse && (fwd || d.k != 5 || d.stride != 1 || d.upsample || d.cout != 2 || d.cin > 4 || d.drop_off >= 0 ||
                  d.gout_mode != 1 || d.gin_off < 0 ||
                  (d.epilogue != GPI_EPI_GAUSS_LOSS && d.epilogue != GPI_EPI_GAUSS_EXP_LOSS)))
@@ -2383,21 +2325,6 @@ extern "C" int gpi_conv_backward_sig(const gpi_conv_desc* op, const gpi_codec_ct
                                      const int64_t* epoch, void* stream) {
     if (!op || !ctx) return GPI_ERR_ARG;
     return launch(*op, *ctx, (hipStream_t)stream, false, false, flag, epoch);
-}
-
-extern "C" int gpi_conv_backward_reduce(const gpi_conv_desc* op, const gpi_codec_ctx* ctx, uint32_t* counters,
-                                        uint32_t* flag, const int64_t* epoch, void* stream) {
-    if (!op || !ctx || !counters) return GPI_ERR_ARG;
-    return launch(*op, *ctx, (hipStream_t)stream, false, false, flag, epoch, counters);
-}
-
-extern "C" int gpi_conv_backward_reduce_counters(const gpi_conv_desc* op, const gpi_groups* groups, int32_t* n) {
-    if (!op || !groups || !n) return GPI_ERR_ARG;
-    ConvGeom G;
-    if (!conv_geom(*op, *groups, G, false, false)) return GPI_ERR_UNSUPPORTED;
-    if (!vsum_op(*op, G) || op->wpart_off < 0 || op->in_bn) return GPI_ERR_UNSUPPORTED;
-    *n = (G.nblocks + RED_GROUP - 1) / RED_GROUP;
-    return GPI_OK;
 }
 
 extern "C" int gpi_codec_forward_sig(const gpi_conv_desc* ops, int n_ops, const gpi_codec_ctx* ctx, uint32_t* flag,

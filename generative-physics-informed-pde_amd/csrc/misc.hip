@@ -321,7 +321,29 @@ __global__ void stream_wait_ge_kernel(const int64_t* a, const int64_t* b, uint32
     }
 }
 
+// gpi_queue_probe: a short bounded spin for the flag's first increment; records whether it came
+constexpr int PROBE_SPIN_MAX = 1 << 16;
+__global__ void queue_probe_kernel(const uint32_t* flag, uint32_t* seen) {
+    if (threadIdx.x != 0) return;
+    uint32_t ok = 0;
+    for (int i = 0; i < PROBE_SPIN_MAX; ++i) {
+        if (count_reached(flag, 1u)) {
+            ok = 1;
+            break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+    __hip_atomic_store(seen, ok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 }  // namespace
+
+extern "C" int gpi_queue_probe(const uint32_t* flag, uint32_t* seen, void* stream) {
+    if (!flag || !seen) return GPI_ERR_ARG;
+    hipLaunchKernelGGL(queue_probe_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, flag, seen);
+    GPI_CHECK_LAUNCH();
+    return GPI_OK;
+}
 
 extern "C" int gpi_stream_wait_ge(const int64_t* a, const int64_t* b, uint32_t* err, void* stream) {
     if (!a || !b) return GPI_ERR_ARG;

@@ -191,8 +191,6 @@ SIGNATURES = {
     'gpi_codec_backward': (C.c_int, [C.POINTER(ConvDesc), C.c_int, C.POINTER(CodecCtx), vp]),
     'gpi_conv_forward_sig': (C.c_int, [C.POINTER(ConvDesc), C.POINTER(CodecCtx), vp, vp, vp]),
     'gpi_conv_backward_sig': (C.c_int, [C.POINTER(ConvDesc), C.POINTER(CodecCtx), vp, vp, vp]),
-    'gpi_conv_backward_reduce': (C.c_int, [C.POINTER(ConvDesc), C.POINTER(CodecCtx), vp, vp, vp, vp]),
-    'gpi_conv_backward_reduce_counters': (C.c_int, [C.POINTER(ConvDesc), C.POINTER(Groups), C.POINTER(i32)]),
     'gpi_codec_forward_sig': (C.c_int, [C.POINTER(ConvDesc), C.c_int, C.POINTER(CodecCtx), vp, vp, vp]),
     'gpi_codec_backward_sig': (C.c_int, [C.POINTER(ConvDesc), C.c_int, C.POINTER(CodecCtx), vp, vp, vp]),
     'gpi_wgrad_reduce': (C.c_int, [C.POINTER(ReduceItem), C.c_int, vp, vp, vp]),
@@ -214,6 +212,7 @@ SIGNATURES = {
     'gpi_stream_signal': (C.c_int, [vp, vp, vp]),
     'gpi_stream_wait': (C.c_int, [vp, vp, vp, vp]),
     'gpi_stream_wait_ge': (C.c_int, [vp, vp, vp, vp]),
+    'gpi_queue_probe': (C.c_int, [vp, vp, vp]),
     'gpi_random_subset': (C.c_int, [vp, i32, i32, u64, vp, u64, vp]),
     'gpi_random_subset_workspace': (C.c_int, [i32, C.POINTER(i64)]),
     'gpi_random_subset_ws': (C.c_int, [vp, i32, i32, u64, vp, u64, vp, i64, vp]),

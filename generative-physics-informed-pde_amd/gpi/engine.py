@@ -359,16 +359,6 @@ class ElboEngine(object):
         # adjacent; a miscount would leave one of its items to the side stream while the main
         # stream's input-conv backward still writes that slab)
         self.n_reduce_in = self.ep.reduce_counts(offE)[0] if self.ep is not None else 0
-        # the input conv's slab reduction inside its own backward launch (gpi_conv_backward_reduce: the
-        # last workgroup of each 32-tile group sums the group's rows into gacc), so the step's tail
-        # is the input conv's backward and the epilogue; GPI_FOLD_IN_REDUCE=0: a wgrad_reduce launch
-        self.red_ctr = None
-        if (self.ep is not None and self.shared_grads and self.n_reduce_in == 1
-                and os.environ.get('GPI_FOLD_IN_REDUCE', '1') != '0'):
-            n = C.c_int32(0)
-            if _lib().gpi_conv_backward_reduce_counters(C.byref(self.enc_descs[0]), C.byref(groups_struct([self.B_u])),
-                                                        C.byref(n)) == 0:
-                self.red_ctr = torch.zeros(max(n.value, 1), dtype=torch.int32, device=dev)
         self.reduce_dec = self.dp.reduce_items(offD)
         self.reduce_items = self.reduce_enc + self.reduce_dec
         gi = []
@@ -685,13 +675,6 @@ class ElboEngine(object):
             return
         if self.bn_sync is not None and self.enc_descs[0].gout_mode == 0:
             self._sync_stats(self.enc_descs[0].out_stat, self.enc_descs[0].cout, 2, 'enc')
-        if self.red_ctr is not None:
-            _run(_lib().gpi_conv_backward_reduce, C.byref(self.enc_descs[0]), C.byref(self.ectx),
-                 C.c_void_p(self.red_ctr.data_ptr()), *(self._sig_args(sig) if sig is not None else (None, None)),
-                 st, what='In_conv backward (+ its slab reduction)')
-            if not enc_split:
-                run_reduce(self.reduce_enc[self.n_reduce_in:], self.ws, self.flat, st)
-            return
         if sig is not None:
             _run(_lib().gpi_conv_backward_sig, C.byref(self.enc_descs[0]), C.byref(self.ectx), *self._sig_args(sig),
                  st, what='In_conv backward')

@@ -97,11 +97,17 @@ class FusedElboStep(object):
         self.idx_next = torch.zeros_like(self.idx)
         # A/B switch (tools/critpath_probe.py): draw the next step's subset on the side stream ahead of the ROM
         self.subset_early = False
-        # captured form: 'single' (one graph spanning both streams) or 'segments' (single-stream
-        # graphs joined by events, _capture_segments: the host launches them ~4x faster, but each
-        # graph boundary leaves the GPU idle ~15 us: 0.673 vs 0.629 ms per step, r03);
+        # captured form: 'streams' (one graph per stream, ordered only by device counters, _capture_streams:
+        # no event edge between the streams at all -- 0.5816 / 0.5827 vs 0.5901 / 0.5904 ms per step with
+        # 'single', interleaved on one box, r04g), 'single' (one graph spanning both streams, forked and
+        # joined by events at its ends) or 'segments' (single-stream graphs joined by events,
+        # _capture_segments: each graph boundary leaves the GPU idle ~15 us: 0.673 vs 0.629 ms, r03).
+        # The split DP form (host-side all-reduce between two graphs) keeps 'single'.
         # GPI_GRAPH_MODE overrides (A/B runs)
-        self.graph_mode = os.environ.get('GPI_GRAPH_MODE', 'single')
+        self.graph_mode = os.environ.get('GPI_GRAPH_MODE', 'streams')
+        if self.graph_mode == 'streams' and self.distributed and not (
+                self.graph_allreduce and dist.get_backend(self.pg) == dist.Backend.NCCL):
+            self.graph_mode = 'single'
         my_idx = self.idx[self.rank * self.B_u:(self.rank + 1) * self.B_u] if self.B_u else None
         self.engine.bind(X_u=self.X_pool, u_index=my_idx, X_s=X_s, Y=Y, F=F)
         n_pool = self.X_pool.shape[0] if self.X_pool is not None else 0
@@ -153,9 +159,9 @@ class FusedElboStep(object):
         # 'streams': the side stream is gated per step by this counter (no event between the streams), so
         # each stream's part of the step is captured as a graph of its own
         self.side_done = torch.zeros(1, dtype=torch.int64, device=dev)
+        self._probed_stream = None
         if self.handoff == 'flags':
-            self.engine.set_flag_handoff(self.handoff_flags[:4], self.step_ctr, self.handoff_flags[4:5],
-                                         side_done=self.side_done if self.graph_mode == 'streams' else None)
+            self._configure_handoff()
             if self.fuse_adam:
                 # the join with the side stream's last reduction inside the fused epilogue + Adam launch
                 self.epi_adam.wait_flag = self.handoff_flags.data_ptr() + 4 * 3
@@ -246,6 +252,7 @@ class FusedElboStep(object):
         self.optimizer._opt_called = True
 
     def step_eager(self):
+        self._check_stream_pair()
         fused = self.fuse_adam
         self._forward_backward(epilogue=not fused)
         self.allreduce()
@@ -314,6 +321,43 @@ class FusedElboStep(object):
                 self.update(fused=fused)
                 self.engine.rejoin()
         self.graph = True
+
+    def _queues_separate(self):
+        """True iff a kernel on the current stream runs while a kernel of the side stream spins
+        (gpi_queue_probe): the two are on different hardware queues.  HIP maps streams to its
+        GPU_MAX_HW_QUEUES queues round-robin, so in a process with many streams two can share one, and
+        a flag wait ahead of its signal on a shared queue blocks it (tools/queue_stress.py: 3 of 18
+        steps timed out with 6 step objects in 'streams' mode, none in 'single', whose graph
+        branches the runtime places itself)."""
+        side = self.engine._side_stream()
+        pr = torch.zeros(2, dtype=torch.int32, device=self.flat.P.device)
+        torch.cuda.synchronize()
+        L.check(L.lib().gpi_queue_probe(L.ptr(pr), L.ptr(pr[1:]), C.c_void_p(side.cuda_stream)), 'queue probe')
+        L.check(L.lib().gpi_stream_signal(L.ptr(pr), L.ptr(self.step_ctr), L.stream_handle()), 'queue probe signal')
+        torch.cuda.synchronize()
+        self._probed_stream = torch.cuda.current_stream()
+        return int(pr[1].item()) == 1
+
+    def _configure_handoff(self):
+        """Flag hand-offs between the streams; graph mode 'streams' (no event between the streams at all)
+        only on a verified pair of hardware queues, else 'single' (one graph whose event fork / join at
+        its ends the runtime orders)."""
+        if self.graph_mode == 'streams' and not self._queues_separate():
+            self.graph_mode = 'single'
+        self.engine.set_flag_handoff(self.handoff_flags[:4], self.step_ctr, self.handoff_flags[4:5],
+                                     side_done=self.side_done if self.graph_mode == 'streams' else None)
+
+    def _check_stream_pair(self):
+        """'streams' mode, before a step: the probe was made against another current stream -- probe this
+        one; on a shared queue fall back to 'single' (and capture again if the step was captured)."""
+        if self.graph_mode != 'streams' or torch.cuda.current_stream() == self._probed_stream:
+            return
+        if self._queues_separate():
+            return
+        self.graph_mode = 'single'
+        self._configure_handoff()
+        if self.graph is not None:
+            self.capture()
 
     def _capture_streams(self):
         """The step as TWO graphs, one per stream, captured at once: the main stream's (encoder, head,
@@ -430,6 +474,8 @@ class FusedElboStep(object):
             self._replay_segments()
             self._mark_optimizer_step()
             return
+        if self.g_side is not None:
+            self._check_stream_pair()
         if self.g_side is not None:
             self.g_fb.replay()
             with torch.cuda.stream(self.engine._side):

@@ -471,17 +471,6 @@ int gpi_conv_forward_sig(const gpi_conv_desc* op, const gpi_codec_ctx* ctx, uint
                          void* stream);
 int gpi_conv_backward_sig(const gpi_conv_desc* op, const gpi_codec_ctx* ctx, uint32_t* flag, const int64_t* epoch,
                           void* stream);
-/* gpi_conv_backward_sig with the launch's weight-gradient slab reduction folded in: ctx->gacc[op->w_off + i]
- * += the sum of the launch's slab rows (what gpi_wgrad_reduce over them would add), so no reduction
- * launch follows it.  Only for the single-channel 7x7 stride-2 input conv's weight-gradient-only
- * backward (Encoder.py:147-149 In_conv; no input BN, wpart_off >= 0): GPI_ERR_UNSUPPORTED otherwise.
- * counters: gpi_conv_backward_reduce_counters() zeroed uint32 words (device memory, persistent), which
- * the launch leaves zero.  flag / epoch as gpi_conv_backward_sig (flag NULL: no signal).  The slab rows
- * are still written (wpart). */
-int gpi_conv_backward_reduce(const gpi_conv_desc* op, const gpi_codec_ctx* ctx, uint32_t* counters, uint32_t* flag,
-                             const int64_t* epoch, void* stream);
-/* Counter words gpi_conv_backward_reduce needs for op at this batch (host only, no device work). */
-int gpi_conv_backward_reduce_counters(const gpi_conv_desc* op, const gpi_groups* groups, int32_t* n);
 int gpi_codec_forward_sig(const gpi_conv_desc* ops, int n_ops, const gpi_codec_ctx* ctx, uint32_t* flag,
                           const int64_t* epoch, void* stream);
 int gpi_codec_backward_sig(const gpi_conv_desc* ops, int n_ops, const gpi_codec_ctx* ctx, uint32_t* flag,
@@ -583,6 +572,13 @@ int gpi_stream_wait(const uint32_t* flag, const int64_t* epoch, uint32_t* err, v
  * stream's step counter (the side stream of a step waits for the main stream's previous step to have
  * ended); timeout as gpi_stream_wait. */
 int gpi_stream_wait_ge(const int64_t* a, const int64_t* b, uint32_t* err, void* stream);
+/* The hand-offs need the waiting and the signalling stream on DIFFERENT hardware queues: on a shared queue
+ * a wait enqueued ahead of its signal blocks the queue until it times out (HIP maps streams to its
+ * GPU_MAX_HW_QUEUES queues round-robin, so a process with many streams shares them).  Probe of a stream
+ * pair: launch gpi_queue_probe on stream A, then gpi_stream_signal(flag) on stream B; *seen = 1 iff the
+ * signal arrived while the probe spun (~40 ms bound), i.e. B's kernels run past a spinning kernel of A.
+ * *flag must be 0 before the pair is launched. */
+int gpi_queue_probe(const uint32_t* flag, uint32_t* seen, void* stream);
 
 /* Device Philox4x32-10 normals: out[i] = N(0,1) for counter (*offset + i);
  * offset is a device uint64 advanced by gpi_rng_advance (graph-replay safe). */

@@ -501,7 +501,9 @@ def test_capture_leaves_training_state_untouched(device, mode):
         graph = FusedElboStep(model_b, Xu, bs, Xs, Y, F, lr=1e-3, seed=3)
     finally:
         del _os.environ['GPI_GRAPH_MODE']
-    assert graph.graph_mode == mode
+    # ('streams' falls back to 'single' when the probe finds the two streams on one hardware queue)
+    assert graph.graph_mode == mode or (mode == 'streams' and graph.graph_mode == 'single')
+    mode = graph.graph_mode
     before = [t.clone() for t in graph._mutable_state()]
     graph.capture()
     torch.cuda.synchronize()
@@ -548,39 +550,6 @@ def test_flag_handoff_matches_event_handoff(device, monkeypatch):
                  (ev.step_ctr, fl.step_ctr)):
         assert torch.equal(a, b)
     assert int(fl.handoff_flags[0].item()) == 4        # the tag of the last step (counter 3, + 1)
-
-
-def test_input_conv_in_launch_reduction(device, monkeypatch):
-    """gpi_conv_backward_reduce (the input conv's slab rows summed into gacc by the last workgroup of each
-    32-tile group, inside the backward launch) delivers the gradient the separate wgrad_reduce launch
-    delivers: the input conv's weight gradient to fp32 summation-order rounding, every other gradient
-    entry bit for bit; the group counters are back at zero after eager and captured steps."""
-    import copy
-    from gpi.train import FusedElboStep
-    d = load('elbo_c32.npz')
-    model_a, bs = build_golden_model(d)
-    model_b = copy.deepcopy(model_a)
-    Xu, Xs, Y, F = cuda(d['Xu']), cuda(d['Xs']), cuda(d['Y']), cuda(d['F'])
-    monkeypatch.setenv('GPI_FOLD_IN_REDUCE', '0')
-    sep = FusedElboStep(model_a, Xu, bs, Xs, Y, F, lr=1e-3, seed=3)
-    monkeypatch.setenv('GPI_FOLD_IN_REDUCE', '1')
-    fold = FusedElboStep(model_b, Xu, bs, Xs, Y, F, lr=1e-3, seed=3)
-    assert sep.engine.red_ctr is None and fold.engine.red_ctr is not None
-    sep.forward_backward()
-    fold.forward_backward()
-    torch.cuda.synchronize()
-    w = fold.model.encoder.get_parameter('features.In_conv.weight')
-    o, n = fold.flat.offset(w), w.numel()
-    ga, gb = sep.flat.G.clone(), fold.flat.G.clone()
-    assert torch.equal(ga[:o], gb[:o]) and torch.equal(ga[o + n:], gb[o + n:])
-    assert torch.allclose(ga[o:o + n], gb[o:o + n], rtol=1e-5, atol=1e-6 * float(ga[o:o + n].abs().max()))
-    assert int(fold.engine.red_ctr.abs().sum()) == 0
-    fold.capture()
-    for _ in range(3):
-        fold.step()
-    torch.cuda.synchronize()
-    assert int(fold.engine.red_ctr.abs().sum()) == 0
-    assert torch.isfinite(fold.flat.P).all()
 
 
 def test_fused_epilogue_adam_matches_two_launches(device):
