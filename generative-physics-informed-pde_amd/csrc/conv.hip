@@ -2181,6 +2181,7 @@ struct ReduceArgs {
     int32_t first_block[GPI_MAX_REDUCE_ITEMS + 1];
     int32_t wchunks[GPI_MAX_REDUCE_ITEMS];
     int32_t n;
+    int32_t rrows;       // slab rows per workgroup (RROWS, or fewer for a small call: see gpi_wgrad_reduce)
 };
 
 __global__ __launch_bounds__(256) void wgrad_reduce(ReduceArgs a, const float* __restrict__ wpart, double* gacc) {
@@ -2195,7 +2196,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce(ReduceArgs a, const float* _
     const int P = 256 / nw;
     const int tid = threadIdx.x;
     const int w = tid % nw, p = tid / nw;
-    const int r0 = rc * RROWS, r1 = min(it.blocks, r0 + RROWS);
+    const int r0 = rc * a.rrows, r1 = min(it.blocks, r0 + a.rrows);
     float s = 0.f;
     if (p < P) {
         // 16 slab loads in flight per thread (the reduction is latency-bound, not bandwidth-bound)
@@ -2363,14 +2364,23 @@ extern "C" int gpi_wgrad_reduce(const gpi_reduce_item* items, int n_items, const
     if (n_items == 0) return GPI_OK;
     ReduceArgs a;
     a.n = n_items;
-    int nb = 0;
-    for (int k = 0; k < n_items; ++k) {
-        a.it[k] = items[k];
-        a.first_block[k] = nb;
-        a.wchunks[k] = (items[k].numel + 255) / 256;
-        nb += a.wchunks[k] * ((items[k].blocks + RROWS - 1) / RROWS);
+    // a call of few workgroups (the input conv's slabs alone, at the step's tail) takes fewer rows per
+    // workgroup, so every thread's loads are ONE round trip: RROWS / 4 below 128 workgroups
+    // (GPI_RROWS_SMALL overrides)
+    static const int rr_small = env_int("GPI_RROWS_SMALL", RROWS / 4);
+    for (int pass = 0; pass < 2; ++pass) {
+        a.rrows = pass == 0 ? RROWS : std::max(1, rr_small);
+        int nb = 0;
+        for (int k = 0; k < n_items; ++k) {
+            a.it[k] = items[k];
+            a.first_block[k] = nb;
+            a.wchunks[k] = (items[k].numel + 255) / 256;
+            nb += a.wchunks[k] * ((items[k].blocks + a.rrows - 1) / a.rrows);
+        }
+        a.first_block[n_items] = nb;
+        if (nb >= 128) break;
     }
-    a.first_block[n_items] = nb;
+    const int nb = a.first_block[n_items];
     hipLaunchKernelGGL(wgrad_reduce, dim3(nb), dim3(256), 0, (hipStream_t)stream, a, wpart, gacc);
     GPI_CHECK_LAUNCH();
     return GPI_OK;

@@ -477,6 +477,7 @@ class FusedElboStep(object):
         if self.g_side is not None:
             self._check_stream_pair()
         if self.g_side is not None:
+            # (the side graph launched first instead: 0.5772-0.5774 vs 0.5767-0.5769 ms, r04k)
             self.g_fb.replay()
             with torch.cuda.stream(self.engine._side):
                 self.g_side.replay()

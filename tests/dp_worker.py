@@ -98,10 +98,17 @@ def run_c64_sync(out):
     dist.destroy_process_group()
 
 
-def shard_model(d, rank, B_u=B_U, ns=NS_RANK):
-    """The fixture model restricted to rank's labeled shard (state rows sliced accordingly)."""
+# labeled samples per rank of the 'sync_uneven' mode (the fixture's 4 split unevenly: the SyncBN
+# statistics of the labeled decoder group then have per-rank counts 1 and 3)
+NS_UNEVEN = (1, 3)
+
+
+def shard_model(d, rank, B_u=B_U, ns=NS_RANK, lo=None):
+    """The fixture model restricted to rank's labeled shard [lo, lo + ns) (default lo = rank * ns; state rows
+    sliced accordingly)."""
     from test_gpu_parity import build_golden_model
-    sl = slice(rank * ns, (rank + 1) * ns)
+    lo = rank * ns if lo is None else lo
+    sl = slice(lo, lo + ns)
     e = dict(d)
     for k in ('Xs', 'Y', 'F'):
         e[k] = d[k][sl]
@@ -114,13 +121,16 @@ def shard_model(d, rank, B_u=B_U, ns=NS_RANK):
 
 def main(out, mode='replica'):
     rank, world = int(os.environ['RANK']), int(os.environ['WORLD_SIZE'])
-    sync_bn = mode == 'sync'     # SyncBN: BN statistics over both ranks' batches (eager: gloo)
+    sync_bn = mode in ('sync', 'sync_uneven')    # SyncBN: BN statistics over both ranks' batches (eager: gloo)
     torch.cuda.set_device(0)                      # every rank on the one GPU of the box
     dist.init_process_group('gloo')
     from elbo_ref import load
     from gpi.train import FusedElboStep
     d = load('elbo_c32.npz')
-    model, _ = shard_model(d, rank)
+    if mode == 'sync_uneven':
+        model, _ = shard_model(d, rank, ns=NS_UNEVEN[rank], lo=sum(NS_UNEVEN[:rank]))
+    else:
+        model, _ = shard_model(d, rank)
     ds = model._datasets['supervised']
     Xu = torch.tensor(d['Xu'], device='cuda')
     try:        # world > 1 without a shared subset seed: refused (ranks would draw different permutations)
@@ -149,6 +159,8 @@ def main(out, mode='replica'):
     names = [k for k, _ in model.named_parameters()]
     rec['names'] = np.array(names)
     rec['offsets'] = np.array([step.flat.name_offsets[k] for k in names])
+    if sync_bn:
+        rec['counts'] = np.array(e.bn_global_counts['dec'] + [e.bn_global_counts['enc']])
     np.savez(os.path.join(out, 'rank%d.npz' % rank), **rec)
     dist.barrier()
     dist.destroy_process_group()

@@ -78,44 +78,51 @@ def test_dp_two_ranks_native_step(device, tmp_path):
     assert np.array_equal(rk[0]['P0'][:ns], rk[1]['P0'][:ns])
 
 
-def test_dp_two_ranks_sync_bn(device, tmp_path):
+@pytest.mark.parametrize('mode', ['sync', 'sync_uneven'])
+def test_dp_two_ranks_sync_bn(device, tmp_path, mode):
     """SyncBN (FusedElboStep(sync_bn=True)): with every BN layer normalised over
     both ranks' batches, the all-reduced shared gradient of two gloo ranks equals the gradient of ONE
     process running the union batch (the reference's semantics at the global batch: train-mode BN over
     the whole codec call, codec.py:164-173), and each rank's q rows equal the union's rows of its
-    labeled shard.  Tolerance 5e-5 per tensor (fp32 sums in another order); the ELBO halves sum to the
-    union ELBO within 1e-5."""
-    from dp_worker import B_U, NS_RANK
+    labeled shard.  'sync_uneven': the labeled shards hold 1 and 3 samples, so the labeled decoder
+    group's per-rank counts differ (each all-reduced BN sum is scaled by the rank's count over the global
+    one).  Tolerance 5e-5 per tensor (fp32 sums in another order); the ELBO halves sum to the union ELBO
+    within 1e-5."""
+    from dp_worker import B_U, NS_RANK, NS_UNEVEN
     from test_gpu_parity import build_golden_model
+    ns_r = list(NS_UNEVEN) if mode == 'sync_uneven' else [NS_RANK, NS_RANK]
     env = dict(os.environ)
     env['PYTHONUNBUFFERED'] = '1'
     cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node=2',
            '--master-addr=127.0.0.1', '--master-port=%d' % _free_port(), os.path.join(HERE, 'dp_worker.py'),
-           str(tmp_path), 'sync']
+           str(tmp_path), mode]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     rk = [dict(np.load(str(tmp_path / ('rank%d.npz' % i)))) for i in range(2)]
+    assert list(rk[0]['counts']) == [2 * B_U, sum(ns_r), 2 * B_U]
     idx = rk[0]['idx']
     ns = int(rk[0]['n_shared'])
     d = load('elbo_c32.npz')
     e = dict(d)
     e['cfg'] = np.array([int(d['cfg'][0]), int(d['cfg'][1]), int(d['cfg'][2]), int(d['cfg'][3]), 2 * B_U,
-                         2 * NS_RANK])
+                         sum(ns_r)])
     for k in ('Xs', 'Y', 'F'):
-        e[k] = d[k][:2 * NS_RANK]
+        e[k] = d[k][:sum(ns_r)]
     model, _ = build_golden_model(e)
     model._datasets['unsupervised'].perm = torch.tensor(idx[:2 * B_U], device='cuda').long()
     dz = rk[0]['eps_z'].shape[1]
     ez = np.concatenate([rk[0]['eps_z'][:B_U], rk[1]['eps_z'][:B_U], rk[0]['eps_z'][B_U:], rk[1]['eps_z'][B_U:]])
     ex = np.concatenate([rk[0]['eps_x'], rk[1]['eps_x']])
-    assert ez.shape == (2 * (B_U + NS_RANK), dz)
+    assert ez.shape == (2 * B_U + sum(ns_r), dz)
     names = list(rk[0]['names'])
+    # the union's q rows: rank 0's shard, then rank 1's (per-row sizes from the union parameter)
+    row_parts = lambda p: [p.numel() // sum(ns_r) * n for n in ns_r]
     with torch.no_grad():       # the ranks' initial parameters (shared: identical; q rows: shard rows)
         for k, p in model.named_parameters():
             i = names.index(k)
             o = [int(rk[j]['offsets'][i]) for j in range(2)]
             if k.startswith(('q_z.', 'q_X.')):
-                parts = [rk[j]['P0'][o[j]:o[j] + p.numel() // 2] for j in range(2)]
+                parts = [rk[j]['P0'][o[j]:o[j] + row_parts(p)[j]] for j in range(2)]
                 p.copy_(torch.tensor(np.concatenate(parts).reshape(p.shape)))
             else:
                 p.copy_(torch.tensor(rk[0]['P0'][o[0]:o[0] + p.numel()].reshape(p.shape)))
@@ -129,10 +136,10 @@ def test_dp_two_ranks_sync_bn(device, tmp_path):
         i = names.index(k)
         g = p.grad.cpu().numpy().ravel()
         if k.startswith(('q_z.', 'q_X.')):
-            half = p.numel() // 2
+            rp = row_parts(p)
             for j in range(2):
-                o = int(rk[j]['offsets'][i])
-                errs['%s[rank%d]' % (k, j)] = tensor_rel(rk[j]['G_red'][o:o + half], g[j * half:(j + 1) * half])
+                o, lo = int(rk[j]['offsets'][i]), sum(rp[:j])
+                errs['%s[rank%d]' % (k, j)] = tensor_rel(rk[j]['G_red'][o:o + rp[j]], g[lo:lo + rp[j]])
         else:
             o = int(rk[0]['offsets'][i])
             assert o + p.numel() <= ns

@@ -20,8 +20,11 @@ for CFG in "$@"; do
     python3 "$R/tools/pmc_traffic_all.py" "$OUT/pmcF_${TAG}_$CFG" "$OUT/pmcW_${TAG}_$CFG" "$M" \
         "$OUT/traffic_${TAG}_$CFG.json" > "$OUT/traffic_${TAG}_$CFG.txt" 2>&1
     rc=$?; echo "$CFG traffic rc=$rc"; [ $rc -eq 0 ] || exit $rc
-    # the config's CPU-baseline + roofline bench line (short)
+    # the traffic file where bench.py looks for it (TRAFFIC_FILES), then the config's CPU-baseline +
+    # roofline bench line (short)
     cd "$R"
+    if [ "$CFG" = "c64" ]; then TF=r04_traffic.json; else TF=r04_traffic_$CFG.json; fi
+    cp "$OUT/traffic_${TAG}_$CFG.json" "$R/profiles/$TF"
     timeout -k 10 300 python3 bench.py --config "$CFG" --steps 50 --warmup 10 > "$OUT/bench_${TAG}_$CFG.json" \
         2> "$OUT/bench_${TAG}_$CFG.err"
     rc=$?; echo "$CFG bench rc=$rc"; [ $rc -eq 0 ] || exit $rc
