@@ -401,6 +401,8 @@ def main():
     ap.add_argument('--warmup', type=int, default=200)
     ap.add_argument('--config', default='c64', choices=sorted(CONFIGS))
     ap.add_argument('--no-graph', action='store_true')
+    ap.add_argument('--unroll', type=int, default=int(os.environ.get('GPI_UNROLL', '1')),
+                    help="steps per graph replay ('streams' graph mode; FusedElboStep.capture(unroll))")
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-roofline', action='store_true')
     ap.add_argument('--kprof', default=None, help='write the per-operator HIP-event profile (JSON) here')
@@ -452,17 +454,15 @@ def main():
                          distributed=distributed, rank=rank, world=world,
                          graph_allreduce=os.environ.get('GPI_GRAPH_ALLREDUCE', '1') == '1', sync_bn=args.sync_bn)
     if not args.no_graph and not (step.sync_bn and backend != 'nccl'):
-        step.capture()
-    log('captured; warm-up')
-    for _ in range(args.warmup):
-        step.step()
+        step.capture(unroll=args.unroll)
+    log('captured (graph mode %s, %d step(s) per replay); warm-up' % (step.graph_mode, step.unroll))
+    step.run(args.warmup)
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step.step()
+    step.run(args.steps)
     t_enq = time.perf_counter()          # host time to enqueue the K steps (graph launches)
     torch.cuda.synchronize()
     if distributed:
@@ -476,6 +476,7 @@ def main():
     if not math.isfinite(elbo):
         raise RuntimeError('non-finite ELBO %r' % elbo)
     step.engine.check_flag()
+    step.check_handoff()                 # no cross-stream flag wait timed out
 
     roof = None
     cpu = None
@@ -548,6 +549,8 @@ def main():
                                                                      physics['rom'].grid.n, physics['rom'].grid.n),
                        'global_batch': world * per_step, 'grid': physics['fom'].grid.n,
                        'parallelism': 'dp%d' % world, 'graph': step.graph is not None,
+                       'graph_mode': step.graph_mode if step.graph is not None else None,
+                       'steps_per_replay': step.unroll,
                        'world': world, 'backend': backend if distributed else None,
                        'allreduce': None if not distributed else
                        ('host-side between graphs' if args.no_graph or getattr(step, 'split_graph', True) else 'in-graph'),

@@ -112,6 +112,8 @@ struct ConvGeom {
                     // to each other), so the halo rows two tiles share are read from HBM once into that
                     // XCD's L2 instead of once per XCD.  0: tile = blockIdx.x (xcd_mode)
     int grid;       // launched workgroups (xcd remap)
+    int alt;        // fused output conv: half the workgroups run the input gradient (VALU) before the weight
+                    // gradient (MFMA), so a CU's co-resident workgroups overlap the two pipes (fuse_alt)
     uint32_t* sig;             // cross-stream hand-off (gpi_*_sig): workgroup 0 increments *sig at entry, i.e.
     const int64_t* sig_epoch;  // once every earlier kernel of the stream has completed (gpi_stream_signal)
     int in_sq, in_sr, in_sc;   // 256 chunks of the input image = (planes, rows, chunks)
@@ -264,6 +266,7 @@ bool conv_geom(const gpi_conv_desc& d, const gpi_groups& g, ConvGeom& G, bool fw
     G.lsum = 0;     // decided by launch() / gpi_conv_blocks from the LDS footprint (lsum_op)
     G.vsum = 0;     // decided by launch() / gpi_conv_blocks (vsum_op)
     G.xcd = 0;      // set by launch() (xcd_mode)
+    G.alt = 0;
     G.grid = 0;     // set by launch()
     G.sig = nullptr;
     G.sig_epoch = nullptr;
@@ -1670,7 +1673,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
             }
         }
     };
-    if (vop) wgrad_phase();
+    // fuse_alt: which workgroups take the weight gradient last -- blocks of one CU are (roughly) those
+    // the XCD's dispatcher deals it 32 apart: bit 8 of the block index alternates among them
+    const int bsel = G.alt == 1 ? (int)(blockIdx.x >> 8) : G.alt == 2 ? (int)(blockIdx.x >> 3) : (int)blockIdx.x;
+    const bool wg_late = FUSE && G.alt != 0 && (bsel & 1) != 0;
+    if (vop && !wg_late) wgrad_phase();
     PHASE(5);
 
     // ---- phase 4b: input gradient (MFMA) + BN backward of the input + S_in (+)= gamma * dbn
@@ -1941,7 +1948,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
             }
         }
     }
-    if (!vop) wgrad_phase();
+    if (!vop || wg_late) wgrad_phase();
     PHASE(6);
     if (lsum) {
         // the four waves' partial rows into LDS (the whole region after the header is dead by now; the
@@ -2151,6 +2158,8 @@ int launch(const gpi_conv_desc& d, const gpi_codec_ctx& c, hipStream_t st, bool 
     const int grid = G.nblocks * (G.split ? 2 : 1);
     G.grid = grid;
     G.xcd = xcd_mode(fwd, fuse, G.split != 0) ? 1 : 0;
+    static const int fuse_alt = env_int("GPI_FUSE_ALT", 0);
+    G.alt = fuse ? fuse_alt : 0;
 #ifdef GPI_PHASE_TIMING
     static const int dbg_print = env_int("GPI_DBG_PRINT", 0);
     if (dbg_print)

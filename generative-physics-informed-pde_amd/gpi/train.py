@@ -160,6 +160,8 @@ class FusedElboStep(object):
         # each stream's part of the step is captured as a graph of its own
         self.side_done = torch.zeros(1, dtype=torch.int64, device=dev)
         self._probed_stream = None
+        self.unroll = 1
+        self.g_fb_k = self.g_side_k = None
         if self.handoff == 'flags':
             self._configure_handoff()
             if self.fuse_adam:
@@ -276,11 +278,17 @@ class FusedElboStep(object):
                 self.flat.gacc, self.flat.G, ws.t_ws, ws.t_scr, ws.t_parts, ws.t_flag, self.last_terms] + \
             self.engine.running.buffers
 
-    def capture(self):
+    def capture(self, unroll=1):
         """Capture the step into HIP graph(s); the all-reduce stays outside the graph.
         The two warm-up steps run on snapshots: capture() leaves parameters, optimizer state,
         step counter, random stream and the pre-drawn subset / noise exactly as it found them, so
-        the first replayed step is the step an eager loop would take next."""
+        the first replayed step is the step an eager loop would take next.
+        unroll > 1 ('streams' mode): also capture `unroll` consecutive steps as one pair of graphs, which
+        run(n) replays (one graph-launch boundary per `unroll` steps; every step still reads its counters,
+        subset, noise and learning rate from device memory, so the steps are the ones step() would take --
+        a learning-rate change reaches the device at the next replay)."""
+        self.unroll = 1
+        self.g_fb_k = self.g_side_k = None
         if self.sync_bn and dist.get_backend(self.pg) != dist.Backend.NCCL:
             raise RuntimeError('FusedElboStep.capture: SyncBN with a host-side backend (gloo) runs eagerly only')
         torch.cuda.synchronize()
@@ -306,6 +314,9 @@ class FusedElboStep(object):
             self._capture_segments()
         elif not self.split_graph and self.graph_mode == 'streams':
             self._capture_streams()
+            if unroll > 1:
+                self.g_fb_k, self.g_side_k = self._capture_streams(unroll)
+                self.unroll = int(unroll)
         elif self.split_graph:
             with torch.cuda.graph(self.g_fb):
                 self.forward_backward()
@@ -357,34 +368,40 @@ class FusedElboStep(object):
         self.graph_mode = 'single'
         self._configure_handoff()
         if self.graph is not None:
-            self.capture()
+            self.capture()          # ('single': no unrolled graphs; run() replays single steps)
 
-    def _capture_streams(self):
+    def _capture_streams(self, steps=1):
         """The step as TWO graphs, one per stream, captured at once: the main stream's (encoder, head,
         decoder, their backward, the epilogue + Adam) and the side stream's (ROM, the variational samples'
         head backward, the slab reductions, the next step's noise), ordered only by the device counters
-        of the flag hand-offs and the side stream's step gate -- no graph edge between the streams."""
+        of the flag hand-offs and the side stream's step gate -- no graph edge between the streams.
+        steps > 1: that many consecutive steps in the pair, returned as (main, side) graphs."""
         fused = self.fuse_adam
         side = self.engine._side_stream()
         cap = torch.cuda.Stream()
         cap.wait_stream(torch.cuda.current_stream())
         side.wait_stream(torch.cuda.current_stream())
-        self.g_side = torch.cuda.CUDAGraph()
+        g_fb = self.g_fb if steps == 1 else torch.cuda.CUDAGraph()
+        g_side = torch.cuda.CUDAGraph()
         with torch.cuda.stream(side):
-            self.g_side.capture_begin(capture_error_mode='relaxed')
+            g_side.capture_begin(capture_error_mode='relaxed')
         try:
             with torch.cuda.stream(cap):
-                self.g_fb.capture_begin(capture_error_mode='relaxed')
+                g_fb.capture_begin(capture_error_mode='relaxed')
                 try:
-                    self._forward_backward(epilogue=not fused)
-                    self.allreduce()        # RCCL: captured as a graph node
-                    self.update(fused=fused)
+                    for _ in range(steps):
+                        self._forward_backward(epilogue=not fused)
+                        self.allreduce()        # RCCL: captured as a graph node
+                        self.update(fused=fused)
                 finally:
-                    self.g_fb.capture_end()
+                    g_fb.capture_end()
         finally:
             with torch.cuda.stream(side):
-                self.g_side.capture_end()
+                g_side.capture_end()
         torch.cuda.current_stream().wait_stream(cap)
+        if steps == 1:
+            self.g_side = g_side
+        return g_fb, g_side
 
     def _capture_segments(self):
         """The step as single-stream graphs, one per stretch of a stream between two cross-stream
@@ -488,6 +505,22 @@ class FusedElboStep(object):
             self.allreduce()
             self.g_up.replay()
         self._mark_optimizer_step()
+
+    def run(self, n):
+        """n steps: with capture(unroll=k), n // k replays of the k-step graphs, then single steps."""
+        n = int(n)
+        if self.graph is not None and self.unroll > 1 and self.g_fb_k is not None:
+            self.sync_lr()
+            self._check_stream_pair()
+            if self.graph_mode == 'streams' and self.g_fb_k is not None:
+                for _ in range(n // self.unroll):
+                    self.g_fb_k.replay()
+                    with torch.cuda.stream(self.engine._side):
+                        self.g_side_k.replay()
+                    self._mark_optimizer_step()
+                n %= self.unroll
+        for _ in range(n):
+            self.step()
 
     def elbo(self):
         """ELBO value of the last completed step (0-d tensor)."""

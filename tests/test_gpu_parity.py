@@ -552,6 +552,34 @@ def test_flag_handoff_matches_event_handoff(device, monkeypatch):
     assert int(fl.handoff_flags[0].item()) == 4        # the tag of the last step (counter 3, + 1)
 
 
+def test_unrolled_graph_matches_single_steps(device):
+    """capture(unroll=3) + run(7) (two replays of the 3-step graph pair, then one single step) leaves
+    exactly what seven step() replays leave: parameters, Adam moments, counters, subsets, flags."""
+    import copy
+    from gpi.train import FusedElboStep
+    d = load('elbo_c32.npz')
+    model_a, bs = build_golden_model(d)
+    model_b = copy.deepcopy(model_a)
+    Xu, Xs, Y, F = cuda(d['Xu']), cuda(d['Xs']), cuda(d['Y']), cuda(d['F'])
+    one = FusedElboStep(model_a, Xu, bs, Xs, Y, F, lr=1e-3, seed=3)
+    unr = FusedElboStep(model_b, Xu, bs, Xs, Y, F, lr=1e-3, seed=3)
+    one.capture()
+    unr.capture(unroll=3)
+    if unr.graph_mode != 'streams':
+        pytest.skip('the stream pair shares a hardware queue here: no unrolled graphs (graph mode single)')
+    assert unr.unroll == 3
+    for _ in range(7):
+        one.step()
+    unr.run(7)
+    torch.cuda.synchronize()
+    unr.check_handoff()
+    for a, b in zip(one._mutable_state(), unr._mutable_state()):
+        if a.data_ptr() == one.side_done.data_ptr() and one.graph_mode != 'streams':
+            continue            # ('single' keeps no side-stream step counter)
+        assert torch.equal(a, b)
+    assert int(unr.step_ctr.item()) == 7 and int(unr.side_done.item()) == 7
+
+
 def test_fused_epilogue_adam_matches_two_launches(device):
     """gpi_step_epilogue_adam (epilogue + Adam in one launch, the single-process default) leaves
     exactly what gpi_step_epilogue followed by gpi_adam leave -- parameters, Adam moments, gradient,
