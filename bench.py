@@ -401,7 +401,8 @@ def main():
     ap.add_argument('--warmup', type=int, default=200)
     ap.add_argument('--config', default='c64', choices=sorted(CONFIGS))
     ap.add_argument('--no-graph', action='store_true')
-    ap.add_argument('--unroll', type=int, default=int(os.environ.get('GPI_UNROLL', '1')),
+    # 4 steps per replay: 0.5726 / 0.5728 vs 0.5768 / 0.5773 ms per step with 1 (r04l, one box)
+    ap.add_argument('--unroll', type=int, default=int(os.environ.get('GPI_UNROLL', '4')),
                     help="steps per graph replay ('streams' graph mode; FusedElboStep.capture(unroll))")
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-roofline', action='store_true')

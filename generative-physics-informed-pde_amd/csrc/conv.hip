@@ -2158,7 +2158,9 @@ int launch(const gpi_conv_desc& d, const gpi_codec_ctx& c, hipStream_t st, bool 
     const int grid = G.nblocks * (G.split ? 2 : 1);
     G.grid = grid;
     G.xcd = xcd_mode(fwd, fuse, G.split != 0) ? 1 : 0;
-    static const int fuse_alt = env_int("GPI_FUSE_ALT", 0);
+    // r04l (2 x 400 steps per arm, one box): 1 -> 0.5761 / 0.5759, off 0.5768 / 0.5773, 2 -> 0.5773 / 0.5777,
+    // 3 -> 0.5776 / 0.5770 ms per step
+    static const int fuse_alt = env_int("GPI_FUSE_ALT", 1);
     G.alt = fuse ? fuse_alt : 0;
 #ifdef GPI_PHASE_TIMING
     static const int dbg_print = env_int("GPI_DBG_PRINT", 0);

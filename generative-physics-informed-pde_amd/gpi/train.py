@@ -340,14 +340,26 @@ class FusedElboStep(object):
         a flag wait ahead of its signal on a shared queue blocks it (tools/queue_stress.py: 3 of 18
         steps timed out with 6 step objects in 'streams' mode, none in 'single', whose graph
         branches the runtime places itself)."""
-        side = self.engine._side_stream()
+        e = self.engine
         pr = torch.zeros(2, dtype=torch.int32, device=self.flat.P.device)
-        torch.cuda.synchronize()
-        L.check(L.lib().gpi_queue_probe(L.ptr(pr), L.ptr(pr[1:]), C.c_void_p(side.cuda_stream)), 'queue probe')
-        L.check(L.lib().gpi_stream_signal(L.ptr(pr), L.ptr(self.step_ctr), L.stream_handle()), 'queue probe signal')
-        torch.cuda.synchronize()
-        self._probed_stream = torch.cuda.current_stream()
-        return int(pr[1].item()) == 1
+        # up to four side-stream candidates (HIP deals new streams round-robin over its queues, so one of
+        # four consecutive ones sits on another queue than the current stream); a replaced candidate is
+        # dropped before any work or capture used it
+        for attempt in range(4):
+            side = e._side_stream()
+            pr.zero_()
+            torch.cuda.synchronize()
+            L.check(L.lib().gpi_queue_probe(L.ptr(pr), L.ptr(pr[1:]), C.c_void_p(side.cuda_stream)), 'queue probe')
+            L.check(L.lib().gpi_stream_signal(L.ptr(pr), L.ptr(self.step_ctr), L.stream_handle()),
+                    'queue probe signal')
+            torch.cuda.synchronize()
+            self._probed_stream = torch.cuda.current_stream()
+            if int(pr[1].item()) == 1:
+                return True
+            if getattr(self, 'graph', None) is not None:
+                return False        # the captured graphs hold this side stream
+            e._side = None          # next candidate
+        return False
 
     def _configure_handoff(self):
         """Flag hand-offs between the streams; graph mode 'streams' (no event between the streams at all)
