@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 record at HEAD (GPU box, repo root): the GPU test suite as the driver runs it, smoke, the default
 # bench line (CPU baseline + roofline), and a rocprofv3 kernel trace of a short bench run (kernel stats and
-# the per-step timeline).  Every GPU step has its own time limit; stops at the first failing step.
+# the per-step timeline; traced at one step per graph replay, so the timeline splits into steps).  Every GPU step has its own time limit; stops at the first failing step.
 # usage: tools/r04_final.sh TAG
 set -u
 TAG=${1:-r04z}
@@ -18,7 +18,7 @@ timeout -k 10 400 python bench.py > "$OUT/bench_$TAG.json" 2> "$OUT/bench_$TAG.l
 rc=$?; tail -1 "$OUT/bench_$TAG.json"; [ $rc -eq 0 ] || exit $rc
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o run -- \
-    python3 "$R/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-roofline > "$OUT/prof_$TAG.log" 2>&1
+    python3 "$R/bench.py" --steps 20 --warmup 5 --unroll 1 --no-cpu-baseline --no-roofline > "$OUT/prof_$TAG.log" 2>&1
 rc=$?; echo "rocprof rc=$rc"; [ $rc -eq 0 ] || exit $rc
 cd "$R"
 python3 tools/prof_summary.py "$OUT/prof_$TAG" > "$OUT/kstats_$TAG.txt" 2>&1

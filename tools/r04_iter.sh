@@ -38,7 +38,7 @@ done
 if [ "${ITER_PROF:-1}" != "0" ]; then
     cd /tmp && export TMPDIR=/tmp
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o run -- \
-        python3 "$R/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-roofline > "$OUT/prof_$TAG.log" 2>&1
+        python3 "$R/bench.py" --steps 20 --warmup 5 --unroll 1 --no-cpu-baseline --no-roofline > "$OUT/prof_$TAG.log" 2>&1
     rc=$?
     echo "rocprof rc=$rc"
     cd "$R"
