@@ -368,6 +368,8 @@ extern "C" int gpi_stream_wait(const uint32_t* flag, const int64_t* epoch, uint3
 
 extern "C" int gpi_version(void) { return 1; }
 
+extern "C" int gpi_replicas(void) { return GPI_REPLICAS; }
+
 extern "C" int gpi_struct_sizes(int64_t* out, int n) {
     const int64_t s[] = {(int64_t)sizeof(gpi_stat), (int64_t)sizeof(gpi_groups), (int64_t)sizeof(gpi_conv_desc),
                          (int64_t)sizeof(gpi_codec_ctx), (int64_t)sizeof(gpi_reduce_item), (int64_t)sizeof(gpi_head_desc),

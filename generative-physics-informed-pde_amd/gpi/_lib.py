@@ -21,7 +21,8 @@ GPI_MAX_CIN = 32
 GPI_MAX_COUT = 8
 GPI_MAX_REDUCE_ITEMS = 48
 GPI_MAX_GEMM_ITEMS = 12
-GPI_REPLICAS = 16
+# statistic / term replicas of the library build (16; a variant build's value by GPI_REPLICAS, checked at load)
+GPI_REPLICAS = int(os.environ.get('GPI_REPLICAS', '16'))
 FINALIZE_ACCUMULATE = 1
 FINALIZE_ZERO = 2
 
@@ -179,6 +180,7 @@ STRUCTS = [Stat, Groups, ConvDesc, CodecCtx, ReduceItem, HeadDesc, GemmItem, Rom
 # name -> (restype, argtypes)
 SIGNATURES = {
     'gpi_version': (C.c_int, []),
+    'gpi_replicas': (C.c_int, []),
     'gpi_struct_sizes': (C.c_int, [C.POINTER(i64), C.c_int]),
     'gpi_error_string': (C.c_char_p, [C.c_int]),
     'gpi_conv_blocks': (C.c_int, [C.POINTER(ConvDesc), C.POINTER(Groups), C.POINTER(i32)]),
@@ -254,6 +256,9 @@ def lib():
         for s, cls in zip(sizes[:k], STRUCTS):
             if s != C.sizeof(cls):
                 raise NativeError('ABI mismatch for %s: C %d bytes, ctypes %d' % (cls.__name__, s, C.sizeof(cls)))
+        if L.gpi_replicas() != GPI_REPLICAS:
+            raise NativeError('ABI mismatch: the library keeps %d statistic replicas, the binding %d (GPI_REPLICAS)'
+                              % (L.gpi_replicas(), GPI_REPLICAS))
         _LIB = L
     return _LIB
 

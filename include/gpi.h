@@ -43,7 +43,9 @@ extern "C" {
  * over GPI_REPLICAS copies indexed by workgroup % GPI_REPLICAS so that
  * thousands of workgroups never serialise on one fp64 atomic address; the
  * reader sums the replicas. */
+#ifndef GPI_REPLICAS
 #define GPI_REPLICAS 16
+#endif
 
 /* Conv epilogues */
 #define GPI_EPI_STORE 0        /* store raw output */
@@ -420,6 +422,8 @@ typedef struct gpi_adam_desc {
 
 /* ---------------------------------------------------------------- API */
 int gpi_version(void);
+/* GPI_REPLICAS of this build (bindings size their statistics / term buffers by it). */
+int gpi_replicas(void);
 /* sizeof of every struct above, in declaration order (ABI self-check); returns the count. */
 int gpi_struct_sizes(int64_t* out, int n);
 const char* gpi_error_string(int code);

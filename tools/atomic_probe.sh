@@ -5,7 +5,7 @@ set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p "$R/gpurun_out/atom"
 for k in 0 4; do
-    GPI_DBG_SKIP=$k timeout -k 10 120 python "$R/bench.py" --steps 20 --warmup 5 --no-cpu-baseline \
+    GPI_LIB_VARIANT=timing GPI_DBG_SKIP=$k timeout -k 10 120 python "$R/bench.py" --steps 20 --warmup 5 --no-cpu-baseline \
         --kprof "$R/gpurun_out/atom/s$k.json" > "$R/gpurun_out/atom/s$k.log" 2>&1 || { tail -3 "$R/gpurun_out/atom/s$k.log"; exit 1; }
 done
 python3 - "$R/gpurun_out/atom" <<'PY'
