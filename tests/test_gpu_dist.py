@@ -163,6 +163,20 @@ def test_rccl_allreduce_captured_in_step_graph(device):
     assert 'max |dP| = 0.000e+00' in r.stdout, r.stdout[-2000:]
 
 
+def test_rccl_allreduce_captured_unrolled(device):
+    """The bench's N > 1 form: two steps per replay of the captured graphs ('streams' mode when the probe
+    allows), i.e. two RCCL all-reduces inside one graph, and run(3) = one 2-step replay + one single step;
+    equal to eager steps (world size 1 on this box)."""
+    env = dict(os.environ)
+    env['PYTHONUNBUFFERED'] = '1'
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node=1',
+           '--master-addr=127.0.0.1', '--master-port=%d' % _free_port(),
+           os.path.join(os.path.dirname(HERE), 'tools', 'dist_capture_probe.py'), '--unroll', '2']
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert 'max |dP| = 0.000e+00' in r.stdout, r.stdout[-2000:]
+
+
 def test_rccl_sync_bn_captured_in_step_graph(device):
     """SyncBN over RCCL inside the captured step (world size 1 on this box; the 8-GPU node runs the
     same graph across ranks): the per-conv collectives of the BN batch sums (26 at C32, 46 at C64) are graph nodes, the

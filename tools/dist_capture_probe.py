@@ -3,7 +3,10 @@ graph replays with eager steps of an identical copy (same seeds) -- parameters a
 --sync-bn: SyncBN (every BN layer's batch sums all-reduced conv by conv, ~46 collectives per step) captured
 into the step graph as well; the replays must equal the eager SyncBN steps bit for bit, and at world size 1
 the SyncBN step must also agree with the replica-BN step to rounding (the same batch statistics).
-usage: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 tools/dist_capture_probe.py [--sync-bn]"""
+--unroll K: the graph copy captures K steps per replay (FusedElboStep.capture(unroll=K), K all-reduces in one
+graph) and takes its 3 steps by run(3).
+usage: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 tools/dist_capture_probe.py
+       [--sync-bn] [--unroll K]"""
 import copy
 import os
 import sys
@@ -41,13 +44,20 @@ def main():
             n_coll[0] += 1
             inner(t)
         graph.engine.bn_sync = counted
-    graph.capture()
+    unroll = int(sys.argv[sys.argv.index('--unroll') + 1]) if '--unroll' in sys.argv else 1
+    graph.capture(unroll=unroll)
     assert not graph.split_graph
     n_per_step = n_coll[0] // 3          # two warm-up steps + the captured one
+    print('rank %d: graph mode %s, %d step(s) per replay' % (rank, graph.graph_mode, graph.unroll), flush=True)
     for _ in range(3):
         eager.step_eager()
-        graph.step()
+    if unroll > 1:
+        graph.run(3)
+    else:
+        for _ in range(3):
+            graph.step()
     torch.cuda.synchronize()
+    graph.check_handoff()
     err = (graph.flat.P - eager.flat.P).abs().max().item()
     what = 'SyncBN (%d codec collectives per step) + ' % n_per_step if sync else ''
     print('rank %d world %d: graph-captured %sall-reduce vs eager, max |dP| = %.3e' % (rank, world, what, err),
