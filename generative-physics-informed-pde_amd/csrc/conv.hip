@@ -112,6 +112,17 @@ struct ConvGeom {
                     // to each other), so the halo rows two tiles share are read from HBM once into that
                     // XCD's L2 instead of once per XCD.  0: tile = blockIdx.x (xcd_mode)
     int grid;       // launched workgroups (xcd remap)
+    // backward (GPI_HALF_TILES): tiles [nfull, nblocks) are half-height tiles (htiles per sample, geometry ha)
+    // of samples [half_b, B).  A batch whose tile count is no multiple of the 256 CUs (the decoder's 288
+    // samples: 1152 tiles) left half the CUs one workgroup more than the rest, and a launch lasts as long as
+    // its busiest CUs (fused output conv: last exits 32.0 us on 5-workgroup CUs, 27.8 us on 4-workgroup
+    // ones, tools/phase_probe.py); with the samples past the first 1024 tiles split into half tiles, every
+    // CU gets four full tiles and one half (0.5679-0.5683 vs 0.5723-0.5730 ms per step, r04v)
+    int nfull, half_b, htiles;
+    struct Alt {
+        int th, rh, gh, ph, zreg, in_sq, in_sr, in_sc, g_sq, g_sr, g_sc;
+        Div d_in4, d_g4, d_tp;
+    } ha;
     int alt;        // fused output conv: half the workgroups run the input gradient (VALU) before the weight
                     // gradient (MFMA), so a CU's co-resident workgroups overlap the two pipes (fuse_alt)
     uint32_t* sig;             // cross-stream hand-off (gpi_*_sig): workgroup 0 increments *sig at entry, i.e.
@@ -293,6 +304,46 @@ bool conv_geom(const gpi_conv_desc& d, const gpi_groups& g, ConvGeom& G, bool fw
     G.d_tp = mkdiv(G.th * d.w_out);
     G.d_wout = mkdiv(d.w_out);
     G.d_w2 = mkdiv(d.w_in >= 2 ? d.w_in / 2 : 1);
+    G.nfull = G.nblocks;
+    G.half_b = B;
+    G.htiles = 0;
+    G.ha = ConvGeom::Alt{G.th, G.rh, G.gh, G.ph, G.zreg, G.in_sq, G.in_sr, G.in_sc, G.g_sq, G.g_sr, G.g_sc,
+                         G.d_in4, G.d_g4, G.d_tp};
+    // half tiles for the samples past the largest multiple of 256 tiles (GPI_HALF_TILES: 0 off, 1 the loss
+    // op's backward only, 2 every backward launch)
+    static const int half_tiles = env_int("GPI_HALF_TILES", 2);
+    const int tot = B * G.tiles, base = tot & ~255;
+    if (half_tiles && !fwd && (half_tiles > 1 || loss_bwd) && (G.th & 1) == 0 && base > 0 && tot != base &&
+        base % G.tiles == 0) {
+        ConvGeom::Alt& a = G.ha;
+        a.th = G.th / 2;
+        int y0;
+        in_rows(d.k, d.stride, d.upsample, d.pad, 0, a.th, y0, a.rh);
+        if (d.upsample) a.rh += 1;
+        if (fuse) a.rh += d.k - 1;
+        g_rows(d.k, d.stride, d.pad, 0, a.th, y0, a.gh);
+        owned_rows(d.stride, d.upsample, 0, a.th, y0, a.ph);
+        a.zreg = (!fwd && d.gout_mode == 0 && (int64_t)d.cout * a.gh * (G.PG / 4) <= (int64_t)ZREG * 256) ? 1 : 0;
+        const int P4 = G.P / 4, pl = a.rh * P4, Q4 = G.PG / 4, gq = a.gh * Q4;
+        a.in_sq = 256 / pl;
+        a.in_sr = (256 % pl) / P4;
+        a.in_sc = (256 % pl) % P4;
+        a.g_sq = 256 / gq;
+        a.g_sr = (256 % gq) / Q4;
+        a.g_sc = (256 % gq) % Q4;
+        a.d_in4 = mkdiv(pl);
+        a.d_g4 = mkdiv(gq);
+        a.d_tp = mkdiv(a.th * d.w_out);
+        const bool ok = d.gin_off < 0 || (((a.ph * d.w_in) & 15) == 0 && (d.stride != 2 || (a.ph & 1) == 0));
+        if (!ok) a = ConvGeom::Alt{G.th, G.rh, G.gh, G.ph, G.zreg, G.in_sq, G.in_sr, G.in_sc, G.g_sq, G.g_sr, G.g_sc,
+                                   G.d_in4, G.d_g4, G.d_tp};
+        else {
+        G.half_b = base / G.tiles;
+        G.nfull = base;
+        G.htiles = 2 * G.tiles;
+        G.nblocks = base + (B - G.half_b) * G.htiles;
+        }
+    }
     return true;
 }
 
@@ -515,8 +566,14 @@ __device__ __forceinline__ int logical_block(const ConvGeom& G) {
 __device__ __forceinline__ TileIdx tile_of(const ConvGeom& G, const gpi_groups& g, int tile = -1) {
     if (tile < 0) tile = logical_block(G);
     TileIdx t;
-    t.b = tile / G.tiles;
-    t.oy0 = (tile - t.b * G.tiles) * G.th;
+    if (tile < G.nfull) {
+        t.b = tile / G.tiles;
+        t.oy0 = (tile - t.b * G.tiles) * G.th;
+    } else {                         // half-height tiles (GPI_HALF_TILES)
+        const int u = tile - G.nfull, q = u / G.htiles;
+        t.b = G.half_b + q;
+        t.oy0 = (u - q * G.htiles) * G.ha.th;
+    }
     t.grp = group_of(g, t.b);
     t.gsz = karg_sel(g.start, t.grp + 1) - karg_sel(g.start, t.grp);
     return t;
@@ -1040,11 +1097,30 @@ __host__ __device__ constexpr bool fuse_wlds(int ky) {
     return GPI_FUSE_WLDS <= 0 ? false : (GPI_FUSE_WLDS >= 5 ? true : (ky & 1 ? (ky / 2) < GPI_FUSE_WLDS : (ky / 2) < GPI_FUSE_WLDS - 2));
 }
 
-template <int K, int S, int UP, bool FUSE = false>
+template <int K, int S, int UP, bool FUSE = false, bool HALF = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (FUSE ? GPI_FUSE_WAVES : 4) : 6))) void conv_bwd_kernel(gpi_conv_desc d, gpi_codec_ctx c, ConvGeom G) {
     touch_kernargs<CONV_KARG_BYTES>();
     entry_signal(G);
     if (SKIP(G, 16)) return;
+    // the tile's geometry: the launch's, or the half-height one of the tiles past nfull (GPI_HALF_TILES)
+    ConvGeom Gt_;
+    if constexpr (HALF) {
+        const int lb0 = logical_block(G);
+        const bool wgr0 = G.split && (G.xcd ? (lb0 & 1) != 0 : lb0 >= G.nblocks);
+        const int tile0 = !G.split ? lb0 : (G.xcd ? lb0 >> 1 : (wgr0 ? lb0 - G.nblocks : lb0));
+        // (HALF: the instantiation for launches with half tiles -- the per-tile geometry copy costs the
+        // prologue ~130 instructions and 7 more argument-load waits, which the launches without half tiles,
+        // e.g. the encoder's, do not pay)
+        Gt_ = G;
+        if (tile0 >= G.nfull) {
+            const ConvGeom::Alt& a = G.ha;
+            Gt_.th = a.th; Gt_.rh = a.rh; Gt_.gh = a.gh; Gt_.ph = a.ph; Gt_.zreg = a.zreg;
+            Gt_.in_sq = a.in_sq; Gt_.in_sr = a.in_sr; Gt_.in_sc = a.in_sc;
+            Gt_.g_sq = a.g_sq; Gt_.g_sr = a.g_sr; Gt_.g_sc = a.g_sc;
+            Gt_.d_in4 = a.d_in4; Gt_.d_g4 = a.d_g4; Gt_.d_tp = a.d_tp;
+        }
+    }
+    const ConvGeom& Gt = HALF ? Gt_ : G;
     constexpr int KK = K * K;
     extern __shared__ __attribute__((aligned(16))) float smem[];
     double* gst = (double*)smem;                      // [cin][4] input stats, then [cout][4] output stats
@@ -1070,18 +1146,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
     float* wD = smem + bwd_hdr(d.cin, d.cout);        // [KD4][16]: W[co][ci][tap] at (co*KK + tap)*16 + ci, zero padded
     const int nwd = (has_gin && !vop) ? KD4 * 16 : 0;
     float* const mid = wD;
-    const int nmid = vop ? vop_mid_floats(G.gh, d.w_out, rowlen, FUSE) : 0;
+    const int nmid = vop ? vop_mid_floats(Gt.gh, d.w_out, rowlen, FUSE) : 0;
     // S1 / UP: [KD4] output-gradient offset of reduction index k; S2: per parity class of the input
     // pixel [4][2][KD4]: (output-gradient offset, weight row) of the class's k-th valid tap
     int* ktab = (int*)(wD + pad256(nwd) + nmid);
     float* gl = (float*)ktab + ((has_gin && !vop) ? pad256((S == 2 ? 8 : 1) * KD4) : 0);   // [cout][gh][PG]
-    const int gplane = G.gh * G.PG;
-    const int gimg = img_floats(d.cout, G.gh, G.PG);
-    const bool zreg = G.zreg != 0;
+    const int gplane = Gt.gh * Gt.PG;
+    const int gimg = img_floats(d.cout, Gt.gh, Gt.PG);
+    const bool zreg = Gt.zreg != 0;
     float* gz = gl + gimg;                            // raw z of the output (BN-backward only, LDS form)
     float* al = gz + ((obn && !zreg) ? gimg : 0);     // [cin][rh][P]
     // FUSE: the image starts K/2 rows above the backward's first input row; alb is the backward's view
-    float* const alb = FUSE ? al + (K / 2) * G.P : al;
+    float* const alb = FUSE ? al + (K / 2) * Gt.P : al;
     // reduction scratch: aliases gz (dead after phase 3) when it is large enough -- 8 KB less LDS
     // per workgroup, one more resident workgroup per CU on the 32x32 planes
     // channel-sum scratch: the offset table's space, dead after the input gradient (in_bn implies has_gin);
@@ -1094,21 +1170,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
     PHASE(0);
     float* const ws = pin(c.ws);
     const float* const params = pin(c.params);
-    const float* const zero = pin(G.zero);
+    const float* const zero = pin(Gt.zero);
     const int64_t w_off = pin(d.w_off), gout_off = pin(d.gout_off), out_off = pin(d.out_off);
     const int64_t gin_off = pin(d.gin_off);
     // split launches: workgroups [0, nblocks) compute the input gradient (+ BN-backward sums, dgamma /
     // dbeta), [nblocks, 2 nblocks) the weight gradient of the same tiles
     // (xcd order: logical blocks 2t / 2t + 1 are tile t's two roles, on one XCD)
     const int lb = logical_block(G);
-    const bool wg_role = G.split && (G.xcd ? (lb & 1) != 0 : lb >= G.nblocks);
+    const bool wg_role = Gt.split && (Gt.xcd ? (lb & 1) != 0 : lb >= Gt.nblocks);
     const bool dg_role = !wg_role;
     // wpart_off < 0: input gradient only (no weight / gamma / beta gradient, no slab row): callers that
     // discard the shared-weight gradients (the PredictionEnsemble's decoder passes)
     const bool wout = d.wpart_off >= 0;
-    const bool do_wgrad = (!G.split || wg_role) && wout;
-    const int tile = !G.split ? lb : (G.xcd ? lb >> 1 : (wg_role ? lb - G.nblocks : lb));
-    const TileIdx T = tile_of(G, c.groups, tile);
+    const bool do_wgrad = (!Gt.split || wg_role) && wout;
+    const int tile = !Gt.split ? lb : (Gt.xcd ? lb >> 1 : (wg_role ? lb - Gt.nblocks : lb));
+    const TileIdx T = tile_of(Gt, c.groups, tile);
     const int HWi = d.h_in * d.w_in, HWo = d.h_out * d.w_out;
     const float* ib = input_base(d, c, T.b);
     PHASE(1);
@@ -1142,7 +1218,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
         });
     PHASE(12);
     int gy0, gh_;
-    g_rows(K, S, d.pad, T.oy0, G.th, gy0, gh_);
+    g_rows(K, S, d.pad, T.oy0, Gt.th, gy0, gh_);
     const int64_t gbase = ((int64_t)T.b * d.out_ctot + d.out_c0) * HWo;
     // FUSE: the Gaussian target of this thread's first forward item (column x, RPF rows), loaded with the
     // operand images into registers (one global round trip less inside the loss phase)
@@ -1153,25 +1229,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
         int trow0 = T.b - karg_sel(c.groups.start, T.grp);
         if (const int32_t* ti = karg_sel(c.tgt_idx, T.grp)) trow0 = ti[trow0];
         tg = karg_sel(c.tgt, T.grp) + (int64_t)trow0 * HWo;
-        const int nitem = ((G.gh + RPF - 1) / RPF) * d.w_out;
-        const int rg = dq(tid, G.d_wout), x = tid - rg * d.w_out;
+        const int nitem = ((Gt.gh + RPF - 1) / RPF) * d.w_out;
+        const int rg = dq(tid, Gt.d_wout), x = tid - rg * d.w_out;
 #pragma unroll
         for (int p = 0; p < RPF; ++p) {
             const int oy = gy0 + rg * RPF + p;
-            const bool ok = tid < nitem && rg * RPF + p < G.gh && oy >= 0 && oy < d.h_out;
+            const bool ok = tid < nitem && rg * RPF + p < Gt.gh && oy >= 0 && oy < d.h_out;
             tv0[p] = *as_gld(ok ? tg + oy * d.w_out + x : zero);
         }
     } else {
-        stage_img(gl, d.cout, G.gh, G.PG, G.d_g4, G.d_PG4, G.g_sq, G.g_sr, G.g_sc, gy0, d.h_out, d.w_out, zero,
+        stage_img(gl, d.cout, Gt.gh, Gt.PG, Gt.d_g4, Gt.d_PG4, Gt.g_sq, Gt.g_sr, Gt.g_sc, gy0, d.h_out, d.w_out, zero,
                   [&](int q) -> const float* { return ws + gout_off + gbase + (int64_t)q * HWo; });
     }
     PHASE(13);
     f32x4 zr[ZREG];           // zreg: this thread's chunks tid + 256 u of the z image
     if (obn && zreg) {
-        const int P4 = G.PG >> 2, plane4 = G.gh * P4, total = d.cout * plane4;
+        const int P4 = Gt.PG >> 2, plane4 = Gt.gh * P4, total = d.cout * plane4;
         const int c4lo = HALO / 4, c4hi = HALO / 4 + d.w_out / 4;
         ChunkIter it;
-        it.init(tid, plane4, P4, G.d_g4, G.d_PG4);
+        it.init(tid, plane4, P4, Gt.d_g4, Gt.d_PG4);
 #pragma unroll
         for (int u = 0; u < ZREG; ++u) {
             const int row = gy0 + it.r;
@@ -1179,30 +1255,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
             const float* src = ok ? ws + out_off + gbase + (int64_t)it.q * HWo + row * d.w_out + 4 * (it.c4 - c4lo)
                                   : zero;
             zr[u] = *as_gld((const f32x4*)src);
-            it.step(G.g_sq, G.g_sr, G.g_sc, P4, G.gh);
+            it.step(Gt.g_sq, Gt.g_sr, Gt.g_sc, P4, Gt.gh);
         }
     } else if (obn) {
-        stage_img(gz, d.cout, G.gh, G.PG, G.d_g4, G.d_PG4, G.g_sq, G.g_sr, G.g_sc, gy0, d.h_out, d.w_out, zero,
+        stage_img(gz, d.cout, Gt.gh, Gt.PG, Gt.d_g4, Gt.d_PG4, Gt.g_sq, Gt.g_sr, Gt.g_sc, gy0, d.h_out, d.w_out, zero,
                   [&](int q) -> const float* { return ws + out_off + gbase + (int64_t)q * HWo; });
     }
     PHASE(14);
     int iy0, rh_;
-    in_rows(K, S, UP, d.pad, T.oy0, G.th, iy0, rh_);
+    in_rows(K, S, UP, d.pad, T.oy0, Gt.th, iy0, rh_);
     const int iyA = FUSE ? iy0 - K / 2 : iy0;        // first row of the LDS input image
-    stage_img(al, d.cin, G.rh, G.P, G.d_in4, G.d_P4, G.in_sq, G.in_sr, G.in_sc, iyA, d.h_in, d.w_in, zero,
+    stage_img(al, d.cin, Gt.rh, Gt.P, Gt.d_in4, Gt.d_P4, Gt.in_sq, Gt.in_sr, Gt.in_sc, iyA, d.h_in, d.w_in, zero,
               [&](int q) -> const float* { return ib + (int64_t)q * HWi; });
     PHASE(8);
     // input-gradient epilogue operand (previous S_in, when accumulating) of this wave's first
     // four pixel blocks: lane (kq, l16) owns channel l16 at the 4 consecutive pixels
     // 16 m + 4 kq + [0, 4).  The input itself is read back from the LDS image.
     int py0, ph_;
-    owned_rows(S, UP, T.oy0, G.th, py0, ph_);
+    owned_rows(S, UP, T.oy0, Gt.th, py0, ph_);
     // cin <= 4 at stride 1: the input gradient runs on the VALU (phase 4b'), the MFMA form would
     // leave >= 3/4 of its N = 16 columns empty
     // (FUSE: always the VALU input gradient -- launch() checks cin <= 4 -- so the MFMA input-gradient
     // path and its operand registers compile away)
     const bool vdg = vop && dg_role;     // (launch() never splits a vop op: dg_role holds)
-    const int nmblk = (!FUSE && has_gin && dg_role && !vdg && !SKIP(G, 2)) ? (G.ph * d.w_in) >> 4 : 0;
+    const int nmblk = (!FUSE && has_gin && dg_role && !vdg && !SKIP(G, 2)) ? (Gt.ph * d.w_in) >> 4 : 0;
     const int ci_l = min(l16, d.cin - 1);
     const bool cok = l16 < d.cin;
     const int64_t ibase = ((int64_t)T.b * d.in_ctot + d.in_c0 + ci_l) * HWi + (int64_t)py0 * d.w_in;
@@ -1267,7 +1343,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
     PHASE(3);
 
     // ---- phase 3: activations in LDS; offset table of the input-gradient reduction
-    if (d.in_bn) activate_img(al, G, d, iyA, i_sc, i_sh);
+    if (d.in_bn) activate_img(al, Gt, d, iyA, i_sc, i_sh);
     if (has_gin && dg_role && S == 2) {
         // input pixel (py, px) = (py0 + 2a + ry, 2b + rx) receives output (oy, ox) through tap (ky, kx)
         // iff 2 oy = py + pad - ky, 2 ox = px + pad - kx: the valid taps depend on the parity class
@@ -1282,7 +1358,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
             if (k < d.cout * nky * nkx) {
                 const int co = k / (nky * nkx), r = k - co * nky * nkx, jy = r / nkx, jx = r - jy * nkx;
                 const int ky = ky0 + 2 * jy, kx = kx0 + 2 * jx;
-                oa = co * gplane + ((ry + d.pad - ky) >> 1) * G.PG + ((rx + d.pad - kx) >> 1);
+                oa = co * gplane + ((ry + d.pad - ky) >> 1) * Gt.PG + ((rx + d.pad - kx) >> 1);
                 ob = co * KK + ky * K + kx;
             }
             ktab[cls * 2 * KD4 + k] = oa;
@@ -1297,18 +1373,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
             int o = 0;
             if (k < KD) {
                 const int co = k / KK, tap = k - co * KK, ky = tap / K, kx = tap - ky * K;
-                o = co * gplane + (ry0 - ky) * G.PG + d.pad - kx + HALO;
+                o = co * gplane + (ry0 - ky) * Gt.PG + d.pad - kx + HALO;
             }
             ktab[k] = o;
         }
     }
     if (obn && zreg) {
         // BN-backward of the output gradient with z from registers: chunk tid + 256 u
-        const int P4 = G.PG >> 2, plane4 = G.gh * P4, total = d.cout * plane4;
+        const int P4 = Gt.PG >> 2, plane4 = Gt.gh * P4, total = d.cout * plane4;
         const int c4lo = HALO / 4, c4hi = HALO / 4 + d.w_out / 4;
         float4* g4 = reinterpret_cast<float4*>(gl);
         ChunkIter it;
-        it.init(tid, plane4, P4, G.d_g4, G.d_PG4);
+        it.init(tid, plane4, P4, Gt.d_g4, Gt.d_PG4);
 #pragma unroll
         for (int u = 0; u < ZREG; ++u) {
             const int e = tid + 256 * u;
@@ -1326,15 +1402,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
                 o.w = ds * ((sv.w - mS - ((zv[3] - m) * inv) * mSx) * inv);
                 g4[e] = o;
             }
-            it.step(G.g_sq, G.g_sr, G.g_sc, P4, G.gh);
+            it.step(Gt.g_sq, Gt.g_sr, Gt.g_sc, P4, Gt.gh);
         }
     } else if (obn) {
-        const int P4 = G.PG >> 2, plane4 = G.gh * P4, total = d.cout * plane4;
+        const int P4 = Gt.PG >> 2, plane4 = Gt.gh * P4, total = d.cout * plane4;
         const int c4lo = HALO / 4, c4hi = HALO / 4 + d.w_out / 4;
         float4* g4 = reinterpret_cast<float4*>(gl);
         const float4* z4 = reinterpret_cast<const float4*>(gz);
         ChunkIter it;
-        it.init(tid, plane4, P4, G.d_g4, G.d_PG4);
+        it.init(tid, plane4, P4, Gt.d_g4, Gt.d_PG4);
         for (int e0 = tid; e0 < total; e0 += 512) {
             float4 sv[2], zv[2];
             bool ok[2];
@@ -1348,7 +1424,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
                     sv[u] = g4[e0 + 256 * u];
                     zv[u] = z4[e0 + 256 * u];
                 }
-                it.step(G.g_sq, G.g_sr, G.g_sc, P4, G.gh);
+                it.step(Gt.g_sq, Gt.g_sr, Gt.g_sc, P4, Gt.gh);
             }
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
@@ -1368,10 +1444,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
     }
     if (!obn && drop) {
         // direct output gradient: scale by the dropout mask (halo / margin zeros stay zero)
-        const int plane4 = G.gh * (G.PG >> 2), total = d.cout * plane4;
+        const int plane4 = Gt.gh * (Gt.PG >> 2), total = d.cout * plane4;
         float4* g4 = reinterpret_cast<float4*>(gl);
         for (int e = tid; e < total; e += 256) {
-            const float ds = o_drop[dq(e, G.d_g4)];
+            const float ds = o_drop[dq(e, Gt.d_g4)];
             float4 v = g4[e];
             v.x *= ds;
             v.y *= ds;
@@ -1397,7 +1473,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
         // 256-B LDS row per read, no bank conflicts) and serve the RPF x K taps.  The weights: a tap's
         // (co 0, co 1) pair by one broadcast ds_read_b64 (fuse_wlds, the default for every tap) or, for
         // taps left to the VALU, by two v_readlane from wr[] (lane l holds WF[64 j + l])
-        const int nrg = (G.gh + RPF - 1) / RPF, nitem = nrg * d.w_out;
+        const int nrg = (Gt.gh + RPF - 1) / RPF, nitem = nrg * d.w_out;
         auto fwd_items = [&](auto ci_c) {
             constexpr int CIN = decltype(ci_c)::value;
             constexpr int NWR = (CIN * KK * 2 + 63) / 64;
@@ -1405,13 +1481,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
 #pragma unroll
             for (int j = 0; j < NWR; ++j) wr[j] = mid[256 + 64 * j + lane];
             for (int it = tid; it < nitem; it += 256) {
-                const int rg = dq(it, G.d_wout), x = it - rg * d.w_out;
+                const int rg = dq(it, Gt.d_wout), x = it - rg * d.w_out;
                 const int j0 = rg * RPF;
                 float tv[RPF];
 #pragma unroll
                 for (int p = 0; p < RPF; ++p) {
                     const int oy = gy0 + j0 + p;
-                    const bool ok = j0 + p < G.gh && oy >= 0 && oy < d.h_out;
+                    const bool ok = j0 + p < Gt.gh && oy >= 0 && oy < d.h_out;
                     tv[p] = it == tid ? tv0[p] : (ok ? as_gld(tg)[oy * d.w_out + x] : 0.f);
                 }
                 f32x2 acc[RPF];
@@ -1420,12 +1496,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
 #pragma unroll
                 for (int ci = 0; ci < CIN; ++ci) {
                     if (ci >= d.cin) break;
-                    const float* acol = al + ci * G.rh * G.P + HALO + x - PADK;
+                    const float* acol = al + ci * Gt.rh * Gt.P + HALO + x - PADK;
 #pragma unroll
                     for (int kx = 0; kx < K; ++kx) {
                         float v[RPF + K - 1];
 #pragma unroll
-                        for (int r = 0; r < RPF + K - 1; ++r) v[r] = acol[min(j0 + r, G.rh - 1) * G.P + kx];
+                        for (int r = 0; r < RPF + K - 1; ++r) v[r] = acol[min(j0 + r, Gt.rh - 1) * Gt.P + kx];
                         f32x2 w[K];
 #pragma unroll
                         for (int ky = 0; ky < K; ++ky) {
@@ -1455,14 +1531,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
 #pragma unroll
                 for (int p = 0; p < RPF; ++p) {
                     const int j = j0 + p, oy = gy0 + j;
-                    if (j >= G.gh || oy < 0 || oy >= d.h_out) continue;
-                    const bool own = j >= PADK && j < PADK + G.th;
+                    if (j >= Gt.gh || oy < 0 || oy >= d.h_out) continue;
+                    const bool own = j >= PADK && j < PADK + Gt.th;
                     const float mu = acc[p][0], ls = acc[p][1];
                     const float e = expf(-2.f * ls);
                     const float emu = ex ? expf(mu) : 1.f;
                     const float r = ex ? expf(tv[p]) - emu : tv[p] - mu;
                     if (own) Lv += -0.5f * (2.f * ls + r * r * e + GPI_LOG2PI);
-                    float* g0 = gl + j * G.PG + HALO + x;
+                    float* g0 = gl + j * Gt.PG + HALO + x;
                     g0[0] = -scl * r * e * emu;
                     g0[gplane] = scl * (1.f - r * r * e);
                 }
@@ -1487,7 +1563,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
     // this wave's partial-slab row: [dW partial over the wave's output rows | dgamma | dbeta partials]
     // (vop: in LDS, summed below into the tile's one slab row)
     float* slab = vop ? mid + 512 + wv * rowlen : c.wpart + d.wpart_off + ((int64_t)tile * SLAB_ROWS + wv) * rowlen;
-    const bool lsum = !vop && G.lsum;   // (lsum_op: never with vwg; at most 2 x 2 accumulator blocks)
+    const bool lsum = !vop && Gt.lsum;   // (lsum_op: never with vwg; at most 2 x 2 accumulator blocks)
     f32x4 hold[2][2];                   // lsum: this wave's weight-gradient blocks [mb][column block]
     // single-channel 7x7 / stride-2 input conv: weight gradient with the reduction over the tile's
     // output pixels (M = cout, N = the 49 taps in 4 column blocks, K = pixels), no zero-interleaved
@@ -1499,34 +1575,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
         if constexpr (K == 7 && S == 2 && !UP) {
             if (vwg && !SKIP(G, 1)) {
                 constexpr int PADC = K / 2, NB = (KK + 15) / 16;
-                const int tp = G.th * d.w_out;
+                const int tp = Gt.th * d.w_out;
                 const int co_a = min(l16, d.cout - 1);                  // A row (rows >= cout never stored)
                 int tap_off[NB];                                        // B column: tap (ky, kx) of this lane
     #pragma unroll
                 for (int nb = 0; nb < NB; ++nb) {
                     const int j = min(16 * nb + l16, KK - 1), ky = j / K, kx = j - ky * K;
-                    tap_off[nb] = ky * G.P + kx - PADC;
+                    tap_off[nb] = ky * Gt.P + kx - PADC;
                 }
                 f32x4 acc[NB];
     #pragma unroll
                 for (int nb = 0; nb < NB; ++nb) acc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
-                const float* gco = gl + co_a * gplane + (T.oy0 - gy0) * G.PG + HALO;
+                const float* gco = gl + co_a * gplane + (T.oy0 - gy0) * Gt.PG + HALO;
                 for (int ps = wv; 4 * ps < tp; ps += 4) {               // 4 output pixels per step, wave-strided
                     const int px = 4 * ps + kq;
-                    const int ty = dq(px, G.d_wout), ox = px - ty * d.w_out;
-                    const float a = gco[ty * G.PG + ox];
-                    const float* xb = alb + (ty * S) * G.P + HALO + S * ox;
+                    const int ty = dq(px, Gt.d_wout), ox = px - ty * d.w_out;
+                    const float a = gco[ty * Gt.PG + ox];
+                    const float* xb = alb + (ty * S) * Gt.P + HALO + S * ox;
                     float bv[NB];
     #pragma unroll
                     for (int nb = 0; nb < NB; ++nb) bv[nb] = xb[tap_off[nb]];
     #pragma unroll
                     for (int nb = 0; nb < NB; ++nb) acc[nb] = mfma4(a, bv[nb], acc[nb]);
                 }
-                // G.vsum: the four waves' tiles summed in LDS (the gradient image, dead after the loop)
+                // Gt.vsum: the four waves' tiles summed in LDS (the gradient image, dead after the loop)
                 // into ONE slab row per tile -- a quarter of the slab bytes the reduction reads, on the
                 // step's critical path at its end; otherwise each wave stores its own row
-                float* const wrow = G.vsum ? gl + wv * rowlen : slab;
-                if (G.vsum) __syncthreads();        // every wave is done reading gl
+                float* const wrow = Gt.vsum ? gl + wv * rowlen : slab;
+                if (Gt.vsum) __syncthreads();        // every wave is done reading gl
     #pragma unroll
                 for (int nb = 0; nb < NB; ++nb) {
     #pragma unroll
@@ -1535,7 +1611,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
                         if (co2 < d.cout && j2 < KK) wrow[co2 * J + j2] = acc[nb][r];
                     }
                 }
-                if (G.vsum) {
+                if (Gt.vsum) {
                     __syncthreads();
                     float* srow = c.wpart + d.wpart_off + (int64_t)tile * rowlen;
                     for (int e = tid; e < d.cout * J; e += 256) {
@@ -1568,13 +1644,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
                     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
                     auto rows = [&](auto two_c) {
                         constexpr bool TWO = decltype(two_c)::value;
-                        for (int ty = wv; ty < G.th; ty += 4) {
-                            const float* grow = gl + (co * G.gh + (T.oy0 + ty - gy0)) * G.PG + HALO - kx;
+                        for (int ty = wv; ty < Gt.th; ty += 4) {
+                            const float* grow = gl + (co * Gt.gh + (T.oy0 + ty - gy0)) * Gt.PG + HALO - kx;
                             const float* brow[2];
     #pragma unroll
                             for (int u = 0; u < 2; ++u) {
                                 const int ry = UP ? fdiv2(T.oy0 + ty - d.pad + ky[u]) - iy0 : ty * S + ky[u];
-                                brow[u] = alb + (ci[u] * G.rh + ry) * G.P + HALO;
+                                brow[u] = alb + (ci[u] * Gt.rh + ry) * Gt.P + HALO;
                             }
                             // operands of four steps are read before their MFMAs (LDS read -> dependent
                             // MFMA would serialise every step)
@@ -1675,8 +1751,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
     };
     // fuse_alt: which workgroups take the weight gradient last -- blocks of one CU are (roughly) those
     // the XCD's dispatcher deals it 32 apart: bit 8 of the block index alternates among them
-    const int bsel = G.alt == 1 ? (int)(blockIdx.x >> 8) : G.alt == 2 ? (int)(blockIdx.x >> 3) : (int)blockIdx.x;
-    const bool wg_late = FUSE && G.alt != 0 && (bsel & 1) != 0;
+    const int bsel = Gt.alt == 1 ? (int)(blockIdx.x >> 8) : Gt.alt == 2 ? (int)(blockIdx.x >> 3) : (int)blockIdx.x;
+    const bool wg_late = FUSE && Gt.alt != 0 && (bsel & 1) != 0;
     if (vop && !wg_late) wgrad_phase();
     PHASE(5);
 
@@ -1690,7 +1766,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
             l_bet = i_sh[ci_l] + i_mean[ci_l] * i_sc[ci_l];     // beta
             l_rgam = 1.f / l_gam;
         }
-        const float* arow0 = alb + (ci_l * G.rh + (py0 - iy0)) * G.P + HALO;   // owned row 0 of channel l16
+        const float* arow0 = alb + (ci_l * Gt.rh + (py0 - iy0)) * Gt.P + HALO;   // owned row 0 of channel l16
         const int nkd = KD4 >> 2;
         for (int round = 0; wv + 16 * round < nmblk; ++round) {
             if (round > 0 && S != 2) own_load(round);
@@ -1699,7 +1775,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
                 const int m = wv + 4 * (4 * round + u);
                 if (m < nmblk) {
                     const int i = 16 * m + l16;                   // owned pixel of this lane's A row
-                    const int qy = dq(i, G.d_win), px = i - qy * d.w_in;
+                    const int qy = dq(i, Gt.d_win), px = i - qy * d.w_in;
                     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
                     if (S == 2) {
                         // parity-class blocks: block m covers 16 consecutive pixels (a, b) of class
@@ -1709,8 +1785,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
                         const int ry = cls >> 1, rx = cls & 1;
                         const int nky = (K - ((ry + d.pad) & 1) + 1) >> 1, nkx = (K - ((rx + d.pad) & 1) + 1) >> 1;
                         const int nk = d.cout * nky * nkx;
-                        const int cp = 16 * mb + l16, a2 = dq(cp, G.d_w2), b2 = cp - a2 * (d.w_in >> 1);
-                        const float* ab = gl + ((py0 >> 1) - gy0 + a2) * G.PG + b2 + HALO;
+                        const int cp = 16 * mb + l16, a2 = dq(cp, Gt.d_w2), b2 = cp - a2 * (d.w_in >> 1);
+                        const float* ab = gl + ((py0 >> 1) - gy0 + a2) * Gt.PG + b2 + HALO;
                         const int* tA = ktab + cls * 2 * KD4;
                         const int* tB = tA + KD4;
                         for (int ks = 0; 4 * ks < nk; ++ks) {
@@ -1719,10 +1795,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
                             acc = mfma4(a, wD[tB[k] * 16 + l16], acc);
                         }
                     } else {
-                        const float* gp0 = gl + (UP ? 2 * (qy * G.PG + px) : qy * G.PG + px);
+                        const float* gp0 = gl + (UP ? 2 * (qy * Gt.PG + px) : qy * Gt.PG + px);
                         auto aval = [&](int k) -> float {
                             const float* ga = gp0 + ktab[k];
-                            return UP ? (ga[0] + ga[1]) + (ga[G.PG] + ga[G.PG + 1]) : ga[0];
+                            return UP ? (ga[0] + ga[1]) + (ga[Gt.PG] + ga[Gt.PG + 1]) : ga[0];
                         };
                         int ks = 0;
                         for (; ks + 4 <= nkd; ks += 4) {   // operands of four steps before their MFMAs
@@ -1744,7 +1820,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
                     if (cok && S == 2) {
                         const int nbc = nmblk >> 2, cls = m / nbc, mb = m - cls * nbc;
                         const int ry = cls >> 1, rx = cls & 1;
-                        const int cp0 = 16 * mb + 4 * kq, a2 = dq(cp0, G.d_w2), b2 = cp0 - a2 * (d.w_in >> 1);
+                        const int cp0 = 16 * mb + 4 * kq, a2 = dq(cp0, Gt.d_w2), b2 = cp0 - a2 * (d.w_in >> 1);
                         const int qy = 2 * a2 + ry;
 #pragma unroll
                         for (int q = 0; q < 4; ++q) {
@@ -1753,7 +1829,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
                             const float pa = d.gin_accumulate ? *as_gld(ws + gin_off + go) : 0.f;
                             float o;
                             if (d.in_bn) {
-                                const float av = arow0[qy * G.P + px];
+                                const float av = arow0[qy * Gt.P + px];
                                 const float dbn = av > 0.f ? acc[q] : 0.f;
                                 o = pa + l_gam * dbn;
                                 sd += dbn;
@@ -1766,8 +1842,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
                     } else if (cok) {
                         float* gp = ws + gin_off + ibase + 16 * m + 4 * kq;
                         const int i0 = 16 * m + 4 * kq;
-                        const int qy0 = dq(i0, G.d_win), px0 = i0 - qy0 * d.w_in;
-                        const f32x4 av = *(const f32x4*)(arow0 + qy0 * G.P + px0);
+                        const int qy0 = dq(i0, Gt.d_win), px0 = i0 - qy0 * d.w_in;
+                        const f32x4 av = *(const f32x4*)(arow0 + qy0 * Gt.P + px0);
                         const float pa[4] = {pv4[u][0], pv4[u][1], pv4[u][2], pv4[u][3]};
                         float o[4];
 #pragma unroll
@@ -1812,9 +1888,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
             float wb[NWB];
     #pragma unroll
             for (int j = 0; j < NWB; ++j) wb[j] = mid[64 * j + lane];
-            const int npq = (G.ph * d.w_in) / Q;
+            const int npq = (Gt.ph * d.w_in) / Q;
             for (int gq = tid; gq < npq; gq += 256) {
-                const int qy = dq(Q * gq, G.d_win), px0 = Q * gq - qy * d.w_in;
+                const int qy = dq(Q * gq, Gt.d_win), px0 = Q * gq - qy * d.w_in;
                 const int64_t pix = (int64_t)(py0 + qy) * d.w_in + px0;
                 const int64_t gbase_in = ((int64_t)T.b * d.in_ctot + d.in_c0) * HWi + pix;
                 f32x2 acc2[CH][Q];
@@ -1827,7 +1903,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
                     if (co >= d.cout) break;
     #pragma unroll
                     for (int ky = 0; ky < K; ++ky) {
-                        const float* grow = gl + co * gplane + (qy + py0 + d.pad - ky - gy0) * G.PG + HALO + px0 +
+                        const float* grow = gl + co * gplane + (qy + py0 + d.pad - ky - gy0) * Gt.PG + HALO + px0 +
                                             d.pad - (K - 1);
                         float gw[K + Q - 1];
                         if constexpr (Q == 4) {
@@ -1870,7 +1946,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
     #pragma unroll
                 for (int ci = 0; ci < CI; ++ci) {
                     if (ci >= d.cin) break;
-                    const float* ap = alb + (ci * G.rh + (py0 - iy0 + qy)) * G.P + HALO + px0;
+                    const float* ap = alb + (ci * Gt.rh + (py0 - iy0 + qy)) * Gt.P + HALO + px0;
                     float av[Q], pv[Q], o[Q];
     #pragma unroll
                     for (int q = 0; q < Q; ++q) {
@@ -1982,8 +2058,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
             lrow[d.cout * J + d.cin + l16] = sd;      // dbeta partial
         }
         __syncthreads();
-        const int c0 = (G.split && !do_wgrad) ? d.cout * J : 0;
-        const int c1 = !wout ? 0 : ((G.split && !dg_role) ? d.cout * J : rowlen);
+        const int c0 = (Gt.split && !do_wgrad) ? d.cout * J : 0;
+        const int c1 = !wout ? 0 : ((Gt.split && !dg_role) ? d.cout * J : rowlen);
         float* srow = c.wpart + d.wpart_off + (int64_t)tile * rowlen;
         for (int e = c0 + tid; e < c1; e += 256) {
             const float* r = wD + e;
@@ -2059,8 +2135,8 @@ conv_kernel_t pick_cp(int cp) {
 }
 
 template <int K, int S, int UP>
-conv_kernel_t pick(int cp, bool fwd, int npx) {
-    if (!fwd) return conv_bwd_kernel<K, S, UP>;
+conv_kernel_t pick(int cp, bool fwd, int npx, bool half) {
+    if (!fwd) return half ? conv_bwd_kernel<K, S, UP, false, true> : conv_bwd_kernel<K, S, UP>;
     if (npx == 4) return pick_cp<K, S, UP, 4>(cp);
     if (npx == 2) return pick_cp<K, S, UP, 2>(cp);
     if constexpr (!UP && K <= 3) {   // channel-group instantiation: the small-plane codec convs only
@@ -2069,15 +2145,15 @@ conv_kernel_t pick(int cp, bool fwd, int npx) {
     return pick_cp<K, S, UP, 1>(cp);
 }
 
-conv_kernel_t select_kernel(const gpi_conv_desc& d, int cp, bool fwd, int npx) {
+conv_kernel_t select_kernel(const gpi_conv_desc& d, int cp, bool fwd, int npx, bool half) {
     const int key = d.k * 100 + d.stride * 10 + d.upsample;
     switch (key) {
-        case 110: return pick<1, 1, 0>(cp, fwd, npx);
-        case 310: return pick<3, 1, 0>(cp, fwd, npx);
-        case 311: return pick<3, 1, 1>(cp, fwd, npx);
-        case 320: return pick<3, 2, 0>(cp, fwd, npx);
-        case 510: return pick<5, 1, 0>(cp, fwd, npx);
-        case 720: return pick<7, 2, 0>(cp, fwd, npx);
+        case 110: return pick<1, 1, 0>(cp, fwd, npx, half);
+        case 310: return pick<3, 1, 0>(cp, fwd, npx, half);
+        case 311: return pick<3, 1, 1>(cp, fwd, npx, half);
+        case 320: return pick<3, 2, 0>(cp, fwd, npx, half);
+        case 510: return pick<5, 1, 0>(cp, fwd, npx, half);
+        case 720: return pick<7, 2, 0>(cp, fwd, npx, half);
         default: return nullptr;
     }
 }
@@ -2111,9 +2187,11 @@ bool aligned_ok(const gpi_conv_desc& d, const gpi_codec_ctx& c, bool fwd) {
 // 1.03x) at unchanged forward and fused launch times, but several backward launches ran 0.6-2.2 us
 // slower (step 0.635 vs 0.625 ms, r03x).  Default 9 (forward + fused): 0.6233 / 0.6219 ms vs 0.6232 /
 // 0.6228 with the fused conv alone and 0.6277 / 0.6250 with the non-split backwards too (r03y).
-bool xcd_mode(bool fwd, bool fuse, bool split) {
+bool xcd_mode(bool fwd, bool fuse, bool split, bool half) {
     static const int mode = env_int("GPI_XCD_MODE", 9);
-    return (mode & (fuse ? 8 : fwd ? 1 : split ? 4 : 2)) != 0;
+    // (a launch with half tiles keeps the dispatch order: the XCD-consecutive order would put every half
+    // tile on the last XCDs -- 0.5714-0.5722 vs 0.5694-0.5709 ms for the fused output conv, r04t)
+    return !half && (mode & (fuse ? 8 : fwd ? 1 : split ? 4 : 2)) != 0;
 }
 
 int launch(const gpi_conv_desc& d, const gpi_codec_ctx& c, hipStream_t st, bool fwd, bool fuse = false,
@@ -2133,8 +2211,8 @@ int launch(const gpi_conv_desc& d, const gpi_codec_ctx& c, hipStream_t st, bool 
     if (!fwd && d.gin_off >= 0 && ((G.ph * d.w_in) & 15)) return GPI_ERR_UNSUPPORTED;
     if (!fwd && d.gin_off >= 0 && d.stride == 2 && ((d.w_in & 7) || (G.ph & 1))) return GPI_ERR_UNSUPPORTED;
     const int cp = cp_of(d);
-    conv_kernel_t k = fuse ? conv_bwd_kernel<5, 1, 0, true>
-                           : select_kernel(d, cp, fwd, G.cg > 1 ? 0 : G.npx);
+    conv_kernel_t k = fuse ? (G.nfull < G.nblocks ? conv_bwd_kernel<5, 1, 0, true, true> : conv_bwd_kernel<5, 1, 0, true>)
+                           : select_kernel(d, cp, fwd, G.cg > 1 ? 0 : G.npx, G.nfull < G.nblocks);
     if (!k) return GPI_ERR_UNSUPPORTED;
     static const float* zero = nullptr;
     if (!zero) {
@@ -2157,7 +2235,7 @@ int launch(const gpi_conv_desc& d, const gpi_codec_ctx& c, hipStream_t st, bool 
     }
     const int grid = G.nblocks * (G.split ? 2 : 1);
     G.grid = grid;
-    G.xcd = xcd_mode(fwd, fuse, G.split != 0) ? 1 : 0;
+    G.xcd = xcd_mode(fwd, fuse, G.split != 0, G.nfull < G.nblocks) ? 1 : 0;
     // r04l (2 x 400 steps per arm, one box): 1 -> 0.5761 / 0.5759, off 0.5768 / 0.5773, 2 -> 0.5773 / 0.5777,
     // 3 -> 0.5776 / 0.5770 ms per step
     static const int fuse_alt = env_int("GPI_FUSE_ALT", 1);

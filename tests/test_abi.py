@@ -59,7 +59,13 @@ def test_conv_blocks_host_query(lib):
     g.start[0], g.start[1] = 0, 288
     nb = C.c_int32()
     assert L.gpi_conv_blocks(C.byref(d), C.byref(g), C.byref(nb)) == 0
-    assert nb.value == 288 * 4 * 4      # full-width tiles of 8 rows on a 32 x 32 plane, one slab row per wave
+    # full-width tiles of 8 rows on a 32 x 32 plane, one slab row per wave; the 1152 tiles are no multiple of
+    # the 256 CUs, so the samples past the first 1024 tiles (256..287) take half-height tiles (GPI_HALF_TILES)
+    assert nb.value == (256 * 4 + 32 * 8) * 4
+    g.start[1] = 256                    # 1024 tiles: no half tiles
+    assert L.gpi_conv_blocks(C.byref(d), C.byref(g), C.byref(nb)) == 0
+    assert nb.value == 256 * 4 * 4
+    g.start[1] = 288
     d.k = 4                             # unsupported kernel size -> error code, no crash
     assert L.gpi_conv_blocks(C.byref(d), C.byref(g), C.byref(nb)) != 0
 
