@@ -313,8 +313,9 @@ bool conv_geom(const gpi_conv_desc& d, const gpi_groups& g, ConvGeom& G, bool fw
     // op's backward only, 2 every backward launch)
     static const int half_tiles = env_int("GPI_HALF_TILES", 2);
     const int tot = B * G.tiles, base = tot & ~255;
-    if (half_tiles && !fwd && (half_tiles > 1 || loss_bwd) && (G.th & 1) == 0 && base > 0 && tot != base &&
-        base % G.tiles == 0) {
+    static const int half_fwd = env_int("GPI_HALF_FWD", 1);
+    if (half_tiles && (fwd ? half_fwd && half_tiles > 1 && G.cg == 1 : (half_tiles > 1 || loss_bwd)) &&
+        (G.th & 1) == 0 && base > 0 && tot != base && base % G.tiles == 0) {
         ConvGeom::Alt& a = G.ha;
         a.th = G.th / 2;
         int y0;
@@ -691,12 +692,23 @@ __device__ __forceinline__ void store_px(float* p, const float (&v)[NPX]) {
 // header floats: gst fp64 [4*MAX_CIN] | sc | sh [MAX_CIN] | scratch [64] | red [16] | dropout scales [8]
 constexpr int FWD_HDR = 8 * GPI_MAX_CIN + 2 * GPI_MAX_CIN + 64 + 16 + 8;
 
-template <int K, int S, int UP, int CP, int NPX>
+template <int K, int S, int UP, int CP, int NPX, bool HALF = false>
 // (the channel-group instantiation NPX == 0 runs one workgroup per CU: no occupancy target)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NPX == 0 ? 1 : 5))) void conv_fwd_kernel(gpi_conv_desc d, gpi_codec_ctx c, ConvGeom G) {
     touch_kernargs<CONV_KARG_BYTES>();
     entry_signal(G);
     if (SKIP(G, 16)) return;
+    // the tile's geometry: the launch's, or the half-height one (HALF instantiation, GPI_HALF_TILES)
+    ConvGeom Gt_;
+    if constexpr (HALF) {
+        Gt_ = G;
+        if (logical_block(G) >= G.nfull) {
+            const ConvGeom::Alt& a = G.ha;
+            Gt_.th = a.th; Gt_.rh = a.rh; Gt_.in_sq = a.in_sq; Gt_.in_sr = a.in_sr; Gt_.in_sc = a.in_sc;
+            Gt_.d_in4 = a.d_in4; Gt_.d_tp = a.d_tp;
+        }
+    }
+    const ConvGeom& Gt = HALF ? Gt_ : G;
     constexpr int KK = K * K;
     extern __shared__ __attribute__((aligned(16))) float smem[];
     double* gst = (double*)smem;
@@ -714,9 +726,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NPX == 0 ? 
     PHASE(0);
     float* const ws = pin(c.ws);
     const float* const params = pin(c.params);
-    const float* const zero = pin(G.zero);
+    const float* const zero = pin(Gt.zero);
     const int64_t w_off = pin(d.w_off);
-    const TileIdx T = tile_of(G, c.groups);
+    const TileIdx T = tile_of(Gt, c.groups);
     const int HWi = d.h_in * d.w_in, HWo = d.h_out * d.w_out;
     const float* ib = input_base(d, c, T.b);
     // Dropout2d after this conv: the sample's output-channel scales (0 or 1/(1-p)) into LDS (read by
@@ -730,8 +742,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NPX == 0 ? 
         return co < d.cout ? params + w_off + (int64_t)co * d.cin * KK + r : nullptr;
     });
     int iy0, rh_;
-    in_rows(K, S, UP, d.pad, T.oy0, G.th, iy0, rh_);
-    stage_img(img, d.cin, G.rh, G.P, G.d_in4, G.d_P4, G.in_sq, G.in_sr, G.in_sc, iy0, d.h_in, d.w_in, zero,
+    in_rows(K, S, UP, d.pad, T.oy0, Gt.th, iy0, rh_);
+    stage_img(img, d.cin, Gt.rh, Gt.P, Gt.d_in4, Gt.d_P4, Gt.in_sq, Gt.in_sr, Gt.in_sc, iy0, d.h_in, d.w_in, zero,
               [&](int q) -> const float* { return ib + (int64_t)q * HWi; });
     // (issued after the DMA; stored to LDS only after the stat loads are issued and waited for -- an
     // LDS store of it right here would drain every outstanding DMA first: one more round trip)
@@ -758,7 +770,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NPX == 0 ? 
         }
         __syncthreads();
         // ---- phase 3: BN + ReLU in LDS
-        activate_img(img, G, d, iy0, sc, sh);
+        activate_img(img, Gt, d, iy0, sc, sh);
     }
     if (drop && tid >= 64 && tid < 64 + d.cout) dsl[tid - 64] = dsv;
     __syncthreads();
@@ -768,7 +780,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NPX == 0 ? 
     // 256-wide upsampled planes, whose tiles pair output rows).  NPX > 1: NPX horizontally adjacent
     // pixels per thread; per (ci, ky) the thread reads the input row window the NPX x K taps cover
     // once into registers, and every weight vector read serves NPX pixels.
-    const int tp = G.th * d.w_out;
+    const int tp = Gt.th * d.w_out;
     float Lv = 0.f;
     float vst[2 * CP];
 #pragma unroll
@@ -782,7 +794,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NPX == 0 ? 
         for (int gbase = 0; gbase < ng; gbase += 256) {
             const int g = gbase + tid;
             const bool active = g < ng;
-            const int ty = dq(g * NPX, G.d_wout), x0 = g * NPX - ty * d.w_out;
+            const int ty = dq(g * NPX, Gt.d_wout), x0 = g * NPX - ty * d.w_out;
             const int oy = T.oy0 + ty;
             float acc[NPX][CP];
 #pragma unroll
@@ -790,7 +802,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NPX == 0 ? 
 #pragma unroll
                 for (int co = 0; co < CP; ++co) acc[p][co] = 0.f;
             if (active && !SKIP(G, 64)) {
-                const int plane = G.rh * G.P;
+                const int plane = Gt.rh * Gt.P;
                 const int cb = UP ? fdiv2(x0 - PADK) + HALO : x0 * S - PADK + HALO;
                 for (int ci = 0; ci < d.cin; ++ci) {
                     const float* tci = img + ci * plane + cb;
@@ -798,7 +810,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NPX == 0 ? 
 #pragma unroll
                     for (int ky = 0; ky < K; ++ky) {
                         const int ry = UP ? (fdiv2(oy - PADK + ky) - iy0) : (ty * S + ky);
-                        const float* trow = tci + ry * G.P;
+                        const float* trow = tci + ry * Gt.P;
                         float win[NW];
                         if constexpr (!UP && (NPX * S) % 4 == 0) {
                             // x0 * S is a multiple of 4: the window starts (HALO - K/2) mod 4 past a 16-B boundary
@@ -908,13 +920,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NPX == 0 ? 
             }
         }
     } else {
-        // NPX == 0: the channel-group instantiation (G.cg > 1), otherwise one group (folds away)
-        const int cg = NPX == 0 ? G.cg : 1;
+        // NPX == 0: the channel-group instantiation (Gt.cg > 1), otherwise one group (folds away)
+        const int cg = NPX == 0 ? Gt.cg : 1;
         for (int pbase = 0; pbase < tp; pbase += 256) {
             // cg > 1 (tp <= 128, one pass): thread = (channel group, pixel)
-            const int grp = NPX == 0 ? dq(tid, G.d_tp) : 0;
+            const int grp = NPX == 0 ? dq(tid, Gt.d_tp) : 0;
             const int pix = NPX == 0 ? tid - grp * tp : pbase + tid;
-            const int ty = dq(pix, G.d_wout), tx = pix - ty * d.w_out;
+            const int ty = dq(pix, Gt.d_wout), tx = pix - ty * d.w_out;
             const int oy = T.oy0 + ty, ox = tx;
             bool active = pix < tp && grp < cg;
             float tgt = 0.f;
@@ -928,7 +940,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NPX == 0 ? 
     #pragma unroll
             for (int co = 0; co < CP; ++co) acc[co] = 0.f;
             if (active && !SKIP(G, 64)) {
-                const int plane = G.rh * G.P;
+                const int plane = Gt.rh * Gt.P;
                 for (int ci = grp; ci < d.cin; ci += cg) {
                     const float* tci = img + ci * plane;
                     // the weight offset held in a VGPR: the uniform LDS reads then take one VGPR base with
@@ -939,7 +951,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NPX == 0 ? 
     #pragma unroll
                     for (int ky = 0; ky < K; ++ky) {
                         const int ry = UP ? (fdiv2(oy - d.pad + ky) - iy0) : (ty * S + ky);
-                        const float* trow = tci + ry * G.P;
+                        const float* trow = tci + ry * Gt.P;
     #pragma unroll
                         for (int kx = 0; kx < K; ++kx) {
                             const int col = UP ? fdiv2(ox - d.pad + kx) + HALO : ox * S - d.pad + kx + HALO;
@@ -950,7 +962,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NPX == 0 ? 
             }
             if (NPX == 0 && cg > 1) {
                 // channel-group partials [grp - 1][pix][CP] after the image; group 0 sums them in group order
-                float* part = img + img_floats(d.cin, G.rh, G.P);
+                float* part = img + img_floats(d.cin, Gt.rh, Gt.P);
                 if (active && grp > 0) {
     #pragma unroll
                     for (int co = 0; co < CP; ++co) part[((grp - 1) * tp + pix) * CP + co] = acc[co];
@@ -2126,23 +2138,32 @@ bool vsum_op(const gpi_conv_desc& d, const ConvGeom& G) {
 
 typedef void (*conv_kernel_t)(gpi_conv_desc, gpi_codec_ctx, ConvGeom);
 
+template <int K, int S, int UP, int NPX, bool HALF>
+conv_kernel_t pick_cp_h(int cp) {
+    if (cp == 2) return conv_fwd_kernel<K, S, UP, 2, NPX, HALF>;
+    if (cp == 4) return conv_fwd_kernel<K, S, UP, 4, NPX, HALF>;
+    if (cp == 6) return conv_fwd_kernel<K, S, UP, 6, NPX, HALF>;
+    return conv_fwd_kernel<K, S, UP, 8, NPX, HALF>;
+}
+
 template <int K, int S, int UP, int NPX>
-conv_kernel_t pick_cp(int cp) {
-    if (cp == 2) return conv_fwd_kernel<K, S, UP, 2, NPX>;
-    if (cp == 4) return conv_fwd_kernel<K, S, UP, 4, NPX>;
-    if (cp == 6) return conv_fwd_kernel<K, S, UP, 6, NPX>;
-    return conv_fwd_kernel<K, S, UP, 8, NPX>;
+conv_kernel_t pick_cp(int cp, bool half = false) {
+    // (no channel-group instantiation with half tiles: conv_geom keeps those launches whole)
+    if constexpr (NPX != 0) {
+        if (half) return pick_cp_h<K, S, UP, NPX, true>(cp);
+    }
+    return pick_cp_h<K, S, UP, NPX, false>(cp);
 }
 
 template <int K, int S, int UP>
 conv_kernel_t pick(int cp, bool fwd, int npx, bool half) {
     if (!fwd) return half ? conv_bwd_kernel<K, S, UP, false, true> : conv_bwd_kernel<K, S, UP>;
-    if (npx == 4) return pick_cp<K, S, UP, 4>(cp);
-    if (npx == 2) return pick_cp<K, S, UP, 2>(cp);
+    if (npx == 4) return pick_cp<K, S, UP, 4>(cp, half);
+    if (npx == 2) return pick_cp<K, S, UP, 2>(cp, half);
     if constexpr (!UP && K <= 3) {   // channel-group instantiation: the small-plane codec convs only
         if (npx == 0) return pick_cp<K, S, UP, 0>(cp);
     }
-    return pick_cp<K, S, UP, 1>(cp);
+    return pick_cp<K, S, UP, 1>(cp, half);
 }
 
 conv_kernel_t select_kernel(const gpi_conv_desc& d, int cp, bool fwd, int npx, bool half) {
