@@ -314,8 +314,11 @@ bool conv_geom(const gpi_conv_desc& d, const gpi_groups& g, ConvGeom& G, bool fw
     static const int half_tiles = env_int("GPI_HALF_TILES", 2);
     const int tot = B * G.tiles, base = tot & ~255;
     static const int half_fwd = env_int("GPI_HALF_FWD", 1);
+    // (only launches of at most five tiles per CU, one round of resident workgroups: with several rounds
+    // the dispatcher evens the CUs out itself, and the half tiles' extra rows and longer prologue cost --
+    // the c128 step 1.616 vs 1.558 ms with every launch split)
     if (half_tiles && (fwd ? half_fwd && half_tiles > 1 && G.cg == 1 : (half_tiles > 1 || loss_bwd)) &&
-        (G.th & 1) == 0 && base > 0 && tot != base && base % G.tiles == 0) {
+        (G.th & 1) == 0 && base > 0 && tot != base && tot <= 5 * 256 && base % G.tiles == 0) {
         ConvGeom::Alt& a = G.ha;
         a.th = G.th / 2;
         int y0;
