@@ -214,10 +214,20 @@ bool conv_geom(const gpi_conv_desc& d, const gpi_groups& g, ConvGeom& G, bool fw
                      t_s2brows = env_int("GPI_TILE_S2BROWS", 4), t_s2c1 = env_int("GPI_TILE_S2C1", 256),
                      t_bwdup = env_int("GPI_TILE_BWDUP", 1024), t_bwdrows = env_int("GPI_TILE_BWDROWS", 8),
                      t_fwdrows = env_int("GPI_TILE_FWDROWS", 8), t_fuse = env_int("GPI_TILE_FUSE", 1024);
-    const int target = d.stride == 2 ? (d.cin == 1 ? t_s2c1 : (fwd ? t_s2 : t_s2brows * d.w_out))
-                                     : (fwd ? (d.w_out >= 64 ? t_fwd64 : (d.w_out >= 32 ? t_fwdrows * d.w_out : t_fwd))
-                                            : (d.upsample && d.w_out >= 32 ? t_bwdup / 64 * min(d.w_out, 64)
-                                                                            : (d.w_out >= 64 ? t_bwd : t_bwdrows * d.w_out)));
+    // Round 4 per-operator sweep with half tiles (profiles/r04z_tile_sweep.txt): 16-row tiles for the upsampling
+    // forward on 32-wide planes (TransUp2.conv2 13.8 -> 11.2 us), the upsampling backward below 32 wide
+    // (TransUp1.conv2 11.6 -> 10.2) and the 3x3 backward of <= 8 input channels on 32-wide planes (EncBlock1.dl1
+    // 20.3 -> 19.0, DecBlock3.dl1 21.5 -> 20.9; with 10 channels the LDS image halves the resident workgroups:
+    // LastTransUp.conv1 23.9 -> 32.5); 512-px tiles for the single-channel input conv's forward only
+    static const int t_fwdup32 = env_int("GPI_TILE_FWDUP32", 16), t_bwdups = env_int("GPI_TILE_BWDUPS", 16),
+                     t_bwd32k3 = env_int("GPI_TILE_BWD32K3", 16), t_s2c1f = env_int("GPI_TILE_S2C1F", 512);
+    const int target =
+        d.stride == 2 ? (d.cin == 1 ? (fwd ? t_s2c1f : t_s2c1) : (fwd ? t_s2 : t_s2brows * d.w_out))
+        : fwd ? (d.w_out >= 64 ? t_fwd64
+                               : (d.w_out >= 32 ? (d.upsample && d.w_out == 32 ? t_fwdup32 : t_fwdrows) * d.w_out : t_fwd))
+              : (d.upsample ? (d.w_out >= 32 ? t_bwdup / 64 * min(d.w_out, 64) : t_bwdups * d.w_out)
+                            : (d.w_out >= 64 ? t_bwd
+                                             : (d.w_out == 32 && d.k == 3 && d.cin <= 8 ? t_bwd32k3 : t_bwdrows) * d.w_out));
     // the backward of the loss-epilogue output conv (fused with its forward, K - 1 extra forward rows
     // per tile): 1024 px (r02 A/B: 16 rows 9 us per step faster than 8).  Keyed on the op, not on the
     // fusion, so gpi_conv_blocks' slab rows fit both launch forms.
