@@ -103,6 +103,7 @@ struct ConvGeom {
     int fuse;       // backward: the fused output-conv launch (forward + loss + backward, gpi_conv_loss_fused)
     int vsum;       // backward, single-channel stride-2 input conv (weight gradient only, vwg): the four waves'
                     // partial slab rows summed in LDS into one row per tile (vsum_op)
+    int vshift;     // ... its weight gradient in the column-shift form (vwg, cout <= 8; GPI_VWG_SHIFT)
     int lsum;       // backward (MFMA weight gradient): the four waves' partial slab rows summed in LDS at the
                     // end into ONE row per tile (accumulators held in registers through the input gradient)
     int split;      // backward: 2 workgroups per tile, input gradient (blockIdx < nblocks) and weight gradient
@@ -275,6 +276,10 @@ bool conv_geom(const gpi_conv_desc& d, const gpi_groups& g, ConvGeom& G, bool fw
     }
     G.cg = 1;
     if (fwd && G.npx == 1 && d.epilogue != GPI_EPI_GAUSS_LOSS && d.epilogue != GPI_EPI_GAUSS_EXP_LOSS) {
+        // (kept on: without channel groups the C64 step is 1.9 us faster in the graph -- 0.5544 / 0.5552 / 0.5547
+        // vs 0.5561 / 0.5567 / 0.5571 ms interleaved, profiles/r04z_ab_fwd_cg.txt -- but the one-chain channel
+        // sum moves the 256^2 codec forward to 1.08e-5 of the fp64 oracle, over the 1e-5 bar, against 6.5e-6
+        // with the groups: profiles/r04z_fwd_err_cg.txt)
         static const int cg_on = env_int("GPI_FWD_CG", 1);
         const int tp = G.th * d.w_out;
         if (cg_on && tp <= 128 && 256 % tp == 0 && !d.upsample && d.k <= 3) G.cg = std::min(256 / tp, d.cin);
@@ -286,6 +291,10 @@ bool conv_geom(const gpi_conv_desc& d, const gpi_groups& g, ConvGeom& G, bool fw
     G.fuse = fuse ? 1 : 0;
     G.lsum = 0;     // decided by launch() / gpi_conv_blocks from the LDS footprint (lsum_op)
     G.vsum = 0;     // decided by launch() / gpi_conv_blocks (vsum_op)
+    {
+        static const int vshift = env_int("GPI_VWG_SHIFT", 1);
+        G.vshift = (!fwd && vshift && d.k == 7 && d.stride == 2 && d.cin == 1 && d.cout <= 8) ? 1 : 0;
+    }
     G.xcd = 0;      // set by launch() (xcd_mode)
     G.alt = 0;
     G.grid = 0;     // set by launch()
@@ -1600,6 +1609,49 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
         if constexpr (K == 7 && S == 2 && !UP) {
             if (vwg && !SKIP(G, 1)) {
                 constexpr int PADC = K / 2, NB = (KK + 15) / 16;
+                float* const wrow = Gt.vsum ? gl + wv * rowlen : slab;
+                if (G.vshift) {
+                    // column-shift form: taps kx = kx0 + 2 s of a stride-2 row are the taps kx0 of the output
+                    // pixel s columns further, so dW[co][ky][kx0 + 2 s] = sum_{ty, x} g[co][ty][x - s] *
+                    // in[2 ty + ky][2 x + kx0 - 3] over the tile's rows and x in [0, w_out + 4) (the zero halo
+                    // columns of the gradient image supply the out-of-range g).  M = (s, co): 4 cout <= 32 rows
+                    // in 2 blocks, N = (ky, kx0): 14 of 16 columns, K = pixels -- 2 MFMAs per 4 pixels against
+                    // 4 (M = cout, N = 49 taps in 4 blocks), 57 % of the MFMA products useful against 29 %
+                    // for the 6-channel C64 input conv.  Each wave takes whole rows (ty = wv, wv + 4, ...).
+                    const int mc = 4 * d.cout;
+                    const float* ga[2];
+#pragma unroll
+                    for (int mb = 0; mb < 2; ++mb) {
+                        const int m = 16 * mb + l16;
+                        const int s = m < mc ? m / d.cout : 0, co = m < mc ? m - s * d.cout : 0;
+                        ga[mb] = gl + co * gplane + (T.oy0 - gy0) * Gt.PG + HALO - s;
+                    }
+                    const int n = min(l16, 13), ky_b = n >> 1, kx0_b = n & 1;
+                    const float* const xb0 = alb + ky_b * Gt.P + HALO + kx0_b - PADC;
+                    const int wx4 = (d.w_out >> 2) + 1;
+                    f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+                    for (int ty = wv; ty < Gt.th; ty += 4) {
+                        const float* const g0 = ga[0] + ty * Gt.PG;
+                        const float* const g1 = ga[1] + ty * Gt.PG;
+                        const float* const xr = xb0 + (2 * ty) * Gt.P;
+                        for (int c4 = 0; c4 < wx4; ++c4) {
+                            const int x = 4 * c4 + kq;
+                            const float a0 = g0[x], a1 = g1[x], b = xr[2 * x];
+                            acc[0] = mfma4(a0, b, acc[0]);
+                            acc[1] = mfma4(a1, b, acc[1]);
+                        }
+                    }
+                    if (Gt.vsum) __syncthreads();        // every wave is done reading gl
+#pragma unroll
+                    for (int mb = 0; mb < 2; ++mb) {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const int m = 16 * mb + 4 * kq + r;
+                            const int s = m / d.cout, co = m - s * d.cout, kx = kx0_b + 2 * s;
+                            if (m < mc && l16 < 14 && kx < K) wrow[co * J + ky_b * K + kx] = acc[mb][r];
+                        }
+                    }
+                } else {
                 const int tp = Gt.th * d.w_out;
                 const int co_a = min(l16, d.cout - 1);                  // A row (rows >= cout never stored)
                 int tap_off[NB];                                        // B column: tap (ky, kx) of this lane
@@ -1626,7 +1678,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
                 // Gt.vsum: the four waves' tiles summed in LDS (the gradient image, dead after the loop)
                 // into ONE slab row per tile -- a quarter of the slab bytes the reduction reads, on the
                 // step's critical path at its end; otherwise each wave stores its own row
-                float* const wrow = Gt.vsum ? gl + wv * rowlen : slab;
                 if (Gt.vsum) __syncthreads();        // every wave is done reading gl
     #pragma unroll
                 for (int nb = 0; nb < NB; ++nb) {
@@ -1635,6 +1686,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
                         const int co2 = kq * 4 + r, j2 = 16 * nb + l16;
                         if (co2 < d.cout && j2 < KK) wrow[co2 * J + j2] = acc[nb][r];
                     }
+                }
                 }
                 if (Gt.vsum) {
                     __syncthreads();
