@@ -104,6 +104,8 @@ struct ConvGeom {
     int vsum;       // backward, single-channel stride-2 input conv (weight gradient only, vwg): the four waves'
                     // partial slab rows summed in LDS into one row per tile (vsum_op)
     int vshift;     // ... its weight gradient in the column-shift form (vwg, cout <= 8; GPI_VWG_SHIFT)
+    int ucls;       // backward, 3x3 upsampling conv: weight-gradient columns (ci, row offset) per output-row parity
+                    // (GPI_UP_ROWCLS; only where it saves a column block: 6 <= cin <= 8)
     int lsum;       // backward (MFMA weight gradient): the four waves' partial slab rows summed in LDS at the
                     // end into ONE row per tile (accumulators held in registers through the input gradient)
     int split;      // backward: 2 workgroups per tile, input gradient (blockIdx < nblocks) and weight gradient
@@ -294,6 +296,9 @@ bool conv_geom(const gpi_conv_desc& d, const gpi_groups& g, ConvGeom& G, bool fw
     {
         static const int vshift = env_int("GPI_VWG_SHIFT", 1);
         G.vshift = (!fwd && vshift && d.k == 7 && d.stride == 2 && d.cin == 1 && d.cout <= 8) ? 1 : 0;
+        static const int ucls = env_int("GPI_UP_ROWCLS", 1);
+        G.ucls = (!fwd && ucls && d.upsample && d.k == 3 && d.pad == 1 && (2 * d.cin + 15) / 16 < (3 * d.cin + 15) / 16)
+                     ? 1 : 0;
     }
     G.xcd = 0;      // set by launch() (xcd_mode)
     G.alt = 0;
@@ -1699,7 +1704,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
             }
         }
         {
-            const int MI = d.cout * K, NJ = d.cin * K;
+            // ucls (3x3 upsampling, pad 1): the output rows of one parity py read input rows i + py - 1 and
+            // i + py only (i = oy / 2), so the columns are (ci, row offset r) -- 2 cin instead of 3 cin, one column
+            // block instead of two for 6 channels -- and the wave's partial sum for (ci, r) is the partial of
+            // every tap ky that reads that row (py 0: r 0 -> ky 0, r 1 -> ky 1, 2; py 1: r 0 -> ky 0, 1, r 1 ->
+            // ky 2).  A wave's rows ty = wv + 4 k all have the parity of T.oy0 + wv.  (UP == 2: launch() picks
+            // that instantiation for ConvGeom::ucls)
+            const bool ucls = UP == 2 && K == 3 && !lsum;
+            const int MI = d.cout * K, NJ = ucls ? 2 * d.cin : d.cin * K;
             const int nmb = (SKIP(G, 1) || vwg || !do_wgrad) ? 0 : (MI + 15) >> 4, nnb = (NJ + 15) >> 4;
             const int XW = UP ? d.w_out + K - 1 : S * (d.w_out - 1) + K;   // virtual input columns
             const int nxs = (XW + 3) >> 2;
@@ -1712,8 +1724,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
     #pragma unroll
                     for (int u = 0; u < 2; ++u) {
                         const int j = 16 * (nb0 + u) + l16;
-                        ci[u] = min(j / K, d.cin - 1);
-                        ky[u] = j - (j / K) * K;
+                        ci[u] = min(ucls ? j >> 1 : j / K, d.cin - 1);
+                        ky[u] = ucls ? j & 1 : j - (j / K) * K;      // ucls: the row offset r
                     }
                     // the second column block is a compile-time branch around the whole row loop, so the
                     // accumulators stay in the MFMA registers (a runtime branch inside the loop made the
@@ -1726,7 +1738,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
                             const float* brow[2];
     #pragma unroll
                             for (int u = 0; u < 2; ++u) {
-                                const int ry = UP ? fdiv2(T.oy0 + ty - d.pad + ky[u]) - iy0 : ty * S + ky[u];
+                                const int oy = T.oy0 + ty;
+                                const int ry = !UP ? ty * S + ky[u]
+                                                   : (ucls ? (oy >> 1) + (oy & 1) - 1 + ky[u] : fdiv2(oy - d.pad + ky[u])) - iy0;
                                 brow[u] = alb + (ci[u] * Gt.rh + ry) * Gt.P + HALO;
                             }
                             // operands of four steps are read before their MFMAs (LDS read -> dependent
@@ -1817,8 +1831,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
                         for (int r = 0; r < 4; ++r) {
                             const int i2 = 16 * mb + 4 * kq + r;
                             if (i2 < MI && j2 < NJ) {
-                                const int co2 = i2 / K, kx2 = i2 - co2 * K, ci2 = j2 / K, ky2 = j2 - ci2 * K;
-                                slab[co2 * J + ci2 * KK + ky2 * K + kx2] = acc[u][r];
+                                const int co2 = i2 / K, kx2 = i2 - co2 * K;
+                                if (ucls) {
+                                    const int ci2 = j2 >> 1, rr = j2 & 1, py = (T.oy0 + wv) & 1;
+                                    const int kyl = rr ? 1 + py : 0, kyh = rr ? 2 : py;
+                                    float* const sp = slab + co2 * J + ci2 * KK + kx2;
+                                    sp[kyl * K] = acc[u][r];
+                                    if (kyh != kyl) sp[kyh * K] = acc[u][r];
+                                } else {
+                                    const int ci2 = j2 / K, ky2 = j2 - ci2 * K;
+                                    slab[co2 * J + ci2 * KK + ky2 * K + kx2] = acc[u][r];
+                                }
                             }
                         }
                     }
@@ -2221,7 +2244,13 @@ conv_kernel_t pick_cp(int cp, bool half = false) {
 }
 
 template <int K, int S, int UP>
-conv_kernel_t pick(int cp, bool fwd, int npx, bool half) {
+conv_kernel_t pick(int cp, bool fwd, int npx, bool half, bool ucls = false) {
+    if constexpr (UP != 0) {
+        // UP = 2: the upsampling backward with the row-parity weight-gradient columns (ConvGeom::ucls), an
+        // instantiation of its own: as a runtime branch its index arithmetic spilled 4 registers of every
+        // upsampling backward (+1.2-1.6 us per launch)
+        if (!fwd && ucls) return half ? conv_bwd_kernel<K, S, 2, false, true> : conv_bwd_kernel<K, S, 2>;
+    }
     if (!fwd) return half ? conv_bwd_kernel<K, S, UP, false, true> : conv_bwd_kernel<K, S, UP>;
     if (npx == 4) return pick_cp<K, S, UP, 4>(cp, half);
     if (npx == 2) return pick_cp<K, S, UP, 2>(cp, half);
@@ -2231,12 +2260,12 @@ conv_kernel_t pick(int cp, bool fwd, int npx, bool half) {
     return pick_cp<K, S, UP, 1>(cp, half);
 }
 
-conv_kernel_t select_kernel(const gpi_conv_desc& d, int cp, bool fwd, int npx, bool half) {
+conv_kernel_t select_kernel(const gpi_conv_desc& d, int cp, bool fwd, int npx, bool half, bool ucls) {
     const int key = d.k * 100 + d.stride * 10 + d.upsample;
     switch (key) {
         case 110: return pick<1, 1, 0>(cp, fwd, npx, half);
         case 310: return pick<3, 1, 0>(cp, fwd, npx, half);
-        case 311: return pick<3, 1, 1>(cp, fwd, npx, half);
+        case 311: return pick<3, 1, 1>(cp, fwd, npx, half, ucls);
         case 320: return pick<3, 2, 0>(cp, fwd, npx, half);
         case 510: return pick<5, 1, 0>(cp, fwd, npx, half);
         case 720: return pick<7, 2, 0>(cp, fwd, npx, half);
@@ -2298,7 +2327,7 @@ int launch(const gpi_conv_desc& d, const gpi_codec_ctx& c, hipStream_t st, bool 
     if (!fwd && d.gin_off >= 0 && d.stride == 2 && ((d.w_in & 7) || (G.ph & 1))) return GPI_ERR_UNSUPPORTED;
     const int cp = cp_of(d);
     conv_kernel_t k = fuse ? (G.nfull < G.nblocks ? conv_bwd_kernel<5, 1, 0, true, true> : conv_bwd_kernel<5, 1, 0, true>)
-                           : select_kernel(d, cp, fwd, G.cg > 1 ? 0 : G.npx, G.nfull < G.nblocks);
+                           : select_kernel(d, cp, fwd, G.cg > 1 ? 0 : G.npx, G.nfull < G.nblocks, G.ucls != 0);
     if (!k) return GPI_ERR_UNSUPPORTED;
     static const float* zero = nullptr;
     if (!zero) {
