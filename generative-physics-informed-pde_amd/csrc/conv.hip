@@ -214,14 +214,15 @@ bool conv_geom(const gpi_conv_desc& d, const gpi_groups& g, ConvGeom& G, bool fw
     // 32- and 64-wide planes, 1024 px on wider ones (per-operator sweeps with bench.py --kprof).
     static const int t_fwd = env_int("GPI_TILE_FWD", 512), t_fwd64 = env_int("GPI_TILE_FWD64", 1024),
                      t_bwd = env_int("GPI_TILE_BWD", 512), t_s2 = env_int("GPI_TILE_S2", 128),
-                     t_s2brows = env_int("GPI_TILE_S2BROWS", 4), t_s2c1 = env_int("GPI_TILE_S2C1", 256),
+                     t_s2brows = env_int("GPI_TILE_S2BROWS", 4), t_s2c1 = env_int("GPI_TILE_S2C1", 512),
                      t_bwdup = env_int("GPI_TILE_BWDUP", 1024), t_bwdrows = env_int("GPI_TILE_BWDROWS", 8),
                      t_fwdrows = env_int("GPI_TILE_FWDROWS", 8), t_fuse = env_int("GPI_TILE_FUSE", 1024);
     // Round 4 per-operator sweep with half tiles (profiles/r04z_tile_sweep.txt): 16-row tiles for the upsampling
     // forward on 32-wide planes (TransUp2.conv2 13.8 -> 11.2 us), the upsampling backward below 32 wide
     // (TransUp1.conv2 11.6 -> 10.2) and the 3x3 backward of <= 8 input channels on 32-wide planes (EncBlock1.dl1
     // 20.3 -> 19.0, DecBlock3.dl1 21.5 -> 20.9; with 10 channels the LDS image halves the resident workgroups:
-    // LastTransUp.conv1 23.9 -> 32.5); 512-px tiles for the single-channel input conv's forward only
+    // LastTransUp.conv1 23.9 -> 32.5); 512-px tiles for the single-channel input conv (forward 11.0 -> 10.3 us;
+    // the backward, with the column-shift weight gradient, 0.5535 vs 0.5554 ms/step: profiles/r04z_ab_s2c1.txt)
     static const int t_fwdup32 = env_int("GPI_TILE_FWDUP32", 16), t_bwdups = env_int("GPI_TILE_BWDUPS", 16),
                      t_bwd32k3 = env_int("GPI_TILE_BWD32K3", 16), t_s2c1f = env_int("GPI_TILE_S2C1F", 512);
     const int target =
