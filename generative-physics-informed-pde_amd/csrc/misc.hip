@@ -57,41 +57,60 @@ __device__ __forceinline__ void adam_element(float g, float& p, float& m, float&
 // epilogue's scratch / subset / dropout duties.  The step counter and the RNG offset are read by every
 // workgroup (bias corrections, the dropout draw) and advanced once all of them have read them: by the
 // last workgroup to finish (arrival counter *done, reset by that workgroup for the next launch).
-__device__ __forceinline__ void epilogue_wait(const uint32_t* flag, const int64_t* epoch, uint32_t* err);
+__device__ __forceinline__ bool epilogue_wait(const uint32_t* flag, const int64_t* epoch, uint32_t* err);
 
+// the sticky error word of a cross-stream wait (gpi_adam_desc.wait_err): set -> no parameter update
+__device__ __forceinline__ bool wait_failed(const uint32_t* err) {
+    return err && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+}
+
+// (grid-stride over at most GPI_EPILOGUE_MAX_WG workgroups: with one element per thread the grid of a 256^2
+// step -- q_X rows of 32 x 2 x 65536 floats, ~16 k workgroups -- would fill every CU slot with workgroups
+// spinning in epilogue_wait while the side stream still had kernels to dispatch)
 __global__ __launch_bounds__(256) void step_epilogue_adam_kernel(gpi_step_epilogue_desc d, gpi_adam_desc a,
-                                                                 uint32_t* done) {
-    if (d.wait_flag) epilogue_wait(d.wait_flag, a.step, d.wait_err);
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+                                                                 uint32_t* done, int64_t m_items) {
+    bool skip = false;
+    if (d.wait_flag) skip = epilogue_wait(d.wait_flag, a.step, d.wait_err);
+    else if (a.wait_err) {
+        __shared__ uint32_t s_bad;
+        if (threadIdx.x == 0) s_bad = wait_failed(a.wait_err) ? 1u : 0u;
+        __syncthreads();
+        skip = s_bad != 0u;
+    }
     const int64_t t = *a.step + 1;              // the step number after this step's increment
     const uint64_t base = d.drop_offset ? *d.drop_offset : 0;
-    if (i < d.n) {
-        const float g = (float)d.gacc[i];
-        d.grad[i] = g;
-        d.gacc[i] = 0.0;
-        const float lr = *a.lr;
-        const double bc1 = 1.0 - pow((double)a.beta1, (double)t);
-        const double bc2 = 1.0 - pow((double)a.beta2, (double)t);
-        const float step_size = (float)((double)lr / bc1);
-        const float bc2_sqrt = (float)sqrt(bc2);
-        float p = a.p[i], m = a.m[i], v = a.v[i];
-        adam_element(g, p, m, v, a.beta1, a.beta2, a.eps, step_size, bc2_sqrt);
-        a.m[i] = m;
-        a.v[i] = v;
-        a.p[i] = p;
-    }
-    if (i < d.n_scratch) {
-        if (i < d.n_terms) d.terms_dst[i] = d.scratch[i];
-        d.scratch[i] = 0.0;
-    }
-    if (i < d.n_idx) d.idx_dst[i] = d.idx_src[i];
-    if (i * 4 < d.drop_n) {
-        const uint4_ r = philox(base + (uint64_t)i, d.drop_sub, d.drop_seed);
-        const float u[4] = {u01(r.x), u01(r.y), u01(r.z), u01(r.w)};
-        const float scale = 1.f / (1.f - d.drop_p);
+    const float lr = *a.lr;
+    const double bc1 = 1.0 - pow((double)a.beta1, (double)t);
+    const double bc2 = 1.0 - pow((double)a.beta2, (double)t);
+    const float step_size = (float)((double)lr / bc1);
+    const float bc2_sqrt = (float)sqrt(bc2);
+    const float scale = 1.f / (1.f - d.drop_p);
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < m_items; i += stride) {
+        if (i < d.n) {
+            const float g = (float)d.gacc[i];
+            d.grad[i] = g;
+            d.gacc[i] = 0.0;
+            if (!skip) {
+                float p = a.p[i], m = a.m[i], v = a.v[i];
+                adam_element(g, p, m, v, a.beta1, a.beta2, a.eps, step_size, bc2_sqrt);
+                a.m[i] = m;
+                a.v[i] = v;
+                a.p[i] = p;
+            }
+        }
+        if (i < d.n_scratch) {
+            if (i < d.n_terms) d.terms_dst[i] = d.scratch[i];
+            d.scratch[i] = 0.0;
+        }
+        if (i < d.n_idx) d.idx_dst[i] = d.idx_src[i];
+        if (i * 4 < d.drop_n) {
+            const uint4_ r = philox(base + (uint64_t)i, d.drop_sub, d.drop_seed);
+            const float u[4] = {u01(r.x), u01(r.y), u01(r.z), u01(r.w)};
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (i * 4 + k < d.drop_n) d.drop_out[i * 4 + k] = u[k] < d.drop_p ? 0.f : scale;
+            for (int k = 0; k < 4; ++k)
+                if (i * 4 + k < d.drop_n) d.drop_out[i * 4 + k] = u[k] < d.drop_p ? 0.f : scale;
+        }
     }
     // every thread's reads of *step / *drop_offset are complete (their values were consumed above), so
     // a relaxed arrival suffices: the last arriver's writes come after every workgroup's reads
@@ -109,6 +128,8 @@ __global__ __launch_bounds__(256) void step_epilogue_adam_kernel(gpi_step_epilog
 // torch.optim.Adam single-tensor math (torch/optim/adam.py, defaults:
 // no weight decay, no amsgrad, maximize=False).
 __global__ __launch_bounds__(256) void adam_kernel(gpi_adam_desc d) {
+    if (d.rng_offset && blockIdx.x == 0 && threadIdx.x == 0) *d.rng_offset += d.rng_advance;
+    if (wait_failed(d.wait_err)) return;        // a timed-out hand-off: the gradient may be incomplete
     const int64_t t = *d.step;
     const float lr = *d.lr;
     const double bc1 = 1.0 - pow((double)d.beta1, (double)t);
@@ -122,7 +143,6 @@ __global__ __launch_bounds__(256) void adam_kernel(gpi_adam_desc d) {
         d.v[i] = v;
         d.p[i] = p;
     }
-    if (d.rng_offset && blockIdx.x == 0 && threadIdx.x == 0) *d.rng_offset += d.rng_advance;
 }
 
 __global__ __launch_bounds__(256) void randn_kernel(float* out, int64_t n, uint64_t seed, const uint64_t* offset,
@@ -277,20 +297,27 @@ __device__ __forceinline__ bool count_reached(const uint32_t* flag, uint32_t wan
     return (int32_t)(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - want) >= 0;
 }
 
-__device__ __forceinline__ void epilogue_wait(const uint32_t* flag, const int64_t* epoch, uint32_t* err) {
+// returns true (every thread) when this wait timed out or an earlier one did (the sticky *err)
+__device__ __forceinline__ bool epilogue_wait(const uint32_t* flag, const int64_t* epoch, uint32_t* err) {
+    __shared__ uint32_t s_bad;
     if (threadIdx.x == 0) {
         const uint32_t want = (uint32_t)(*epoch + 1);
+        uint32_t bad = 0u;
         for (int i = 0; !count_reached(flag, want); ++i) {
             __builtin_amdgcn_s_sleep(2);
             if (i > WAIT_SPIN_MAX) {
                 if (err) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                bad = 1u;
                 break;
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (wait_failed(err)) bad = 1u;
+        s_bad = bad;
     }
     __syncthreads();
+    return s_bad != 0u;
 }
 
 __global__ void stream_signal_kernel(uint32_t* flag) {
@@ -437,9 +464,10 @@ extern "C" int gpi_step_epilogue_adam(const gpi_step_epilogue_desc* d, const gpi
     int64_t m = d->n > d->n_scratch ? d->n : d->n_scratch;
     if (d->n_idx > m) m = d->n_idx;
     if ((d->drop_n + 3) / 4 > m) m = (d->drop_n + 3) / 4;
-    const int64_t nb = m > 0 ? (m + 255) / 256 : 1;
-    if (nb > 0x7fffffff) return GPI_ERR_ARG;
-    hipLaunchKernelGGL(step_epilogue_adam_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, *d, *a, done);
+    int64_t nb = m > 0 ? (m + 255) / 256 : 1;
+    if (nb > GPI_EPILOGUE_MAX_WG) nb = GPI_EPILOGUE_MAX_WG;
+    hipLaunchKernelGGL(step_epilogue_adam_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, *d, *a, done,
+                       m);
     GPI_CHECK_LAUNCH();
     return GPI_OK;
 }

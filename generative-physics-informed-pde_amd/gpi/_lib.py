@@ -112,7 +112,7 @@ class ResidualDesc(C.Structure):
 class AdamDesc(C.Structure):
     _fields_ = [('p', vp), ('g', vp), ('m', vp), ('v', vp), ('n', i64), ('lr', vp), ('step', vp),
                 ('beta1', f32), ('beta2', f32), ('eps', f32), ('_pad', f32), ('rng_offset', vp),
-                ('rng_advance', C.c_uint64)]
+                ('rng_advance', C.c_uint64), ('wait_err', vp)]
 
 
 class VoQueryDesc(C.Structure):
@@ -181,6 +181,7 @@ STRUCTS = [Stat, Groups, ConvDesc, CodecCtx, ReduceItem, HeadDesc, GemmItem, Rom
 SIGNATURES = {
     'gpi_version': (C.c_int, []),
     'gpi_replicas': (C.c_int, []),
+    'gpi_source_sha': (C.c_char_p, []),
     'gpi_struct_sizes': (C.c_int, [C.POINTER(i64), C.c_int]),
     'gpi_error_string': (C.c_char_p, [C.c_int]),
     'gpi_conv_blocks': (C.c_int, [C.POINTER(ConvDesc), C.POINTER(Groups), C.POINTER(i32)]),
@@ -232,6 +233,35 @@ SIGNATURES = {
 }
 
 _LIB = None
+SRC_DIR = os.path.join(os.path.dirname(HERE), 'csrc')
+INCLUDE_H = os.path.join(os.path.dirname(os.path.dirname(HERE)), 'include', 'gpi.h')
+
+
+def source_sha():
+    """sha1 of the library's sources as csrc/Makefile computes it (csrc/*.hip in name order, csrc/common.h,
+    include/gpi.h, concatenated); None when the sources are not next to the package."""
+    import glob
+    import hashlib
+    files = sorted(glob.glob(os.path.join(SRC_DIR, '*.hip')), key=os.path.basename)
+    files += [os.path.join(SRC_DIR, 'common.h'), INCLUDE_H]
+    if not all(os.path.exists(f) for f in files):
+        return None
+    h = hashlib.sha1()
+    for f in files:
+        with open(f, 'rb') as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
+def check_source_sha(L, path=None):
+    """Refuse a library built from other sources than the ones next to it (a stale build would run
+    silently otherwise).  GPI_ALLOW_STALE_LIB=1 overrides (A/B builds of earlier sources)."""
+    want = source_sha()
+    got = L.gpi_source_sha().decode()
+    if want is not None and got != want and os.environ.get('GPI_ALLOW_STALE_LIB') != '1':
+        raise NativeError('stale native library %s: built from sources sha1 %s, the sources here are %s; '
+                          'rebuild (make -C csrc) or set GPI_ALLOW_STALE_LIB=1' % (path or LIB_PATH, got, want))
+    return got
 
 
 class NativeError(RuntimeError):
@@ -256,6 +286,7 @@ def lib():
         for s, cls in zip(sizes[:k], STRUCTS):
             if s != C.sizeof(cls):
                 raise NativeError('ABI mismatch for %s: C %d bytes, ctypes %d' % (cls.__name__, s, C.sizeof(cls)))
+        check_source_sha(L)
         if L.gpi_replicas() != GPI_REPLICAS:
             raise NativeError('ABI mismatch: the library keeps %d statistic replicas, the binding %d (GPI_REPLICAS)'
                               % (L.gpi_replicas(), GPI_REPLICAS))

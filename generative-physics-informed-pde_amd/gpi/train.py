@@ -168,6 +168,16 @@ class FusedElboStep(object):
                 # the join with the side stream's last reduction inside the fused epilogue + Adam launch
                 self.epi_adam.wait_flag = self.handoff_flags.data_ptr() + 4 * 3
                 self.epi_adam.wait_err = self.handoff_flags.data_ptr() + 4 * 4
+            # a timed-out hand-off (sticky error word) stops every later parameter update: the gradient of
+            # such a step may be incomplete, so no step after it may move the parameters
+            self.adam.wait_err = self.handoff_flags.data_ptr() + 4 * 4
+        # lazy surfacing of that error word without a host sync: an async copy to pinned memory after
+        # a replay, read once its event has completed (at the next step() / run() / check_handoff())
+        self._err_host = torch.zeros(1, dtype=torch.int32, pin_memory=True) if dev.type == 'cuda' else None
+        self._err_ev = None
+        self._err_every = int(os.environ.get('GPI_ERR_CHECK_EVERY', '16'))
+        self._n_steps = 0
+        self._fb_pending = False
         self.graph = None
         # the first step's noise; every step then draws the next step's during its backward
         self._launch_noise(L.stream_handle(), self.idx, sub0=100)
@@ -202,9 +212,15 @@ class FusedElboStep(object):
 
     def forward_backward(self, stream=None):
         """One step without the parameter update (gradient in flat.G and the ELBO terms delivered;
-        update() then applies Adam)."""
+        update() then applies Adam).  Every forward_backward() must be followed by update() before the
+        next one: the cross-stream flags count one signal per step, and the step counter that their waits
+        compare against advances only in the update (an unpaired pass would leave the flags ahead and every
+        later wait would pass at once)."""
+        if self._fb_pending:
+            raise RuntimeError('FusedElboStep.forward_backward() called twice without update() in between')
         self._forward_backward(stream, epilogue=True)
         self.engine.rejoin()
+        self._fb_pending = True
 
     def _forward_backward(self, stream=None, epilogue=True):
         """One step without the parameter update.  The step's noise and subset were drawn by the
@@ -241,6 +257,7 @@ class FusedElboStep(object):
         """Adam (+ RNG offset advance).  fused: the step epilogue and Adam in one launch -- after
         _forward_backward(epilogue=False), single-process steps only."""
         st = stream if stream is not None else L.stream_handle()
+        self._fb_pending = False
         if fused:
             L.check(L.lib().gpi_step_epilogue_adam(C.byref(self.epi_adam), C.byref(self.adam),
                                                    L.ptr(self.done_ctr), st), 'step epilogue + adam')
@@ -263,9 +280,28 @@ class FusedElboStep(object):
         self._mark_optimizer_step()
 
     def check_handoff(self):
-        """Raise if a side-stream flag wait timed out (host sync; results of that step are invalid)."""
+        """Raise if a side-stream flag wait timed out (host sync).  The step that timed out and every step
+        after it have left the parameters and Adam moments untouched (the error word is sticky)."""
         if int(self.handoff_flags[4].item()) != 0:
-            raise RuntimeError('FusedElboStep: a cross-stream flag wait timed out (gpi_stream_wait)')
+            raise RuntimeError('FusedElboStep: a cross-stream flag wait timed out (gpi_stream_wait); '
+                               'parameter updates were skipped from that step on')
+
+    def _poll_error(self):
+        """Raise if the last posted copy of the error word (see _post_error_copy) shows a timed-out wait;
+        never blocks (an unfinished copy is read at a later call)."""
+        ev = self._err_ev
+        if ev is not None and ev.query():
+            self._err_ev = None
+            if int(self._err_host[0]) != 0:
+                raise RuntimeError('FusedElboStep: a cross-stream flag wait timed out (gpi_stream_wait); '
+                                   'parameter updates were skipped from that step on')
+
+    def _post_error_copy(self):
+        if self._err_host is None or self.handoff != 'flags' or self._err_ev is not None:
+            return
+        self._err_host.copy_(self.handoff_flags[4:5], non_blocking=True)
+        self._err_ev = torch.cuda.Event()
+        self._err_ev.record()
 
     # ------------------------------------------------------------------
     def _mutable_state(self):
@@ -300,6 +336,7 @@ class FusedElboStep(object):
                 self.step_eager()
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
+        self.check_handoff()            # (the restore below would erase a warm-up step's timeout)
         for t, v in zip(self._mutable_state(), saved):
             t.copy_(v)
         del saved
@@ -496,6 +533,15 @@ class FusedElboStep(object):
         g['m5'].replay()
 
     def step(self):
+        """One training step (graph replay once captured).  A timed-out cross-stream wait raises at a
+        later step() (its error word is copied back every GPI_ERR_CHECK_EVERY steps, no host sync)."""
+        self._poll_error()
+        self._step()
+        self._n_steps += 1
+        if self._err_every > 0 and self._n_steps % self._err_every == 0:
+            self._post_error_copy()
+
+    def _step(self):
         self.sync_lr()
         if self.graph is None:
             return self.step_eager()
@@ -521,6 +567,7 @@ class FusedElboStep(object):
     def run(self, n):
         """n steps: with capture(unroll=k), n // k replays of the k-step graphs, then single steps."""
         n = int(n)
+        self._poll_error()
         if self.graph is not None and self.unroll > 1 and self.g_fb_k is not None:
             self.sync_lr()
             self._check_stream_pair()
@@ -532,7 +579,8 @@ class FusedElboStep(object):
                     self._mark_optimizer_step()
                 n %= self.unroll
         for _ in range(n):
-            self.step()
+            self._step()
+        self._post_error_copy()
 
     def elbo(self):
         """ELBO value of the last completed step (0-d tensor)."""

@@ -46,6 +46,9 @@ extern "C" {
 #ifndef GPI_REPLICAS
 #define GPI_REPLICAS 16
 #endif
+/* workgroups of the fused step epilogue + Adam launch (grid-stride): well under one resident round of
+ * 256-thread workgroups on 256 CUs, so its cross-stream wait cannot starve the signalling stream */
+#define GPI_EPILOGUE_MAX_WG 512
 
 /* Conv epilogues */
 #define GPI_EPI_STORE 0        /* store raw output */
@@ -418,12 +421,19 @@ typedef struct gpi_adam_desc {
     float beta1, beta2, eps, _pad;
     uint64_t* rng_offset;      /* optional: device RNG offset advanced by rng_advance after the update */
     uint64_t rng_advance;      /*           (replaces a separate gpi_rng_advance launch) */
+    /* optional: a cross-stream wait's error word (gpi_stream_wait / the fused epilogue's wait_err).  While
+     * it is non-zero the update leaves p, m and v untouched (a timed-out hand-off means the gradient may be
+     * incomplete; the word is sticky, the host raises on it); counters and the RNG offset still advance. */
+    const uint32_t* wait_err;
 } gpi_adam_desc;
 
 /* ---------------------------------------------------------------- API */
 int gpi_version(void);
 /* GPI_REPLICAS of this build (bindings size their statistics / term buffers by it). */
 int gpi_replicas(void);
+/* sha1 (40 hex digits) of the sources this library was built from: csrc/*.hip in name order, then
+ * csrc/common.h and include/gpi.h, concatenated (bindings refuse a library older than its sources). */
+const char* gpi_source_sha(void);
 /* sizeof of every struct above, in declaration order (ABI self-check); returns the count. */
 int gpi_struct_sizes(int64_t* out, int n);
 const char* gpi_error_string(int code);
@@ -548,7 +558,10 @@ typedef struct gpi_step_epilogue_desc {
     /* optional cross-stream wait folded into the epilogue (gpi_step_epilogue_adam only): every
      * workgroup waits until *wait_flag >= *step + 1 (the Adam step counter; see gpi_stream_wait) and
      * acquires before it reads the gradient accumulator -- the join with another stream's final
-     * reductions without a wait launch; a timeout sets *wait_err.  NULL: no wait. */
+     * reductions without a wait launch; a timeout sets *wait_err, and while *wait_err is set the launch
+     * skips the parameter / moment update (gpi_adam_desc.wait_err).  NULL: no wait.  The launch is a
+     * grid-stride loop over at most GPI_EPILOGUE_MAX_WG workgroups, so the waiting workgroups never
+     * hold every CU slot the signalling stream's remaining kernels need. */
     const uint32_t* wait_flag;
     uint32_t* wait_err;
 } gpi_step_epilogue_desc;

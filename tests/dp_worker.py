@@ -41,20 +41,13 @@ def c64_data(world, rank):
     return Xu, Xs, Y, F
 
 
-def run_c64_sync(out):
-    """One SyncBN step of the NATIVE FusedElboStep at config 3's per-rank shape; records the inputs it
-    drew, the kernels' ReLU decisions (for the fp64 union-batch oracle), the local and all-reduced
-    gradients and the ELBO."""
-    import ctypes as C
+def c64_model(world, rank):
+    """The config-3 model (highres factory: C64 codec, Dropout2d 0.2, ROM 8x8; torch.manual_seed(0), so the
+    shared parameters and q rows are identical on every rank) with rank `rank`'s datasets registered, and
+    the step's device inputs (X_pool, X_s, Y, F)."""
     from factories.model import ModelFactory
-    from gpi.train import FusedElboStep
-    from gpi import _lib as L
-    from gpu_masks import engine_relu_masks
     from test_gpu_c64 import _DS
-    rank, world = int(os.environ['RANK']), int(os.environ['WORLD_SIZE'])
-    torch.cuda.set_device(0)
-    dist.init_process_group('gloo')
-    torch.manual_seed(0)                    # identical shared parameters (and q rows) on every rank
+    torch.manual_seed(0)
     fac = ModelFactory.FromIdentifier('highres')
     fac.set('device', 'cuda')
     physics_, model, _, encoder, _, _ = fac.setup()
@@ -65,7 +58,22 @@ def run_c64_sync(out):
                              'unsupervised': _DS(perm=None, X=cu(Xu))}, None,
                             create_unsupervised_variational_approximation=False)
     model.cuda()
-    step = FusedElboStep(model, cu(Xu), C64_BU, cu(Xs), cu(Y), cu(F), lr=1e-3, seed=50 + rank, subset_seed=9,
+    return model, (cu(Xu), cu(Xs), cu(Y), cu(F))
+
+
+def run_c64_sync(out):
+    """One SyncBN step of the NATIVE FusedElboStep at config 3's per-rank shape; records the inputs it
+    drew, the kernels' ReLU decisions (for the fp64 union-batch oracle), the local and all-reduced
+    gradients and the ELBO."""
+    import ctypes as C
+    from gpi.train import FusedElboStep
+    from gpi import _lib as L
+    from gpu_masks import engine_relu_masks
+    rank, world = int(os.environ['RANK']), int(os.environ['WORLD_SIZE'])
+    torch.cuda.set_device(0)
+    dist.init_process_group('gloo')
+    model, (Xu, Xs, Y, F) = c64_model(world, rank)
+    step = FusedElboStep(model, Xu, C64_BU, Xs, Y, F, lr=1e-3, seed=50 + rank, subset_seed=9,
                          distributed=True, rank=rank, world=world, sync_bn=True)
     assert step.sync_bn and step.engine.bn_sync is not None
     e = step.engine

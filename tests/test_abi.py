@@ -96,3 +96,36 @@ def test_random_subset_workspace_host_query(lib):
     assert L.gpi_random_subset_workspace(1 << 20, C.byref(nb)) == 0
     assert nb.value == 4 * ((1 << 16) + 64) + 8 * (1 << 20)
     assert L.gpi_random_subset_workspace(0, C.byref(nb)) != 0
+
+
+def test_library_source_sha_matches_sources(lib):
+    """gpi_source_sha() of the built library equals the sha1 of the sources next to it:
+    a library built from other sources is refused at load."""
+    so = C.CDLL(lib.LIB_PATH)
+    so.gpi_source_sha.restype = C.c_char_p
+    got = so.gpi_source_sha().decode()
+    assert re.fullmatch(r'[0-9a-f]{40}', got), got
+    assert got == lib.source_sha()
+    assert lib.check_source_sha(so) == got
+
+
+def test_stale_library_is_refused(lib, tmp_path, monkeypatch):
+    """A touched source (copied tree with one byte appended to a kernel file) no longer matches the
+    library's embedded sha: loading it raises, unless GPI_ALLOW_STALE_LIB=1."""
+    import shutil
+    pkg = os.path.join(ROOT, 'generative-physics-informed-pde_amd')
+    src = tmp_path / 'csrc'
+    shutil.copytree(os.path.join(pkg, 'csrc'), str(src), ignore=shutil.ignore_patterns('build*', '*.o'))
+    inc = tmp_path / 'gpi.h'
+    shutil.copy(HEADER, str(inc))
+    monkeypatch.setattr(lib, 'SRC_DIR', str(src))
+    monkeypatch.setattr(lib, 'INCLUDE_H', str(inc))
+    so = C.CDLL(lib.LIB_PATH)
+    so.gpi_source_sha.restype = C.c_char_p
+    assert lib.check_source_sha(so)              # the unchanged copy matches
+    with open(str(src / 'misc.hip'), 'a') as fh:
+        fh.write('\n// touched\n')
+    with pytest.raises(lib.NativeError, match='stale native library'):
+        lib.check_source_sha(so)
+    monkeypatch.setenv('GPI_ALLOW_STALE_LIB', '1')
+    assert lib.check_source_sha(so)

@@ -177,43 +177,47 @@ def test_rccl_allreduce_captured_unrolled(device):
     assert 'max |dP| = 0.000e+00' in r.stdout, r.stdout[-2000:]
 
 
-def test_rccl_sync_bn_captured_in_step_graph(device):
+@pytest.mark.parametrize('cfg,n_coll', [('c32', 26), ('c64', 46)])
+def test_rccl_sync_bn_captured_in_step_graph(device, cfg, n_coll):
     """SyncBN over RCCL inside the captured step (world size 1 on this box; the 8-GPU node runs the
-    same graph across ranks): the per-conv collectives of the BN batch sums (26 at C32, 46 at C64) are graph nodes, the
-    replays equal eager SyncBN steps bit for bit, and at one rank SyncBN agrees with replica-BN to
-    rounding."""
+    same graph across ranks): the per-conv collectives of the BN batch sums (26 at C32; 46 at C64, the
+    graph an 8-GPU config-3 SyncBN bench captures: highres codec, B_u = 256, N_s = 32, Dropout2d 0.2) are
+    graph nodes, the replays equal eager SyncBN steps bit for bit, and at one rank SyncBN agrees with
+    replica-BN to rounding."""
     env = dict(os.environ)
     env['PYTHONUNBUFFERED'] = '1'
     cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node=1',
            '--master-addr=127.0.0.1', '--master-port=%d' % _free_port(),
-           os.path.join(os.path.dirname(HERE), 'tools', 'dist_capture_probe.py'), '--sync-bn']
+           os.path.join(os.path.dirname(HERE), 'tools', 'dist_capture_probe.py'), '--sync-bn', '--config', cfg]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert 'max |dP| = 0.000e+00' in r.stdout, r.stdout[-2000:]
     n = int(r.stdout.split('SyncBN (')[1].split()[0])
-    assert n >= 20, r.stdout[-2000:]          # C32 codec: 26 (C64: 46)
+    assert n == n_coll, r.stdout[-2000:]
     assert 'SyncBN vs replica-BN' in r.stdout, r.stdout[-2000:]
 
 
-def test_dp_config3_shape_sync_bn_vs_union_oracle(device, tmp_path):
-    """BASELINE config 3's global-batch semantics through the real DP code: 4 gloo ranks, each running
-    the NATIVE FusedElboStep with SyncBN at config 3's per-rank shape (C64 highres, B_u = 256 of a shared
-    pool + N_s = 32 rank-owned labeled samples, Dropout2d 0.2), against the fp64 oracle of ONE process
-    on the union batch (B_u = 1024, N_s = 128: train-mode BN over the whole codec call,
-    codec.py:164-173) on the ranks' own subsets, noise and dropout scales, with the kernels' ReLU
+def test_dp_config3_sync_bn_vs_union_oracle(device, tmp_path):
+    """BASELINE config 3 at its own global batch through the real DP code: 8 gloo ranks (config 3's
+    world), each running the NATIVE FusedElboStep with SyncBN at config 3's per-rank shape (C64 highres,
+    B_u = 256 of a shared pool + N_s = 32 rank-owned labeled samples, Dropout2d 0.2), against the fp64
+    oracle of ONE process on the union batch (B_u = 2048, N_s = 256: train-mode BN over the whole codec
+    call, codec.py:164-173) on the ranks' own subsets, noise and dropout scales, with the kernels' ReLU
     decisions (tests/gpu_masks.py).  The ranks' ELBOs sum to the union ELBO within 1e-5; the
-    all-reduced shared gradient and each rank's q rows match the union gradient at 5e-5 per tensor."""
+    all-reduced shared gradient and each rank's q rows match the union gradient at 5e-5 per tensor.
+    (The ranks share the box's one GPU over gloo; only the RCCL-over-xGMI wire itself stays for the
+    8-GPU node.)"""
     from dp_worker import C64_BU, C64_NS, c64_data
     from elbo_ref import oracle_elbo
     from test_gpu_c64 import check_mask_audit
     from oracle import codec as ocodec
-    world = 4
+    world = 8
     env = dict(os.environ)
     env['PYTHONUNBUFFERED'] = '1'
     cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node=%d' % world,
            '--master-addr=127.0.0.1', '--master-port=%d' % _free_port(), os.path.join(HERE, 'dp_worker.py'),
            str(tmp_path), 'c64sync']
-    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=420)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     rk = [dict(np.load(str(tmp_path / ('rank%d.npz' % i)))) for i in range(world)]
     idx = rk[0]['idx']

@@ -6,7 +6,9 @@ the SyncBN step must also agree with the replica-BN step to rounding (the same b
 --unroll K: the graph copy captures K steps per replay (FusedElboStep.capture(unroll=K), K all-reduces in one
 graph) and takes its 3 steps by run(3).
 usage: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 tools/dist_capture_probe.py
-       [--sync-bn] [--unroll K]"""
+       [--sync-bn] [--unroll K] [--config c32|c64]
+--config c64: BASELINE config 3's per-rank shape (C64 highres codec, B_u = 256, N_s = 32, Dropout2d 0.2; 46 SyncBN
+collectives per step) instead of the C32 golden fixture."""
 import copy
 import os
 import sys
@@ -25,10 +27,17 @@ def main():
     from elbo_ref import load
     from test_gpu_parity import build_golden_model, cuda
     from gpi.train import FusedElboStep
-    d = load('elbo_c32.npz')
-    ma, bs = build_golden_model(d)
+    cfg = sys.argv[sys.argv.index('--config') + 1] if '--config' in sys.argv else 'c32'
+    if cfg == 'c64':
+        # BASELINE config 3's per-rank step (C64 highres, B_u = 256 of a shared pool, N_s = 32, Dropout2d 0.2)
+        from dp_worker import c64_model, C64_BU
+        ma, (Xu, Xs, Y, F) = c64_model(world, rank)
+        args = (Xu, C64_BU, Xs, Y, F)
+    else:
+        d = load('elbo_c32.npz')
+        ma, bs = build_golden_model(d)
+        args = (cuda(d['Xu']), bs // world, cuda(d['Xs']), cuda(d['Y']), cuda(d['F']))
     mb = copy.deepcopy(ma)
-    args = (cuda(d['Xu']), bs // world, cuda(d['Xs']), cuda(d['Y']), cuda(d['F']))
     sync = '--sync-bn' in sys.argv
     mc = copy.deepcopy(ma) if sync and world == 1 else None
     kw = dict(lr=1e-3, seed=5 + rank, subset_seed=1, distributed=True, rank=rank, world=world, sync_bn=sync)
@@ -59,7 +68,7 @@ def main():
     torch.cuda.synchronize()
     graph.check_handoff()
     err = (graph.flat.P - eager.flat.P).abs().max().item()
-    what = 'SyncBN (%d codec collectives per step) + ' % n_per_step if sync else ''
+    what = 'SyncBN (%d codec collectives per step, %s) + ' % (n_per_step, cfg) if sync else ''
     print('rank %d world %d: graph-captured %sall-reduce vs eager, max |dP| = %.3e' % (rank, world, what, err),
           flush=True)
     assert err < 1e-6
