@@ -17,8 +17,11 @@
 // over boundary facets), u = y on free nodes and 0 on the Dirichlet nodes (the reduced
 // Gamma keeps free columns only).  Same closed forms as vo.hip's vo_query_flux.
 #include "common.h"
+#include <stdlib.h>
 
 using namespace gpi;
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 namespace {
 
@@ -159,6 +162,215 @@ __global__ __launch_bounds__(64 * CGR_MAXW) void cgr_kernel(gpi_residual_desc d,
     for (int e = threadIdx.x; e < nT; e += blockDim.x) d.r_flux[(int64_t)f * nT + e] = (float)racc[e];
 }
 
+// Streaming form (16-B aligned fields, n % 16 == 0, n <= 256, r % 4 == 0: 32^2 ... 256^2 at nc = 8).
+// One workgroup of NT = 4 n threads per field walks the field bottom-up in chunks of CR = 16 node rows.
+// Every thread loads ONE float4 of log kappa and ONE float4 of y per chunk, DEPTH chunks ahead of the
+// chunk it consumes (registers: the loads of DEPTH chunks are in flight while a chunk is computed), takes
+// exp once per pixel, and writes both into LDS rings indexed by the field-flat element index masked to a
+// power of two (y rows are (n - 1) floats: not 16-B aligned, so y's ring index is relative to the field's
+// 16-B aligned-down base and a float4 never straddles the wrap).  After one barrier per chunk, every
+// thread computes 4 adjacent nodes of one row from LDS (the same arithmetic as cgr_kernel), accumulates
+// their W^T contributions -- all four in one coarse square, r % 4 == 0 -- and adds them (after a shuffle
+// over the r / 4 threads of the square's row) into the fp64 LDS accumulators.  The ring holds 2 CR + 2
+// rows, so chunk s + 1's writes never touch the rows chunk s's computation reads (one barrier per chunk).
+constexpr int CGRS_CR = 16;        // node rows per chunk
+#ifndef GPI_CGR_DEPTH
+#define GPI_CGR_DEPTH 3            // chunks in flight ahead of the one computed
+#endif
+template <int DEPTH, bool FLUX>
+__global__ __launch_bounds__(1024) void cgr_stream_kernel(gpi_residual_desc d, int kmask, int ymask) {
+    extern __shared__ __attribute__((aligned(16))) double smd[];
+    const int n = d.n_fine, nc = d.nc, nn = (nc + 1) * (nc + 1), nT = 2 * nc * nc;
+    const int r = n / nc;
+    const float rinv = 1.f / (float)r;
+    const int NT = blockDim.x, tid = threadIdx.x;
+    double* acc = smd;                                   // [nn]
+    double* racc = smd + nn;                             // [nT]
+    float* kr = (float*)(smd + ((nn + nT + 1) & ~1));    // kappa ring [kmask + 1] (16-B aligned)
+    float* yr = kr + kmask + 1;                          // y ring [ymask + 1]
+    const int f = blockIdx.x;
+    const int ny = (n + 1) * (n - 1);                    // y values per field
+    const float* lk = d.logkappa + (int64_t)f * n * n;
+    const int64_t ybase = (int64_t)f * ny;               // field's first y element (flat, whole array)
+    const int64_t yal = ybase & ~(int64_t)3;             // ... aligned down to 16 B
+    const int mis = (int)(ybase - yal);
+    const int64_t ytotal = (int64_t)d.n * ny;
+    const float u0b = d.bc[4 * f], u1b = d.bc[4 * f + 1], u2b = d.bc[4 * f + 2], u3b = d.bc[4 * f + 3];
+    for (int e = tid; e < nn + nT; e += NT) smd[e] = 0.0;
+    const int nsteps = n / CGRS_CR + 1;                  // chunk s: kappa pixel rows / y node rows [16 s, 16 s + 16)
+    const int npr = n >> 2;                              // threads per row (4 columns each)
+    const int npr4 = npr;                                // float4s per image row
+    // ---- the loads of chunk s into registers (kv: kappa float4, yv: y float4; kok / yok: issued)
+    // (branch-free: every thread issues both loads of every chunk -- clamped to a valid address where the
+    // chunk has no such data -- so the compiler's wait counts stay exact and the prefetch stays in flight)
+    const int64_t ycl = ytotal >= 4 ? ((ytotal - 4) & ~(int64_t)3) : 0;   // last 16-B load inside the array
+    // y's partial last float4 (N (n^2 - 1) % 4 != 0), by uniform (scalar) loads up front, outside the loop
+    const int64_t ytail = ytotal & ~(int64_t)3;
+    const int yrem = (int)(ytotal - ytail);
+    f32x4 tailv = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (yrem)
+        for (int k = 0; k < 3; ++k) tailv[k] = k < yrem ? d.y[ytail + k] : 0.f;
+    auto load_chunk = [&](int s, f32x4& kv, f32x4& yv) {
+        const int b0 = s * CGRS_CR;
+        // pixel rows [b0, b0 + 16) = image rows [n - b0 - 16, n - b0): one contiguous run
+        const int kro = b0 < n ? n - b0 - CGRS_CR : 0;
+        kv = *(const f32x4*)(lk + kro * n + 4 * tid);
+        const int64_t gs = (ybase + (int64_t)min(b0, n) * (n - 1)) & ~(int64_t)3;   // (uniform) aligned start
+        const int64_t g = min(gs + 4 * tid, ycl);
+        yv = *(const f32x4*)(d.y + g);
+    };
+    auto store_chunk = [&](int s, const f32x4& kv, const f32x4& yv) {
+        const int b0 = s * CGRS_CR;
+        if (b0 < n) {
+            const int ir = n - b0 - CGRS_CR + tid / npr4;              // image row of this float4 (4 | n)
+            const int a = 4 * tid - (tid / npr4) * n;
+            const int o = ((n - 1 - ir) * n + a) & kmask;
+            f32x4 k4;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) k4[k] = expf(kv[k]);
+            *(f32x4*)(kr + o) = k4;
+        }
+        const int j1 = min(b0 + CGRS_CR, n + 1);
+        const int64_t gs = (ybase + (int64_t)b0 * (n - 1)) & ~(int64_t)3;
+        const int lo = b0 * (n - 1), hi = j1 * (n - 1);                 // field-flat range of this chunk
+        const int idx0 = (int)(gs - ybase) + 4 * tid;
+        if (idx0 < hi) {
+            const int o = ((int)(gs - yal) + 4 * tid) & ymask;          // 16-B aligned ring slot
+            f32x4 v = yv;
+            if (gs + 4 * tid == ytail && yrem) v = tailv;      // the array's partial last float4 (loaded clamped)
+            if (idx0 >= lo && idx0 + 3 < hi) {
+                *(f32x4*)(yr + o) = v;
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (idx0 + k >= lo && idx0 + k < hi) yr[o + k] = v[k];
+            }
+        }
+    };
+    f32x4 kb[DEPTH], yb[DEPTH];
+#pragma unroll
+    for (int u = 0; u < DEPTH; ++u) load_chunk(u, kb[u], yb[u]);
+    // LDS reads with the masks; out-of-field indices are never formed (callers test the ranges)
+    auto KP = [&](int a, int b) -> float { return kr[(b * n + a) & kmask]; };
+    auto YV = [&](int i, int j) -> float { return yr[(mis + j * (n - 1) + i - 1) & ymask]; };
+    auto bcv = [&](int i, int j) -> float {
+        const float t = (float)j / (float)n;
+        return i == 0 ? (u0b * (1.f - t) + u1b * t) : (u2b * (1.f - t) + u3b * t);
+    };
+    const int ro = tid / npr, q = tid - ro * npr;
+    const int i0 = 4 * q;
+    int I = i0 / r;
+    if (I > nc - 1) I = nc - 1;
+    const int lanes_sq = r >> 2;                         // threads of one square's row (consecutive lanes)
+    for (int s0 = 0; s0 < nsteps; s0 += DEPTH) {
+#pragma unroll
+        for (int u = 0; u < DEPTH; ++u) {
+            const int s = s0 + u;
+            if (s < nsteps) store_chunk(s, kb[u], yb[u]);     // (uniform)
+            load_chunk(s + DEPTH, kb[u], yb[u]);              // (past the last chunk: clamped, unused)
+            __syncthreads();
+            // node rows of this chunk: [16 s - 1, 16 s + 15) (the last chunk: [n - 1, n])
+            const int j = s * CGRS_CR - 1 + ro;
+            const bool rowok = s < nsteps && j >= 0 && j <= n && (s < nsteps - 1 || ro < 2);
+            float c0 = 0.f, c1 = 0.f, c2 = 0.f, c3 = 0.f, flr = 0.f, ful = 0.f;
+            int J = 0;
+            if (rowok) {
+                J = min(j / r, nc - 1);
+                const int j0 = J * r;
+                const float eta = (float)(j - j0) * rinv;
+                const int tj = j - j0;
+                // row windows: y of rows j - 1, j, j + 1 at columns i0 - 1 .. i0 + 4, kappa of pixel rows j - 1, j
+                // at columns i0 - 1 .. i0 + 3
+                float yc[6], yd[4], yu[5], kc[5], kd[5];
+#pragma unroll
+                for (int t = 0; t < 6; ++t) {
+                    const int i = i0 - 1 + t;
+                    yc[t] = (i >= 1 && i <= n - 1) ? YV(i, j) : ((i == 0 || i == n) ? bcv(i, j) : 0.f);
+                }
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const int i = i0 + t;
+                    yd[t] = (i >= 1 && i <= n - 1 && j > 0) ? YV(i, j - 1) : 0.f;
+                }
+#pragma unroll
+                for (int t = 0; t < 5; ++t) {
+                    const int i = i0 + t;
+                    yu[t] = (i >= 1 && i <= n - 1 && j < n) ? YV(i, j + 1) : 0.f;
+                }
+#pragma unroll
+                for (int t = 0; t < 5; ++t) {
+                    const int a = i0 - 1 + t;
+                    kc[t] = (a >= 0 && a < n && j < n) ? KP(a, j) : 0.f;
+                    kd[t] = (a >= 0 && a < n && j > 0) ? KP(a, j - 1) : 0.f;
+                }
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const int i = i0 + t;
+                    const bool act = i >= 1 && i <= n - 1;
+                    const bool rf = i + 1 <= n - 1;
+                    const float kul = act ? kc[t] : 0.f, kur = kc[t + 1];
+                    const float kdl = act ? kd[t] : 0.f, kdr = kd[t + 1];
+                    const float ycm = act ? yc[t + 1] : 0.f, ydm = act ? yd[t] : 0.f, yum = act ? yu[t] : 0.f;
+                    const float yR = rf ? yc[t + 2] : 0.f;              // y(i + 1, j), free neighbour only
+                    const float yl = act ? yc[t] : 0.f;                 // yhat(i - 1, j)
+                    const float yrr = act ? yc[t + 2] : 0.f;            // yhat(i + 1, j)
+                    float Ky = (kul + kdl) * (ycm - yl) + (kur + kdr) * (ycm - yrr);
+                    if (j > 0) Ky += (kdl + kdr) * (ycm - ydm);
+                    if (j < n) Ky += (kul + kur) * (ycm - yum);
+                    Ky = act ? 0.5f * Ky : 0.f;
+                    const float xi = (float)(i - I * r) * rinv;
+                    if (xi >= eta) {
+                        c0 += (1.f - xi) * Ky; c1 += (xi - eta) * Ky; c3 += eta * Ky;
+                    } else {
+                        c0 += (1.f - eta) * Ky; c2 += (eta - xi) * Ky; c3 += xi * Ky;
+                    }
+                    if (FLUX && i < n && j < n) {
+                        const float u0 = ycm, u1 = yR, u2 = yum;
+                        const float u3 = rf ? yu[t + 1] : 0.f;
+                        const int tr = i - I * r;
+                        float vl = 0.f, vu = 0.f;
+                        if (tj == 0 && J > 0) vl += u1 - u3;             // bottom edge (not on y = 0)
+                        if (tr == r - 1) vl += u1 - u0;                  // right edge
+                        if (tr == 0) vu += u2 - u3;                      // left edge
+                        if (tj == r - 1 && J < nc - 1) vu += u2 - u0;    // top edge (not on y = 1)
+                        if (tr == tj) { vl += u0 - 2.f * u1 + u3; vu += u0 - 2.f * u2 + u3; }   // diagonal
+                        flr = fmaf(kur, vl, flr);
+                        ful = fmaf(kur, vu, ful);
+                    }
+                }
+            }
+            // the r / 4 threads of one square's row are consecutive lanes (npr | 64 or 64 | npr)
+            for (int o = 1; o < lanes_sq; o <<= 1) {
+                c0 += __shfl_xor(c0, o, 64);
+                c1 += __shfl_xor(c1, o, 64);
+                c2 += __shfl_xor(c2, o, 64);
+                c3 += __shfl_xor(c3, o, 64);
+                if (FLUX) {
+                    flr += __shfl_xor(flr, o, 64);
+                    ful += __shfl_xor(ful, o, 64);
+                }
+            }
+            if (rowok && (q % lanes_sq) == 0) {
+                const int v0 = I + (nc + 1) * J;
+                atomicAdd(&acc[v0], (double)c0);
+                atomicAdd(&acc[v0 + 1], (double)c1);
+                atomicAdd(&acc[v0 + nc + 1], (double)c2);
+                atomicAdd(&acc[v0 + nc + 2], (double)c3);
+                if (FLUX && j < n) {
+                    const int qq = I + nc * J;
+                    atomicAdd(&racc[2 * qq], (double)flr);
+                    atomicAdd(&racc[2 * qq + 1], (double)ful);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    if (d.r)
+        for (int e = tid; e < nn; e += NT) d.r[(int64_t)f * nn + e] = (float)acc[e];
+    if (!FLUX) return;
+    for (int e = tid; e < nT; e += NT) d.r_flux[(int64_t)f * nT + e] = (float)racc[e];
+}
+
 template <int MM>
 void launch_cgr(const gpi_residual_desc& d, int G, dim3 grid, dim3 block, size_t lds, hipStream_t st) {
     if (d.r_flux) hipLaunchKernelGGL((cgr_kernel<MM, true>), grid, block, lds, st, d, G);
@@ -177,6 +389,29 @@ extern "C" int gpi_cgr_residual(const gpi_residual_desc* d, void* stream) {
     const size_t lds = sizeof(double) * (nn + 2 * d->nc * d->nc);
     if (lds > 160 * 1024) return GPI_ERR_UNSUPPORTED;
     const int r = d->n_fine / d->nc;
+    {
+        // streaming form (cgr_stream_kernel) where its layout holds; GPI_CGR_STREAM=0 keeps the band kernel (A/B)
+        static const int stream_on = [] { const char* v = getenv("GPI_CGR_STREAM"); return v && *v ? atoi(v) : 1; }();
+        const int n = d->n_fine, ls = r >> 2;
+        const bool ok = stream_on && n % CGRS_CR == 0 && n >= CGRS_CR && n <= 256 && r % 4 == 0 &&
+                        (ls & (ls - 1)) == 0 && ((uintptr_t)d->logkappa & 15) == 0 && ((uintptr_t)d->y & 15) == 0;
+        if (ok) {
+            auto p2 = [](int v) { int p = 4; while (p < v) p <<= 1; return p; };
+            const int kr = p2(34 * n), yrn = p2(34 * (n - 1) + 4);
+            const int nd = (nn + 2 * d->nc * d->nc + 1) & ~1;
+            const size_t lds2 = sizeof(double) * nd + sizeof(float) * (kr + yrn);
+            if (lds2 <= 160 * 1024) {
+                const dim3 grid(d->n), block(4 * n);
+                const hipStream_t st = (hipStream_t)stream;
+                if (d->r_flux)
+                    hipLaunchKernelGGL((cgr_stream_kernel<GPI_CGR_DEPTH, true>), grid, block, lds2, st, *d, kr - 1, yrn - 1);
+                else
+                    hipLaunchKernelGGL((cgr_stream_kernel<GPI_CGR_DEPTH, false>), grid, block, lds2, st, *d, kr - 1, yrn - 1);
+                GPI_CHECK_LAUNCH();
+                return GPI_OK;
+            }
+        }
+    }
     const int G = (r & (r - 1)) == 0 ? (r < 64 ? r : 64) : 1;   // lanes per coarse square (see cgr_kernel)
     const int waves = d->nc < CGR_MAXW ? d->nc : CGR_MAXW;
     const int M = (d->n_fine + 63) / 64;

@@ -125,6 +125,44 @@ def test_cgr_residual_large_grids(device, n, N):
         assert np.abs(out[i] - ref).max() / np.abs(ref).max() < 1e-5
 
 
+@pytest.mark.parametrize('n,N', [(64, 7), (128, 3)])
+def test_cgr_residual_streaming_vs_band_kernel(device, n, N):
+    """The streaming residual kernel (16-B aligned fields: cgr_stream_kernel, chunked through LDS rings)
+    and the band kernel (taken for an unaligned y view, cgr_kernel) on the same fields, CGR and flux
+    rows: both within 1e-5 of the oracle's matrix-free fp64 residual, and of each other.  N (n^2 - 1) is
+    odd here, so y's last float4 is partial (the streaming kernel's clamped tail load)."""
+    import ctypes as C
+    from gpi import _lib as L
+    rng = np.random.default_rng(n + N)
+    nc = 8
+    mc, mf = fem.unit_square_mesh(nc), fem.unit_square_mesh(n)
+    W = fem.prolongation_free(mc, mf)
+    imgs = rng.normal(0.4, 0.8, (N, n, n))
+    U = rng.uniform(-0.5, 0.5, (N, 4))
+    y = rng.normal(0, 0.3, (N, W.shape[0]))
+    lk, bc = cuda(imgs), cuda(U)
+    y_al = cuda(y)
+    buf = torch.zeros(y.size + 1, device='cuda')
+    buf[1:] = y_al.reshape(-1)
+    y_un = buf[1:].view(N, -1)                        # 4-B aligned only: the band kernel
+    assert y_al.data_ptr() % 16 == 0 and y_un.data_ptr() % 16 != 0
+    outs = []
+    for yy in (y_al, y_un):
+        r = torch.zeros(N, (nc + 1) ** 2, device='cuda')
+        rf = torch.zeros(N, 2 * nc * nc, device='cuda')
+        d = L.ResidualDesc(n_fine=n, nc=nc, n=N, logkappa=lk.data_ptr(), y=yy.data_ptr(), bc=bc.data_ptr(),
+                           r=r.data_ptr(), r_flux=rf.data_ptr())
+        L.check(L.lib().gpi_cgr_residual(C.byref(d), L.stream_handle()), 'residual')
+        outs.append((r.cpu().numpy(), rf.cpu().numpy()))
+    for i in range(N):
+        ref = W.T @ fem.fom_residual(mf, np.exp(fem.image_to_cells(imgs[i])), U[i], y[i])
+        for r, _ in outs:
+            assert np.abs(r[i] - ref).max() / np.abs(ref).max() < 1e-5
+    (ra, fa), (rb, fb) = outs
+    assert np.abs(ra - rb).max() / np.abs(rb).max() < 1e-5
+    assert np.abs(fa - fb).max() / np.abs(fb).max() < 1e-5
+
+
 def test_cgr_residual_vanishes_at_fom_solution(device):
     from gpi.engine import cgr_residual
     rng = np.random.default_rng(0)

@@ -7,7 +7,7 @@ the SyncBN step must also agree with the replica-BN step to rounding (the same b
 graph) and takes its 3 steps by run(3).
 usage: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 tools/dist_capture_probe.py
        [--sync-bn] [--unroll K] [--config c32|c64]
---config c64: BASELINE config 3's per-rank shape (C64 highres codec, B_u = 256, N_s = 32, Dropout2d 0.2; 46 SyncBN
+--config c64: BASELINE config 3's per-rank shape (C64 highres codec, B_u = 256, N_s = 32, Dropout2d 0.2; 42 SyncBN
 collectives per step) instead of the C32 golden fixture."""
 import copy
 import os
