@@ -1,1 +1,1 @@
-extern "C" const char* gpi_source_sha(void) { return "921dc086b6a93a0ab6694d0b10cd3b2106015a40"; }
+extern "C" const char* gpi_source_sha(void) { return "affa6b66e18b4558afbc4bb738844e97589162bd"; }

@@ -22,6 +22,7 @@
 using namespace gpi;
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 namespace {
 
@@ -162,105 +163,98 @@ __global__ __launch_bounds__(64 * CGR_MAXW) void cgr_kernel(gpi_residual_desc d,
     for (int e = threadIdx.x; e < nT; e += blockDim.x) d.r_flux[(int64_t)f * nT + e] = (float)racc[e];
 }
 
-// Streaming form (16-B aligned fields, n % 16 == 0, n <= 256, r % 4 == 0: 32^2 ... 256^2 at nc = 8).
-// One workgroup of NT = 4 n threads per field walks the field bottom-up in chunks of CR = 16 node rows.
-// Every thread loads ONE float4 of log kappa and ONE float4 of y per chunk, DEPTH chunks ahead of the
-// chunk it consumes (registers: the loads of DEPTH chunks are in flight while a chunk is computed), takes
-// exp once per pixel, and writes both into LDS rings indexed by the field-flat element index masked to a
-// power of two (y rows are (n - 1) floats: not 16-B aligned, so y's ring index is relative to the field's
-// 16-B aligned-down base and a float4 never straddles the wrap).  After one barrier per chunk, every
-// thread computes 4 adjacent nodes of one row from LDS (the same arithmetic as cgr_kernel), accumulates
-// their W^T contributions -- all four in one coarse square, r % 4 == 0 -- and adds them (after a shuffle
-// over the r / 4 threads of the square's row) into the fp64 LDS accumulators.  The ring holds 2 CR + 2
-// rows, so chunk s + 1's writes never touch the rows chunk s's computation reads (one barrier per chunk).
+// Streaming form (16-B aligned fields, n % 16 == 0, 16 <= n <= 256, r = n / nc a power of two >= 4: 32^2 ...
+// 256^2 at nc = 8).  One workgroup of NT = 4 n threads per field walks the field bottom-up in chunks of CR = 16
+// node rows.  Every thread loads ONE float4 of log kappa and ONE float4 of y per chunk, DEPTH chunks ahead of
+// the one it consumes, takes exp once per pixel and scatters both into LDS rows: three chunk slots of 16 rows,
+// pitch n + 4, column i of a row at 1 + i.  y rows carry yhat: the Dirichlet data of columns 0 and n are written
+// next to the free values, so the stencil needs no boundary branch; the pad columns (-1, n + 1, n + 2) stay
+// zero.  After one barrier per chunk, thread (ro, q) computes the 4 nodes i0 = 4q .. 4q + 3 of node row
+// j = 16 s - 1 + ro from 16-B LDS reads (3 y rows, 2 kappa rows), restricts them with W^T -- the four are in one
+// coarse square, r % 4 == 0; the P1 weights by min / max, no branch -- and adds the square's four corner sums
+// (after a shuffle over the r / 4 threads of the square's row) into fp64 LDS accumulators.  The arithmetic per
+// node is cgr_kernel's (same products, same order).  Chunk s + 1 is written into the slot of chunk s - 2,
+// which no thread reads after the barrier of chunk s: one barrier per chunk.
 constexpr int CGRS_CR = 16;        // node rows per chunk
 #ifndef GPI_CGR_DEPTH
-#define GPI_CGR_DEPTH 3            // chunks in flight ahead of the one computed
+#define GPI_CGR_DEPTH 2            // chunks in flight ahead of the one computed
 #endif
+__host__ __device__ inline int cgrs_pitch(int n) { return n + 4; }
 template <int DEPTH, bool FLUX>
-__global__ __launch_bounds__(1024) void cgr_stream_kernel(gpi_residual_desc d, int kmask, int ymask) {
+__global__ __launch_bounds__(1024) void cgr_stream_kernel(gpi_residual_desc d, int lr) {
     extern __shared__ __attribute__((aligned(16))) double smd[];
     const int n = d.n_fine, nc = d.nc, nn = (nc + 1) * (nc + 1), nT = 2 * nc * nc;
-    const int r = n / nc;
+    const int r = 1 << lr;
     const float rinv = 1.f / (float)r;
     const int NT = blockDim.x, tid = threadIdx.x;
+    const int PT = cgrs_pitch(n), SLOT = CGRS_CR * PT;
     double* acc = smd;                                   // [nn]
     double* racc = smd + nn;                             // [nT]
-    float* kr = (float*)(smd + ((nn + nT + 1) & ~1));    // kappa ring [kmask + 1] (16-B aligned)
-    float* yr = kr + kmask + 1;                          // y ring [ymask + 1]
+    float* kr = (float*)(smd + ((nn + nT + 1) & ~1));    // kappa rows [3 slots][16][PT] (16-B aligned)
+    float* yr = kr + 3 * SLOT;                           // y rows, the same layout
     const int f = blockIdx.x;
     const int ny = (n + 1) * (n - 1);                    // y values per field
     const float* lk = d.logkappa + (int64_t)f * n * n;
-    const int64_t ybase = (int64_t)f * ny;               // field's first y element (flat, whole array)
-    const int64_t yal = ybase & ~(int64_t)3;             // ... aligned down to 16 B
-    const int mis = (int)(ybase - yal);
+    const int64_t ybase = (int64_t)f * ny;
     const int64_t ytotal = (int64_t)d.n * ny;
     const float u0b = d.bc[4 * f], u1b = d.bc[4 * f + 1], u2b = d.bc[4 * f + 2], u3b = d.bc[4 * f + 3];
     for (int e = tid; e < nn + nT; e += NT) smd[e] = 0.0;
+    for (int e = tid; e < (6 * SLOT + PT) / 4; e += NT) reinterpret_cast<f32x4*>(kr)[e] = f32x4{0.f, 0.f, 0.f, 0.f};
+    __syncthreads();                                     // (the pads stay zero; chunk stores come after)
     const int nsteps = n / CGRS_CR + 1;                  // chunk s: kappa pixel rows / y node rows [16 s, 16 s + 16)
     const int npr = n >> 2;                              // threads per row (4 columns each)
-    const int npr4 = npr;                                // float4s per image row
-    // ---- the loads of chunk s into registers (kv: kappa float4, yv: y float4; kok / yok: issued)
-    // (branch-free: every thread issues both loads of every chunk -- clamped to a valid address where the
+    const int ro = tid / npr, q = tid - ro * npr;
+    // (branch-free: every thread issues all loads of every chunk -- clamped to a valid address where the
     // chunk has no such data -- so the compiler's wait counts stay exact and the prefetch stays in flight)
-    const int64_t ycl = ytotal >= 4 ? ((ytotal - 4) & ~(int64_t)3) : 0;   // last 16-B load inside the array
-    // y's partial last float4 (N (n^2 - 1) % 4 != 0), by uniform (scalar) loads up front, outside the loop
-    const int64_t ytail = ytotal & ~(int64_t)3;
-    const int yrem = (int)(ytotal - ytail);
-    f32x4 tailv = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (yrem)
-        for (int k = 0; k < 3; ++k) tailv[k] = k < yrem ? d.y[ytail + k] : 0.f;
+    // y: thread (ro, q) loads the free values 4 q .. 4 q + 3 (columns 4 q + 1 .. 4 q + 4) of node row 16 s + ro by
+    // four dword loads (rows of n - 1 floats are not 16-B aligned); the last one of q = n / 4 - 1 is column n,
+    // whose Dirichlet value it writes instead
+    const int64_t ylast = ytotal - 1;
     auto load_chunk = [&](int s, f32x4& kv, f32x4& yv) {
         const int b0 = s * CGRS_CR;
         // pixel rows [b0, b0 + 16) = image rows [n - b0 - 16, n - b0): one contiguous run
         const int kro = b0 < n ? n - b0 - CGRS_CR : 0;
         kv = *(const f32x4*)(lk + kro * n + 4 * tid);
-        const int64_t gs = (ybase + (int64_t)min(b0, n) * (n - 1)) & ~(int64_t)3;   // (uniform) aligned start
-        const int64_t g = min(gs + 4 * tid, ycl);
-        yv = *(const f32x4*)(d.y + g);
+        const int jj = min(b0 + ro, n);
+        const int64_t g = ybase + (int64_t)jj * (n - 1) + 4 * q;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) yv[k] = d.y[min(g + k, ylast)];
     };
+    // LDS position of column i (-1 .. n + 2) of node / pixel row j (>= 0); zrow: a zero row
+    auto rowpos = [&](int j) -> int { return ((j >> 4) % 3) * SLOT + (j & 15) * PT + 1; };
+    const int zrow = 6 * SLOT + 1;
+    const float fn = (float)n;
+    auto bcv = [&](int i, int j) -> float {
+        const float t = (float)j / fn;
+        return i == 0 ? (u0b * (1.f - t) + u1b * t) : (u2b * (1.f - t) + u3b * t);
+    };
+    constexpr float LOG2E = 1.4426950408889634f;
     auto store_chunk = [&](int s, const f32x4& kv, const f32x4& yv) {
         const int b0 = s * CGRS_CR;
         if (b0 < n) {
-            const int ir = n - b0 - CGRS_CR + tid / npr4;              // image row of this float4 (4 | n)
-            const int a = 4 * tid - (tid / npr4) * n;
-            const int o = ((n - 1 - ir) * n + a) & kmask;
-            f32x4 k4;
+            const int q4 = tid / npr;
+            const int pb = b0 + CGRS_CR - 1 - q4;                       // pixel row (from the bottom) of image row
+            const int a = 4 * (tid - q4 * npr);                         // n - b0 - 16 + q4
+            float* p = kr + rowpos(pb) + a;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) k4[k] = expf(kv[k]);
-            *(f32x4*)(kr + o) = k4;
+            for (int k = 0; k < 4; ++k) p[k] = __builtin_amdgcn_exp2f(kv[k] * LOG2E);
         }
-        const int j1 = min(b0 + CGRS_CR, n + 1);
-        const int64_t gs = (ybase + (int64_t)b0 * (n - 1)) & ~(int64_t)3;
-        const int lo = b0 * (n - 1), hi = j1 * (n - 1);                 // field-flat range of this chunk
-        const int idx0 = (int)(gs - ybase) + 4 * tid;
-        if (idx0 < hi) {
-            const int o = ((int)(gs - yal) + 4 * tid) & ymask;          // 16-B aligned ring slot
+        const int jj = b0 + ro;
+        if (jj <= n) {
+            float* p = yr + rowpos(jj) + 4 * q + 1;                     // column 4 q + 1 (8-B aligned)
             f32x4 v = yv;
-            if (gs + 4 * tid == ytail && yrem) v = tailv;      // the array's partial last float4 (loaded clamped)
-            if (idx0 >= lo && idx0 + 3 < hi) {
-                *(f32x4*)(yr + o) = v;
-            } else {
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    if (idx0 + k >= lo && idx0 + k < hi) yr[o + k] = v[k];
-            }
+            if (q == npr - 1) v[3] = bcv(n, jj);
+            *(f32x2*)p = f32x2{v[0], v[1]};
+            *(f32x2*)(p + 2) = f32x2{v[2], v[3]};
+            if (q == 0) p[-1] = bcv(0, jj);
         }
     };
     f32x4 kb[DEPTH], yb[DEPTH];
 #pragma unroll
     for (int u = 0; u < DEPTH; ++u) load_chunk(u, kb[u], yb[u]);
-    // LDS reads with the masks; out-of-field indices are never formed (callers test the ranges)
-    auto KP = [&](int a, int b) -> float { return kr[(b * n + a) & kmask]; };
-    auto YV = [&](int i, int j) -> float { return yr[(mis + j * (n - 1) + i - 1) & ymask]; };
-    auto bcv = [&](int i, int j) -> float {
-        const float t = (float)j / (float)n;
-        return i == 0 ? (u0b * (1.f - t) + u1b * t) : (u2b * (1.f - t) + u3b * t);
-    };
-    const int ro = tid / npr, q = tid - ro * npr;
     const int i0 = 4 * q;
-    int I = i0 / r;
-    if (I > nc - 1) I = nc - 1;
+    const int I = i0 >> lr;                              // < nc (i0 + 3 < n)
+    const int tr0 = i0 - (I << lr);
     const int lanes_sq = r >> 2;                         // threads of one square's row (consecutive lanes)
     for (int s0 = 0; s0 < nsteps; s0 += DEPTH) {
 #pragma unroll
@@ -275,59 +269,49 @@ __global__ __launch_bounds__(1024) void cgr_stream_kernel(gpi_residual_desc d, i
             float c0 = 0.f, c1 = 0.f, c2 = 0.f, c3 = 0.f, flr = 0.f, ful = 0.f;
             int J = 0;
             if (rowok) {
-                J = min(j / r, nc - 1);
-                const int j0 = J * r;
-                const float eta = (float)(j - j0) * rinv;
-                const int tj = j - j0;
-                // row windows: y of rows j - 1, j, j + 1 at columns i0 - 1 .. i0 + 4, kappa of pixel rows j - 1, j
-                // at columns i0 - 1 .. i0 + 3
-                float yc[6], yd[4], yu[5], kc[5], kd[5];
-#pragma unroll
-                for (int t = 0; t < 6; ++t) {
-                    const int i = i0 - 1 + t;
-                    yc[t] = (i >= 1 && i <= n - 1) ? YV(i, j) : ((i == 0 || i == n) ? bcv(i, j) : 0.f);
-                }
-#pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    const int i = i0 + t;
-                    yd[t] = (i >= 1 && i <= n - 1 && j > 0) ? YV(i, j - 1) : 0.f;
-                }
-#pragma unroll
-                for (int t = 0; t < 5; ++t) {
-                    const int i = i0 + t;
-                    yu[t] = (i >= 1 && i <= n - 1 && j < n) ? YV(i, j + 1) : 0.f;
-                }
-#pragma unroll
-                for (int t = 0; t < 5; ++t) {
-                    const int a = i0 - 1 + t;
-                    kc[t] = (a >= 0 && a < n && j < n) ? KP(a, j) : 0.f;
-                    kd[t] = (a >= 0 && a < n && j > 0) ? KP(a, j - 1) : 0.f;
-                }
+                J = min(j >> lr, nc - 1);
+                const int tj = j - J * r;
+                const float eta = (float)tj * rinv;
+                // row windows (columns i0 - 1 .. i0 + 6): yhat of rows j - 1, j, j + 1; kappa of pixel rows j - 1, j;
+                // rows outside the field (y row -1 / n + 1, kappa row -1 / n) read the zero row
+                const bool jdn = j > 0, jup = j < n;
+                const int pc = rowpos(j) + i0 - 1;
+                const int pd = (jdn ? rowpos(j - 1) : zrow) + i0 - 1, pu = (jup ? rowpos(j + 1) : zrow) + i0 - 1;
+                const int pk = (jup ? rowpos(j) : zrow) + i0 - 1;
+                const f32x4 yc0 = *(const f32x4*)(yr + pc), yd0 = *(const f32x4*)(yr + pd), yu0 = *(const f32x4*)(yr + pu);
+                const f32x4 yc1 = *(const f32x4*)(yr + pc + 4), yd1 = *(const f32x4*)(yr + pd + 4),
+                            yu1 = *(const f32x4*)(yr + pu + 4);
+                const f32x4 kc0 = *(const f32x4*)(kr + pk), kd0 = *(const f32x4*)(kr + pd);
+                const float kc4 = kr[pk + 4], kd4 = kr[pd + 4];
+                const float yc[6] = {yc0[0], yc0[1], yc0[2], yc0[3], yc1[0], yc1[1]};
+                const float yd[4] = {yd0[1], yd0[2], yd0[3], yd1[0]};
+                const float yu[5] = {yu0[1], yu0[2], yu0[3], yu1[0], yu1[1]};
+                const float kc[5] = {kc0[0], kc0[1], kc0[2], kc0[3], kc4};
+                const float kd[5] = {kd0[0], kd0[1], kd0[2], kd0[3], kd4};
 #pragma unroll
                 for (int t = 0; t < 4; ++t) {
                     const int i = i0 + t;
-                    const bool act = i >= 1 && i <= n - 1;
-                    const bool rf = i + 1 <= n - 1;
+                    const bool act = t > 0 || i0 > 0;                   // i >= 1 (i <= n - 1 always)
                     const float kul = act ? kc[t] : 0.f, kur = kc[t + 1];
                     const float kdl = act ? kd[t] : 0.f, kdr = kd[t + 1];
                     const float ycm = act ? yc[t + 1] : 0.f, ydm = act ? yd[t] : 0.f, yum = act ? yu[t] : 0.f;
-                    const float yR = rf ? yc[t + 2] : 0.f;              // y(i + 1, j), free neighbour only
                     const float yl = act ? yc[t] : 0.f;                 // yhat(i - 1, j)
                     const float yrr = act ? yc[t + 2] : 0.f;            // yhat(i + 1, j)
+                    // (rows outside the field: zero conductances, the terms add +-0)
                     float Ky = (kul + kdl) * (ycm - yl) + (kur + kdr) * (ycm - yrr);
-                    if (j > 0) Ky += (kdl + kdr) * (ycm - ydm);
-                    if (j < n) Ky += (kul + kur) * (ycm - yum);
+                    Ky += (kdl + kdr) * (ycm - ydm);
+                    Ky += (kul + kur) * (ycm - yum);
                     Ky = act ? 0.5f * Ky : 0.f;
-                    const float xi = (float)(i - I * r) * rinv;
-                    if (xi >= eta) {
-                        c0 += (1.f - xi) * Ky; c1 += (xi - eta) * Ky; c3 += eta * Ky;
-                    } else {
-                        c0 += (1.f - eta) * Ky; c2 += (eta - xi) * Ky; c3 += xi * Ky;
-                    }
-                    if (FLUX && i < n && j < n) {
-                        const float u0 = ycm, u1 = yR, u2 = yum;
+                    const float xi = (float)(tr0 + t) * rinv;
+                    c0 += (1.f - fmaxf(xi, eta)) * Ky;
+                    c1 += fmaxf(xi - eta, 0.f) * Ky;
+                    c2 += fmaxf(eta - xi, 0.f) * Ky;
+                    c3 += fminf(xi, eta) * Ky;
+                    if (FLUX && jup) {
+                        const bool rf = i + 1 <= n - 1;
+                        const float u0 = ycm, u1 = rf ? yc[t + 2] : 0.f, u2 = yum;
                         const float u3 = rf ? yu[t + 1] : 0.f;
-                        const int tr = i - I * r;
+                        const int tr = tr0 + t;
                         float vl = 0.f, vu = 0.f;
                         if (tj == 0 && J > 0) vl += u1 - u3;             // bottom edge (not on y = 0)
                         if (tr == r - 1) vl += u1 - u0;                  // right edge
@@ -350,7 +334,7 @@ __global__ __launch_bounds__(1024) void cgr_stream_kernel(gpi_residual_desc d, i
                     ful += __shfl_xor(ful, o, 64);
                 }
             }
-            if (rowok && (q % lanes_sq) == 0) {
+            if (rowok && (q & (lanes_sq - 1)) == 0) {
                 const int v0 = I + (nc + 1) * J;
                 atomicAdd(&acc[v0], (double)c0);
                 atomicAdd(&acc[v0 + 1], (double)c1);
@@ -392,21 +376,32 @@ extern "C" int gpi_cgr_residual(const gpi_residual_desc* d, void* stream) {
     {
         // streaming form (cgr_stream_kernel) where its layout holds; GPI_CGR_STREAM=0 keeps the band kernel (A/B)
         static const int stream_on = [] { const char* v = getenv("GPI_CGR_STREAM"); return v && *v ? atoi(v) : 1; }();
-        const int n = d->n_fine, ls = r >> 2;
-        const bool ok = stream_on && n % CGRS_CR == 0 && n >= CGRS_CR && n <= 256 && r % 4 == 0 &&
-                        (ls & (ls - 1)) == 0 && ((uintptr_t)d->logkappa & 15) == 0 && ((uintptr_t)d->y & 15) == 0;
+        const int n = d->n_fine;
+        const bool ok = stream_on && n % CGRS_CR == 0 && n >= CGRS_CR && n <= 256 && r >= 4 && (r & (r - 1)) == 0 &&
+                        ((uintptr_t)d->logkappa & 15) == 0 && ((uintptr_t)d->y & 15) == 0;
         if (ok) {
-            auto p2 = [](int v) { int p = 4; while (p < v) p <<= 1; return p; };
-            const int kr = p2(34 * n), yrn = p2(34 * (n - 1) + 4);
+            int lr = 0;
+            while ((1 << lr) < r) ++lr;
             const int nd = (nn + 2 * d->nc * d->nc + 1) & ~1;
-            const size_t lds2 = sizeof(double) * nd + sizeof(float) * (kr + yrn);
+            const size_t lds2 = sizeof(double) * nd + sizeof(float) * (6 * CGRS_CR + 1) * cgrs_pitch(n);
             if (lds2 <= 160 * 1024) {
+                if (lds2 > 64 * 1024) {
+                    static bool attr = false;
+                    if (!attr) {
+                        for (const void* k : {(const void*)cgr_stream_kernel<GPI_CGR_DEPTH, true>,
+                                              (const void*)cgr_stream_kernel<GPI_CGR_DEPTH, false>})
+                            if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
+                                hipSuccess)
+                                return GPI_ERR_LAUNCH;
+                        attr = true;
+                    }
+                }
                 const dim3 grid(d->n), block(4 * n);
                 const hipStream_t st = (hipStream_t)stream;
                 if (d->r_flux)
-                    hipLaunchKernelGGL((cgr_stream_kernel<GPI_CGR_DEPTH, true>), grid, block, lds2, st, *d, kr - 1, yrn - 1);
+                    hipLaunchKernelGGL((cgr_stream_kernel<GPI_CGR_DEPTH, true>), grid, block, lds2, st, *d, lr);
                 else
-                    hipLaunchKernelGGL((cgr_stream_kernel<GPI_CGR_DEPTH, false>), grid, block, lds2, st, *d, kr - 1, yrn - 1);
+                    hipLaunchKernelGGL((cgr_stream_kernel<GPI_CGR_DEPTH, false>), grid, block, lds2, st, *d, lr);
                 GPI_CHECK_LAUNCH();
                 return GPI_OK;
             }

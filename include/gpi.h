@@ -431,7 +431,7 @@ typedef struct gpi_adam_desc {
 int gpi_version(void);
 /* GPI_REPLICAS of this build (bindings size their statistics / term buffers by it). */
 int gpi_replicas(void);
-/* sha1 (40 hex digits) of the sources this library was built from: csrc/*.hip in name order, then
+/* sha1 (40 hex digits) of the sources this library was built from: the csrc .hip files in name order, then
  * csrc/common.h and include/gpi.h, concatenated (bindings refuse a library older than its sources). */
 const char* gpi_source_sha(void);
 /* sizeof of every struct above, in declaration order (ABI self-check); returns the count. */
