@@ -18,6 +18,7 @@
 // Gamma keeps free columns only).  Same closed forms as vo.hip's vo_query_flux.
 #include "common.h"
 #include <stdlib.h>
+#include <type_traits>
 
 using namespace gpi;
 
@@ -180,7 +181,8 @@ constexpr int CGRS_CR = 16;        // node rows per chunk
 #define GPI_CGR_DEPTH 2            // chunks in flight ahead of the one computed
 #endif
 __host__ __device__ inline int cgrs_pitch(int n) { return n + 4; }
-template <int DEPTH, bool FLUX>
+template <int DEPTH, bool FLUX, int NS>   // NS > 0: the chunk count n / 16 + 1 at compile time (loop fully
+                                         // unrolled: exact wait counts, every chunk's loads DEPTH chunks ahead)
 __global__ __launch_bounds__(1024) void cgr_stream_kernel(gpi_residual_desc d, int lr) {
     extern __shared__ __attribute__((aligned(16))) double smd[];
     const int n = d.n_fine, nc = d.nc, nn = (nc + 1) * (nc + 1), nT = 2 * nc * nc;
@@ -201,7 +203,7 @@ __global__ __launch_bounds__(1024) void cgr_stream_kernel(gpi_residual_desc d, i
     for (int e = tid; e < nn + nT; e += NT) smd[e] = 0.0;
     for (int e = tid; e < (6 * SLOT + PT) / 4; e += NT) reinterpret_cast<f32x4*>(kr)[e] = f32x4{0.f, 0.f, 0.f, 0.f};
     __syncthreads();                                     // (the pads stay zero; chunk stores come after)
-    const int nsteps = n / CGRS_CR + 1;                  // chunk s: kappa pixel rows / y node rows [16 s, 16 s + 16)
+    const int nsteps = NS > 0 ? NS : n / CGRS_CR + 1;   // chunk s: kappa pixel rows / y node rows [16 s, 16 s + 16)
     const int npr = n >> 2;                              // threads per row (4 columns each)
     const int ro = tid / npr, q = tid - ro * npr;
     // (branch-free: every thread issues all loads of every chunk -- clamped to a valid address where the
@@ -256,7 +258,8 @@ __global__ __launch_bounds__(1024) void cgr_stream_kernel(gpi_residual_desc d, i
     const int I = i0 >> lr;                              // < nc (i0 + 3 < n)
     const int tr0 = i0 - (I << lr);
     const int lanes_sq = r >> 2;                         // threads of one square's row (consecutive lanes)
-    for (int s0 = 0; s0 < nsteps; s0 += DEPTH) {
+#pragma unroll
+    for (int s0 = 0; s0 < (NS > 0 ? NS : nsteps); s0 += DEPTH) {
 #pragma unroll
         for (int u = 0; u < DEPTH; ++u) {
             const int s = s0 + u;
@@ -385,23 +388,29 @@ extern "C" int gpi_cgr_residual(const gpi_residual_desc* d, void* stream) {
             const int nd = (nn + 2 * d->nc * d->nc + 1) & ~1;
             const size_t lds2 = sizeof(double) * nd + sizeof(float) * (6 * CGRS_CR + 1) * cgrs_pitch(n);
             if (lds2 <= 160 * 1024) {
-                if (lds2 > 64 * 1024) {
-                    static bool attr = false;
-                    if (!attr) {
-                        for (const void* k : {(const void*)cgr_stream_kernel<GPI_CGR_DEPTH, true>,
-                                              (const void*)cgr_stream_kernel<GPI_CGR_DEPTH, false>})
-                            if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
-                                hipSuccess)
-                                return GPI_ERR_LAUNCH;
-                        attr = true;
-                    }
-                }
                 const dim3 grid(d->n), block(4 * n);
                 const hipStream_t st = (hipStream_t)stream;
-                if (d->r_flux)
-                    hipLaunchKernelGGL((cgr_stream_kernel<GPI_CGR_DEPTH, true>), grid, block, lds2, st, *d, lr);
-                else
-                    hipLaunchKernelGGL((cgr_stream_kernel<GPI_CGR_DEPTH, false>), grid, block, lds2, st, *d, lr);
+                const bool fl = d->r_flux != nullptr;
+                auto go = [&](auto ns_c) -> int {
+                    constexpr int NS = decltype(ns_c)::value;
+                    const void* k = fl ? (const void*)cgr_stream_kernel<GPI_CGR_DEPTH, true, NS>
+                                       : (const void*)cgr_stream_kernel<GPI_CGR_DEPTH, false, NS>;
+                    if (lds2 > 64 * 1024 &&
+                        hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2) != hipSuccess)
+                        return GPI_ERR_LAUNCH;
+                    if (fl) hipLaunchKernelGGL((cgr_stream_kernel<GPI_CGR_DEPTH, true, NS>), grid, block, lds2, st, *d, lr);
+                    else hipLaunchKernelGGL((cgr_stream_kernel<GPI_CGR_DEPTH, false, NS>), grid, block, lds2, st, *d, lr);
+                    return GPI_OK;
+                };
+                int rc;
+                switch (n) {
+                    case 32: rc = go(std::integral_constant<int, 3>{}); break;
+                    case 64: rc = go(std::integral_constant<int, 5>{}); break;
+                    case 128: rc = go(std::integral_constant<int, 9>{}); break;
+                    case 256: rc = go(std::integral_constant<int, 17>{}); break;
+                    default: rc = go(std::integral_constant<int, 0>{}); break;
+                }
+                if (rc != GPI_OK) return rc;
                 GPI_CHECK_LAUNCH();
                 return GPI_OK;
             }

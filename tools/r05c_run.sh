@@ -3,10 +3,9 @@ R=$(pwd); OUT=$R/gpurun_out; mkdir -p $OUT
 T=${1:-r05c}
 timeout -k 10 300 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 200 --timeout-method thread -k "cgr or flux or residual" > $OUT/${T}_tests.log 2>&1
 rc=$?; tail -4 $OUT/${T}_tests.log; [ $rc -eq 0 ] || exit $rc
-for arm in "-" "GPI_LIB_VARIANT=d3"; do
+for arm in "-" "GPI_LIB_VARIANT=d3" "GPI_LIB_VARIANT=d4"; do
   E=""; [ "$arm" = "-" ] || E="$arm"
-  env $E timeout -k 10 200 python -u tools/residual_bench.py > $OUT/${T}_res_${arm%%=*}.log 2>&1
-  rc=$?; echo "residual [$arm] rc=$rc"; grep '"flux"' $OUT/${T}_res_${arm%%=*}.log | cut -c1-150; [ $rc -eq 0 ] || exit $rc
+  env $E timeout -k 10 200 python -u tools/residual_bench.py > $OUT/${T}_res_$(echo $arm | tr = _).log 2>&1
+  rc=$?; echo "residual [$arm] rc=$rc"; grep '"flux"' $OUT/${T}_res_$(echo $arm | tr = _).log | cut -c1-150; [ $rc -eq 0 ] || exit $rc
 done
 cd /tmp && export TMPDIR=/tmp
-timeout -s KILL 90 rocprofv3 -L > $OUT/${T}_counters_list.txt 2>&1; echo "list rc=$?"
