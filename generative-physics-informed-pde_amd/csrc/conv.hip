@@ -1106,6 +1106,17 @@ struct IntC {
     static constexpr int value = V;
 };
 
+// GPI_IG_PRE: the MFMA input gradient's accumulated S_in operands of the second pixel round (tiles of > 256
+// owned pixels) are loaded in phase 1 with the first round's, instead of at the round's start (a global
+// round trip inside the compute phase)
+#ifndef GPI_IG_PRE
+#define GPI_IG_PRE 0
+#endif
+// occupancy target (waves per SIMD) of the 1x1 / 3x3 / 7x7 backward instantiations (no C64 backward launch
+// holds more than 5 workgroups per CU; 4 / 5 / 6 measured alike, r04r)
+#ifndef GPI_BWD_WAVES
+#define GPI_BWD_WAVES 6
+#endif
 // per-wave input-channel sums [2][4 waves][32] (256 floats) alias the offset table (>= 256 floats)
 constexpr int SLAB_ROWS = 4;    // partial-slab rows per workgroup: one per wave (no cross-wave dW reduction;
                                 // vop ops: summed in LDS, one row per workgroup)
@@ -1138,7 +1149,7 @@ __host__ __device__ constexpr bool fuse_wlds(int ky) {
 }
 
 template <int K, int S, int UP, bool FUSE = false, bool HALF = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (FUSE ? GPI_FUSE_WAVES : 4) : 6))) void conv_bwd_kernel(gpi_conv_desc d, gpi_codec_ctx c, ConvGeom G) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (FUSE ? GPI_FUSE_WAVES : 4) : GPI_BWD_WAVES))) void conv_bwd_kernel(gpi_conv_desc d, gpi_codec_ctx c, ConvGeom G) {
     touch_kernargs<CONV_KARG_BYTES>();
     entry_signal(G);
     if (SKIP(G, 16)) return;
@@ -1323,17 +1334,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
     const bool cok = l16 < d.cin;
     const int64_t ibase = ((int64_t)T.b * d.in_ctot + d.in_c0 + ci_l) * HWi + (int64_t)py0 * d.w_in;
     f32x4 pv4[4];
-    auto own_load = [&](int round) {
+#if GPI_IG_PRE
+    f32x4 pv4b[4];            // round 1's operands, loaded with round 0's in phase 1 (GPI_IG_PRE)
+#endif
+    auto own_load = [&](int round, f32x4 (&dst)[4]) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int m = wv + 4 * (4 * round + u);
             const bool ok = m < nmblk && cok;
             const int64_t o = ibase + 16 * m + 4 * kq;
-            if (d.gin_accumulate) pv4[u] = *as_gld((const f32x4*)(ok ? ws + gin_off + o : zero));
-            else pv4[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (d.gin_accumulate) dst[u] = *as_gld((const f32x4*)(ok ? ws + gin_off + o : zero));
+            else dst[u] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
     };
-    if (nmblk > 0 && S != 2) own_load(0);
+    if (nmblk > 0 && S != 2) {
+        own_load(0, pv4);
+#if GPI_IG_PRE
+        if (nmblk > 16) own_load(1, pv4b);
+#endif
+    }
     PHASE(9);
     float gam = 0.f, bet = 0.f;
     if (d.in_bn && tid < d.cin) {
@@ -1870,7 +1889,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
         const float* arow0 = alb + (ci_l * Gt.rh + (py0 - iy0)) * Gt.P + HALO;   // owned row 0 of channel l16
         const int nkd = KD4 >> 2;
         for (int round = 0; wv + 16 * round < nmblk; ++round) {
-            if (round > 0 && S != 2) own_load(round);
+            if (round > 0 && S != 2) {
+#if GPI_IG_PRE
+                if (round == 1) {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) pv4[u] = pv4b[u];
+                } else
+#endif
+                own_load(round, pv4);
+            }
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const int m = wv + 4 * (4 * round + u);
