@@ -358,6 +358,253 @@ __global__ __launch_bounds__(1024) void cgr_stream_kernel(gpi_residual_desc d, i
     for (int e = tid; e < nT; e += NT) d.r_flux[(int64_t)f * nT + e] = (float)racc[e];
 }
 
+// Band form without barriers (nc <= 16 bands of r = n / nc rows, 64 * MM >= n columns): one wave per coarse
+// row band, lane = column (MM columns per lane, 64 apart), rows in order with the band's rows loaded
+// PF rows ahead into registers (the loop is unrolled: R rows, + 1 in the top band, at compile time), one exp
+// per pixel, the row neighbours (kappa of pixel i - 1, yhat of nodes i -+ 1) by DPP wave shifts (the lane
+// crossing a 64-column chunk edge takes its neighbour's value by readlane), the W^T-restricted contributions
+// of a lane's nodes -- all in one coarse square over the band -- accumulated in registers over the band
+// and reduced once at its end (shuffles over the square's r lanes, 4 fp64 LDS adds per square).  The
+// arithmetic per node is cgr_kernel's.
+__device__ __forceinline__ float dpp_shr1(float v, float in0) {      // lane l <- lane l - 1; lane 0 <- in0
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(in0), __float_as_int(v), 0x138, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float dpp_shl1(float v, float in63) {     // lane l <- lane l + 1; lane 63 <- in63
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(in63), __float_as_int(v), 0x130, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float lane_of(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+// f(0), f(1), ..., f(N - 1) with compile-time arguments (a fully unrolled loop whatever the body's size)
+template <int I, int N>
+struct StaticFor {
+    template <typename F>
+    __device__ __forceinline__ static void run(F& f) {
+        f(std::integral_constant<int, I>{});
+        StaticFor<I + 1, N>::run(f);
+    }
+};
+template <int N>
+struct StaticFor<N, N> {
+    template <typename F>
+    __device__ __forceinline__ static void run(F&) {}
+};
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F& f) { StaticFor<0, N>::run(f); }
+
+#ifndef GPI_CGR_PF
+#define GPI_CGR_PF 8               // band rows loaded ahead
+#endif
+template <int R, int MM, bool FLUX>
+__global__ __launch_bounds__(512) void cgr_band_kernel(gpi_residual_desc d) {
+    extern __shared__ __attribute__((aligned(16))) double smd[];
+    constexpr int PF0 = GPI_CGR_PF / MM > 2 ? GPI_CGR_PF / MM : 2;        // ~ the same bytes in flight per wave for any MM
+    constexpr int PF = PF0 < R + 1 ? PF0 : R + 1;
+    const int nc = d.nc, n = nc * R, nn = (nc + 1) * (nc + 1), nT = 2 * nc * nc;
+    constexpr float rinv = 1.f / (float)R;
+    double* acc = smd;
+    double* racc = smd + nn;
+    const int f = blockIdx.x;
+    const int lane = threadIdx.x & 63;
+    const int J = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // one wave per band (blockDim = 64 nc)
+    const float* lk = d.logkappa + (int64_t)f * n * n;
+    const float* y = d.y + (int64_t)f * (n + 1) * (n - 1);
+    const float u0b = d.bc[4 * f], u1b = d.bc[4 * f + 1], u2b = d.bc[4 * f + 2], u3b = d.bc[4 * f + 3];
+    for (int e = threadIdx.x; e < nn + nT; e += blockDim.x) smd[e] = 0.0;
+    __syncthreads();
+    const float fn = (float)n;
+    const int j0 = J * R;
+    const bool top = J == nc - 1;                                  // the top band also owns node row n
+    // raw loads of band row jr (node row j = j0 + jr): kappa pixel row j (log), y node row j + 1; clamped
+    // addresses, masked after the load (branch-free: exact wait counts)
+    // buffer loads: the row in the (scalar) soffset, the column in a per-lane voffset fixed for the band, so
+    // no per-row 64-bit addresses are held in registers across the unrolled rows
+    const auto rk = __builtin_amdgcn_make_buffer_rsrc((void*)lk, (short)0, 4 * n * n, 0x00020000);
+    const auto ry = __builtin_amdgcn_make_buffer_rsrc((void*)y, (short)0, 4 * (n + 1) * (n - 1), 0x00020000);
+    int vk[MM], vy[MM];
+#pragma unroll
+    for (int m = 0; m < MM; ++m) {
+        const int i = 64 * m + lane;
+        vk[m] = 4 * min(i, n - 1);
+        vy[m] = 4 * (min(max(i, 1), n - 1) - 1);
+    }
+    auto load_k = [&](int j, int m) -> float {
+        const int jj = min(max(j, 0), n - 1);
+        return __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rk, vk[m], 4 * (n - 1 - jj) * n, 0));
+    };
+    auto load_y = [&](int j, int m) -> float {
+        const int jj = min(max(j, 0), n);
+        return __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(ry, vy[m], 4 * jj * (n - 1), 0));
+    };
+    float kraw[PF][MM], yraw[PF][MM];
+#pragma unroll
+    for (int p = 0; p < PF; ++p)
+#pragma unroll
+        for (int m = 0; m < MM; ++m) {
+            kraw[p][m] = load_k(j0 + p, m);
+            yraw[p][m] = load_y(j0 + p + 1, m);
+        }
+    // carried rows: kappa of pixel row j - 1 (kd, and kdl = kd of pixel i - 1), y of rows j - 1 (yd) and j
+    // (yc, free values only: 0 at the Dirichlet columns)
+    float kd[MM], kdl[MM], yd[MM], yc[MM];
+    float c[MM][4], flr[MM], ful[MM];
+    {
+        float kp[MM];
+#pragma unroll
+        for (int m = 0; m < MM; ++m) {
+            const int i = 64 * m + lane;
+            const float k = expf(load_k(j0 - 1, m));
+            kp[m] = (j0 > 0 && i < n) ? k : 0.f;
+            const bool fr = i >= 1 && i <= n - 1;
+            const float a = load_y(j0 - 1, m), b = load_y(j0, m);
+            yd[m] = (j0 > 0 && fr) ? a : 0.f;
+            yc[m] = fr ? b : 0.f;
+            c[m][0] = c[m][1] = c[m][2] = c[m][3] = 0.f;
+            flr[m] = ful[m] = 0.f;
+        }
+#pragma unroll
+        for (int m = 0; m < MM; ++m) {
+            kd[m] = kp[m];
+            kdl[m] = dpp_shr1(kp[m], m > 0 ? lane_of(kp[m > 0 ? m - 1 : 0], 63) : 0.f);
+        }
+    }
+    auto row = [&](auto jr_c) {
+        constexpr int jr = decltype(jr_c)::value;
+        // (j and eta pass through an empty asm at the row's start, so the row's divisions, weights and
+        // Dirichlet data are computed here, not hoisted to the kernel's top for every row at once)
+        int j = j0 + jr;
+        asm volatile("" : "+s"(j));
+        const int p = jr % PF;
+        float eta = (float)jr * rinv;
+        asm volatile("" : "+v"(eta));
+        // the Dirichlet data of row j (x = 0 / x = 1), uniform: one division per row
+        const float tb = (float)j / fn;
+        const float bl = u0b * (1.f - tb) + u1b * tb, br = u2b * (1.f - tb) + u3b * tb;
+        float ku[MM], yu[MM], yhc[MM];
+#pragma unroll
+        for (int m = 0; m < MM; ++m) {
+            const int i = 64 * m + lane;
+            const float k = __builtin_amdgcn_exp2f(kraw[p][m] * 1.4426950408889634f);
+            ku[m] = (j < n && i < n) ? k : 0.f;                      // kappa(i, j) = kur
+            yu[m] = (j < n && i >= 1 && i <= n - 1) ? yraw[p][m] : 0.f;   // y(i, j + 1), free values
+            // yhat of row j: the Dirichlet data at columns 0 and n
+            yhc[m] = i == 0 ? bl : (i == n ? br : yc[m]);
+        }
+        // the next row's loads into the freed slot
+        if (jr + PF <= R) {
+#pragma unroll
+            for (int m = 0; m < MM; ++m) {
+                kraw[p][m] = load_k(j + PF, m);
+                yraw[p][m] = load_y(j + PF + 1, m);
+            }
+        }
+        // (keeps the scheduler from hoisting every row's loads to the top: PF rows in flight, not R)
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int m = 0; m < MM; ++m) {
+            const int i = 64 * m + lane;
+            const bool act = i >= 1 && i <= n - 1;
+            // neighbours across the 64-column chunk edges
+            const float kl_in = m > 0 ? lane_of(ku[m > 0 ? m - 1 : 0], 63) : 0.f;
+            const float yl_in = m > 0 ? lane_of(yhc[m > 0 ? m - 1 : 0], 63) : 0.f;
+            const float yr_in = m < MM - 1 ? lane_of(yhc[m < MM - 1 ? m + 1 : 0], 0) : (64 * MM == n ? br : 0.f);
+            // (the wave shifts run unconditionally: a DPP move under a lane condition became a branch)
+            const float sk = dpp_shr1(ku[m], kl_in), sl = dpp_shr1(yhc[m], yl_in), sr = dpp_shl1(yhc[m], yr_in);
+            const float kul = act ? sk : 0.f;
+            const float kur = ku[m];
+            const float kdlm = act ? kdl[m] : 0.f, kdr = kd[m];
+            const float ycm = yc[m];                                  // 0 unless act
+            const float yl = act ? sl : 0.f;
+            const float yrr = act ? sr : 0.f;
+            const float ydm = yd[m], yum = act ? yu[m] : 0.f;
+            float Ky = (kul + kdlm) * (ycm - yl) + (kur + kdr) * (ycm - yrr);
+            if (j > 0) Ky += (kdlm + kdr) * (ycm - ydm);
+            if (j < n) Ky += (kul + kur) * (ycm - yum);
+            Ky = act ? 0.5f * Ky : 0.f;
+            int I = i / R;
+            if (I > nc - 1) I = nc - 1;
+            const float xi = (float)(i - I * R) * rinv;
+            c[m][0] += (1.f - fmaxf(xi, eta)) * Ky;
+            c[m][1] += fmaxf(xi - eta, 0.f) * Ky;
+            c[m][2] += fmaxf(eta - xi, 0.f) * Ky;
+            c[m][3] += fminf(xi, eta) * Ky;
+            // u1 = y(i + 1, j), u3 = y(i + 1, j + 1): free values of the right neighbour (0 at column n)
+            float u1 = 0.f, u3 = 0.f;
+            if (FLUX) {
+                const float y1_in = m < MM - 1 ? lane_of(yc[m < MM - 1 ? m + 1 : 0], 0) : 0.f;
+                const float y3_in = m < MM - 1 ? lane_of(yu[m < MM - 1 ? m + 1 : 0], 0) : 0.f;
+                u1 = dpp_shl1(yc[m], y1_in);
+                u3 = dpp_shl1(yu[m], y3_in);
+            }
+            if (FLUX && i < n && j < n) {
+                const float u0 = ycm, u2 = yum;
+                const int tr = i - (i / R) * R, tj = jr;
+                float vl = 0.f, vu = 0.f;
+                if (tj == 0 && J > 0) vl += u1 - u3;             // bottom edge (not on y = 0)
+                if (tr == R - 1) vl += u1 - u0;                  // right edge
+                if (tr == 0) vu += u2 - u3;                      // left edge
+                if (tj == R - 1 && J < nc - 1) vu += u2 - u0;    // top edge (not on y = 1)
+                if (tr == tj) { vl += u0 - 2.f * u1 + u3; vu += u0 - 2.f * u2 + u3; }   // diagonal
+                flr[m] = fmaf(kur, vl, flr[m]);
+                ful[m] = fmaf(kur, vu, ful[m]);
+            }
+        }
+        // (the accumulators pass through an empty asm at the row's end: the row's arithmetic runs here,
+        // not sunk to the band's end with every row's operands held live until then)
+#pragma unroll
+        for (int m = 0; m < MM; ++m) {
+            asm volatile("" : "+v"(c[m][0]), "+v"(c[m][1]), "+v"(c[m][2]), "+v"(c[m][3]));
+            if (FLUX) asm volatile("" : "+v"(flr[m]), "+v"(ful[m]));
+        }
+        // carry: row j becomes the row below
+#pragma unroll
+        for (int m = 0; m < MM; ++m) {
+            kdl[m] = dpp_shr1(ku[m], m > 0 ? lane_of(ku[m > 0 ? m - 1 : 0], 63) : 0.f);   // (= sk: CSE)
+            kd[m] = ku[m];
+            yd[m] = yc[m];
+            yc[m] = yu[m];
+        }
+    };
+    static_for<R>(row);
+    if (top) row(std::integral_constant<int, R>{});                // node row n (uniform branch)
+    // the r lanes of one coarse square (r a power of two <= 64: one group of consecutive lanes; otherwise
+    // lane by lane)
+    constexpr int G = (R & (R - 1)) == 0 ? (R < 64 ? R : 64) : 1;
+#pragma unroll
+    for (int m = 0; m < MM; ++m) {
+#pragma unroll
+        for (int o = 1; o < G; o <<= 1) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) c[m][k] += __shfl_xor(c[m][k], o, 64);
+            if (FLUX) {
+                flr[m] += __shfl_xor(flr[m], o, 64);
+                ful[m] += __shfl_xor(ful[m], o, 64);
+            }
+        }
+        const int i = 64 * m + lane;
+        if ((lane % G) == 0 && i < n) {
+            int I = i / R;
+            if (I > nc - 1) I = nc - 1;
+            const int v0 = I + (nc + 1) * J;
+            atomicAdd(&acc[v0], (double)c[m][0]);
+            atomicAdd(&acc[v0 + 1], (double)c[m][1]);
+            atomicAdd(&acc[v0 + nc + 1], (double)c[m][2]);
+            atomicAdd(&acc[v0 + nc + 2], (double)c[m][3]);
+            if (FLUX) {
+                const int q = I + nc * J;
+                atomicAdd(&racc[2 * q], (double)flr[m]);
+                atomicAdd(&racc[2 * q + 1], (double)ful[m]);
+            }
+        }
+    }
+    __syncthreads();
+    if (d.r)
+        for (int e = threadIdx.x; e < nn; e += blockDim.x) d.r[(int64_t)f * nn + e] = (float)acc[e];
+    if (!FLUX) return;
+    for (int e = threadIdx.x; e < nT; e += blockDim.x) d.r_flux[(int64_t)f * nT + e] = (float)racc[e];
+}
+
 template <int MM>
 void launch_cgr(const gpi_residual_desc& d, int G, dim3 grid, dim3 block, size_t lds, hipStream_t st) {
     if (d.r_flux) hipLaunchKernelGGL((cgr_kernel<MM, true>), grid, block, lds, st, d, G);
@@ -376,6 +623,32 @@ extern "C" int gpi_cgr_residual(const gpi_residual_desc* d, void* stream) {
     const size_t lds = sizeof(double) * (nn + 2 * d->nc * d->nc);
     if (lds > 160 * 1024) return GPI_ERR_UNSUPPORTED;
     const int r = d->n_fine / d->nc;
+    {
+        // barrier-free band form (cgr_band_kernel) for its (r, columns) instantiations; GPI_CGR_FORM=1 the
+        // streaming form, 0 the original band kernel (A/B)
+        static const int form = [] { const char* v = getenv("GPI_CGR_FORM"); return v && *v ? atoi(v) : 2; }();
+        const int n = d->n_fine, MM = (n + 63) / 64;
+        if (form == 2 && d->nc <= 8) {
+            const dim3 grid(d->n), block(64 * d->nc);
+            const hipStream_t st = (hipStream_t)stream;
+            const bool fl = d->r_flux != nullptr;
+            bool done = true;
+#define GPI_CGR_BAND(RR, M)                                                                             \
+    if (fl) hipLaunchKernelGGL((cgr_band_kernel<RR, M, true>), grid, block, lds, st, *d);              \
+    else hipLaunchKernelGGL((cgr_band_kernel<RR, M, false>), grid, block, lds, st, *d);
+            if (r == 4 && MM == 1) { GPI_CGR_BAND(4, 1) }
+            else if (r == 8 && MM == 1) { GPI_CGR_BAND(8, 1) }
+            else if (r == 16 && MM == 1) { GPI_CGR_BAND(16, 1) }
+            else if (r == 16 && MM == 2) { GPI_CGR_BAND(16, 2) }
+            else if (r == 32 && MM == 4) { GPI_CGR_BAND(32, 4) }
+            else done = false;
+#undef GPI_CGR_BAND
+            if (done) {
+                GPI_CHECK_LAUNCH();
+                return GPI_OK;
+            }
+        }
+    }
     {
         // streaming form (cgr_stream_kernel) where its layout holds; GPI_CGR_STREAM=0 keeps the band kernel (A/B)
         static const int stream_on = [] { const char* v = getenv("GPI_CGR_STREAM"); return v && *v ? atoi(v) : 1; }();
