@@ -1112,10 +1112,21 @@ struct IntC {
 #ifndef GPI_IG_PRE
 #define GPI_IG_PRE 0
 #endif
+// GPI_VDG3: the input gradient of the 3x3 / stride-1 backwards on the VALU (v_pk_fma_f32 over input-channel
+// pairs, the weights by broadcast LDS reads, as the fused output conv's) instead of the MFMA gather form
+// (16 x 16 x 4 blocks, N = cin padded to 16, two dependent LDS reads per step: ~460 cycles per MFMA measured)
+#ifndef GPI_VDG3
+#define GPI_VDG3 1
+#endif
 // occupancy target (waves per SIMD) of the 1x1 / 3x3 / 7x7 backward instantiations (no C64 backward launch
 // holds more than 5 workgroups per CU; 4 / 5 / 6 measured alike, r04r)
 #ifndef GPI_BWD_WAVES
 #define GPI_BWD_WAVES 6
+#endif
+// ... of the 3x3 / stride-1 instantiation with the VALU input gradient (its per-thread channel sums and
+// accumulators: 12 spilled VGPRs at 5 waves, none at 4; its launches hold <= 5 workgroups per CU)
+#ifndef GPI_BWD3_WAVES
+#define GPI_BWD3_WAVES 4
 #endif
 // per-wave input-channel sums [2][4 waves][32] (256 floats) alias the offset table (>= 256 floats)
 constexpr int SLAB_ROWS = 4;    // partial-slab rows per workgroup: one per wave (no cross-wave dW reduction;
@@ -1149,7 +1160,7 @@ __host__ __device__ constexpr bool fuse_wlds(int ky) {
 }
 
 template <int K, int S, int UP, bool FUSE = false, bool HALF = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (FUSE ? GPI_FUSE_WAVES : 4) : GPI_BWD_WAVES))) void conv_bwd_kernel(gpi_conv_desc d, gpi_codec_ctx c, ConvGeom G) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (FUSE ? GPI_FUSE_WAVES : 4) : (K == 3 && S == 1 && UP == 0 && GPI_VDG3 ? GPI_BWD3_WAVES : GPI_BWD_WAVES)))) void conv_bwd_kernel(gpi_conv_desc d, gpi_codec_ctx c, ConvGeom G) {
     touch_kernargs<CONV_KARG_BYTES>();
     entry_signal(G);
     if (SKIP(G, 16)) return;
@@ -1192,6 +1203,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
     // the channel-sum scratch (256) and the four waves' weight-gradient partial rows, summed in LDS
     // into ONE slab row per tile (a quarter of the slab bytes, one coalesced store)
     const bool vop = FUSE || (K == 5 && S == 1 && !UP && has_gin && d.cin <= 4 && d.cout <= 2);
+    // v3: the VALU input gradient of a 3x3 / stride-1 op (GPI_VDG3; tiles of >= 256 owned pixels, cin <= 12):
+    // weights staged as WB3[((co K + ky) K + kx) CIV3 + ci], CIV3 = cin rounded up to 4, in wD's place
+    const bool v3 = GPI_VDG3 && K == 3 && S == 1 && !UP && !FUSE && has_gin && d.cin <= 12 && Gt.ph * d.w_in >= 256;
+    const int CIV3 = (d.cin + 3) & ~3;
     const int J = d.cin * KK;
     const int rowlen = d.cout * J + (d.in_bn ? 2 * d.cin : 0);
     float* wD = smem + bwd_hdr(d.cin, d.cout);        // [KD4][16]: W[co][ci][tap] at (co*KK + tap)*16 + ci, zero padded
@@ -1261,7 +1276,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
                 return params + w_off + ((int64_t)co * d.cin + ci) * KK + ky * K + kx;
             });
     }
-    if (has_gin && dg_role && !vop)
+    if (has_gin && dg_role && v3)
+        stage(wD, d.cout * KK * CIV3, zero, [&](int e) -> const float* {
+            const int t = e / CIV3, ci = e - t * CIV3, co = t / KK, tap = t - co * KK;
+            return ci < d.cin ? params + w_off + ((int64_t)co * d.cin + ci) * KK + tap : nullptr;
+        });
+    else if (has_gin && dg_role && !vop)
         stage(wD, nwd, zero, [&](int e) -> const float* {
             const int ci = e & 15, k = e >> 4;
             const int co = k / KK, t = k - co * KK;
@@ -1329,7 +1349,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
     // (FUSE: always the VALU input gradient -- launch() checks cin <= 4 -- so the MFMA input-gradient
     // path and its operand registers compile away)
     const bool vdg = vop && dg_role;     // (launch() never splits a vop op: dg_role holds)
-    const int nmblk = (!FUSE && has_gin && dg_role && !vdg && !SKIP(G, 2)) ? (Gt.ph * d.w_in) >> 4 : 0;
+    const int nmblk = (!FUSE && has_gin && dg_role && !vdg && !v3 && !SKIP(G, 2)) ? (Gt.ph * d.w_in) >> 4 : 0;
     const int ci_l = min(l16, d.cin - 1);
     const bool cok = l16 < d.cin;
     const int64_t ibase = ((int64_t)T.b * d.in_ctot + d.in_c0 + ci_l) * HWi + (int64_t)py0 * d.w_in;
@@ -1424,7 +1444,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
             ktab[cls * 2 * KD4 + KD4 + k] = ob;
         }
     }
-    if (has_gin && dg_role && S != 2 && !vop) {
+    if (has_gin && dg_role && S != 2 && !vop && !v3) {
         // A operand of reduction index k = (co, ky, kx) for owned pixel (qy, px):
         // gl[(S1) qy*PG + px | (UP) 2 qy*PG + 2 px] + ktab[k]
         const int ry0 = (UP ? 2 * py0 : py0) + d.pad - gy0;
@@ -1991,6 +2011,115 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
             }
         }
     }
+#if GPI_VDG3
+    // ---- phase 4b (v3): the 3x3 / stride-1 input gradient on the VALU.  Q consecutive pixels of an owned
+    // row per thread (2 when the tile has >= 512 owned pixels, else 1), all input channels as packed pairs:
+    // per (co, ky) the output-gradient window of the Q pixels (Q + 2 values) from the LDS image, per tap the
+    // CIV3 weights by CIV3 / 4 broadcast ds_read_b128, then Q x CIV3 / 2 v_pk_fma_f32.  The previous S_in
+    // (accumulating ops) is loaded at the item's start, under the compute.  Epilogue as the MFMA form's: ReLU
+    // mask, BN-backward sums, S_in (+)= gamma * dbn; the per-channel sums are wave-summed (DPP) and handed
+    // to the MFMA form's reduction as the kq = 0 lanes' values of channel l16.
+    if constexpr (K == 3 && S == 1 && !UP && !FUSE) {
+        if (v3 && dg_role && !SKIP(G, 2)) {
+            auto v3_rows = [&](auto ci_c, auto q_c) {
+                constexpr int CI = decltype(ci_c)::value, Q = decltype(q_c)::value, CH = CI / 2;
+                float s1[CI], s2[CI];
+#pragma unroll
+                for (int ci = 0; ci < CI; ++ci) s1[ci] = s2[ci] = 0.f;
+                const int npq = (Gt.ph * d.w_in) / Q;
+                for (int gq = tid; gq < npq; gq += 256) {
+                    const int qy = dq(Q * gq, Gt.d_win), px0 = Q * gq - qy * d.w_in;
+                    const int64_t gb_in = ((int64_t)T.b * d.in_ctot + d.in_c0) * HWi + (int64_t)(py0 + qy) * d.w_in + px0;
+                    float pv[CI][Q];
+#pragma unroll
+                    for (int ci = 0; ci < CI; ++ci) {
+                        const bool ok = ci < d.cin && d.gin_accumulate;
+                        const float* pp = ok ? ws + gin_off + gb_in + (int64_t)ci * HWi : zero;
+#pragma unroll
+                        for (int q = 0; q < Q; ++q) pv[ci][q] = as_gld(pp)[ok ? q : 0];
+                    }
+                    f32x2 acc2[CH][Q];
+#pragma unroll
+                    for (int h = 0; h < CH; ++h)
+#pragma unroll
+                        for (int q = 0; q < Q; ++q) acc2[h][q] = f32x2{0.f, 0.f};
+                    for (int co = 0; co < d.cout; ++co) {
+#pragma unroll
+                        for (int ky = 0; ky < K; ++ky) {
+                            const float* grow = gl + co * gplane + (qy + py0 + d.pad - ky - gy0) * Gt.PG + HALO + px0 +
+                                                d.pad - (K - 1);
+                            float gw[K + Q - 1];
+#pragma unroll
+                            for (int t = 0; t < K + Q - 1; ++t) gw[t] = grow[t];
+                            const float* wrow = wD + (co * K + ky) * K * CI;
+#pragma unroll
+                            for (int kx = 0; kx < K; ++kx) {
+                                f32x4 w4[CI / 4];
+#pragma unroll
+                                for (int v = 0; v < CI / 4; ++v) w4[v] = *reinterpret_cast<const f32x4*>(wrow + kx * CI + 4 * v);
+#pragma unroll
+                                for (int q = 0; q < Q; ++q) {
+                                    const float gv = gw[q + K - 1 - kx];
+#pragma unroll
+                                    for (int h = 0; h < CH; ++h) {
+                                        const f32x2 w = f32x2{w4[h >> 1][2 * (h & 1)], w4[h >> 1][2 * (h & 1) + 1]};
+                                        acc2[h][q] = __builtin_elementwise_fma(w, f32x2{gv, gv}, acc2[h][q]);
+                                    }
+                                }
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int ci = 0; ci < CI; ++ci) {
+                        if (ci >= d.cin) break;
+                        const float* ap = alb + (ci * Gt.rh + (py0 - iy0 + qy)) * Gt.P + HALO + px0;
+                        // (the channel's BN constants by uniform LDS reads here, not held across the item)
+                        const float lg = d.in_bn ? i_gam[ci] : 0.f;
+                        const float lb = d.in_bn ? i_sh[ci] + i_mean[ci] * i_sc[ci] : 0.f;
+                        const float lr = d.in_bn ? 1.f / lg : 0.f;
+                        float o[Q];
+#pragma unroll
+                        for (int q = 0; q < Q; ++q) {
+                            const float a = acc2[ci >> 1][q][ci & 1];
+                            if (d.in_bn) {
+                                const float av = ap[q];
+                                const float dbn = av > 0.f ? a : 0.f;
+                                o[q] = pv[ci][q] + lg * dbn;
+                                s1[ci] += dbn;
+                                s2[ci] += dbn * ((av - lb) * lr);
+                            } else {
+                                o[q] = pv[ci][q] + a;
+                            }
+                        }
+                        store_px<Q>(ws + gin_off + gb_in + (int64_t)ci * HWi, o);
+                    }
+                }
+                if (d.in_bn) {
+                    // wave sums (DPP) of the 2 CI channel sums; lane l16 of the kq = 0 lanes takes channel l16's
+                    float v2[2 * CI];
+#pragma unroll
+                    for (int ci = 0; ci < CI; ++ci) {
+                        v2[ci] = s1[ci];
+                        v2[CI + ci] = s2[ci];
+                    }
+                    wave_sums(v2);
+                    float a = 0.f, b = 0.f;
+#pragma unroll
+                    for (int ci = 0; ci < CI; ++ci) {
+                        a = l16 == ci ? v2[ci] : a;
+                        b = l16 == ci ? v2[CI + ci] : b;
+                    }
+                    sd = kq == 0 ? a : 0.f;
+                    sdx = kq == 0 ? b : 0.f;
+                }
+            };
+            const bool q2 = Gt.ph * d.w_in >= 512;
+            if (d.cin <= 4) { if (q2) v3_rows(IntC<4>{}, IntC<2>{}); else v3_rows(IntC<4>{}, IntC<1>{}); }
+            else if (d.cin <= 8) { if (q2) v3_rows(IntC<8>{}, IntC<2>{}); else v3_rows(IntC<8>{}, IntC<1>{}); }
+            else v3_rows(IntC<12>{}, IntC<1>{});
+        }
+    }
+#endif
     // ---- phase 4b': input gradient on the VALU (cin <= 4, 5x5, stride 1): Q consecutive pixels of an
     // owned row per thread (4 for cin <= 2, 2 otherwise), all (<= 4) input channels at once.  The
     // weights W[co][ci][ky][kx] are wave-uniform: scalar loads from the parameters (constant address
@@ -2121,11 +2250,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
                 }
             }
         } else {
-            // lanes 16 apart share a channel: fold them
-            sd += __shfl_xor(sd, 16, 64);
-            sdx += __shfl_xor(sdx, 16, 64);
-            sd += __shfl_xor(sd, 32, 64);
-            sdx += __shfl_xor(sdx, 32, 64);
+            // lanes 16 apart share a channel: fold them (v3: wave sums already in the kq = 0 lanes)
+            if (!v3) {
+                sd += __shfl_xor(sd, 16, 64);
+                sdx += __shfl_xor(sdx, 16, 64);
+                sd += __shfl_xor(sd, 32, 64);
+                sdx += __shfl_xor(sdx, 32, 64);
+            }
             if (kq == 0) {
                 red[wv * 32 + l16] = sd;
                 red[128 + wv * 32 + l16] = sdx;

@@ -394,7 +394,7 @@ template <int N, typename F>
 __device__ __forceinline__ void static_for(F& f) { StaticFor<0, N>::run(f); }
 
 #ifndef GPI_CGR_PF
-#define GPI_CGR_PF 8               // band rows loaded ahead
+#define GPI_CGR_PF 4               // band rows loaded ahead (x columns per lane: 4 measured ahead of 8, r05f)
 #endif
 template <int R, int MM, bool FLUX>
 __global__ __launch_bounds__(512) void cgr_band_kernel(gpi_residual_desc d) {
@@ -413,7 +413,7 @@ __global__ __launch_bounds__(512) void cgr_band_kernel(gpi_residual_desc d) {
     const float u0b = d.bc[4 * f], u1b = d.bc[4 * f + 1], u2b = d.bc[4 * f + 2], u3b = d.bc[4 * f + 3];
     for (int e = threadIdx.x; e < nn + nT; e += blockDim.x) smd[e] = 0.0;
     __syncthreads();
-    const float fn = (float)n;
+    const float rfn = 1.f / (float)n;
     const int j0 = J * R;
     const bool top = J == nc - 1;                                  // the top band also owns node row n
     // raw loads of band row jr (node row j = j0 + jr): kappa pixel row j (log), y node row j + 1; clamped
@@ -479,7 +479,7 @@ __global__ __launch_bounds__(512) void cgr_band_kernel(gpi_residual_desc d) {
         float eta = (float)jr * rinv;
         asm volatile("" : "+v"(eta));
         // the Dirichlet data of row j (x = 0 / x = 1), uniform: one division per row
-        const float tb = (float)j / fn;
+        const float tb = (float)j * rfn;
         const float bl = u0b * (1.f - tb) + u1b * tb, br = u2b * (1.f - tb) + u3b * tb;
         float ku[MM], yu[MM], yhc[MM];
 #pragma unroll
