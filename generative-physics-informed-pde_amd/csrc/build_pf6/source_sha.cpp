@@ -1,1 +1,1 @@
-extern "C" const char* gpi_source_sha(void) { return "e8b146c63c2287877936c73f42701879bfac0c1f"; }
+extern "C" const char* gpi_source_sha(void) { return "ca46497efb98ec6a2b9f901bc1541a88c22cd3fa"; }

@@ -14,7 +14,8 @@ LIB_PATH = os.path.join(HERE, 'libgpi_hip.so')
 if os.environ.get('GPI_LIB_VARIANT'):               # tools: A/B builds of the same sources (libgpi_hip_<v>.so)
     LIB_PATH = os.path.join(HERE, 'libgpi_hip_%s.so' % os.environ['GPI_LIB_VARIANT'])
 if os.environ.get('GPI_PHASE_TIMING') == '1':      # tools/phase_probe.py: the stamped build of the same kernels
-    LIB_PATH = os.path.join(HERE, 'libgpi_hip_timing.so')
+    LIB_PATH = os.path.join(HERE, 'libgpi_hip_timing%s.so' % (
+        ('_' + os.environ['GPI_LIB_VARIANT']) if os.environ.get('GPI_LIB_VARIANT') else ''))
 
 GPI_MAX_GROUPS = 4
 GPI_MAX_CIN = 32

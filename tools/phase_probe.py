@@ -70,6 +70,11 @@ def main():
             print('%-44s %s blocks %5d  life %6.2f us  span %6.2f us  in-flight %5.1f' %
                   (op.name, 'fwd' if fwd else 'bwd', nb, life.mean(), span, inflight))
             print('    cycles/phase: ' + '  '.join('%d:%6.0f' % (k + 1, d[:, k].mean()) for k in used))
+            if os.environ.get('GPI_PROBE_HALVES') and nb % 2 == 0:
+                # split launches (role by block half: input gradient first, weight gradient second)
+                for hname, sl in (('first half ', slice(0, nb // 2)), ('second half', slice(nb // 2, nb))):
+                    print('    %s life %6.2f us  cycles/phase: %s' % (hname, life[sl].mean(), '  '.join(
+                        '%d:%6.0f' % (k + 1, d[sl, k].mean()) for k in used)))
             if os.environ.get('GPI_PROBE_RAW'):
                 base = p[:, 5]
                 print('    raw (cycles after stamp 5): ' + '  '.join('%d:%6.0f' % (k, (p[:, k] - base).mean())
