@@ -1,1 +1,1 @@
-extern "C" const char* gpi_source_sha(void) { return "ca46497efb98ec6a2b9f901bc1541a88c22cd3fa"; }
+extern "C" const char* gpi_source_sha(void) { return "ae07b18d8aee5e9b17510fe899521a0384fcd685"; }

@@ -1159,8 +1159,8 @@ __host__ __device__ constexpr bool fuse_wlds(int ky) {
     return GPI_FUSE_WLDS <= 0 ? false : (GPI_FUSE_WLDS >= 5 ? true : (ky & 1 ? (ky / 2) < GPI_FUSE_WLDS : (ky / 2) < GPI_FUSE_WLDS - 2));
 }
 
-template <int K, int S, int UP, bool FUSE = false, bool HALF = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (FUSE ? GPI_FUSE_WAVES : 4) : (K == 3 && S == 1 && UP == 0 && GPI_VDG3 ? GPI_BWD3_WAVES : GPI_BWD_WAVES)))) void conv_bwd_kernel(gpi_conv_desc d, gpi_codec_ctx c, ConvGeom G) {
+template <int K, int S, int UP, bool FUSE = false, bool HALF = false, bool V3 = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (FUSE ? GPI_FUSE_WAVES : 4) : (V3 ? GPI_BWD3_WAVES : GPI_BWD_WAVES)))) void conv_bwd_kernel(gpi_conv_desc d, gpi_codec_ctx c, ConvGeom G) {
     touch_kernargs<CONV_KARG_BYTES>();
     entry_signal(G);
     if (SKIP(G, 16)) return;
@@ -1205,7 +1205,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
     const bool vop = FUSE || (K == 5 && S == 1 && !UP && has_gin && d.cin <= 4 && d.cout <= 2);
     // v3: the VALU input gradient of a 3x3 / stride-1 op (GPI_VDG3; tiles of >= 256 owned pixels, cin <= 12):
     // weights staged as WB3[((co K + ky) K + kx) CIV3 + ci], CIV3 = cin rounded up to 4, in wD's place
-    const bool v3 = GPI_VDG3 && K == 3 && S == 1 && !UP && !FUSE && has_gin && d.cin <= 12 && Gt.ph * d.w_in >= 256;
+    // (V3: an instantiation of its own -- its accumulators and prefetched operands need a 4-wave VGPR budget,
+    // which the MFMA form's launches of up to 5 workgroups per CU must not pay; picked by v3_op on the host)
+    const bool v3 = V3 && K == 3 && S == 1 && !UP && !FUSE && has_gin && d.cin <= 8 && Gt.ph * d.w_in >= 256;
     const int CIV3 = (d.cin + 3) & ~3;
     const int J = d.cin * KK;
     const int rowlen = d.cout * J + (d.in_bn ? 2 * d.cin : 0);
@@ -1367,6 +1369,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
             else dst[u] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
     };
+    // v3: the previous S_in of this thread's first item (Q = 2 pixels of channels < cin), with the operand loads
+    float pv3[8][2];
+    if (v3 && dg_role && d.gin_accumulate && !SKIP(G, 2)) {
+        const int Q = Gt.ph * d.w_in >= 512 ? 2 : 1;
+        const int gq = tid;
+        const int qy = dq(Q * gq, Gt.d_win), px0 = Q * gq - qy * d.w_in;
+        const bool iok = gq < (Gt.ph * d.w_in) / Q;
+        const int64_t gb_in = ((int64_t)T.b * d.in_ctot + d.in_c0) * HWi + (int64_t)(py0 + qy) * d.w_in + px0;
+#pragma unroll
+        for (int ci = 0; ci < 8; ++ci) {
+            const bool ok = iok && ci < d.cin;
+            const float* pp = ok ? ws + gin_off + gb_in + (int64_t)ci * HWi : zero;
+            pv3[ci][0] = *as_gld(pp);
+            pv3[ci][1] = *as_gld(ok && Q == 2 ? pp + 1 : zero);
+        }
+    }
     if (nmblk > 0 && S != 2) {
         own_load(0, pv4);
 #if GPI_IG_PRE
@@ -2031,12 +2049,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
                     const int qy = dq(Q * gq, Gt.d_win), px0 = Q * gq - qy * d.w_in;
                     const int64_t gb_in = ((int64_t)T.b * d.in_ctot + d.in_c0) * HWi + (int64_t)(py0 + qy) * d.w_in + px0;
                     float pv[CI][Q];
+                    if (gq == tid) {           // (loaded in phase 1)
 #pragma unroll
-                    for (int ci = 0; ci < CI; ++ci) {
-                        const bool ok = ci < d.cin && d.gin_accumulate;
-                        const float* pp = ok ? ws + gin_off + gb_in + (int64_t)ci * HWi : zero;
+                        for (int ci = 0; ci < CI; ++ci)
 #pragma unroll
-                        for (int q = 0; q < Q; ++q) pv[ci][q] = as_gld(pp)[ok ? q : 0];
+                            for (int q = 0; q < Q; ++q) pv[ci][q] = d.gin_accumulate ? pv3[ci][q] : 0.f;
+                    } else {
+#pragma unroll
+                        for (int ci = 0; ci < CI; ++ci) {
+                            const bool ok = ci < d.cin && d.gin_accumulate;
+                            const float* pp = ok ? ws + gin_off + gb_in + (int64_t)ci * HWi : zero;
+#pragma unroll
+                            for (int q = 0; q < Q; ++q) pv[ci][q] = as_gld(pp)[ok ? q : 0];
+                        }
                     }
                     f32x2 acc2[CH][Q];
 #pragma unroll
@@ -2116,7 +2141,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
             const bool q2 = Gt.ph * d.w_in >= 512;
             if (d.cin <= 4) { if (q2) v3_rows(IntC<4>{}, IntC<2>{}); else v3_rows(IntC<4>{}, IntC<1>{}); }
             else if (d.cin <= 8) { if (q2) v3_rows(IntC<8>{}, IntC<2>{}); else v3_rows(IntC<8>{}, IntC<1>{}); }
-            else v3_rows(IntC<12>{}, IntC<1>{});
+
         }
     }
 #endif
@@ -2410,6 +2435,10 @@ conv_kernel_t pick(int cp, bool fwd, int npx, bool half, bool ucls = false) {
         // upsampling backward (+1.2-1.6 us per launch)
         if (!fwd && ucls) return half ? conv_bwd_kernel<K, S, 2, false, true> : conv_bwd_kernel<K, S, 2>;
     }
+    if constexpr (K == 3 && S == 1 && UP == 0) {
+        // (the ucls slot carries v3_op for this shape)
+        if (!fwd && ucls) return half ? conv_bwd_kernel<3, 1, 0, false, true, true> : conv_bwd_kernel<3, 1, 0, false, false, true>;
+    }
     if (!fwd) return half ? conv_bwd_kernel<K, S, UP, false, true> : conv_bwd_kernel<K, S, UP>;
     if (npx == 4) return pick_cp<K, S, UP, 4>(cp, half);
     if (npx == 2) return pick_cp<K, S, UP, 2>(cp, half);
@@ -2419,11 +2448,16 @@ conv_kernel_t pick(int cp, bool fwd, int npx, bool half, bool ucls = false) {
     return pick_cp<K, S, UP, 1>(cp, half);
 }
 
+// the backward ops that take the VALU input gradient (GPI_VDG3; the kernel's v3 condition at full tiles)
+bool v3_op(const gpi_conv_desc& d, const ConvGeom& G) {
+    return GPI_VDG3 && d.k == 3 && d.stride == 1 && !d.upsample && d.gin_off >= 0 && d.cin <= 8 && G.ph * d.w_in >= 256;
+}
+
 conv_kernel_t select_kernel(const gpi_conv_desc& d, int cp, bool fwd, int npx, bool half, bool ucls) {
     const int key = d.k * 100 + d.stride * 10 + d.upsample;
     switch (key) {
         case 110: return pick<1, 1, 0>(cp, fwd, npx, half);
-        case 310: return pick<3, 1, 0>(cp, fwd, npx, half);
+        case 310: return pick<3, 1, 0>(cp, fwd, npx, half, ucls);
         case 311: return pick<3, 1, 1>(cp, fwd, npx, half, ucls);
         case 320: return pick<3, 2, 0>(cp, fwd, npx, half);
         case 510: return pick<5, 1, 0>(cp, fwd, npx, half);
@@ -2486,7 +2520,8 @@ int launch(const gpi_conv_desc& d, const gpi_codec_ctx& c, hipStream_t st, bool 
     if (!fwd && d.gin_off >= 0 && d.stride == 2 && ((d.w_in & 7) || (G.ph & 1))) return GPI_ERR_UNSUPPORTED;
     const int cp = cp_of(d);
     conv_kernel_t k = fuse ? (G.nfull < G.nblocks ? conv_bwd_kernel<5, 1, 0, true, true> : conv_bwd_kernel<5, 1, 0, true>)
-                           : select_kernel(d, cp, fwd, G.cg > 1 ? 0 : G.npx, G.nfull < G.nblocks, G.ucls != 0);
+                           : select_kernel(d, cp, fwd, G.cg > 1 ? 0 : G.npx, G.nfull < G.nblocks,
+                                           G.ucls != 0 || (!fwd && v3_op(d, G)));
     if (!k) return GPI_ERR_UNSUPPORTED;
     static const float* zero = nullptr;
     if (!zero) {
