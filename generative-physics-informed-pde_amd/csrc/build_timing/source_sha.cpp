@@ -1,1 +1,1 @@
-extern "C" const char* gpi_source_sha(void) { return "ae07b18d8aee5e9b17510fe899521a0384fcd685"; }
+extern "C" const char* gpi_source_sha(void) { return "d1a42813cd3668ef7d9434fdb821976f2a690eaf"; }

@@ -1114,9 +1114,12 @@ struct IntC {
 #endif
 // GPI_VDG3: the input gradient of the 3x3 / stride-1 backwards on the VALU (v_pk_fma_f32 over input-channel
 // pairs, the weights by broadcast LDS reads, as the fused output conv's) instead of the MFMA gather form
-// (16 x 16 x 4 blocks, N = cin padded to 16, two dependent LDS reads per step: ~460 cycles per MFMA measured)
+// (16 x 16 x 4 blocks, N = cin padded to 16, two dependent LDS reads per step).  Measured r05 (phase probe,
+// tools/phase_probe.py): EncBlock1.dl1.bwd phase 6 18.3 k -> 13.8 k cycles, DecBlock3.dl1 23.1 k -> 20.2 k,
+// launch time -1.0 / -1.3 us (kprof), but the step 0.5591-0.5608 vs 0.5538-0.5544 ms with it off
+// (profiles/r05i_ab_vdg3.txt): off by default; cin 10 (LastTransUp.conv1) was slower still (weight reads)
 #ifndef GPI_VDG3
-#define GPI_VDG3 1
+#define GPI_VDG3 0
 #endif
 // occupancy target (waves per SIMD) of the 1x1 / 3x3 / 7x7 backward instantiations (no C64 backward launch
 // holds more than 5 workgroups per CU; 4 / 5 / 6 measured alike, r04r)

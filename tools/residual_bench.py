@@ -1,16 +1,23 @@
-"""Throughput of the coarse-grained residual kernel (gpi_cgr_residual: CGR rows, optionally the
-flux rows) against the HBM roofline, with a CPU baseline.
+"""Throughput of the coarse-grained residual kernel (gpi_cgr_residual: CGR rows, optionally the flux rows
+fused into the same pass) against the HBM roofline, with a CPU baseline -- the measured line for the
+fixed-stencil residual that north_star names.
 
-usage: python tools/residual_bench.py [out.json]
+usage: python tools/residual_bench.py [out.json] [--quick] [--no-cpu]
 
 Per field the kernel must read log kappa [n, n], y [(n+1)(n-1)], the 4 BC values and write
 r [(nc+1)^2] (+ r_flux [2 nc^2]): algorithmic bytes = 4 (n^2 + (n+1)(n-1) + 4 + (nc+1)^2 [+ 2 nc^2]).
-Fields resident in HBM, HIP events on the launch stream, 20 launches averaged.
-CPU baseline ("port"): the same residual per field with scipy.sparse (K assembled once per field
-from kappa, K_f yhat restricted by W^T) on one host core -- the reference assembles Gamma with
-FEniCS per VO sample (physics/LinearElliptic.py:137-159) and evaluates Gamma y - alpha
+Fields resident in HBM, HIP events on the launch stream, 20 launches averaged (after one warm launch).
+`traffic`: HBM bytes per launch from the PMC passes of tools/r05_residual_pmc.sh (FETCH_SIZE / WRITE_SIZE,
+(2 FETCH + WRITE) x 1 KiB on gfx950), taken from profiles/*residual_traffic*.json only when the sha1 of
+csrc/stencil.hip + csrc/common.h recorded there is the current one (else null).
+CPU baseline ("port", oracle.fem): the same residual per field with scipy.sparse (K assembled from kappa,
+K_f yhat restricted by W^T) on one host core, a bounded sample of fields -- the reference assembles Gamma
+with FEniCS per VO sample (physics/LinearElliptic.py:137-159) and evaluates Gamma y - alpha
 (VirtualObservables.py:990), which is slower still.
 """
+import ctypes as C
+import glob
+import hashlib
 import json
 import os
 import sys
@@ -22,9 +29,30 @@ sys.path.insert(0, os.path.join(ROOT, 'generative-physics-informed-pde_amd'))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 from gpi import _lib as L  # noqa: E402
-import ctypes as C  # noqa: E402
 
-PEAK = 8000.0
+PEAK = 8000.0          # GB/s, MI355X HBM3E (MI355X_MICROARCH.md)
+CONFIGS = ((64, 8, 4096), (128, 8, 1024), (256, 8, 256))
+
+
+def stencil_sha():
+    h = hashlib.sha1()
+    for f in ('stencil.hip', 'common.h'):
+        with open(os.path.join(ROOT, 'generative-physics-informed-pde_amd', 'csrc', f), 'rb') as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
+def traffic_entries():
+    """{(grid, flux): traffic bytes per launch} from the newest sha-matched traffic file in profiles/."""
+    sha = stencil_sha()
+    for f in sorted(glob.glob(os.path.join(ROOT, 'profiles', '*residual_traffic*.json')), reverse=True):
+        try:
+            t = json.load(open(f))
+        except ValueError:
+            continue
+        if t.get('stencil_sha1') == sha:
+            return {(e['grid'], e['flux']): e for e in t['entries']}, os.path.basename(f)
+    return {}, None
 
 
 def launch(lk, y, bc, nc, r, rf):
@@ -36,7 +64,7 @@ def launch(lk, y, bc, nc, r, rf):
 
 
 def cpu_port(lk, y, bc, nc, n_fields):
-    """scipy.sparse restatement of one CGR residual per field (oracle-style, 1 core)."""
+    """scipy.sparse restatement of one CGR residual per field (oracle-style, 1 core); seconds per field."""
     from oracle import fem
     n = lk.shape[-1]
     mf = fem.unit_square_mesh(n)
@@ -50,16 +78,27 @@ def cpu_port(lk, y, bc, nc, n_fields):
 
 
 def main():
-    out = sys.argv[1] if len(sys.argv) > 1 else None
+    args = [a for a in sys.argv[1:] if not a.startswith('--')]
+    out = args[0] if args else None
+    quick = '--quick' in sys.argv
     dev = torch.device('cuda', 0)
+    tr, tr_file = traffic_entries()
     res = []
-    for n, nc, N in ((64, 8, 4096), (128, 8, 1024), (256, 8, 256)):
+    for n, nc, N in CONFIGS:
         g = torch.Generator(device='cpu').manual_seed(n)
         lk = (0.8 * torch.randn(N, n, n, generator=g)).to(dev)
         y = torch.randn(N, (n + 1) * (n - 1), generator=g).to(dev)
         bc = (torch.rand(N, 4, generator=g) - 0.5).to(dev)
         r = torch.empty(N, (nc + 1) ** 2, device=dev)
         rf = torch.empty(N, 2 * nc * nc, device=dev)
+        cpu = None
+        if n <= 128 and '--no-cpu' not in sys.argv:
+            ncpu = (2 if quick else 24) if n == 64 else (1 if quick else 3)
+            s = cpu_port(lk[:ncpu].cpu().numpy().astype(np.float64), y[:ncpu].cpu().numpy().astype(np.float64),
+                         bc[:ncpu].cpu().numpy().astype(np.float64), nc, ncpu)
+            cpu = dict(value=round(1.0 / s, 3), unit='fields/s', cores=1, kind='port',
+                       sample='%d fields of the %d^2 batch: oracle.fem scipy.sparse assembly + K yhat - f, W^T, '
+                              '1 host core' % (ncpu, n))
         for flux in (False, True):
             launch(lk, y, bc, nc, r, rf if flux else None)
             torch.cuda.synchronize()
@@ -72,17 +111,19 @@ def main():
             us = t0.elapsed_time(t1) * 1e3 / 20
             byt = 4.0 * N * (n * n + (n + 1) * (n - 1) + 4 + (nc + 1) ** 2 + (2 * nc * nc if flux else 0))
             gbs = byt / us / 1e3
-            res.append(dict(grid=n, nc=nc, fields=N, flux=flux, us_per_launch=round(us, 2),
-                            fields_per_s=round(N / us * 1e6), bytes_per_launch=byt, achieved_GBs=round(gbs, 1),
-                            peak_GBs=PEAK, frac=round(gbs / PEAK, 4)))
-            print(json.dumps(res[-1]))
-        if n <= 128:
-            ncpu = 8 if n == 64 else 2
-            s = cpu_port(lk[:ncpu].cpu().numpy().astype(np.float64), y[:ncpu].cpu().numpy().astype(np.float64),
-                         bc[:ncpu].cpu().numpy().astype(np.float64), nc, ncpu)
-            res.append(dict(grid=n, cpu_port_fields_per_s=round(1.0 / s, 2), cores=1,
-                            sample='%d fields, scipy.sparse assembly + K yhat + W^T (oracle.fem), 1 core' % ncpu))
-            print(json.dumps(res[-1]))
+            te = tr.get((n, flux))
+            line = dict(metric='coarse-grained residual fields/sec (%d^2 grid, nc %d%s)' % (n, nc, ', + flux rows'
+                                                                                        if flux else ''),
+                        value=round(N / us * 1e6), unit='fields/s', higher_is_better=True,
+                        grid=n, nc=nc, fields=N, flux=flux, us_per_launch=round(us, 2), dtype='f32',
+                        data='synthetic', roofline=dict(bound='hbm', achieved=round(gbs, 1), peak=PEAK,
+                                                        unit='GB/s', frac=round(gbs / PEAK, 4),
+                                                        algorithmic_bytes=byt,
+                                                        traffic=round(te['traffic_bytes']) if te else None,
+                                                        traffic_file=tr_file if te else None),
+                        cpu_baseline=cpu)
+            res.append(line)
+            print(json.dumps(line), flush=True)
     if out:
         with open(out, 'w') as fh:
             json.dump(res, fh, indent=1)
