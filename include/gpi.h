@@ -48,7 +48,9 @@ extern "C" {
 #endif
 /* workgroups of the fused step epilogue + Adam launch (grid-stride): well under one resident round of
  * 256-thread workgroups on 256 CUs, so its cross-stream wait cannot starve the signalling stream */
+#ifndef GPI_EPILOGUE_MAX_WG
 #define GPI_EPILOGUE_MAX_WG 512
+#endif
 
 /* Conv epilogues */
 #define GPI_EPI_STORE 0        /* store raw output */
