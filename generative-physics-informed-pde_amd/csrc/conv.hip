@@ -84,6 +84,10 @@ __host__ __device__ inline int fdiv2(int x) { return x >= 0 ? x / 2 : -((-x + 1)
 __host__ __device__ inline int cdiv2(int x) { return -fdiv2(-x); }
 __host__ __device__ inline int pad256(int n) { return (n + 255) & ~255; }
 
+// forward statistics epilogue: each wave's sums as fp64 atomics of its own (1) or the workgroup's sum through LDS (0)
+#ifndef GPI_FWD_WAVE_ATOMICS
+#define GPI_FWD_WAVE_ATOMICS 0
+#endif
 // forward (one pixel per thread): the per-channel weight offset forced into a VGPR (1) or left to the compiler (0)
 #ifndef GPI_FWD_WVGPR
 #define GPI_FWD_WVGPR 1
@@ -1058,11 +1062,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NPX == 0 ? 
         return;
     }
     if (d.epilogue == GPI_EPI_STORE_STATS && !SKIP(G, 128)) {
+#if GPI_FWD_WAVE_ATOMICS
+        // per-wave sums straight to the fp64 replicas (no LDS stage, no barrier): 4 atomics per (channel, stat)
+        // per workgroup instead of 1, the wave's own replica (4 blockIdx + wave)
+        wave_sums(vst);
+        const int lane = tid & 63;
+        if (lane < 2 * d.cout && !SKIP(G, 4)) {
+            float v = vst[0];
+#pragma unroll
+            for (int q = 1; q < 2 * CP; ++q) v = lane == q ? vst[q] : v;
+            gpi_stat* st = c.stats + ((int64_t)((4 * blockIdx.x + (tid >> 6)) % GPI_REPLICAS) * GPI_MAX_GROUPS + T.grp) *
+                                         c.n_stats + d.out_stat + (lane >> 1);
+            atomicAdd((lane & 1) ? &st->sumsq : &st->sum, (double)v);
+        }
+#else
         block_sum<2 * CP>(vst, scratch, red);   // thread t < 2 CP wrote red[t] itself: no barrier
         if (tid < 2 * d.cout && !SKIP(G, 4)) {
             gpi_stat* st = stat_slot(c, d.out_stat + (tid >> 1), T.grp);
             atomicAdd((tid & 1) ? &st->sumsq : &st->sum, (double)red[tid]);
         }
+#endif
     }
     PHASE(7);
     RTSTAMP(1);

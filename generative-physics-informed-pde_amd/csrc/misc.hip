@@ -263,7 +263,10 @@ __global__ __launch_bounds__(256) void subset_compact_kernel(uint2* cand, uint32
     }
 }
 
-// one wave per candidate (grid-stride over the waves): its rank among all C candidates
+// one wave per candidate (grid-stride over the waves): its rank among all C candidates.  O(C^2) compares
+// (C ~ k + n / 65536): the path draws k of a few hundred to a few thousand (the reference's subset and
+// batch sizes), where this is a handful of microseconds; a k of tens of thousands would want a
+// segmented radix sort of the candidates instead.
 __global__ __launch_bounds__(256) void subset_cand_rank_kernel(int32_t* out, const uint2* cand, const uint32_t* ctl,
                                                                int32_t k) {
     const int C = (int)ctl[1];

@@ -1,0 +1,13 @@
+set -u
+R=$(pwd); OUT=$R/gpurun_out; mkdir -p $OUT
+T=${1:-r05n}
+GPI_LIB_VARIANT=wat timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -q -x -p no:cacheprovider --timeout 120 --timeout-method thread > $OUT/${T}_wat_tests.log 2>&1; rc=$?; tail -2 $OUT/${T}_wat_tests.log; [ $rc -le 1 ] || exit $rc
+ITER_TESTS=none ITER_REPS=3 ITER_STEPS=400 ITER_PROF=0 bash tools/r04_iter.sh ${T}_ab - GPI_LIB_VARIANT=wat
+cd /tmp && export TMPDIR=/tmp
+for arm in "-" "wat"; do
+  if [ "$arm" = "-" ]; then unset GPI_LIB_VARIANT; else export GPI_LIB_VARIANT=$arm; fi
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_${T}_$arm" -o run -- \
+    python3 "$R/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-roofline > "$OUT/prof_${T}_$arm.log" 2>&1
+  rc=$?; echo "rocprof [$arm] rc=$rc"; [ $rc -eq 0 ] || exit $rc
+  python3 $R/tools/prof_summary.py "$OUT/prof_${T}_$arm" 60 | grep -i "conv_fwd\|epilogue" | head -20
+done
