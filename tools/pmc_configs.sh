@@ -23,7 +23,8 @@ for CFG in "$@"; do
     # the traffic file where bench.py looks for it (TRAFFIC_FILES), then the config's CPU-baseline +
     # roofline bench line (short)
     cd "$R"
-    if [ "$CFG" = "c64" ]; then TF=r04_traffic.json; else TF=r04_traffic_$CFG.json; fi
+    P=${TPFX:-r05}
+    if [ "$CFG" = "c64" ]; then TF=${P}_traffic.json; else TF=${P}_traffic_$CFG.json; fi
     cp "$OUT/traffic_${TAG}_$CFG.json" "$R/profiles/$TF"
     timeout -k 10 300 python3 bench.py --config "$CFG" --steps 50 --warmup 10 > "$OUT/bench_${TAG}_$CFG.json" \
         2> "$OUT/bench_${TAG}_$CFG.err"
