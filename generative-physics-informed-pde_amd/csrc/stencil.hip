@@ -372,6 +372,9 @@ __device__ __forceinline__ float dpp_shr1(float v, float in0) {      // lane l <
 __device__ __forceinline__ float dpp_shl1(float v, float in63) {     // lane l <- lane l + 1; lane 63 <- in63
     return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(in63), __float_as_int(v), 0x130, 0xf, 0xf, false));
 }
+__device__ __forceinline__ float dpp_shr1_z(float v) {              // lane l <- lane l - 1; lane 0 <- 0
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x138, 0xf, 0xf, true));
+}
 __device__ __forceinline__ float lane_of(float v, int l) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
@@ -393,6 +396,12 @@ struct StaticFor<N, N> {
 template <int N, typename F>
 __device__ __forceinline__ void static_for(F& f) { StaticFor<0, N>::run(f); }
 
+// FLUX, band rows r <= this: the edge terms as per-lane sums and the diagonal term at the band's end from five
+// loads per lane; above, every term per row (the end loads hit r rows per square, uncoalesced, and the extra
+// sums cost registers: both slower at r = 16 / 32, r05r)
+#ifndef GPI_CGR_DIAG_END_R
+#define GPI_CGR_DIAG_END_R 8
+#endif
 #ifndef GPI_CGR_PF
 #define GPI_CGR_PF 4               // band rows loaded ahead (x columns per lane: 4 measured ahead of 8, r05f)
 #endif
@@ -417,7 +426,9 @@ __global__ __launch_bounds__(512) void cgr_band_kernel(gpi_residual_desc d) {
     const int j0 = J * R;
     const bool top = J == nc - 1;                                  // the top band also owns node row n
     // raw loads of band row jr (node row j = j0 + jr): kappa pixel row j (log), y node row j + 1; clamped
-    // addresses, masked after the load (branch-free: exact wait counts)
+    // row addresses (branch-free: exact wait counts); the y lanes off the free columns (0, n and past n) read
+    // past the buffer's end, i.e. 0, so no per-row lane masks (kappa of the lanes >= n is finite and only
+    // reaches the non-free lanes, whose sums are dropped at the band's end)
     // buffer loads: the row in the (scalar) soffset, the column in a per-lane voffset fixed for the band, so
     // no per-row 64-bit addresses are held in registers across the unrolled rows
     const auto rk = __builtin_amdgcn_make_buffer_rsrc((void*)lk, (short)0, 4 * n * n, 0x00020000);
@@ -427,7 +438,7 @@ __global__ __launch_bounds__(512) void cgr_band_kernel(gpi_residual_desc d) {
     for (int m = 0; m < MM; ++m) {
         const int i = 64 * m + lane;
         vk[m] = 4 * min(i, n - 1);
-        vy[m] = 4 * (min(max(i, 1), n - 1) - 1);
+        vy[m] = (i >= 1 && i <= n - 1) ? 4 * (i - 1) : 0x7ffffff0;   // out of range: the load returns 0
     }
     auto load_k = [&](int j, int m) -> float {
         const int jj = min(max(j, 0), n - 1);
@@ -447,8 +458,17 @@ __global__ __launch_bounds__(512) void cgr_band_kernel(gpi_residual_desc d) {
         }
     // carried rows: kappa of pixel row j - 1 (kd, and kdl = kd of pixel i - 1), y of rows j - 1 (yd) and j
     // (yc, free values only: 0 at the Dirichlet columns)
-    float kd[MM], kdl[MM], yd[MM], yc[MM];
+    float kd[MM], kdl[MM], yd[MM], yc[MM], kdd[MM];
+    // per lane over the band: S = sum Ky, E = sum eta Ky, C1 = sum max(xi - eta, 0) Ky (Ky without its factor
+    // 1/2); the four W^T weights of a node (1 - max(xi, eta), max(xi - eta, 0), max(eta - xi, 0), min(xi, eta))
+    // follow from these and xi at the band's end (max(xi, eta) = eta + P, min(xi, eta) = eta - Q, Q = P - xi + eta)
     float c[MM][4], flr[MM], ful[MM];
+    // FLUX, per lane over the band: fe1 = sum kur (u1 - u0) (the right-edge term), fe2 = sum kur (u2 - u3)
+    // (left edge), and in flr / ful the bottom / top edge terms (band rows 0 / r - 1); the edge sums enter on
+    // the edge lanes at the band's end, with the diagonal term (row tr = the lane's column in its square), whose
+    // five operands are loaded there (L2 hits: the band has just streamed them)
+    float fe1[MM], fe2[MM];
+    constexpr bool DEND = R <= GPI_CGR_DIAG_END_R;
     {
         float kp[MM];
 #pragma unroll
@@ -456,18 +476,30 @@ __global__ __launch_bounds__(512) void cgr_band_kernel(gpi_residual_desc d) {
             const int i = 64 * m + lane;
             const float k = expf(load_k(j0 - 1, m));
             kp[m] = (j0 > 0 && i < n) ? k : 0.f;
-            const bool fr = i >= 1 && i <= n - 1;
             const float a = load_y(j0 - 1, m), b = load_y(j0, m);
-            yd[m] = (j0 > 0 && fr) ? a : 0.f;
-            yc[m] = fr ? b : 0.f;
+            yd[m] = j0 > 0 ? a : 0.f;
+            yc[m] = b;
             c[m][0] = c[m][1] = c[m][2] = c[m][3] = 0.f;
-            flr[m] = ful[m] = 0.f;
+            flr[m] = ful[m] = fe1[m] = fe2[m] = 0.f;
         }
 #pragma unroll
         for (int m = 0; m < MM; ++m) {
             kd[m] = kp[m];
             kdl[m] = dpp_shr1(kp[m], m > 0 ? lane_of(kp[m > 0 ? m - 1 : 0], 63) : 0.f);
+            kdd[m] = kdl[m] + kd[m];
         }
+    }
+    // the Dirichlet data (x = 0: u0 + (u1 - u0) t, x = 1: u2 + (u3 - u2) t at t = j / n), linear in the band row
+    // jr: per lane dA + dB jr on columns 0 and n (0 elsewhere), added to the free values; bra + brb jr the
+    // right neighbour of the last chunk's lane 63 when 64 MM = n
+    float dA[MM], dB[MM];
+    const float dl = (u1b - u0b) * rfn, dr = (u3b - u2b) * rfn;
+    const float bra = fmaf(dr, (float)j0, u2b), brb = dr;
+#pragma unroll
+    for (int m = 0; m < MM; ++m) {
+        const int i = 64 * m + lane;
+        dA[m] = i == 0 ? fmaf(dl, (float)j0, u0b) : (i == n ? bra : 0.f);
+        dB[m] = i == 0 ? dl : (i == n ? dr : 0.f);
     }
     auto row = [&](auto jr_c) {
         constexpr int jr = decltype(jr_c)::value;
@@ -478,19 +510,16 @@ __global__ __launch_bounds__(512) void cgr_band_kernel(gpi_residual_desc d) {
         const int p = jr % PF;
         float eta = (float)jr * rinv;
         asm volatile("" : "+v"(eta));
-        // the Dirichlet data of row j (x = 0 / x = 1), uniform: one division per row
-        const float tb = (float)j * rfn;
-        const float bl = u0b * (1.f - tb) + u1b * tb, br = u2b * (1.f - tb) + u3b * tb;
         float ku[MM], yu[MM], yhc[MM];
 #pragma unroll
         for (int m = 0; m < MM; ++m) {
-            const int i = 64 * m + lane;
-            const float k = __builtin_amdgcn_exp2f(kraw[p][m] * 1.4426950408889634f);
-            ku[m] = (j < n && i < n) ? k : 0.f;                      // kappa(i, j) = kur
-            yu[m] = (j < n && i >= 1 && i <= n - 1) ? yraw[p][m] : 0.f;   // y(i, j + 1), free values
+            // kappa(i, j) = kur and y(i, j + 1) (free values); none above node row n (the top band's row R)
+            ku[m] = jr == R ? 0.f : __builtin_amdgcn_exp2f(kraw[p][m] * 1.4426950408889634f);
+            yu[m] = jr == R ? 0.f : yraw[p][m];
             // yhat of row j: the Dirichlet data at columns 0 and n
-            yhc[m] = i == 0 ? bl : (i == n ? br : yc[m]);
+            yhc[m] = fmaf(dB[m], (float)jr, dA[m]) + yc[m];
         }
+        const float br = fmaf(brb, (float)jr, bra);
         // the next row's loads into the freed slot
         if (jr + PF <= R) {
 #pragma unroll
@@ -504,31 +533,27 @@ __global__ __launch_bounds__(512) void cgr_band_kernel(gpi_residual_desc d) {
 #pragma unroll
         for (int m = 0; m < MM; ++m) {
             const int i = 64 * m + lane;
-            const bool act = i >= 1 && i <= n - 1;
             // neighbours across the 64-column chunk edges
-            const float kl_in = m > 0 ? lane_of(ku[m > 0 ? m - 1 : 0], 63) : 0.f;
-            const float yl_in = m > 0 ? lane_of(yhc[m > 0 ? m - 1 : 0], 63) : 0.f;
             const float yr_in = m < MM - 1 ? lane_of(yhc[m < MM - 1 ? m + 1 : 0], 0) : (64 * MM == n ? br : 0.f);
-            // (the wave shifts run unconditionally: a DPP move under a lane condition became a branch)
-            const float sk = dpp_shr1(ku[m], kl_in), sl = dpp_shr1(yhc[m], yl_in), sr = dpp_shl1(yhc[m], yr_in);
-            const float kul = act ? sk : 0.f;
-            const float kur = ku[m];
-            const float kdlm = act ? kdl[m] : 0.f, kdr = kd[m];
-            const float ycm = yc[m];                                  // 0 unless act
-            const float yl = act ? sl : 0.f;
-            const float yrr = act ? sr : 0.f;
-            const float ydm = yd[m], yum = act ? yu[m] : 0.f;
-            float Ky = (kul + kdlm) * (ycm - yl) + (kur + kdr) * (ycm - yrr);
-            if (j > 0) Ky += (kdlm + kdr) * (ycm - ydm);
-            if (j < n) Ky += (kul + kur) * (ycm - yum);
-            Ky = act ? 0.5f * Ky : 0.f;
+            // (the wave shifts run unconditionally: a DPP move under a lane condition became a branch; the
+            // first chunk's take 0 at lane 0 by the DPP bound control, no extra move)
+            const float sk = m > 0 ? dpp_shr1(ku[m], lane_of(ku[m > 0 ? m - 1 : 0], 63)) : dpp_shr1_z(ku[m]);
+            const float sl = m > 0 ? dpp_shr1(yhc[m], lane_of(yhc[m > 0 ? m - 1 : 0], 63)) : dpp_shr1_z(yhc[m]);
+            const float sr = dpp_shl1(yhc[m], yr_in);
+            // no lane masks inside: every operand is finite, the rows below 0 / above n have kappa 0 (their
+            // terms vanish), and the lanes off the free columns are zeroed once at the band's end
+            const float kul = sk, kur = ku[m], kdlm = kdl[m], kdr = kd[m];
+            const float ycm = yc[m], yl = sl, yrr = sr, ydm = yd[m], yum = yu[m];
+            const float a = kul + kdlm, b = kur + kdr, dd = kul + kur, cc = kdd[m];
+            // 2 Ky = (a + b + cc + dd) ycm - a yl - b yr - cc yd - dd yu, a + b + cc + dd = 2 (cc + dd)
+            const float s4 = fmaf(a, yl, fmaf(b, yrr, fmaf(cc, ydm, dd * yum)));
+            const float Ky = fmaf(2.f * (cc + dd), ycm, -s4);
             int I = i / R;
             if (I > nc - 1) I = nc - 1;
             const float xi = (float)(i - I * R) * rinv;
-            c[m][0] += (1.f - fmaxf(xi, eta)) * Ky;
-            c[m][1] += fmaxf(xi - eta, 0.f) * Ky;
-            c[m][2] += fmaxf(eta - xi, 0.f) * Ky;
-            c[m][3] += fminf(xi, eta) * Ky;
+            c[m][0] += Ky;
+            c[m][1] = fmaf(eta, Ky, c[m][1]);
+            c[m][2] = fmaf(fmaxf(xi - eta, 0.f), Ky, c[m][2]);
             // u1 = y(i + 1, j), u3 = y(i + 1, j + 1): free values of the right neighbour (0 at column n)
             float u1 = 0.f, u3 = 0.f;
             if (FLUX) {
@@ -537,15 +562,23 @@ __global__ __launch_bounds__(512) void cgr_band_kernel(gpi_residual_desc d) {
                 u1 = dpp_shl1(yc[m], y1_in);
                 u3 = dpp_shl1(yu[m], y3_in);
             }
-            if (FLUX && i < n && j < n) {
+            if (FLUX && DEND && jr < R) {      // (lanes >= n: their square's sums are never stored)
                 const float u0 = ycm, u2 = yum;
-                const int tr = i - (i / R) * R, tj = jr;
+                fe1[m] = fmaf(kur, u1 - u0, fe1[m]);            // right edge (tr = r - 1 lanes)
+                fe2[m] = fmaf(kur, u2 - u3, fe2[m]);            // left edge (tr = 0 lanes)
+                if (jr == 0 && J > 0) flr[m] = kur * (u1 - u3);          // bottom edge (not on y = 0)
+                if (jr == R - 1 && J < nc - 1) ful[m] = fmaf(kur, u2 - u0, ful[m]);   // top edge (not on y = 1)
+            }
+            if (FLUX && !DEND && jr < R) {
+                // r >= 16: every term per row (the edge sums as extra accumulators measured slower at r = 32)
+                const float u0 = ycm, u2 = yum;
+                const int tr = i - (i / R) * R;
                 float vl = 0.f, vu = 0.f;
-                if (tj == 0 && J > 0) vl += u1 - u3;             // bottom edge (not on y = 0)
+                if (jr == 0 && J > 0) vl += u1 - u3;             // bottom edge (not on y = 0)
                 if (tr == R - 1) vl += u1 - u0;                  // right edge
                 if (tr == 0) vu += u2 - u3;                      // left edge
-                if (tj == R - 1 && J < nc - 1) vu += u2 - u0;    // top edge (not on y = 1)
-                if (tr == tj) { vl += u0 - 2.f * u1 + u3; vu += u0 - 2.f * u2 + u3; }   // diagonal
+                if (jr == R - 1 && J < nc - 1) vu += u2 - u0;    // top edge (not on y = 1)
+                if (tr == jr) { vl += u0 - 2.f * u1 + u3; vu += u0 - 2.f * u2 + u3; }   // diagonal
                 flr[m] = fmaf(kur, vl, flr[m]);
                 ful[m] = fmaf(kur, vu, ful[m]);
             }
@@ -554,14 +587,16 @@ __global__ __launch_bounds__(512) void cgr_band_kernel(gpi_residual_desc d) {
         // not sunk to the band's end with every row's operands held live until then)
 #pragma unroll
         for (int m = 0; m < MM; ++m) {
-            asm volatile("" : "+v"(c[m][0]), "+v"(c[m][1]), "+v"(c[m][2]), "+v"(c[m][3]));
+            asm volatile("" : "+v"(c[m][0]), "+v"(c[m][1]), "+v"(c[m][2]));
             if (FLUX) asm volatile("" : "+v"(flr[m]), "+v"(ful[m]));
+            if (FLUX && DEND) asm volatile("" : "+v"(fe1[m]), "+v"(fe2[m]));
         }
         // carry: row j becomes the row below
 #pragma unroll
         for (int m = 0; m < MM; ++m) {
-            kdl[m] = dpp_shr1(ku[m], m > 0 ? lane_of(ku[m > 0 ? m - 1 : 0], 63) : 0.f);   // (= sk: CSE)
+            kdl[m] = m > 0 ? dpp_shr1(ku[m], lane_of(ku[m > 0 ? m - 1 : 0], 63)) : dpp_shr1_z(ku[m]);   // (= sk: CSE)
             kd[m] = ku[m];
+            kdd[m] = kdl[m] + kd[m];                                  // (= dd: CSE)
             yd[m] = yc[m];
             yc[m] = yu[m];
         }
@@ -573,6 +608,39 @@ __global__ __launch_bounds__(512) void cgr_band_kernel(gpi_residual_desc d) {
     constexpr int G = (R & (R - 1)) == 0 ? (R < 64 ? R : 64) : 1;
 #pragma unroll
     for (int m = 0; m < MM; ++m) {
+        {
+            const int i = 64 * m + lane;
+            int I = i / R;
+            if (I > nc - 1) I = nc - 1;
+            const float xi = (float)(i - I * R) * rinv;
+            const float h = (i >= 1 && i <= n - 1) ? 0.5f : 0.f;     // Ky's 1/2; the free columns only
+            const float S = h * c[m][0], E = h * c[m][1], C1 = h * c[m][2];
+            const float C2 = C1 - xi * S + E;
+            c[m][0] = S - E - C1;
+            c[m][1] = C1;
+            c[m][2] = C2;
+            c[m][3] = E - C2;
+            if (FLUX && DEND) {
+                const int tr = i - (i / R) * R;
+                if (tr == R - 1) flr[m] += fe1[m];
+                if (tr == 0) ful[m] += fe2[m];
+                // the diagonal node (i, j0 + tr) of the lane's square: kappa(i, jd), y(i | i + 1, jd | jd + 1)
+                const int jd = j0 + tr;
+                {
+                const int vy1 = (i + 1 >= 1 && i + 1 <= n - 1) ? 4 * i : 0x7ffffff0;
+                const float kdg = __builtin_amdgcn_exp2f(
+                    __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rk, vk[m] + 4 * (n - 1 - jd) * n, 0, 0)) *
+                    1.4426950408889634f);
+                const int o0 = 4 * jd * (n - 1), o1 = o0 + 4 * (n - 1);
+                const float u0 = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(ry, vy[m] + o0, 0, 0));
+                const float u1 = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(ry, vy1 + o0, 0, 0));
+                const float u2 = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(ry, vy[m] + o1, 0, 0));
+                const float u3 = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(ry, vy1 + o1, 0, 0));
+                flr[m] = fmaf(kdg, u0 - 2.f * u1 + u3, flr[m]);
+                ful[m] = fmaf(kdg, u0 - 2.f * u2 + u3, ful[m]);
+                }
+            }
+        }
 #pragma unroll
         for (int o = 1; o < G; o <<= 1) {
 #pragma unroll
