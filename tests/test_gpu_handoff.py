@@ -5,6 +5,7 @@ that step (and of every later one: the word is sticky) leaves parameters and Ada
 the host raises (check_handoff at once, step() / run() lazily from an async copy of the word)."""
 import ctypes as C
 
+import numpy as np
 import pytest
 import torch
 
@@ -67,3 +68,113 @@ def test_fused_step_wait_timeout_skips_update_and_raises(device):
     torch.cuda.synchronize()
     with pytest.raises(RuntimeError, match='timed out'):
         st.step()
+
+
+def _c256_step(seed):
+    """FusedElboStep at BASELINE config 5's per-GPU shape (256^2, B_u = 128 of 256, N_s = 32, droprate 0.2):
+    the largest flat vector the fused epilogue + Adam launch covers."""
+    from factories.model import ModelFactory
+    from gpi.train import FusedElboStep
+    from test_gpu_c64 import _DS
+    n, Nu, bs, Ns = 256, 256, 128, 32
+    torch.manual_seed(seed)
+    fac = ModelFactory.FromIdentifier('highres256')
+    fac.set('device', 'cuda')
+    physics_, model, _, encoder, _, _ = fac.setup()
+    model.encoder = encoder.cuda()
+    nc = physics_['rom'].grid.n
+    rng = np.random.default_rng(n)
+    Xu = torch.tensor(rng.normal(0.3, 0.6, (Nu, n, n)), dtype=torch.float32, device='cuda')
+    Xs = torch.tensor(rng.normal(0.3, 0.6, (Ns, n, n)), dtype=torch.float32, device='cuda')
+    Y = torch.tensor(rng.normal(0.0, 0.3, (Ns, (n + 1) * (n - 1))), dtype=torch.float32, device='cuda')
+    F = np.zeros((Ns, (nc + 1) ** 2), dtype=np.float32)
+    F[:, [e for e in range((nc + 1) ** 2) if e % (nc + 1) in (0, nc)]] = rng.uniform(-0.5, 0.5, (Ns, 2 * (nc + 1)))
+    F = torch.tensor(F, device='cuda')
+    model.register_datasets({'supervised': _DS(X=Xs, Y=Y, F_ROM_BC=F),
+                             'unsupervised': _DS(perm=torch.arange(Nu, device='cuda'), X=Xu)}, None,
+                            create_unsupervised_variational_approximation=False)
+    model.cuda()
+    return FusedElboStep(model, Xu, bs, Xs, Y, F, lr=1e-3, seed=5)
+
+
+def test_fused_epilogue_progresses_with_a_delayed_side_stream(device):
+    """the fused epilogue + Adam launch spins on the side stream's flag in every
+    workgroup, so it must never hold enough workgroups to keep the side stream's kernels off the CUs.  At
+    config 5's per-GPU shape (the largest flat vector) the side stream is held back ~0.1 s by a sleep
+    kernel ahead of its work, so the main stream reaches the epilogue first and spins there: the step still
+    completes without a wait timeout, and its parameters match an undelayed step's (atomic-order rounding
+    of the BN statistics aside: 1e-6 of the largest parameter)."""
+    a = _c256_step(11)
+    if a.handoff != 'flags' or not a.fuse_adam:
+        pytest.skip('no flag hand-off into the fused epilogue in this configuration')
+    a.step()
+    torch.cuda.synchronize()
+    a.check_handoff()
+    b = _c256_step(11)
+    side = b.engine._side_stream()
+    with torch.cuda.stream(side):
+        torch.cuda._sleep(int(2.5e8))           # ~0.1 s at the shader clock
+    import time
+    t0 = time.perf_counter()
+    b.step()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    e = b.epi
+    m = max(e.n, e.n_scratch, e.n_idx, (e.drop_n + 3) // 4)
+    print('epilogue items %d (%d workgroups uncapped), delayed step %.3f s' % (m, (m + 255) // 256, dt))
+    b.check_handoff()                           # raises on a wait timeout
+    scale = float(a.flat.P.abs().max())
+    assert float((a.flat.P - b.flat.P).abs().max()) <= 1e-6 * scale
+
+
+def _separate_side_stream():
+    """A stream on another hardware queue than the current one (as FusedElboStep._queues_separate)."""
+    from gpi import _lib as L
+    pr = torch.zeros(2, dtype=torch.int32, device='cuda')
+    ctr = torch.zeros(1, dtype=torch.int64, device='cuda')
+    for _ in range(4):
+        side = torch.cuda.Stream()
+        pr.zero_()
+        torch.cuda.synchronize()
+        L.check(L.lib().gpi_queue_probe(L.ptr(pr), L.ptr(pr[1:]), C.c_void_p(side.cuda_stream)), 'queue probe')
+        L.check(L.lib().gpi_stream_signal(L.ptr(pr), L.ptr(ctr), L.stream_handle()), 'queue probe signal')
+        torch.cuda.synchronize()
+        if int(pr[1].item()) == 1:
+            return side
+    pytest.skip('no stream on a separate hardware queue')
+
+
+def test_epilogue_grid_leaves_room_for_the_signalling_stream(device):
+    """ADVICE r04 (high), at the ABI: gpi_step_epilogue_adam over 2^23 elements (32 768 workgroups if one
+    element per thread -- far more than the chip holds) whose every workgroup spins on a flag that another
+    stream signals only after a ~20 ms sleep kernel.  The grid-stride launch of <= GPI_EPILOGUE_MAX_WG
+    workgroups leaves CU slots for the signal kernel: no wait timeout, the update done, the accumulator
+    delivered and zeroed.  (A one-element-per-thread grid fills every slot with spinning workgroups: the
+    signal cannot run until they time out, and the error word is set -- checked with the cap lifted.)"""
+    from gpi import _lib as L
+    n = 1 << 23
+    torch.manual_seed(1)
+    gacc = torch.randn(n, dtype=torch.float64, device='cuda')
+    g0 = gacc.float()
+    grad = torch.empty(n, device='cuda')
+    p = torch.randn(n, device='cuda')
+    p0 = p.clone()
+    m, v = torch.zeros_like(p), torch.zeros_like(p)
+    lr = torch.tensor([1e-3], device='cuda')
+    step = torch.zeros(1, dtype=torch.int64, device='cuda')
+    flag, err, done = (torch.zeros(1, dtype=torch.int32, device='cuda') for _ in range(3))
+    side = _separate_side_stream()
+    d = L.StepEpilogueDesc(gacc=gacc.data_ptr(), grad=grad.data_ptr(), n=n, flags=2, wait_flag=flag.data_ptr(),
+                           wait_err=err.data_ptr())
+    a = L.AdamDesc(p=p.data_ptr(), g=grad.data_ptr(), m=m.data_ptr(), v=v.data_ptr(), n=n, lr=lr.data_ptr(),
+                   step=step.data_ptr(), beta1=0.9, beta2=0.999, eps=1e-8, wait_err=err.data_ptr())
+    torch.cuda.synchronize()
+    with torch.cuda.stream(side):
+        torch.cuda._sleep(int(5e7))
+    L.check(L.lib().gpi_step_epilogue_adam(C.byref(d), C.byref(a), L.ptr(done), L.stream_handle()), 'epilogue')
+    L.check(L.lib().gpi_stream_signal(L.ptr(flag), L.ptr(step), C.c_void_p(side.cuda_stream)), 'signal')
+    torch.cuda.synchronize()
+    assert int(err.item()) == 0, 'the epilogue wait timed out: its workgroups kept the signal off the CUs'
+    assert int(step.item()) == 1 and int(done.item()) == 0
+    assert torch.equal(grad, g0) and int(gacc.abs().max().item() == 0) == 1
+    assert not torch.equal(p, p0)
