@@ -40,17 +40,53 @@ def test_fom_labels_match_oracle(device, n, N):
         assert np.abs(y[k] - ref).max() < 1e-9, (n, k, np.abs(y[k] - ref).max(), iters[k])
 
 
+@pytest.mark.parametrize('n,N', [(8, 4), (32, 6), (64, 3)])
+def test_fom_multigrid_labels_match_oracle(device, monkeypatch, n, N):
+    """The multigrid-preconditioned CG (fom_mgcg_kernel, the default from 32^2) forced onto every
+    power-of-two grid from 8^2 (GPI_FOM_MG_MIN=8): labels vs the oracle's dense FE solve at 1e-9, in a few
+    tens of iterations where the Jacobi form needs hundreds (407 on average at 64^2)."""
+    monkeypatch.setenv('GPI_FOM_MG_MIN', '8')
+    xd, U = fields(n, N, n + 1, l=0.04 if n == 64 else 0.15)
+    y, iters, flag = solve(xd, U, n)
+    assert flag == 0 and iters.max() <= 40, iters
+    mesh = fem.unit_square_mesh(n)
+    for k in range(N):
+        ref = fem.solve_fom(mesh, np.exp(xd[k]), U[k])
+        assert np.abs(y[k] - ref).max() < 1e-9, (n, k, np.abs(y[k] - ref).max(), iters[k])
+    U[0] = 0.0                                   # zero data: converged on entry
+    y0, it0, flag0 = solve(xd, U, n)
+    assert flag0 == 0 and it0[0] == 0 and np.abs(y0[0]).max() == 0.0
+    _, it2, flag2 = solve(xd, U, n, max_iter=2)  # iteration cap reported
+    assert flag2 == N - 1 and it2.max() == 2
+
+
 @pytest.mark.parametrize('n,N', [(128, 3), (256, 2)])
 def test_fom_large_grid_residual(device, n, N):
     xd, U = fields(n, N, n, l=0.04)
     y, iters, flag = solve(xd, U, n)
-    assert flag == 0
+    assert flag == 0 and iters.max() <= 40, iters      # multigrid-preconditioned from 32^2
     mesh = fem.unit_square_mesh(n)
     for k in range(N):
         kap = np.exp(xd[k])
         r = fem.fom_residual(mesh, kap, U[k], y[k])
         b = fem.fom_residual(mesh, kap, U[k], np.zeros_like(y[k]))
         assert np.linalg.norm(r) <= 1e-10 * np.linalg.norm(b), (n, k, np.linalg.norm(r) / np.linalg.norm(b))
+
+
+def test_fom_jacobi_workspace_kernel_residual(device, monkeypatch):
+    """The Jacobi-preconditioned workspace kernel (fom_pcg_kernel: grids past the register form, non-powers
+    of two, or GPI_FOM_MG_MIN=0) at 128^2: FE residual 1e-10 of ||f_eff||, as the multigrid form's."""
+    monkeypatch.setenv('GPI_FOM_MG_MIN', '0')
+    n, N = 128, 2
+    xd, U = fields(n, N, n + 5, l=0.04)
+    y, iters, flag = solve(xd, U, n)
+    assert flag == 0 and iters.min() > 100, iters
+    mesh = fem.unit_square_mesh(n)
+    for k in range(N):
+        kap = np.exp(xd[k])
+        r = fem.fom_residual(mesh, kap, U[k], y[k])
+        b = fem.fom_residual(mesh, kap, U[k], np.zeros_like(y[k]))
+        assert np.linalg.norm(r) <= 1e-10 * np.linalg.norm(b), (k, np.linalg.norm(r) / np.linalg.norm(b))
 
 
 def test_fom_edge_cases(device):
