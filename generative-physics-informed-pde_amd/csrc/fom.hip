@@ -466,19 +466,64 @@ __global__ __launch_bounds__(FT) void fom_mgcg_kernel(gpi_fom_desc d, FomGeom G,
     };
     // one red-black half sweep of A e = b (zero: e = 0 before it, so the colour's neighbours are 0 and
     // the other colour is zeroed in the same pass)
+    // (every pass below handles MGU nodes per thread and trip, their loads issued before any store: the
+    // passes are latency-bound, one workgroup per sample)
+    constexpr int MGU = 4;
     auto half = [&](const MgLev& L, int colour, bool zero) {
-        const int mm = L.n - 1;
-        const int64_t ny = mg_dy(L.n);
-        for (int64_t p = tid; p < ny; p += FT) {
-            const int j = (int)(p / mm), i = (int)(p - (int64_t)j * mm) + 1;
-            if (((i + j) & 1) != colour) {
-                if (zero) L.e[p] = 0.0;
-                continue;
+        const int m = L.n, mm = m - 1;
+        if (zero) {
+            const int64_t ny = mg_dy(m);
+            for (int64_t p0 = tid; p0 < ny; p0 += MGU * FT) {
+                double dg[MGU], bv[MGU];
+                bool red[MGU];
+#pragma unroll
+                for (int u = 0; u < MGU; ++u) {
+                    const int64_t p = p0 + (int64_t)u * FT;
+                    red[u] = false;
+                    if (p >= ny) continue;
+                    const int j = (int)(p / mm), i = (int)(p - (int64_t)j * mm) + 1;
+                    red[u] = ((i + j) & 1) == colour;
+                    const double cl = L.ch[j * m + i - 1], cr = L.ch[j * m + i];
+                    const double cd = j > 0 ? L.cv[(j - 1) * (m + 1) + i] : 0.0, cu = j < m ? L.cv[j * (m + 1) + i] : 0.0;
+                    dg[u] = cl + cr + cd + cu;
+                    bv[u] = L.b[p];
+                }
+#pragma unroll
+                for (int u = 0; u < MGU; ++u) {
+                    const int64_t p = p0 + (int64_t)u * FT;
+                    if (p < ny) L.e[p] = red[u] ? bv[u] / dg[u] : 0.0;
+                }
             }
-            double dg;
-            const double s = zero ? 0.0 : nb_sum(L, L.e, (int)p, i, j, dg);
-            if (zero) nb_sum(L, L.b, (int)p, i, j, dg);       // (the diagonal only)
-            L.e[p] = (L.b[p] + s) / dg;
+        } else {
+            // the colour's nodes only: row j holds them at i = i0(j) + 2 k, k < m / 2
+            const int hr = m / 2;
+            const int64_t nq = (int64_t)(m + 1) * hr;
+            for (int64_t q0 = tid; q0 < nq; q0 += MGU * FT) {
+                double val[MGU];
+                int64_t pp[MGU];
+#pragma unroll
+                for (int u = 0; u < MGU; ++u) {
+                    const int64_t q = q0 + (int64_t)u * FT;
+                    pp[u] = -1;
+                    if (q >= nq) continue;
+                    const int j = (int)(q / hr), k = (int)(q - (int64_t)j * hr);
+                    const int i = (((1 + j) & 1) == colour ? 1 : 2) + 2 * k;
+                    if (i > mm) continue;
+                    const int64_t p = (int64_t)j * mm + i - 1;
+                    pp[u] = p;
+                    const double cl = L.ch[j * m + i - 1], cr = L.ch[j * m + i];
+                    const double cd = j > 0 ? L.cv[(j - 1) * (m + 1) + i] : 0.0, cu = j < m ? L.cv[j * (m + 1) + i] : 0.0;
+                    double sum = L.b[p];
+                    if (i > 1) sum += cl * L.e[p - 1];
+                    if (i < mm) sum += cr * L.e[p + 1];
+                    if (j > 0) sum += cd * L.e[p - mm];
+                    if (j < m) sum += cu * L.e[p + mm];
+                    val[u] = sum / (cl + cr + cd + cu);
+                }
+#pragma unroll
+                for (int u = 0; u < MGU; ++u)
+                    if (pp[u] >= 0) L.e[pp[u]] = val[u];
+            }
         }
         __syncthreads();
     };
@@ -489,11 +534,22 @@ __global__ __launch_bounds__(FT) void fom_mgcg_kernel(gpi_fom_desc d, FomGeom G,
             half(L, 1, false);
             const int m = L.n, mm = m - 1;
             const int64_t ny = mg_dy(m);
-            for (int64_t p = tid; p < ny; p += FT) {                  // t = b - A e
-                const int j = (int)(p / mm), i = (int)(p - (int64_t)j * mm) + 1;
-                double dg;
-                const double s = nb_sum(L, L.e, (int)p, i, j, dg);
-                L.t[p] = L.b[p] - (dg * L.e[p] - s);
+            for (int64_t p0 = tid; p0 < ny; p0 += MGU * FT) {        // t = b - A e
+                double tv[MGU];
+#pragma unroll
+                for (int u = 0; u < MGU; ++u) {
+                    const int64_t p = p0 + (int64_t)u * FT;
+                    if (p >= ny) continue;
+                    const int j = (int)(p / mm), i = (int)(p - (int64_t)j * mm) + 1;
+                    double dg;
+                    const double s = nb_sum(L, L.e, (int)p, i, j, dg);
+                    tv[u] = L.b[p] - (dg * L.e[p] - s);
+                }
+#pragma unroll
+                for (int u = 0; u < MGU; ++u) {
+                    const int64_t p = p0 + (int64_t)u * FT;
+                    if (p < ny) L.t[p] = tv[u];
+                }
             }
             __syncthreads();
             const MgLev& Cl = lev[l + 1];
@@ -533,19 +589,30 @@ __global__ __launch_bounds__(FT) void fom_mgcg_kernel(gpi_fom_desc d, FomGeom G,
             const MgLev& Cl = lev[l + 1];
             const int m = L.n, mm = m - 1, mc = Cl.n, mcm = mc - 1;
             const int64_t ny = mg_dy(m);
-            for (int64_t p = tid; p < ny; p += FT) {                  // e += P e_c
-                const int j = (int)(p / mm), i = (int)(p - (int64_t)j * mm) + 1;
-                double s = 0.0;
-                const int I0 = i >> 1, J0 = j >> 1;
-                const int ni = (i & 1) ? 2 : 1, nj = (j & 1) ? 2 : 1;
-                const double wx = ni == 2 ? 0.5 : 1.0, wyv = nj == 2 ? 0.5 : 1.0;
-                for (int b2 = 0; b2 < nj; ++b2)
-                    for (int a2 = 0; a2 < ni; ++a2) {
-                        const int I = I0 + a2, J = J0 + b2;
-                        if (I < 1 || I > mcm) continue;                // Dirichlet columns: 0
-                        s += wx * wyv * Cl.e[(int64_t)J * mcm + I - 1];
-                    }
-                L.e[p] += s;
+            for (int64_t p0 = tid; p0 < ny; p0 += MGU * FT) {        // e += P e_c
+                double nv[MGU];
+#pragma unroll
+                for (int u = 0; u < MGU; ++u) {
+                    const int64_t p = p0 + (int64_t)u * FT;
+                    if (p >= ny) continue;
+                    const int j = (int)(p / mm), i = (int)(p - (int64_t)j * mm) + 1;
+                    double s = 0.0;
+                    const int I0 = i >> 1, J0 = j >> 1;
+                    const int ni = (i & 1) ? 2 : 1, nj = (j & 1) ? 2 : 1;
+                    const double wx = ni == 2 ? 0.5 : 1.0, wyv = nj == 2 ? 0.5 : 1.0;
+                    for (int b2 = 0; b2 < nj; ++b2)
+                        for (int a2 = 0; a2 < ni; ++a2) {
+                            const int I = I0 + a2, J = J0 + b2;
+                            if (I < 1 || I > mcm) continue;            // Dirichlet columns: 0
+                            s += wx * wyv * Cl.e[(int64_t)J * mcm + I - 1];
+                        }
+                    nv[u] = L.e[p] + s;
+                }
+#pragma unroll
+                for (int u = 0; u < MGU; ++u) {
+                    const int64_t p = p0 + (int64_t)u * FT;
+                    if (p < ny) L.e[p] = nv[u];
+                }
             }
             __syncthreads();
             half(L, 1, false);
@@ -588,21 +655,45 @@ __global__ __launch_bounds__(FT) void fom_mgcg_kernel(gpi_fom_desc d, FomGeom G,
     int it = 0;
     while (!conv && it < d.max_iter) {
         double pq = 0.0;
-        for (int64_t p = tid; p < dy; p += FT) {
-            const int j = (int)(p / nm), i = (int)(p - (int64_t)j * nm) + 1;
-            double dg;
-            const double s = nb_sum(lev[0], pv, (int)p, i, j, dg);
-            const double q = dg * pv[p] - s;
-            qv[p] = q;
-            pq += pv[p] * q;
+        for (int64_t p0 = tid; p0 < dy; p0 += MGU * FT) {
+            double qq[MGU];
+#pragma unroll
+            for (int u = 0; u < MGU; ++u) {
+                const int64_t p = p0 + (int64_t)u * FT;
+                if (p >= dy) continue;
+                const int j = (int)(p / nm), i = (int)(p - (int64_t)j * nm) + 1;
+                double dg;
+                const double s = nb_sum(lev[0], pv, (int)p, i, j, dg);
+                const double pp = pv[p];
+                qq[u] = dg * pp - s;
+                pq += pp * qq[u];
+            }
+#pragma unroll
+            for (int u = 0; u < MGU; ++u) {
+                const int64_t p = p0 + (int64_t)u * FT;
+                if (p < dy) qv[p] = qq[u];
+            }
         }
         const double alpha = rz / block_sum_d(pq, red);
         double r2 = 0.0;
-        for (int64_t p = tid; p < dy; p += FT) {
-            x[p] += alpha * pv[p];
-            const double rv = r[p] - alpha * qv[p];
-            r[p] = rv;
-            r2 += rv * rv;
+        for (int64_t p0 = tid; p0 < dy; p0 += MGU * FT) {
+            double xv[MGU], rv[MGU];
+#pragma unroll
+            for (int u = 0; u < MGU; ++u) {
+                const int64_t p = p0 + (int64_t)u * FT;
+                if (p >= dy) continue;
+                xv[u] = x[p] + alpha * pv[p];
+                rv[u] = r[p] - alpha * qv[p];
+                r2 += rv[u] * rv[u];
+            }
+#pragma unroll
+            for (int u = 0; u < MGU; ++u) {
+                const int64_t p = p0 + (int64_t)u * FT;
+                if (p < dy) {
+                    x[p] = xv[u];
+                    r[p] = rv[u];
+                }
+            }
         }
         r2 = block_sum_d(r2, red);
         ++it;
@@ -610,11 +701,33 @@ __global__ __launch_bounds__(FT) void fom_mgcg_kernel(gpi_fom_desc d, FomGeom G,
         if (conv) break;
         vcycle();
         double rz2 = 0.0;
-        for (int64_t p = tid; p < dy; p += FT) rz2 += r[p] * z[p];
+        for (int64_t p0 = tid; p0 < dy; p0 += MGU * FT) {
+            double a[MGU], c[MGU];
+#pragma unroll
+            for (int u = 0; u < MGU; ++u) {
+                const int64_t p = p0 + (int64_t)u * FT;
+                a[u] = p < dy ? r[p] : 0.0;
+                c[u] = p < dy ? z[p] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < MGU; ++u) rz2 += a[u] * c[u];
+        }
         rz2 = block_sum_d(rz2, red);
         const double beta = rz2 / rz;
         rz = rz2;
-        for (int64_t p = tid; p < dy; p += FT) pv[p] = z[p] + beta * pv[p];
+        for (int64_t p0 = tid; p0 < dy; p0 += MGU * FT) {
+            double nv[MGU];
+#pragma unroll
+            for (int u = 0; u < MGU; ++u) {
+                const int64_t p = p0 + (int64_t)u * FT;
+                if (p < dy) nv[u] = z[p] + beta * pv[p];
+            }
+#pragma unroll
+            for (int u = 0; u < MGU; ++u) {
+                const int64_t p = p0 + (int64_t)u * FT;
+                if (p < dy) pv[p] = nv[u];
+            }
+        }
         __syncthreads();
     }
     if (tid == 0) {
@@ -722,10 +835,11 @@ extern "C" int gpi_fom_solve(const gpi_fom_desc* d, void* stream) {
                                 150 * 1024) != hipSuccess)
             return GPI_ERR_LAUNCH;
     }
-    // multigrid-preconditioned CG for power-of-two grids of >= GPI_FOM_MG_MIN (default 32) squares per side (0: off;
-    // r05u: 64^2 163 k vs 112 k labels/s, 128^2 50 k vs 2.9 k, 256^2 6.3 k vs 196 -- 15 iterations instead of 400-1600)
+    // multigrid-preconditioned CG for power-of-two grids of >= GPI_FOM_MG_MIN (default 64) squares per side (0: off;
+    // r05w: 64^2 164 k vs 112 k labels/s, 128^2 55 k vs 2.9 k, 256^2 7.5 k vs 196 -- 15 iterations instead of 400-1600;
+    // at 32^2 the register-resident Jacobi form is as fast: 330 k vs 325 k)
     // (read per call: a data-generation call, not a per-step one)
-    const int mg_min = [] { const char* v = getenv("GPI_FOM_MG_MIN"); return v && *v ? atoi(v) : 32; }();
+    const int mg_min = [] { const char* v = getenv("GPI_FOM_MG_MIN"); return v && *v ? atoi(v) : 64; }();
     const int nf = d->n_fine;
     if (mg_min > 0 && nf >= mg_min && (nf & (nf - 1)) == 0 && nf >= 2 * MG_COARSE) {
         int nlev = 0;

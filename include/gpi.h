@@ -621,7 +621,7 @@ int gpi_random_subset_ws(int32_t* out, int32_t n, int32_t k, uint64_t seed, cons
 /* ---- FOM data generation (setup side; reference utils/data.py:72-103 DataLoader.assemble ->
  * physics/LinearElliptic.py:85-101 solve, one PETSc LU per sample).  Batched conjugate gradients on the
  * matrix-free 5-point stencil of the NDP problem, one workgroup per sample, fp64 throughout: preconditioned
- * by one geometric-multigrid V(1,1) cycle on power-of-two grids from GPI_FOM_MG_MIN (env, default 32; 0 off),
+ * by one geometric-multigrid V(1,1) cycle on power-of-two grids from GPI_FOM_MG_MIN (env, default 64; 0 off),
  * by Jacobi in the Chronopoulos-Gear form (one fused reduction per iteration) otherwise.  Stops at the same
  * recurrence-residual criterion either way. */
 #define GPI_FOM_WARM 1   /* y holds the initial guess (default: linear interpolation of the BCs in x) */

@@ -42,7 +42,7 @@ def test_fom_labels_match_oracle(device, n, N):
 
 @pytest.mark.parametrize('n,N', [(8, 4), (32, 6), (64, 3)])
 def test_fom_multigrid_labels_match_oracle(device, monkeypatch, n, N):
-    """The multigrid-preconditioned CG (fom_mgcg_kernel, the default from 32^2) forced onto every
+    """The multigrid-preconditioned CG (fom_mgcg_kernel, the default from 64^2) forced onto every
     power-of-two grid from 8^2 (GPI_FOM_MG_MIN=8): labels vs the oracle's dense FE solve at 1e-9, in a few
     tens of iterations where the Jacobi form needs hundreds (407 on average at 64^2)."""
     monkeypatch.setenv('GPI_FOM_MG_MIN', '8')
@@ -64,7 +64,7 @@ def test_fom_multigrid_labels_match_oracle(device, monkeypatch, n, N):
 def test_fom_large_grid_residual(device, n, N):
     xd, U = fields(n, N, n, l=0.04)
     y, iters, flag = solve(xd, U, n)
-    assert flag == 0 and iters.max() <= 40, iters      # multigrid-preconditioned from 32^2
+    assert flag == 0 and iters.max() <= 40, iters      # multigrid-preconditioned from 64^2
     mesh = fem.unit_square_mesh(n)
     for k in range(N):
         kap = np.exp(xd[k])

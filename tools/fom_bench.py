@@ -61,7 +61,7 @@ def run(n, cpu_sample):
     res.check()
     iters = res.iters.cpu().numpy()
     dy = (n + 1) * (n - 1)
-    mg_min = int(os.environ.get('GPI_FOM_MG_MIN', '32'))
+    mg_min = int(os.environ.get('GPI_FOM_MG_MIN', '64'))
     mg = mg_min > 0 and n >= mg_min and n & (n - 1) == 0 and n >= 8
     # algorithmic bytes per fine node and iteration.  Jacobi-PCG: update pass reads u w p s x r dinv,
     # writes p s x r u; stencil pass reads u r + 2 conductances, writes w -> 17 doubles.  Multigrid-PCG
