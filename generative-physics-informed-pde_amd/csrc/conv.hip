@@ -1131,6 +1131,16 @@ struct IntC {
 #ifndef GPI_IG_PRE
 #define GPI_IG_PRE 0
 #endif
+// GPI_S2_IG_SERIAL: the stride-2 input gradient's reduction one MFMA step at a time (table read -> gathered
+// gradient read -> MFMA, the form before r05; A/B only).  Default: four steps' operands in flight per MFMA group
+// GPI_IG_PAIR: the stride-1 / upsampling MFMA input gradient by pixel-block pairs (m, m + 4) sharing the
+// offset-table and weight reads (A/B)
+#ifndef GPI_IG_PAIR
+#define GPI_IG_PAIR 0
+#endif
+#ifndef GPI_S2_IG_SERIAL
+#define GPI_S2_IG_SERIAL 0
+#endif
 // GPI_VDG3: the input gradient of the 3x3 / stride-1 backwards on the VALU (v_pk_fma_f32 over input-channel
 // pairs, the weights by broadcast LDS reads, as the fused output conv's) instead of the MFMA gather form
 // (16 x 16 x 4 blocks, N = cin padded to 16, two dependent LDS reads per step).  Measured r05 (phase probe,
@@ -1480,8 +1490,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
                 oa = co * gplane + ((ry + d.pad - ky) >> 1) * Gt.PG + ((rx + d.pad - kx) >> 1);
                 ob = co * KK + ky * K + kx;
             }
-            ktab[cls * 2 * KD4 + k] = oa;
-            ktab[cls * 2 * KD4 + KD4 + k] = ob;
+            // (interleaved (A, 16 B) pairs: one ds_read_b64 per reduction step)
+            ktab[cls * 2 * KD4 + 2 * k] = oa;
+            ktab[cls * 2 * KD4 + 2 * k + 1] = 16 * ob;
         }
     }
     if (has_gin && dg_role && S != 2 && !vop && !v3) {
@@ -1948,6 +1959,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
         }
         const float* arow0 = alb + (ci_l * Gt.rh + (py0 - iy0)) * Gt.P + HALO;   // owned row 0 of channel l16
         const int nkd = KD4 >> 2;
+#if GPI_IG_PAIR
+        bool paired = false;
+        f32x4 acc_next = {0.f, 0.f, 0.f, 0.f};
+#endif
         for (int round = 0; wv + 16 * round < nmblk; ++round) {
             if (round > 0 && S != 2) {
 #if GPI_IG_PRE
@@ -1972,22 +1987,95 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
                         const int nbc = nmblk >> 2, cls = m / nbc, mb = m - cls * nbc;
                         const int ry = cls >> 1, rx = cls & 1;
                         const int nky = (K - ((ry + d.pad) & 1) + 1) >> 1, nkx = (K - ((rx + d.pad) & 1) + 1) >> 1;
-                        const int nk = d.cout * nky * nkx;
+                        // (wave-uniform: m is; readfirstlane keeps the reduction loop's control scalar)
+                        const int nk = __builtin_amdgcn_readfirstlane(d.cout * nky * nkx);
                         const int cp = 16 * mb + l16, a2 = dq(cp, Gt.d_w2), b2 = cp - a2 * (d.w_in >> 1);
                         const float* ab = gl + ((py0 >> 1) - gy0 + a2) * Gt.PG + b2 + HALO;
-                        const int* tA = ktab + cls * 2 * KD4;
-                        const int* tB = tA + KD4;
-                        for (int ks = 0; 4 * ks < nk; ++ks) {
+                        const int2* tAB = reinterpret_cast<const int2*>(ktab + cls * 2 * KD4);
+                        const int nks = (nk + 3) >> 2;            // (4 nks <= KD4: every table read in range)
+#if GPI_S2_IG_SERIAL
+                        for (int ks = 0; ks < nks; ++ks) {
                             const int k = 4 * ks + kq;
-                            const float a = k < nk ? ab[tA[k]] : 0.f;
-                            acc = mfma4(a, wD[tB[k] * 16 + l16], acc);
+                            const int2 t = tAB[k];
+                            const float a = k < nk ? ab[t.x] : 0.f;
+                            acc = mfma4(a, wD[t.y + l16], acc);
                         }
+#else
+                        // operands of four steps in flight before their MFMAs (the serial form was a chain of two
+                        // dependent LDS round trips per MFMA); the padded entries k >= nk hold (0, 0): their
+                        // loads stay in range, the select zeroes their A value -- the sums, and their order, are
+                        // the serial form's
+                        int ks = 0;
+                        for (; ks + 4 <= nks; ks += 4) {
+                            int2 t[4];
+                            float a[4], b[4];
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) t[u] = tAB[4 * (ks + u) + kq];
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) {
+                                a[u] = ab[t[u].x];
+                                b[u] = wD[t[u].y + l16];
+                            }
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) acc = mfma4(4 * (ks + u) + kq < nk ? a[u] : 0.f, b[u], acc);
+                        }
+                        for (; ks < nks; ++ks) {
+                            const int k = 4 * ks + kq;
+                            const int2 t = tAB[k];
+                            const float a = ab[t.x], b = wD[t.y + l16];
+                            acc = mfma4(k < nk ? a : 0.f, b, acc);
+                        }
+#endif
                     } else {
                         const float* gp0 = gl + (UP ? 2 * (qy * Gt.PG + px) : qy * Gt.PG + px);
                         auto aval = [&](int k) -> float {
                             const float* ga = gp0 + ktab[k];
                             return UP ? (ga[0] + ga[1]) + (ga[Gt.PG] + ga[Gt.PG + 1]) : ga[0];
                         };
+#if GPI_IG_PAIR
+                        // block pairs (m, m + 4): one offset-table and weight read per step serve both blocks'
+                        // gathers and MFMAs (two independent accumulator chains); each block's sum and its
+                        // order are the single-block form's
+                        if ((u & 1) && paired) {
+                            acc = acc_next;
+                        } else if (!(u & 1) && m + 4 < nmblk) {
+                            const int i1 = i + 64;
+                            const int qy1 = dq(i1, Gt.d_win), px1 = i1 - qy1 * d.w_in;
+                            const float* gp1 = gl + (UP ? 2 * (qy1 * Gt.PG + px1) : qy1 * Gt.PG + px1);
+                            auto at = [&](const float* ga) -> float {
+                                return UP ? (ga[0] + ga[1]) + (ga[Gt.PG] + ga[Gt.PG + 1]) : ga[0];
+                            };
+                            f32x4 acc1 = {0.f, 0.f, 0.f, 0.f};
+                            int ks = 0;
+                            for (; ks + 4 <= nkd; ks += 4) {
+                                int o[4];
+                                float a0[4], a1[4], b[4];
+#pragma unroll
+                                for (int v = 0; v < 4; ++v) o[v] = ktab[4 * (ks + v) + kq];
+#pragma unroll
+                                for (int v = 0; v < 4; ++v) {
+                                    a0[v] = at(gp0 + o[v]);
+                                    a1[v] = at(gp1 + o[v]);
+                                    b[v] = wD[(4 * (ks + v) + kq) * 16 + l16];
+                                }
+#pragma unroll
+                                for (int v = 0; v < 4; ++v) {
+                                    acc = mfma4(a0[v], b[v], acc);
+                                    acc1 = mfma4(a1[v], b[v], acc1);
+                                }
+                            }
+                            for (; ks < nkd; ++ks) {
+                                const int k = 4 * ks + kq;
+                                const int o = ktab[k];
+                                const float b = wD[k * 16 + l16];
+                                acc = mfma4(at(gp0 + o), b, acc);
+                                acc1 = mfma4(at(gp1 + o), b, acc1);
+                            }
+                            acc_next = acc1;
+                            paired = true;
+                        } else {
+                        paired = false;
+#endif
                         int ks = 0;
                         for (; ks + 4 <= nkd; ks += 4) {   // operands of four steps before their MFMAs
                             float a[4], b[4];
@@ -2004,6 +2092,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
                             const int k = 4 * ks + kq;
                             acc = mfma4(aval(k), wD[k * 16 + l16], acc);
                         }
+#if GPI_IG_PAIR
+                        }
+#endif
                     }
                     if (cok && S == 2) {
                         const int nbc = nmblk >> 2, cls = m / nbc, mb = m - cls * nbc;
