@@ -33,6 +33,8 @@ def main():
             if pat not in op.name:
                 continue
             fn = lib.gpi_conv_forward if which == 'fwd' else lib.gpi_conv_backward
+            if prog is e.dp and i == e.n_dec_sep and e.n_dec_sep < len(e.dec_descs) and which != 'fwd':
+                fn = lib.gpi_conv_loss_fused          # the decoder output conv runs fused in the step
             t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             t0.record()
             for _ in range(reps):
