@@ -1191,7 +1191,7 @@ __host__ __device__ constexpr bool fuse_wlds(int ky) {
     return GPI_FUSE_WLDS <= 0 ? false : (GPI_FUSE_WLDS >= 5 ? true : (ky & 1 ? (ky / 2) < GPI_FUSE_WLDS : (ky / 2) < GPI_FUSE_WLDS - 2));
 }
 
-template <int K, int S, int UP, bool FUSE = false, bool HALF = false, bool V3 = false>
+template <int K, int S, int UP, bool FUSE = false, bool HALF = false, bool V3 = false, bool EXF = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (FUSE ? GPI_FUSE_WAVES : 4) : (V3 ? GPI_BWD3_WAVES : GPI_BWD_WAVES)))) void conv_bwd_kernel(gpi_conv_desc d, gpi_codec_ctx c, ConvGeom G) {
     touch_kernargs<CONV_KARG_BYTES>();
     entry_signal(G);
@@ -1595,7 +1595,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (F
         // waits used to drain the LDS reads as well (r03: 22.5 k cycles per workgroup for this phase)
         constexpr int PADK = K / 2;
         float Lv = 0.f;
-        const bool ex = d.epilogue == GPI_EPI_GAUSS_EXP_LOSS;
+        // the exp-field loss is an instantiation of its own (EXF; launch() picks it from d.epilogue): as a
+        // runtime flag its two extra exps per pixel ran as selects in the log-field form as well
+        constexpr bool ex = EXF;
         const float scl = karg_sel(c.loss_scale, T.grp);
         // RPF vertically adjacent pixels of one column per thread: items (column, row group) fill the
         // 256 lanes exactly on 64-wide planes (20 rows = 4 groups x 64 columns with 16-row tiles).  Per
@@ -2632,7 +2634,9 @@ int launch(const gpi_conv_desc& d, const gpi_codec_ctx& c, hipStream_t st, bool 
     if (!fwd && d.gin_off >= 0 && ((G.ph * d.w_in) & 15)) return GPI_ERR_UNSUPPORTED;
     if (!fwd && d.gin_off >= 0 && d.stride == 2 && ((d.w_in & 7) || (G.ph & 1))) return GPI_ERR_UNSUPPORTED;
     const int cp = cp_of(d);
-    conv_kernel_t k = fuse ? (G.nfull < G.nblocks ? conv_bwd_kernel<5, 1, 0, true, true> : conv_bwd_kernel<5, 1, 0, true>)
+    const bool exf = d.epilogue == GPI_EPI_GAUSS_EXP_LOSS;
+    conv_kernel_t k = fuse ? (G.nfull < G.nblocks ? (exf ? conv_bwd_kernel<5, 1, 0, true, true, false, true> : conv_bwd_kernel<5, 1, 0, true, true>)
+                                                  : (exf ? conv_bwd_kernel<5, 1, 0, true, false, false, true> : conv_bwd_kernel<5, 1, 0, true>))
                            : select_kernel(d, cp, fwd, G.cg > 1 ? 0 : G.npx, G.nfull < G.nblocks,
                                            G.ucls != 0 || (!fwd && v3_op(d, G)));
     if (!k) return GPI_ERR_UNSUPPORTED;
