@@ -407,6 +407,11 @@ __device__ __forceinline__ void stage(float* dst, int total, const float* zero, 
 // Chunk (16 B) e of a row image of planes of nr rows x P4 chunks decomposed as
 // (plane q, row r, chunk c4), advanced by 256 chunks per step with constant carries
 // (sq, sr, sc) = decomposition of 256, so a loop pays no division per chunk.
+// GPI_STAGE_SEL: the row-image staging loops take each chunk's source by a select of the computed plane address
+// and the zero page (0: the compiler's branchy form, A/B)
+#ifndef GPI_STAGE_SEL
+#define GPI_STAGE_SEL 1
+#endif
 struct ChunkIter {
     int q, r, c4;
     __device__ __forceinline__ void init(int e, int plane4, int P4, Div d_q4, Div d_p4) {
@@ -444,7 +449,16 @@ __device__ __forceinline__ void stage_img(float* dst, int nq, int nr, int P, Div
         if (e0 + wb < total) {
             const int row = r0 + it.r;
             const bool ok = it.q < nq && row >= 0 && row < h && it.c4 >= c4lo && it.c4 < c4hi;
+#if GPI_STAGE_SEL
+            // the chunk's plane address computed for every lane (never dereferenced where !ok), then ONE select:
+            // without the empty asm the compiler sank the address arithmetic under three exec-masked branches
+            // (the bounds tests), ≈ 10 SALU + branch issue per chunk in the staging loops of every conv launch
+            const float* pv = plane(it.q) + row * w + 4 * (it.c4 - c4lo);
+            asm volatile("" : "+v"(pv));
+            const float* p = ok ? pv : zero;
+#else
             const float* p = ok ? plane(it.q) + row * w + 4 * (it.c4 - c4lo) : zero;
+#endif
             glds16(p, dst + 4 * (e0 + wb));
         }
         it.step(sq, sr, sc, P4, nr);
