@@ -631,11 +631,14 @@ __global__ __launch_bounds__(512) void cgr_band_kernel(gpi_residual_desc d) {
                 const float kdg = __builtin_amdgcn_exp2f(
                     __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(rk, vk[m] + 4 * (n - 1 - jd) * n, 0, 0)) *
                     1.4426950408889634f);
-                const int o0 = 4 * jd * (n - 1), o1 = o0 + 4 * (n - 1);
-                const float u0 = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(ry, vy[m] + o0, 0, 0));
-                const float u1 = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(ry, vy1 + o0, 0, 0));
-                const float u2 = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(ry, vy[m] + o1, 0, 0));
-                const float u3 = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(ry, vy1 + o1, 0, 0));
+                // (per-lane rows: the row offset joins the VGPR offset, added as uint32 so that the sentinel of a
+                // non-free column wraps to an out-of-range offset -- the load returns 0 -- without signed overflow)
+                const uint32_t o0 = 4u * (uint32_t)jd * (uint32_t)(n - 1), o1 = o0 + 4u * (uint32_t)(n - 1);
+                const uint32_t va = (uint32_t)vy[m], vb = (uint32_t)vy1;
+                const float u0 = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(ry, (int)(va + o0), 0, 0));
+                const float u1 = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(ry, (int)(vb + o0), 0, 0));
+                const float u2 = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(ry, (int)(va + o1), 0, 0));
+                const float u3 = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(ry, (int)(vb + o1), 0, 0));
                 flr[m] = fmaf(kdg, u0 - 2.f * u1 + u3, flr[m]);
                 ful[m] = fmaf(kdg, u0 - 2.f * u2 + u3, ful[m]);
                 }
@@ -691,71 +694,74 @@ extern "C" int gpi_cgr_residual(const gpi_residual_desc* d, void* stream) {
     const size_t lds = sizeof(double) * (nn + 2 * d->nc * d->nc);
     if (lds > 160 * 1024) return GPI_ERR_UNSUPPORTED;
     const int r = d->n_fine / d->nc;
-    {
-        // barrier-free band form (cgr_band_kernel) for its (r, columns) instantiations; GPI_CGR_FORM=1 the
-        // streaming form, 0 the original band kernel (A/B)
-        static const int form = [] { const char* v = getenv("GPI_CGR_FORM"); return v && *v ? atoi(v) : 2; }();
+    // form: d->form (GPI_CGR_*); GPI_CGR_AUTO takes the first that applies of the barrier-free band form
+    // (cgr_band_kernel, its (r, columns) instantiations), the streaming form (cgr_stream_kernel, aligned fields,
+    // n <= 256) and the general band kernel (cgr_kernel<M>, any grid).  GPI_CGR_FORM (A/B runs) changes AUTO's
+    // first choice: 2 band (default), 1 streaming, 0 general.
+    if (d->form < GPI_CGR_AUTO || d->form > GPI_CGR_GENERAL) return GPI_ERR_ARG;
+    static const int env_form = [] { const char* v = getenv("GPI_CGR_FORM"); return v && *v ? atoi(v) : 2; }();
+    const bool auto_ = d->form == GPI_CGR_AUTO;
+    if (d->form == GPI_CGR_BAND || (auto_ && env_form >= 2)) {
         const int n = d->n_fine, MM = (n + 63) / 64;
-        if (form == 2 && d->nc <= 8) {
+        bool done = false;
+        if (d->nc <= 8) {
             const dim3 grid(d->n), block(64 * d->nc);
             const hipStream_t st = (hipStream_t)stream;
             const bool fl = d->r_flux != nullptr;
-            bool done = true;
-#define GPI_CGR_BAND(RR, M)                                                                             \
+            done = true;
+#define GPI_CGR_BAND_LAUNCH(RR, M)                                                                             \
     if (fl) hipLaunchKernelGGL((cgr_band_kernel<RR, M, true>), grid, block, lds, st, *d);              \
     else hipLaunchKernelGGL((cgr_band_kernel<RR, M, false>), grid, block, lds, st, *d);
-            if (r == 4 && MM == 1) { GPI_CGR_BAND(4, 1) }
-            else if (r == 8 && MM == 1) { GPI_CGR_BAND(8, 1) }
-            else if (r == 16 && MM == 1) { GPI_CGR_BAND(16, 1) }
-            else if (r == 16 && MM == 2) { GPI_CGR_BAND(16, 2) }
-            else if (r == 32 && MM == 4) { GPI_CGR_BAND(32, 4) }
+            if (r == 4 && MM == 1) { GPI_CGR_BAND_LAUNCH(4, 1) }
+            else if (r == 8 && MM == 1) { GPI_CGR_BAND_LAUNCH(8, 1) }
+            else if (r == 16 && MM == 1) { GPI_CGR_BAND_LAUNCH(16, 1) }
+            else if (r == 16 && MM == 2) { GPI_CGR_BAND_LAUNCH(16, 2) }
+            else if (r == 32 && MM == 4) { GPI_CGR_BAND_LAUNCH(32, 4) }
             else done = false;
-#undef GPI_CGR_BAND
-            if (done) {
-                GPI_CHECK_LAUNCH();
-                return GPI_OK;
-            }
+#undef GPI_CGR_BAND_LAUNCH
         }
+        if (done) {
+            GPI_CHECK_LAUNCH();
+            return GPI_OK;
+        }
+        if (d->form == GPI_CGR_BAND) return GPI_ERR_UNSUPPORTED;
     }
-    {
-        // streaming form (cgr_stream_kernel) where its layout holds; GPI_CGR_STREAM=0 keeps the band kernel (A/B)
-        static const int stream_on = [] { const char* v = getenv("GPI_CGR_STREAM"); return v && *v ? atoi(v) : 1; }();
+    if (d->form == GPI_CGR_STREAM || (auto_ && env_form >= 1)) {
         const int n = d->n_fine;
-        const bool ok = stream_on && n % CGRS_CR == 0 && n >= CGRS_CR && n <= 256 && r >= 4 && (r & (r - 1)) == 0 &&
+        const bool ok = n % CGRS_CR == 0 && n >= CGRS_CR && n <= 256 && r >= 4 && (r & (r - 1)) == 0 &&
                         ((uintptr_t)d->logkappa & 15) == 0 && ((uintptr_t)d->y & 15) == 0;
-        if (ok) {
-            int lr = 0;
-            while ((1 << lr) < r) ++lr;
-            const int nd = (nn + 2 * d->nc * d->nc + 1) & ~1;
-            const size_t lds2 = sizeof(double) * nd + sizeof(float) * (6 * CGRS_CR + 1) * cgrs_pitch(n);
-            if (lds2 <= 160 * 1024) {
-                const dim3 grid(d->n), block(4 * n);
-                const hipStream_t st = (hipStream_t)stream;
-                const bool fl = d->r_flux != nullptr;
-                auto go = [&](auto ns_c) -> int {
-                    constexpr int NS = decltype(ns_c)::value;
-                    const void* k = fl ? (const void*)cgr_stream_kernel<GPI_CGR_DEPTH, true, NS>
-                                       : (const void*)cgr_stream_kernel<GPI_CGR_DEPTH, false, NS>;
-                    if (lds2 > 64 * 1024 &&
-                        hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2) != hipSuccess)
-                        return GPI_ERR_LAUNCH;
-                    if (fl) hipLaunchKernelGGL((cgr_stream_kernel<GPI_CGR_DEPTH, true, NS>), grid, block, lds2, st, *d, lr);
-                    else hipLaunchKernelGGL((cgr_stream_kernel<GPI_CGR_DEPTH, false, NS>), grid, block, lds2, st, *d, lr);
-                    return GPI_OK;
-                };
-                int rc;
-                switch (n) {
-                    case 32: rc = go(std::integral_constant<int, 3>{}); break;
-                    case 64: rc = go(std::integral_constant<int, 5>{}); break;
-                    case 128: rc = go(std::integral_constant<int, 9>{}); break;
-                    case 256: rc = go(std::integral_constant<int, 17>{}); break;
-                    default: rc = go(std::integral_constant<int, 0>{}); break;
-                }
-                if (rc != GPI_OK) return rc;
-                GPI_CHECK_LAUNCH();
+        int lr = 0;
+        while ((1 << lr) < r) ++lr;
+        const int nd = (nn + 2 * d->nc * d->nc + 1) & ~1;
+        const size_t lds2 = sizeof(double) * nd + sizeof(float) * (6 * CGRS_CR + 1) * cgrs_pitch(n);
+        if (ok && lds2 <= 160 * 1024) {
+            const dim3 grid(d->n), block(4 * n);
+            const hipStream_t st = (hipStream_t)stream;
+            const bool fl = d->r_flux != nullptr;
+            auto go = [&](auto ns_c) -> int {
+                constexpr int NS = decltype(ns_c)::value;
+                const void* k = fl ? (const void*)cgr_stream_kernel<GPI_CGR_DEPTH, true, NS>
+                                   : (const void*)cgr_stream_kernel<GPI_CGR_DEPTH, false, NS>;
+                if (lds2 > 64 * 1024 &&
+                    hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2) != hipSuccess)
+                    return GPI_ERR_LAUNCH;
+                if (fl) hipLaunchKernelGGL((cgr_stream_kernel<GPI_CGR_DEPTH, true, NS>), grid, block, lds2, st, *d, lr);
+                else hipLaunchKernelGGL((cgr_stream_kernel<GPI_CGR_DEPTH, false, NS>), grid, block, lds2, st, *d, lr);
                 return GPI_OK;
+            };
+            int rc;
+            switch (n) {
+                case 32: rc = go(std::integral_constant<int, 3>{}); break;
+                case 64: rc = go(std::integral_constant<int, 5>{}); break;
+                case 128: rc = go(std::integral_constant<int, 9>{}); break;
+                case 256: rc = go(std::integral_constant<int, 17>{}); break;
+                default: rc = go(std::integral_constant<int, 0>{}); break;
             }
+            if (rc != GPI_OK) return rc;
+            GPI_CHECK_LAUNCH();
+            return GPI_OK;
         }
+        if (d->form == GPI_CGR_STREAM) return GPI_ERR_UNSUPPORTED;
     }
     const int G = (r & (r - 1)) == 0 ? (r < 64 ? r : 64) : 1;   // lanes per coarse square (see cgr_kernel)
     const int waves = d->nc < CGR_MAXW ? d->nc : CGR_MAXW;

@@ -29,7 +29,7 @@ FINALIZE_ZERO = 2
 
 EPI_STORE, EPI_STORE_STATS, EPI_GAUSS_LOSS, EPI_GAUSS_EXP_LOSS = 0, 1, 2, 3
 HEAD_ENC, HEAD_REPARAM, HEAD_QZ, HEAD_LATENT, HEAD_GP, HEAD_LOCKX = 0x01, 0x02, 0x04, 0x08, 0x10, 0x20
-HEAD_PART_ENC, HEAD_PART_Q = 0x100, 0x200
+HEAD_PART_ENC, HEAD_PART_Q, HEAD_VALU = 0x100, 0x200, 0x400
 ROM_FORWARD, ROM_LOGLIK, ROM_BACKWARD = 0, 1, 2
 VO_CGR, VO_FLUX = 0x1, 0x2
 FOM_WARM = 1
@@ -105,8 +105,11 @@ class RomDesc(C.Structure):
                 ('gacc_logsig', vp), ('loss_acc', vp), ('flag', vp), ('uc', vp), ('gls_part', vp)]
 
 
+CGR_AUTO, CGR_BAND, CGR_STREAM, CGR_GENERAL = 0, 1, 2, 3
+
+
 class ResidualDesc(C.Structure):
-    _fields_ = [('n_fine', i32), ('nc', i32), ('n', i32), ('_pad', i32),
+    _fields_ = [('n_fine', i32), ('nc', i32), ('n', i32), ('form', i32),
                 ('logkappa', vp), ('y', vp), ('bc', vp), ('r', vp), ('r_flux', vp)]
 
 
@@ -276,6 +279,18 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise NativeError('libgpi_hip.so not built (%s); run __graft_entry__.build() / make -C csrc' % LIB_PATH)
         L = C.CDLL(LIB_PATH)
+        stale_ok = os.environ.get('GPI_ALLOW_STALE_LIB') == '1'
+        # the source check first: a library built before an entry point existed (gpi_source_sha included)
+        # is a stale build, reported as one, not as an undefined symbol
+        if hasattr(L, 'gpi_source_sha'):
+            L.gpi_source_sha.restype, L.gpi_source_sha.argtypes = SIGNATURES['gpi_source_sha']
+            check_source_sha(L)
+        elif not stale_ok:
+            raise NativeError('stale native library %s: built before gpi_source_sha existed; rebuild (make -C csrc) '
+                              'or set GPI_ALLOW_STALE_LIB=1' % LIB_PATH)
+        missing = [name for name in SIGNATURES if not hasattr(L, name)]
+        if missing:
+            raise NativeError('stale native library %s: no %s; rebuild (make -C csrc)' % (LIB_PATH, ', '.join(missing)))
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(L, name)
             fn.restype = res
@@ -287,7 +302,6 @@ def lib():
         for s, cls in zip(sizes[:k], STRUCTS):
             if s != C.sizeof(cls):
                 raise NativeError('ABI mismatch for %s: C %d bytes, ctypes %d' % (cls.__name__, s, C.sizeof(cls)))
-        check_source_sha(L)
         if L.gpi_replicas() != GPI_REPLICAS:
             raise NativeError('ABI mismatch: the library keeps %d statistic replicas, the binding %d (GPI_REPLICAS)'
                               % (L.gpi_replicas(), GPI_REPLICAS))

@@ -10,6 +10,12 @@ The Parameter objects themselves are unchanged, so optimizers built on
 """
 import torch
 
+# Every matrix parameter (nn.Linear weights, per-sample variational rows) starts on a 16-byte boundary
+# of the flat buffers, so the dense-layer kernels (head.hip) read weight rows as aligned float4; vectors
+# and conv kernels stay packed (a BN layer's gamma and beta adjacent: one slab-reduction item).  The
+# padding floats are zero in P, G and gacc and stay zero under Adam (zero gradient, zero moments).
+ALIGN = 4
+
 
 class FlatParameters(object):
 
@@ -24,11 +30,13 @@ class FlatParameters(object):
         self.name_offsets = {}
         total = 0
         for n, p in named:
+            if p.dim() == 2:
+                total = (total + ALIGN - 1) // ALIGN * ALIGN
             self.offsets[id(p)] = total
             self.name_offsets[n] = total
             total += p.numel()
         self.numel = total
-        self.P = torch.empty(total, dtype=torch.float32, device=device)
+        self.P = torch.zeros(total, dtype=torch.float32, device=device)
         self.G = torch.zeros(total, dtype=torch.float32, device=device)
         self.gacc = torch.zeros(total, dtype=torch.float64, device=device)
         for n, p in named:

@@ -112,10 +112,11 @@ class PredictionEnsembleEngine(object):
                 [('q.' + n, p) for n, p in q_z.named_parameters()]
         dev = X.device
         self.flat = FlatParameters(named, dev)
-        self.n_dec = sum(p.numel() for p in self._src)
         self.q_off = min(self.flat.offset(q_z._mean), self.flat.offset(q_z._logsigma))
+        self.n_dec = self.q_off                       # the shadow decoder's span (parameters + alignment padding)
         self.q_n = self.flat.numel - self.q_off
-        assert self.q_off == self.n_dec and self.q_n == 2 * q_z._mean.numel()
+        assert self.q_n == max(self.flat.offset(q_z._mean), self.flat.offset(q_z._logsigma)) - self.q_off + \
+            q_z._mean.numel()
         em = _EngineModel(self.shadow, model.gp, model.g, q_z, self.flat, getattr(model, 'config', {}))
         # the PE's decoder calls are the model's decoder's in the reference (components.py:371): its BN
         # running statistics are model.f's
@@ -154,19 +155,14 @@ class PredictionEnsembleEngine(object):
         src_flat = getattr(self.model.f, '_gpi_flat', None)
         if src_flat is not None and all(src_flat.owns(p) for p in self._src):
             o = src_flat.offset(self._src[0])
-            if all(src_flat.offset(p) == o + k for p, k in zip(self._src, self._cum())):
+            # one copy when the decoder's parameters sit in the model's flat buffer with the same relative
+            # offsets (alignment padding included) as in the shadow's
+            if all(src_flat.offset(p) - o == self.flat.offset(d) for p, d in zip(self._src, self.shadow.parameters())):
                 self.flat.P[:self.n_dec].copy_(src_flat.P[o:o + self.n_dec])
                 return
         with torch.no_grad():
             for d, s in zip(self.shadow.parameters(), self._src):
                 d.copy_(s)
-
-    def _cum(self):
-        out, c = [], 0
-        for p in self._src:
-            out.append(c)
-            c += p.numel()
-        return out
 
     def _sync_lr(self):
         self._set_lr(float(self._lr_source()))

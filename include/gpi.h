@@ -157,6 +157,9 @@ typedef struct gpi_reduce_item {
  * two halves can run on different streams (the variational half needs the ROM adjoint) */
 #define GPI_HEAD_PART_ENC 0x100
 #define GPI_HEAD_PART_Q   0x200
+/* the per-sample VALU form of the dense layers instead of the batched MFMA form (A/B and parity tests;
+ * the MFMA form is the default wherever its width / alignment preconditions hold) */
+#define GPI_HEAD_VALU     0x400
 
 typedef struct gpi_head_desc {
     int32_t flags;
@@ -193,7 +196,8 @@ typedef struct gpi_head_desc {
  *   gacc[bias_off + m]    += sum_s A[s*lda + m]       (bias_off >= 0)   */
 typedef struct gpi_gemm_item {
     int64_t a_off, b_off, c_off, bias_off;
-    int32_t S, M, N, lda, ldb, flags;   /* flags bit 0: ReLU applied to B */
+    int32_t S, M, N, lda, ldb, flags;   /* flags bit 0: ReLU applied to B; bit 1 (item 0): the scalar
+                                         * VALU tile form instead of MFMA (A/B and parity tests) */
 } gpi_gemm_item;
 
 /* Coarse-grained model (ROM) on the nc x nc "/" mesh: K(kappa) from the
@@ -239,8 +243,18 @@ typedef struct gpi_rom_desc {
  * kappa = exp(logkappa image) per pixel, yhat = y on free nodes and the NDP
  * Dirichlet data u0..u3 on x=0 / x=1.  Matrix-free 5-point stencil, flux rows (r_flux) in the
  * same pass; any n_fine <= 512 with n_fine % nc == 0 (GPI_ERR_UNSUPPORTED above). */
+/* kernel form of gpi_cgr_residual (gpi_residual_desc.form; every form computes the same residual):
+ * AUTO the first that applies of BAND (cgr_band_kernel: one wave per coarse row band, no barrier; nc <= 8 and
+ * r in {4, 8, 16, 32} at n_fine / 64 columns per lane in {1, 2, 4}), STREAM (cgr_stream_kernel: 16-row chunks
+ * through LDS rings; 16-byte aligned fields, n_fine a multiple of 16 up to 256, r a power of two >= 4) and
+ * GENERAL (cgr_kernel: any grid); an explicit form that does not apply returns GPI_ERR_UNSUPPORTED. */
+#define GPI_CGR_AUTO    0
+#define GPI_CGR_BAND    1
+#define GPI_CGR_STREAM  2
+#define GPI_CGR_GENERAL 3
+
 typedef struct gpi_residual_desc {
-    int32_t n_fine, nc, n, _pad;
+    int32_t n_fine, nc, n, form;
     const float* logkappa;     /* [n, n_fine, n_fine] image (row 0 = top) */
     const float* y;            /* [n, d_y] fine free values */
     const float* bc;           /* [n, 4] u0..u3 */

@@ -184,6 +184,67 @@ def test_elbo_c64_module_path(device):
     print(check_grads(errs, tol_all=5e-5, frac_tight=1.0))
 
 
+def test_head_mfma_matches_valu_form(device):
+    """The dense layers of the step (encoder FC -> ReLU -> mu / logsigma heads, reparametrisation, KL,
+    decoder latent map, gp map, q_X draw and their backward, Encoder.py:175-182, codec.py:495-504,
+    Decoder.py:213, components.py:167-256) on the matrix cores (head_fwd_mfma / head_bwd_mfma /
+    outer_gemm_mfma, the default) vs the per-sample VALU kernels (GPI_HEAD_VALU) on the same workspace
+    state at the bench shape: every output region and every gradient tensor within 1e-5 of the VALU
+    form's (max|d| / max|ref|; both are fp32, the sums differ only in order), the ELBO terms within
+    1e-6.  The fp64 oracle checks of the whole step (above and below) run through the MFMA form."""
+    import ctypes as C
+    from gpi import _lib as L
+    d = load('elbo_c64.npz')
+    model, bs = highres_model(d)
+    eps = (torch.cat([cuda(d['eps_enc']), cuda(d['eps_qz'])]), cuda(d['eps_qX']))
+    (-model.elbo(step=0, armortized_bs=bs, eps=eps)).backward()
+    e = model._elbo_engine(bs, int(d['cfg'][5]), False)
+    lib, st = L.lib(), L.stream_handle()
+    P, ws, scr, gacc = e.flat.P, e.ws.t_ws, e.ws.t_scr, e.flat.gacc
+    ws0 = ws.clone()
+
+    def run(valu):
+        ws.copy_(ws0)
+        scr.zero_()
+        gacc.zero_()
+        hd = L.HeadDesc.from_buffer_copy(e.head)
+        if valu:
+            hd.flags |= L.HEAD_VALU
+        items = (L.GemmItem * len(e.gemm_items))(*[L.GemmItem.from_buffer_copy(it) for it in e.gemm_items])
+        if valu:
+            items[0].flags |= 2
+        L.check(lib.gpi_head_forward(C.byref(hd), L.ptr(P), L.ptr(ws), st), 'head forward')
+        L.check(lib.gpi_head_backward(C.byref(hd), L.ptr(P), L.ptr(ws), L.ptr(gacc), st), 'head backward')
+        L.check(lib.gpi_outer_gemm(items, len(items), L.ptr(ws), L.ptr(gacc), st), 'outer gemm')
+        torch.cuda.synchronize()
+        return ws.clone(), e.ws.terms.clone(), gacc.clone()
+
+    wm, tm, gm = run(False)
+    wv, tv, gv = run(True)
+    B, dz = e.B, e.dz
+    h = e.head
+    regions = {k: (e.hb[k], n) for k, n in (('hpre', e.B_u * h.d_feat), ('dhpre', e.B_u * h.d_feat),
+                                            ('zmu', B * dz), ('zls', B * dz), ('z', B * dz), ('dzmu', B * dz),
+                                            ('dzls', B * dz), ('mux', e.N_s * h.d_x), ('xs', e.N_s * h.d_x),
+                                            ('gmux', e.N_s * h.d_x))}
+    regions['lat'] = (h.lat, B * h.d_lat)
+    regions['gfeat'] = (h.gfeat, e.B_u * h.d_feat)
+    for k, (o, n) in regions.items():
+        a, b = wm[o:o + n].double(), wv[o:o + n].double()
+        assert float(b.abs().max()) > 0, k
+        assert float((a - b).abs().max()) <= 1e-5 * float(b.abs().max()), k
+    assert torch.allclose(tm, tv, rtol=1e-6, atol=0), (tm, tv)
+    off = e.flat.name_offsets
+    n_checked = 0
+    for k, p in model.named_parameters():
+        a, b = gm[off[k]:off[k] + p.numel()], gv[off[k]:off[k] + p.numel()]
+        if float(b.abs().max()) == 0:
+            continue
+        n_checked += 1
+        assert float((a - b).abs().max()) <= 1e-5 * float(b.abs().max()), k
+    assert n_checked >= 12, n_checked
+
+
 @pytest.mark.parametrize('droprate', [0.0, 0.2])
 def test_fused_step_c64(device, droprate):
     """FusedElboStep -- the graph-captured step bench.py times -- at the benchmarked shape over three

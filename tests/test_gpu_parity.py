@@ -125,42 +125,62 @@ def test_cgr_residual_large_grids(device, n, N):
         assert np.abs(out[i] - ref).max() / np.abs(ref).max() < 1e-5
 
 
-@pytest.mark.parametrize('n,N', [(64, 7), (128, 3)])
-def test_cgr_residual_streaming_vs_band_kernel(device, n, N):
-    """The streaming residual kernel (16-B aligned fields: cgr_stream_kernel, chunked through LDS rings)
-    and the band kernel (taken for an unaligned y view, cgr_kernel) on the same fields, CGR and flux
-    rows: both within 1e-5 of the oracle's matrix-free fp64 residual, and of each other.  N (n^2 - 1) is
-    odd here, so y's last float4 is partial (the streaming kernel's clamped tail load)."""
+_BAND_RM = {(4, 1), (8, 1), (16, 1), (16, 2), (32, 4)}
+
+
+@pytest.mark.parametrize('n,nc,N', [(64, 8, 7), (128, 8, 3), (256, 8, 1), (64, 16, 3), (48, 3, 3), (60, 5, 3)])
+@pytest.mark.parametrize('form', ['band', 'stream', 'general'])
+def test_cgr_residual_every_kernel_form(device, n, nc, N, form):
+    """Each kernel form of gpi_cgr_residual, selected per call (gpi_residual_desc.form): the barrier-free
+    band form (cgr_band_kernel), the streaming form (cgr_stream_kernel, LDS ring chunks) and the general
+    band kernel (cgr_kernel<M>), CGR rows vs the oracle's matrix-free fp64 FE residual (W^T (K yhat)_free,
+    VirtualObservables.py:57-69,297-302 / physics/LinearElliptic.py:137-159) and flux rows vs its closed-form
+    flux rows (bottleneck/flux.py:81-158), max error <= 1e-5 of the largest entry; AUTO (the ELBO / VO path's
+    choice) equal to the form it picks.  A form whose preconditions fail returns GPI_ERR_UNSUPPORTED: band
+    needs nc <= 8 and (r, n / 64 columns per lane) instantiated, streaming a 16-multiple n <= 256, a power-of-
+    two r >= 4 and 16-byte aligned fields.  N (n^2 - 1) is odd at N = 7 / 3 / 1, so y's last float4 is partial
+    (the streaming kernel's clamped tail load)."""
     import ctypes as C
     from gpi import _lib as L
-    rng = np.random.default_rng(n + N)
-    nc = 8
+    r_ = n // nc
+    mm = (n + 63) // 64
+    applies = {'band': nc <= 8 and (r_, mm) in _BAND_RM,
+               'stream': n % 16 == 0 and 16 <= n <= 256 and r_ >= 4 and (r_ & (r_ - 1)) == 0,
+               'general': True}
+    auto = next(f for f in ('band', 'stream', 'general') if applies[f])
+    code = {'auto': L.CGR_AUTO, 'band': L.CGR_BAND, 'stream': L.CGR_STREAM, 'general': L.CGR_GENERAL}
+    rng = np.random.default_rng(1000 * n + nc)
     mc, mf = fem.unit_square_mesh(nc), fem.unit_square_mesh(n)
     W = fem.prolongation_free(mc, mf)
     imgs = rng.normal(0.4, 0.8, (N, n, n))
     U = rng.uniform(-0.5, 0.5, (N, 4))
     y = rng.normal(0, 0.3, (N, W.shape[0]))
-    lk, bc = cuda(imgs), cuda(U)
-    y_al = cuda(y)
-    buf = torch.zeros(y.size + 1, device='cuda')
-    buf[1:] = y_al.reshape(-1)
-    y_un = buf[1:].view(N, -1)                        # 4-B aligned only: the band kernel
-    assert y_al.data_ptr() % 16 == 0 and y_un.data_ptr() % 16 != 0
-    outs = []
-    for yy in (y_al, y_un):
-        r = torch.zeros(N, (nc + 1) ** 2, device='cuda')
-        rf = torch.zeros(N, 2 * nc * nc, device='cuda')
-        d = L.ResidualDesc(n_fine=n, nc=nc, n=N, logkappa=lk.data_ptr(), y=yy.data_ptr(), bc=bc.data_ptr(),
-                           r=r.data_ptr(), r_flux=rf.data_ptr())
-        L.check(L.lib().gpi_cgr_residual(C.byref(d), L.stream_handle()), 'residual')
-        outs.append((r.cpu().numpy(), rf.cpu().numpy()))
+    lk, bc, yy = cuda(imgs), cuda(U), cuda(y)
+    assert yy.data_ptr() % 16 == 0 and lk.data_ptr() % 16 == 0
+
+    def run(f):
+        rc_ = torch.zeros(N, (nc + 1) ** 2, device='cuda')
+        rf_ = torch.zeros(N, 2 * nc * nc, device='cuda')
+        d = L.ResidualDesc(n_fine=n, nc=nc, n=N, form=code[f], logkappa=lk.data_ptr(), y=yy.data_ptr(),
+                           bc=bc.data_ptr(), r=rc_.data_ptr(), r_flux=rf_.data_ptr())
+        ret = L.lib().gpi_cgr_residual(C.byref(d), L.stream_handle())
+        torch.cuda.synchronize()
+        return ret, rc_.cpu().numpy(), rf_.cpu().numpy()
+
+    ret, rc, rf = run(form)
+    if not applies[form]:
+        assert ret == -3, (form, n, nc, ret)      # GPI_ERR_UNSUPPORTED, nothing launched
+        return
+    assert ret == 0, ret
     for i in range(N):
         ref = W.T @ fem.fom_residual(mf, np.exp(fem.image_to_cells(imgs[i])), U[i], y[i])
-        for r, _ in outs:
-            assert np.abs(r[i] - ref).max() / np.abs(ref).max() < 1e-5
-    (ra, fa), (rb, fb) = outs
-    assert np.abs(ra - rb).max() / np.abs(rb).max() < 1e-5
-    assert np.abs(fa - fb).max() / np.abs(fb).max() < 1e-5
+        assert np.abs(rc[i] - ref).max() / np.abs(ref).max() < 1e-5, (form, i)
+        kap = np.exp(fem.image_to_square_kappa(imgs[i].astype(np.float32).astype(np.float64)))
+        ref_f = fem.flux_residual_structured(nc, r_, kap, kap, y[i].astype(np.float32).astype(np.float64))
+        assert np.abs(rf[i] - ref_f).max() / np.abs(ref_f).max() < 1e-5, (form, i)
+    if form == auto:
+        ret_a, rca, rfa = run('auto')
+        assert ret_a == 0 and np.array_equal(rca, rc) and np.array_equal(rfa, rf)
 
 
 def test_cgr_residual_vanishes_at_fom_solution(device):
@@ -751,7 +771,10 @@ def test_fused_output_conv_matches_separate_launches(device, monkeypatch):
     """gpi_conv_loss_fused (the decoder output conv's forward + Gaussian loss + backward in one launch,
     the loss gradient kept in LDS) against the separate forward and backward launches of the same op
     (GPI_FUSE_OUT=0 at engine construction): same ELBO (1e-6, the loss block-sum order differs) and
-    the same gradients of every parameter (1e-6 of each tensor's max)."""
+    the same gradients of every parameter (4e-6 of each tensor's max: the two launch forms sum the weight-
+    gradient slab rows and the BN-backward channel sums in different orders, fp32 rounding of sums with
+    cancellation -- a BN gamma gradient of ~10^3 from ~10^5 terms measured 1.3e-6 apart (r06); both forms are
+    held to the fp64 oracle at 5e-5 per tensor by the ELBO tests)."""
     d = load('elbo_c32.npz')
     eps = (torch.cat([cuda(d['eps_enc']), cuda(d['eps_qz'])]), cuda(d['eps_qX']))
     out = {}
@@ -766,4 +789,4 @@ def test_fused_output_conv_matches_separate_launches(device, monkeypatch):
     (v1, g1), (v0, g0) = out['fused'], out['separate']
     assert abs(v1 - v0) <= 1e-6 * abs(v0), (v1, v0)
     for k in g0:
-        assert np.abs(g1[k] - g0[k]).max() <= 1e-6 * max(np.abs(g0[k]).max(), 1e-30), k
+        assert np.abs(g1[k] - g0[k]).max() <= 4e-6 * max(np.abs(g0[k]).max(), 1e-30), k
