@@ -174,7 +174,7 @@ class GenerativeModel(lamp.modules.BaseModule):
         if self._flat is None or not all(self._flat.owns(p) for _, p in params) or \
                 len(params) != len(self._flat.params):
             dev = params[0][1].device
-            self._flat = FlatParameters(params, dev, shared_prefixes=SHARED_PREFIXES)
+            self._flat = FlatParameters(params, dev, shared_prefixes=SHARED_PREFIXES, err_slot=True)
             set_flat(self, self._flat)
         return self._flat
 

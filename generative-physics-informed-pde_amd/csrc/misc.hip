@@ -19,7 +19,10 @@ __global__ __launch_bounds__(256) void step_epilogue_kernel(gpi_step_epilogue_de
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (d.step && i == 0) *d.step += 1;
     if (i < d.n) {
-        const float g = (float)d.gacc[i];
+        float g = (float)d.gacc[i];
+        // the data-parallel error slot: this rank's hand-off timeout, summed over the ranks by the all-reduce
+        if (i == d.err_slot && d.wait_err && __hip_atomic_load(d.wait_err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            g = 1.f;
         d.grad[i] = (d.flags & GPI_FINALIZE_ACCUMULATE) ? d.grad[i] + g : g;
         if (d.flags & GPI_FINALIZE_ZERO) d.gacc[i] = 0.0;
     }
@@ -67,6 +70,11 @@ __device__ __forceinline__ bool wait_failed(const uint32_t* err) {
 // (grid-stride over at most GPI_EPILOGUE_MAX_WG workgroups: with one element per thread the grid of a 256^2
 // step -- q_X rows of 32 x 2 x 65536 floats, ~16 k workgroups -- would fill every CU slot with workgroups
 // spinning in epilogue_wait while the side stream still had kernels to dispatch)
+// The skip decision is per workgroup: each re-reads the sticky error word after its own wait, so a workgroup
+// that passes its wait after another one's timeout has been stored skips as well.  Only a timeout stored in the
+// same instant as another workgroup's final re-read (the flag arriving just as the spin budget of ~10 s runs out)
+// can leave part of that step's update applied -- the host raises on the word either way and no later step
+// updates (the word is sticky): the "untouched" guarantee is best-effort within that window.
 __global__ __launch_bounds__(256) void step_epilogue_adam_kernel(gpi_step_epilogue_desc d, gpi_adam_desc a,
                                                                  uint32_t* done, int64_t m_items) {
     bool skip = false;
@@ -130,6 +138,11 @@ __global__ __launch_bounds__(256) void step_epilogue_adam_kernel(gpi_step_epilog
 __global__ __launch_bounds__(256) void adam_kernel(gpi_adam_desc d) {
     if (d.rng_offset && blockIdx.x == 0 && threadIdx.x == 0) *d.rng_offset += d.rng_advance;
     if (wait_failed(d.wait_err)) return;        // a timed-out hand-off: the gradient may be incomplete
+    if (d.skip_if && *d.skip_if != 0.f) {      // ... on another rank (the all-reduced error slot)
+        if (d.wait_err && blockIdx.x == 0 && threadIdx.x == 0)
+            __hip_atomic_store(d.wait_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
     const int64_t t = *d.step;
     const float lr = *d.lr;
     const double bc1 = 1.0 - pow((double)d.beta1, (double)t);

@@ -116,7 +116,7 @@ class ResidualDesc(C.Structure):
 class AdamDesc(C.Structure):
     _fields_ = [('p', vp), ('g', vp), ('m', vp), ('v', vp), ('n', i64), ('lr', vp), ('step', vp),
                 ('beta1', f32), ('beta2', f32), ('eps', f32), ('_pad', f32), ('rng_offset', vp),
-                ('rng_advance', C.c_uint64), ('wait_err', vp)]
+                ('rng_advance', C.c_uint64), ('wait_err', vp), ('skip_if', vp)]
 
 
 class VoQueryDesc(C.Structure):
@@ -164,7 +164,13 @@ class StepEpilogueDesc(C.Structure):
     _fields_ = [('gacc', vp), ('grad', vp), ('n', i64), ('flags', i32), ('n_terms', i32), ('step', vp),
                 ('scratch', vp), ('n_scratch', i64), ('terms_dst', vp), ('idx_src', vp), ('idx_dst', vp),
                 ('n_idx', i64), ('drop_out', vp), ('drop_n', i64), ('drop_p', f32), ('_pad2', i32),
-                ('drop_seed', u64), ('drop_offset', vp), ('drop_sub', u64), ('wait_flag', vp), ('wait_err', vp)]
+                ('drop_seed', u64), ('drop_offset', vp), ('drop_sub', u64), ('wait_flag', vp), ('wait_err', vp),
+                ('err_slot', i64)]
+
+    def __init__(self, *a, **k):
+        super().__init__(*a, **k)
+        if 'err_slot' not in k:
+            self.err_slot = -1
 
 
 class FomDesc(C.Structure):

@@ -19,7 +19,9 @@ ALIGN = 4
 
 class FlatParameters(object):
 
-    def __init__(self, named_params, device, shared_prefixes=None):
+    def __init__(self, named_params, device, shared_prefixes=None, err_slot=False):
+        """err_slot: reserve one float at the end of the shared prefix (inside the data-parallel all-reduce,
+        no parameter): FusedElboStep's hand-off error flag, summed over the ranks (gpi_step_epilogue_desc)."""
         named = [(n, p) for n, p in named_params]
         # shared parameters first, rank-local ones (per-sample variational params) last
         if shared_prefixes is not None:
@@ -29,12 +31,20 @@ class FlatParameters(object):
         self.offsets = {}
         self.name_offsets = {}
         total = 0
+        self.err_slot = -1
         for n, p in named:
+            if err_slot and self.err_slot < 0 and shared_prefixes is not None and \
+                    not any(n.startswith(s) for s in shared_prefixes):
+                self.err_slot = total
+                total += 1
             if p.dim() == 2:
                 total = (total + ALIGN - 1) // ALIGN * ALIGN
             self.offsets[id(p)] = total
             self.name_offsets[n] = total
             total += p.numel()
+        if err_slot and self.err_slot < 0:
+            self.err_slot = total
+            total += 1
         self.numel = total
         self.P = torch.zeros(total, dtype=torch.float32, device=device)
         self.G = torch.zeros(total, dtype=torch.float32, device=device)
@@ -47,6 +57,8 @@ class FlatParameters(object):
         if shared_prefixes is not None:
             local = [n for n in self.names if not any(n.startswith(s) for s in shared_prefixes)]
             self.n_shared = self.name_offsets[local[0]] if local else total
+            if self.err_slot >= 0:
+                assert self.err_slot < self.n_shared
 
     def offset(self, p):
         return self.offsets[id(p)]

@@ -171,6 +171,14 @@ class FusedElboStep(object):
             # a timed-out hand-off (sticky error word) stops every later parameter update: the gradient of
             # such a step may be incomplete, so no step after it may move the parameters
             self.adam.wait_err = self.handoff_flags.data_ptr() + 4 * 4
+            if self.distributed and self.flat.err_slot >= 0:
+                # data parallel: the epilogue writes the word into the flat gradient's error slot (inside the
+                # all-reduced prefix) and Adam reads the SUM, so one rank's timeout stops every rank's update
+                # (and sets every rank's word: all of them raise) -- no rank applies a gradient averaged with
+                # an incomplete one
+                self.epi.wait_err = self.handoff_flags.data_ptr() + 4 * 4
+                self.epi.err_slot = self.flat.err_slot
+                self.adam.skip_if = self.flat.G.data_ptr() + 4 * self.flat.err_slot
         # lazy surfacing of that error word without a host sync: an async copy to pinned memory after
         # a replay, read once its event has completed (at the next step() / run() / check_handoff())
         self._err_host = torch.zeros(1, dtype=torch.int32, pin_memory=True) if dev.type == 'cuda' else None

@@ -440,7 +440,11 @@ typedef struct gpi_adam_desc {
     /* optional: a cross-stream wait's error word (gpi_stream_wait / the fused epilogue's wait_err).  While
      * it is non-zero the update leaves p, m and v untouched (a timed-out hand-off means the gradient may be
      * incomplete; the word is sticky, the host raises on it); counters and the RNG offset still advance. */
-    const uint32_t* wait_err;
+    uint32_t* wait_err;
+    /* optional (data-parallel steps): the all-reduced error slot of gpi_step_epilogue_desc.err_slot; non-zero
+     * -> some rank's hand-off timed out: this rank skips the update too and sets its own *wait_err, so every
+     * rank keeps identical parameters and raises. */
+    const float* skip_if;
 } gpi_adam_desc;
 
 /* ---------------------------------------------------------------- API */
@@ -580,6 +584,11 @@ typedef struct gpi_step_epilogue_desc {
      * hold every CU slot the signalling stream's remaining kernels need. */
     const uint32_t* wait_flag;
     uint32_t* wait_err;
+    /* data-parallel steps (gpi_step_epilogue, before the gradient all-reduce): grad[err_slot] = 1 when
+     * *wait_err is set -- a flat-buffer slot inside the all-reduced shared prefix that holds no parameter,
+     * so after the SUM every rank sees whether ANY rank's hand-off timed out (gpi_adam_desc.skip_if).
+     * -1: none. */
+    int64_t err_slot;
 } gpi_step_epilogue_desc;
 int gpi_step_epilogue(const gpi_step_epilogue_desc* d, void* stream);
 int gpi_adam(const gpi_adam_desc* d, void* stream);

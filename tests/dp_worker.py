@@ -174,8 +174,49 @@ def main(out, mode='replica'):
     dist.destroy_process_group()
 
 
+def run_timeout(out):
+    """Two eager data-parallel steps; in the second, rank 1's side-stream flag can never reach its target
+    (set 2^30 below it), so rank 1's hand-off wait times out (~10 s).  Records whether each rank's
+    parameters / Adam moments moved in that step, the all-reduced error slot and whether check_handoff
+    raises."""
+    from gpi.train import FusedElboStep
+    from elbo_ref import load
+    rank, world = int(os.environ['RANK']), int(os.environ['WORLD_SIZE'])
+    torch.cuda.set_device(0)
+    dist.init_process_group('gloo')
+    d = load('elbo_c32.npz')
+    model, _ = shard_model(d, rank)
+    ds = model._datasets['supervised']
+    Xu = torch.tensor(d['Xu'], device='cuda')
+    step = FusedElboStep(model, Xu, B_U, ds.get('X'), ds.get('Y'), ds.get('F_ROM_BC'), lr=1e-3, seed=50 + rank,
+                         subset_seed=9, distributed=True, rank=rank, world=world)
+    rec = dict(handoff=np.array(step.handoff), err_slot=np.int64(step.flat.err_slot))
+    step.step_eager()
+    torch.cuda.synchronize()
+    step.check_handoff()
+    P0, m0, v0 = step.flat.P.clone(), step.m.clone(), step.v.clone()
+    if rank == 1:
+        step.handoff_flags[3] -= (1 << 30)
+    step.step_eager()
+    torch.cuda.synchronize()
+    rec['err_word'] = np.int64(step.handoff_flags[4].item())
+    rec['slot_sum'] = np.float64(step.flat.G[step.flat.err_slot].item()) if step.flat.err_slot >= 0 else np.nan
+    rec['P_same'] = np.int64(torch.equal(step.flat.P, P0))
+    rec['mv_same'] = np.int64(torch.equal(step.m, m0) and torch.equal(step.v, v0))
+    try:
+        step.check_handoff()
+        rec['raised'] = np.int64(0)
+    except RuntimeError:
+        rec['raised'] = np.int64(1)
+    np.savez(os.path.join(out, 'rank%d.npz' % rank), **rec)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 if __name__ == '__main__':
     if len(sys.argv) > 2 and sys.argv[2] == 'c64sync':
         run_c64_sync(sys.argv[1])
+    elif len(sys.argv) > 2 and sys.argv[2] == 'timeout':
+        run_timeout(sys.argv[1])
     else:
         main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else 'replica')

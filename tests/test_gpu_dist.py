@@ -280,3 +280,27 @@ def test_dp_config3_sync_bn_vs_union_oracle(device, tmp_path):
     bad = {k: v for k, v in errs.items() if not v < 5e-5}
     assert not bad, (bad, sorted(errs.items(), key=lambda kv: -kv[1])[:8])
 
+
+
+def test_dp_hand_off_timeout_on_one_rank_stops_every_rank(device, tmp_path):
+    """a hand-off wait that times out on ONE rank (its gradient may be incomplete) must not let
+    the other ranks apply the all-reduced gradient.  Rank 1's side-stream flag is pushed out of reach in the
+    second of two data-parallel steps: its wait times out (~10 s), its epilogue writes 1 into the flat
+    gradient's error slot (inside the all-reduced shared prefix), the SUM carries it to rank 0, and BOTH ranks
+    leave parameters and Adam moments untouched and raise (check_handoff)."""
+    env = dict(os.environ)
+    env['PYTHONUNBUFFERED'] = '1'
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node=2',
+           '--master-addr=127.0.0.1', '--master-port=%d' % _free_port(), os.path.join(HERE, 'dp_worker.py'),
+           str(tmp_path), 'timeout']
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    rk = [dict(np.load(str(tmp_path / ('rank%d.npz' % i)))) for i in range(2)]
+    if str(rk[0]['handoff']) != 'flags':
+        pytest.skip('no flag hand-off in this configuration')
+    for i in range(2):
+        assert int(rk[i]['err_slot']) >= 0
+        assert float(rk[i]['slot_sum']) == 1.0, i          # rank 1's timeout, summed over both ranks
+        assert int(rk[i]['err_word']) == 1, i              # rank 1: its wait; rank 0: set by its Adam
+        assert int(rk[i]['P_same']) == 1 and int(rk[i]['mv_same']) == 1, i
+        assert int(rk[i]['raised']) == 1, i
