@@ -158,11 +158,9 @@ __global__ __launch_bounds__(256) void adam_kernel(gpi_adam_desc d) {
     }
 }
 
-__global__ __launch_bounds__(256) void randn_kernel(float* out, int64_t n, uint64_t seed, const uint64_t* offset,
-                                                    uint64_t sub) {
-    const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;   // one Philox block -> 4 normals
+__device__ __forceinline__ void randn_body(int64_t q, float* out, int64_t n, uint64_t seed, uint64_t base,
+                                           uint64_t sub) {   // one Philox block q -> 4 normals
     if (q * 4 >= n) return;
-    const uint64_t base = offset ? *offset : 0;
     const uint4_ r = philox(base + (uint64_t)q, sub, seed);
     const float u0 = u01(r.x), u1 = u01(r.y), u2 = u01(r.z), u3 = u01(r.w);
     const float r0 = sqrtf(-2.f * logf(u0)), r1 = sqrtf(-2.f * logf(u2));
@@ -173,16 +171,24 @@ __global__ __launch_bounds__(256) void randn_kernel(float* out, int64_t n, uint6
         if (q * 4 + k < n) out[q * 4 + k] = v[k];
 }
 
-__global__ __launch_bounds__(256) void dropout_mask_kernel(float* out, int64_t n, float p, float scale, uint64_t seed,
-                                                          const uint64_t* offset, uint64_t sub) {
-    const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;   // one Philox block -> 4 channels
+__device__ __forceinline__ void dropout_body(int64_t q, float* out, int64_t n, float p, float scale, uint64_t seed,
+                                             uint64_t base, uint64_t sub) {   // one Philox block -> 4 channels
     if (q * 4 >= n) return;
-    const uint64_t base = offset ? *offset : 0;
     const uint4_ r = philox(base + (uint64_t)q, sub, seed);
     const float u[4] = {u01(r.x), u01(r.y), u01(r.z), u01(r.w)};
 #pragma unroll
     for (int k = 0; k < 4; ++k)
         if (q * 4 + k < n) out[q * 4 + k] = u[k] < p ? 0.f : scale;
+}
+
+__global__ __launch_bounds__(256) void randn_kernel(float* out, int64_t n, uint64_t seed, const uint64_t* offset,
+                                                    uint64_t sub) {
+    randn_body((int64_t)blockIdx.x * 256 + threadIdx.x, out, n, seed, offset ? *offset : 0, sub);
+}
+
+__global__ __launch_bounds__(256) void dropout_mask_kernel(float* out, int64_t n, float p, float scale, uint64_t seed,
+                                                          const uint64_t* offset, uint64_t sub) {
+    dropout_body((int64_t)blockIdx.x * 256 + threadIdx.x, out, n, p, scale, seed, offset ? *offset : 0, sub);
 }
 
 __global__ void rng_advance_kernel(uint64_t* offset, uint64_t by) { *offset += by; }
@@ -193,15 +199,13 @@ __global__ void rng_advance_kernel(uint64_t* offset, uint64_t by) { *offset += b
 // elements, TPE = 256 / EPB threads per element over strided slices of the keys, partial counts
 // summed across the TPE lanes.  Same result as sorting the pairs (ranks of distinct pairs are
 // distinct), without the sort's log^2 n dependent barrier steps in one workgroup (15 us at n = 1024).
-__global__ __launch_bounds__(256) void subset_rank_kernel(int32_t* out, int32_t n, int32_t k, uint64_t seed,
-                                                          const uint64_t* offset, uint64_t sub, int32_t epb) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t hk[];
-    const uint64_t base = offset ? *offset : 0;
+__device__ __forceinline__ void subset_rank_body(int blk, uint32_t* hk, int32_t* out, int32_t n, int32_t k,
+                                                 uint64_t seed, uint64_t base, uint64_t sub, int32_t epb) {
     for (int j = threadIdx.x; j < n; j += 256) hk[j] = philox(base + (uint64_t)j, sub, seed).x;
     __syncthreads();
     const int tpe = 256 / epb;
     const int e = threadIdx.x / tpe, part = threadIdx.x - e * tpe;
-    const int i = blockIdx.x * epb + e;
+    const int i = blk * epb + e;
     int cnt = 0;
     if (i < n) {
         const uint32_t ki = hk[i];
@@ -213,6 +217,42 @@ __global__ __launch_bounds__(256) void subset_rank_kernel(int32_t* out, int32_t 
     // tpe consecutive lanes (a power of two <= 64 within one wave) hold one element's partial counts
     for (int m = 1; m < tpe; m <<= 1) cnt += __shfl_xor(cnt, m, 64);
     if (i < n && part == 0 && cnt < k) out[cnt] = i;
+}
+
+__global__ __launch_bounds__(256) void subset_rank_kernel(int32_t* out, int32_t n, int32_t k, uint64_t seed,
+                                                          const uint64_t* offset, uint64_t sub, int32_t epb) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t hk[];
+    subset_rank_body(blockIdx.x, hk, out, n, k, seed, offset ? *offset : 0, sub, epb);
+}
+
+// elements per workgroup of the one-launch subset: about n / 256 (>= 4, <= 64, a power of two): enough
+// workgroups to spread the n^2 comparisons, few enough that the n key draws per workgroup stay cheap
+int subset_epb(int32_t n) {
+    int32_t epb = 4;                      // >= 4: an element's 256 / epb lanes stay inside one wave
+    while (epb < 64 && epb * 256 < n) epb <<= 1;
+    return epb;
+}
+
+struct DrawArgs {
+    gpi_draw_item it[GPI_MAX_DRAWS];
+    int32_t first_block[GPI_MAX_DRAWS + 1];
+    int32_t epb;
+    int32_t n;
+};
+
+// gpi_draws: the items' workgroups by block range; every item's arithmetic is its own kernel's
+__global__ __launch_bounds__(256) void draws_kernel(DrawArgs a, uint64_t seed, const uint64_t* offset) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t hk[];
+    int k = 0;
+#pragma unroll
+    for (int j = 1; j < GPI_MAX_DRAWS; ++j) k += (j < a.n && (int)blockIdx.x >= a.first_block[j]) ? 1 : 0;
+    const gpi_draw_item it = a.it[k];
+    const int blk = blockIdx.x - a.first_block[k];
+    const uint64_t base = offset ? *offset : 0;
+    const int64_t q = (int64_t)blk * 256 + threadIdx.x;
+    if (it.kind == GPI_DRAW_RANDN) randn_body(q, (float*)it.out, it.n, seed, base, it.sub);
+    else if (it.kind == GPI_DRAW_DROPOUT) dropout_body(q, (float*)it.out, it.n, it.p, 1.f / (1.f - it.p), seed, base, it.sub);
+    else subset_rank_body(blk, hk, (int32_t*)it.out, (int32_t)it.n, (int32_t)it.k, seed, base, it.sub, a.epb);
 }
 
 // Any pool size (gpi_random_subset_ws): the same order -- the first k of the n indices by (Philox key,
@@ -422,7 +462,7 @@ extern "C" int gpi_struct_sizes(int64_t* out, int n) {
                          (int64_t)sizeof(gpi_vo_precision_desc), (int64_t)sizeof(gpi_gp_sample_desc),
                          (int64_t)sizeof(gpi_vo_galerkin_desc), (int64_t)sizeof(gpi_step_epilogue_desc),
                          (int64_t)sizeof(gpi_fom_desc), (int64_t)sizeof(gpi_random_field_desc),
-                         (int64_t)sizeof(gpi_vo_sparse)};
+                         (int64_t)sizeof(gpi_vo_sparse), (int64_t)sizeof(gpi_draw_item)};
     const int k = (int)(sizeof(s) / sizeof(s[0]));
     if (!out || n < k) return GPI_ERR_ARG;
     for (int i = 0; i < k; ++i) out[i] = s[i];
@@ -561,14 +601,44 @@ extern "C" int gpi_random_subset(int32_t* out, int32_t n, int32_t k, uint64_t se
                                  uint64_t sub, void* stream) {
     if (!out || n <= 0 || k < 0 || k > n || n > 16384) return GPI_ERR_ARG;
     if (k == 0) return GPI_OK;
-    // elements per workgroup: about n / 256 (>= 4, <= 64, a power of two): enough workgroups to
-    // spread the n^2 comparisons, few enough that the n key draws per workgroup stay cheap
-    int32_t epb = 4;                      // >= 4: an element's 256 / epb lanes stay inside one wave
-    while (epb < 64 && epb * 256 < n) epb <<= 1;
+    const int32_t epb = subset_epb(n);
     const size_t lds = sizeof(uint32_t) * n;
     if (lds > 64 * 1024) return GPI_ERR_ARG;
     hipLaunchKernelGGL(subset_rank_kernel, dim3((unsigned)((n + epb - 1) / epb)), dim3(256), lds, (hipStream_t)stream,
                        out, n, k, seed, offset, sub, epb);
+    GPI_CHECK_LAUNCH();
+    return GPI_OK;
+}
+
+extern "C" int gpi_draws(const gpi_draw_item* items, int n_items, uint64_t seed, const uint64_t* offset, void* stream) {
+    if (!items || n_items < 0 || n_items > GPI_MAX_DRAWS) return GPI_ERR_ARG;
+    DrawArgs a;
+    a.n = n_items;
+    a.epb = 4;
+    size_t lds = 0;
+    int nb = 0, n_sub = 0;
+    for (int k = 0; k < n_items; ++k) {
+        const gpi_draw_item& it = items[k];
+        a.it[k] = it;
+        a.first_block[k] = nb;
+        if (!it.out || it.n < 0) return GPI_ERR_ARG;
+        if (it.kind == GPI_DRAW_RANDN) {
+            nb += (int)((((it.n + 3) / 4) + 255) / 256);
+        } else if (it.kind == GPI_DRAW_DROPOUT) {
+            if (!(it.p >= 0.f && it.p < 1.f)) return GPI_ERR_ARG;
+            nb += (int)((((it.n + 3) / 4) + 255) / 256);
+        } else if (it.kind == GPI_DRAW_SUBSET) {
+            if (it.n <= 0 || it.n > 16384 || it.k < 0 || it.k > it.n || ++n_sub > 1) return GPI_ERR_ARG;
+            a.epb = subset_epb((int32_t)it.n);
+            lds = sizeof(uint32_t) * (size_t)it.n;
+            if (it.k > 0) nb += (int)((it.n + a.epb - 1) / a.epb);
+        } else {
+            return GPI_ERR_ARG;
+        }
+    }
+    for (int k = n_items; k <= GPI_MAX_DRAWS; ++k) a.first_block[k] = nb;
+    if (nb == 0) return GPI_OK;
+    hipLaunchKernelGGL(draws_kernel, dim3((unsigned)nb), dim3(256), lds, (hipStream_t)stream, a, seed, offset);
     GPI_CHECK_LAUNCH();
     return GPI_OK;
 }

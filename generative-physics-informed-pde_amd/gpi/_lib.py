@@ -183,9 +183,17 @@ class RandomFieldDesc(C.Structure):
                 ('ly', vp), ('lxt', vp), ('scale', vp), ('gamma', vp), ('seed', u64), ('sub', u64), ('work', vp), ('x', vp)]
 
 
+GPI_MAX_DRAWS = 6
+DRAW_RANDN, DRAW_DROPOUT, DRAW_SUBSET = 0, 1, 2
+
+
+class DrawItem(C.Structure):
+    _fields_ = [('kind', i32), ('p', f32), ('out', vp), ('n', i64), ('k', i64), ('sub', u64)]
+
+
 STRUCTS = [Stat, Groups, ConvDesc, CodecCtx, ReduceItem, HeadDesc, GemmItem, RomDesc, ResidualDesc, AdamDesc,
            VoQueryDesc, VoMomentsDesc, VoConditionDesc, VoPrecisionDesc, GpSampleDesc,
-           VoGalerkinDesc, StepEpilogueDesc, FomDesc, RandomFieldDesc, VoSparse]
+           VoGalerkinDesc, StepEpilogueDesc, FomDesc, RandomFieldDesc, VoSparse, DrawItem]
 
 # name -> (restype, argtypes)
 SIGNATURES = {
@@ -220,6 +228,7 @@ SIGNATURES = {
     'gpi_fom_solve': (C.c_int, [C.POINTER(FomDesc), vp]),
     'gpi_random_field': (C.c_int, [C.POINTER(RandomFieldDesc), vp]),
     'gpi_randn': (C.c_int, [vp, i64, u64, vp, u64, vp]),
+    'gpi_draws': (C.c_int, [vp, C.c_int, u64, vp, vp]),
     'gpi_dropout_masks': (C.c_int, [vp, i64, f32, u64, vp, u64, vp]),
     'gpi_rng_advance': (C.c_int, [vp, u64, vp]),
     'gpi_stream_signal': (C.c_int, [vp, vp, vp]),

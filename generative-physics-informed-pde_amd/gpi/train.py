@@ -187,6 +187,7 @@ class FusedElboStep(object):
         self._n_steps = 0
         self._fb_pending = False
         self.graph = None
+        self._one_draw = os.environ.get('GPI_ONE_DRAW', '1') != '0'
         # the first step's noise; every step then draws the next step's during its backward
         self._launch_noise(L.stream_handle(), self.idx, sub0=100)
 
@@ -206,8 +207,29 @@ class FusedElboStep(object):
         """Random subset into ``idx`` and the reparametrisation noise into the engine's eps
         buffers.  Philox streams: the step's offset (advanced by Adam at the end of every step)
         and sub ids sub0 + {1, 2, 3}; the noise drawn during step k (for step k+1) therefore
-        differs from step k's own, which was drawn during step k-1 or by the prologue (sub0 = 100)."""
+        differs from step k's own, which was drawn during step k-1 or by the prologue (sub0 = 100).
+        All of it in ONE launch (gpi_draws: the same draws as the separate entry points, bit for bit)
+        unless the pool needs the multi-launch subset form or GPI_ONE_DRAW=0."""
         lib = L.lib()
+        if self._one_draw and (not subset or not self.B_u or self._subset_ws is None):
+            items = []
+            e = self.engine
+            if e.has_dropout and codecs:
+                for k, (c, prog) in enumerate((('enc', e.ep), ('dec', e.dp))):
+                    if c in codecs and prog is not None and prog.drop_numel:
+                        items.append(L.DrawItem(kind=L.DRAW_DROPOUT, p=prog.drop_rate, out=e.ws.fptr(prog.drop_off).value,
+                                                n=prog.drop_numel, sub=sub0 + 4 + k))
+            if subset and self.B_u:
+                items.append(L.DrawItem(kind=L.DRAW_SUBSET, out=idx.data_ptr(), n=self.n_pool, k=self.n_sub,
+                                        sub=sub0 + 1))
+            ez = e.eps_z()
+            items.append(L.DrawItem(kind=L.DRAW_RANDN, out=ez.data_ptr(), n=ez.numel(), sub=sub0 + 2))
+            if e.N_ex:
+                ex = e.eps_x()
+                items.append(L.DrawItem(kind=L.DRAW_RANDN, out=ex.data_ptr(), n=ex.numel(), sub=sub0 + 3))
+            arr = (L.DrawItem * len(items))(*items)
+            L.check(lib.gpi_draws(arr, len(items), self.seed, L.ptr(self.rng_off), st), 'step draws')
+            return
         if self.engine.has_dropout and codecs:   # Dropout2d channel scales (sub ids sub0 + 4 enc, + 5 dec)
             self.engine.draw_dropout(st, self.seed, L.ptr(self.rng_off), sub0 + 4, codecs=codecs)
         if subset:

@@ -624,6 +624,24 @@ int gpi_queue_probe(const uint32_t* flag, uint32_t* seen, void* stream);
 
 /* Device Philox4x32-10 normals: out[i] = N(0,1) for counter (*offset + i);
  * offset is a device uint64 advanced by gpi_rng_advance (graph-replay safe). */
+/* Several Philox draws of one step in ONE launch (the fused step's next-step draws on its side stream: the
+ * decoder's Dropout2d scales, the random subset, the reparametrisation noise), each item bit-identical to its
+ * own entry point's launch with the same seed / offset / sub: GPI_DRAW_RANDN = gpi_randn(out, n, ...),
+ * GPI_DRAW_DROPOUT = gpi_dropout_masks(out, n, p, ...), GPI_DRAW_SUBSET = gpi_random_subset(out, n, k, ...)
+ * (pool n <= 16384; at most one subset item).  Workgroups are dealt to the items by block ranges. */
+#define GPI_MAX_DRAWS 6
+#define GPI_DRAW_RANDN   0
+#define GPI_DRAW_DROPOUT 1
+#define GPI_DRAW_SUBSET  2
+typedef struct gpi_draw_item {
+    int32_t kind;
+    float p;                   /* dropout probability (GPI_DRAW_DROPOUT) */
+    void* out;                 /* float* (randn, dropout) or int32_t* (subset) */
+    int64_t n;                 /* values (randn, dropout) or pool size (subset) */
+    int64_t k;                 /* subset size */
+    uint64_t sub;              /* Philox sub stream */
+} gpi_draw_item;
+int gpi_draws(const gpi_draw_item* items, int n_items, uint64_t seed, const uint64_t* offset, void* stream);
 int gpi_randn(float* out, int64_t n, uint64_t seed, const uint64_t* offset, uint64_t sub, void* stream);
 int gpi_rng_advance(uint64_t* offset, uint64_t by, void* stream);
 /* Dropout2d channel scales (nn.Dropout2d train mode, codec.py:177-178): out[i] = 0 with

@@ -403,6 +403,37 @@ def test_random_subset_exact(device, n, k, off):
     assert np.array_equal(idx.cpu().numpy(), random_subset(n, k, 1234567, off, 11))
 
 
+@pytest.mark.parametrize('n,k', [(1024, 256), (2048, 256), (16384, 64), (7, 3)])
+def test_step_draws_one_launch_matches_separate_launches(device, n, k):
+    """gpi_draws (the fused step's next-step draws in ONE launch: Dropout2d scales, random subset, two noise
+    blocks) = gpi_dropout_masks / gpi_random_subset / gpi_randn launched one by one with the same seed,
+    offset and sub streams, bit for bit, and the subset = the numpy Philox restatement's."""
+    from gpi import _lib as L
+    from philox_ref import random_subset
+    lib, st = L.lib(), L.stream_handle()
+    o = torch.tensor([1 << 33], dtype=torch.int64, device='cuda')
+    seed = 97531
+    nz, nx, nd = 288 * 64 + 3, 32 * 128, 288 * 23 + 1
+    a = dict(idx=torch.full((k,), -1, dtype=torch.int32, device='cuda'), z=torch.full((nz,), 7.0, device='cuda'),
+             x=torch.full((nx,), 7.0, device='cuda'), d=torch.full((nd,), 7.0, device='cuda'))
+    b = {kk: v.clone() for kk, v in a.items()}
+    items = [L.DrawItem(kind=L.DRAW_DROPOUT, p=0.2, out=a['d'].data_ptr(), n=nd, sub=5),
+             L.DrawItem(kind=L.DRAW_SUBSET, out=a['idx'].data_ptr(), n=n, k=k, sub=1),
+             L.DrawItem(kind=L.DRAW_RANDN, out=a['z'].data_ptr(), n=nz, sub=2),
+             L.DrawItem(kind=L.DRAW_RANDN, out=a['x'].data_ptr(), n=nx, sub=3)]
+    arr = (L.DrawItem * len(items))(*items)
+    L.check(lib.gpi_draws(arr, len(items), seed, L.ptr(o), st), 'draws')
+    L.check(lib.gpi_dropout_masks(L.ptr(b['d']), nd, 0.2, seed, L.ptr(o), 5, st), 'masks')
+    L.check(lib.gpi_random_subset(L.ptr(b['idx']), n, k, seed, L.ptr(o), 1, st), 'subset')
+    L.check(lib.gpi_randn(L.ptr(b['z']), nz, seed, L.ptr(o), 2, st), 'randn z')
+    L.check(lib.gpi_randn(L.ptr(b['x']), nx, seed, L.ptr(o), 3, st), 'randn x')
+    torch.cuda.synchronize()
+    for kk in a:
+        assert torch.equal(a[kk], b[kk]), kk
+    assert np.array_equal(a['idx'].cpu().numpy(), random_subset(n, k, seed, 1 << 33, 1))
+    assert set(torch.unique(a['d']).tolist()) <= {0.0, 1.25}
+
+
 @pytest.mark.parametrize('n,k,off', [(7, 3, 5), (16384, 64, 9), (16385, 256, 0), (65536, 256, 17),
                                       (65536, 65536, 3), (200003, 2048, 1 << 40), (1 << 20, 1024, 5)])
 def test_random_subset_any_pool_exact(device, n, k, off):
