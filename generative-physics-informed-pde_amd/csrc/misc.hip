@@ -1,5 +1,6 @@
 // Step plumbing kernels: gradient finalisation, flat Adam, device RNG.
 #include "common.h"
+#include <string.h>
 
 using namespace gpi;
 
@@ -241,7 +242,7 @@ struct DrawArgs {
 };
 
 // gpi_draws: the items' workgroups by block range; every item's arithmetic is its own kernel's
-__global__ __launch_bounds__(256) void draws_kernel(DrawArgs a, uint64_t seed, const uint64_t* offset) {
+__global__ __launch_bounds__(256) void draws_kernel(DrawArgs a, const uint64_t* offset) {
     extern __shared__ __attribute__((aligned(16))) uint32_t hk[];
     int k = 0;
 #pragma unroll
@@ -250,9 +251,9 @@ __global__ __launch_bounds__(256) void draws_kernel(DrawArgs a, uint64_t seed, c
     const int blk = blockIdx.x - a.first_block[k];
     const uint64_t base = offset ? *offset : 0;
     const int64_t q = (int64_t)blk * 256 + threadIdx.x;
-    if (it.kind == GPI_DRAW_RANDN) randn_body(q, (float*)it.out, it.n, seed, base, it.sub);
-    else if (it.kind == GPI_DRAW_DROPOUT) dropout_body(q, (float*)it.out, it.n, it.p, 1.f / (1.f - it.p), seed, base, it.sub);
-    else subset_rank_body(blk, hk, (int32_t*)it.out, (int32_t)it.n, (int32_t)it.k, seed, base, it.sub, a.epb);
+    if (it.kind == GPI_DRAW_RANDN) randn_body(q, (float*)it.out, it.n, it.seed, base, it.sub);
+    else if (it.kind == GPI_DRAW_DROPOUT) dropout_body(q, (float*)it.out, it.n, it.p, 1.f / (1.f - it.p), it.seed, base, it.sub);
+    else subset_rank_body(blk, hk, (int32_t*)it.out, (int32_t)it.n, (int32_t)it.k, it.seed, base, it.sub, a.epb);
 }
 
 // Any pool size (gpi_random_subset_ws): the same order -- the first k of the n indices by (Philox key,
@@ -453,6 +454,74 @@ extern "C" int gpi_version(void) { return 1; }
 
 extern "C" int gpi_replicas(void) { return GPI_REPLICAS; }
 
+// ---------------------------------------------------------------- SyncBN seam exchange (gpi_bn_exchange)
+// Lane t < 2 G n of one wave owns message element (group g, channel c, field f).  Cross-process words (the
+// flags, the peers' buffers) are touched only by system-scope atomics: the stores write through to the owner's
+// memory, the loads bypass this GPU's caches; the data stores are complete (vmcnt) before the flag's release.
+__global__ __launch_bounds__(64) void bn_exchange_kernel(gpi_bn_exchange_desc d) {
+    const int t = threadIdx.x;
+    const int m = GPI_MAX_GROUPS * d.n * 2;
+    const int g = t / (2 * d.n), c = (t >> 1) - g * d.n, f = t & 1;
+    double* rec0 = (double*)d.stats + ((int64_t)g * d.n_stats + d.stat0 + c) * 4 + d.f0 + f;
+    const int64_t rstride = (int64_t)GPI_MAX_GROUPS * d.n_stats * 4;   // doubles per replica
+    double v = 0.0;
+    if (d.mode != GPI_BNX_UNFOLD && t < m) {
+        double r[GPI_REPLICAS];
+#pragma unroll
+        for (int k = 0; k < GPI_REPLICAS; ++k) r[k] = rec0[k * rstride];
+#pragma unroll
+        for (int k = 0; k < GPI_REPLICAS; ++k) v += r[k];              // replica order
+    }
+    if (d.mode == GPI_BNX_FOLD) {
+        if (t < m) d.msg[t] = v;
+        return;
+    }
+    if (d.mode == GPI_BNX_UNFOLD) {
+        if (t < m) v = d.msg[t];
+    } else {
+        const uint32_t seq = *d.seq + 1u;
+        const int slot = (int)(seq & 1u) * GPI_BNX_MSG;
+        if (t < m)
+            __hip_atomic_store(d.peer_buf[d.rank] + slot + t, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __builtin_amdgcn_s_waitcnt(0);                                  // this lane's message store is done
+        __syncthreads();
+        __shared__ uint32_t s_bad;
+        if (t == 0) {
+            // (no release fence: the message went out by write-through system-scope stores that are complete;
+            // a fence would write back this XCD's whole L2)
+            __hip_atomic_store(d.peer_flag[d.rank], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            uint32_t bad = 0u;
+            for (int p = 0; p < d.world && !bad; ++p) {
+                for (int i = 0; (int32_t)(__hip_atomic_load(d.peer_flag[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) -
+                                          seq) < 0; ++i) {
+                    __builtin_amdgcn_s_sleep(2);
+                    if (i > WAIT_SPIN_MAX) {
+                        bad = 1u;
+                        if (d.err) __hip_atomic_store(d.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        break;
+                    }
+                }
+            }
+            *d.seq = seq;       // (the peers' messages are read by system-scope loads below: no acquire fence)
+            s_bad = bad;
+        }
+        __syncthreads();
+        v = 0.0;
+        if (t < m) {
+            double r[GPI_MAX_RANKS];
+            for (int p = 0; p < d.world; ++p)
+                r[p] = __hip_atomic_load(d.peer_buf[p] + slot + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            for (int p = 0; p < d.world; ++p) v += r[p];                // rank order
+        }
+        (void)s_bad;
+    }
+    if (t < m) {
+        rec0[0] = v * d.scale[g];
+#pragma unroll
+        for (int k = 1; k < GPI_REPLICAS; ++k) rec0[k * rstride] = 0.0;
+    }
+}
+
 extern "C" int gpi_struct_sizes(int64_t* out, int n) {
     const int64_t s[] = {(int64_t)sizeof(gpi_stat), (int64_t)sizeof(gpi_groups), (int64_t)sizeof(gpi_conv_desc),
                          (int64_t)sizeof(gpi_codec_ctx), (int64_t)sizeof(gpi_reduce_item), (int64_t)sizeof(gpi_head_desc),
@@ -462,7 +531,8 @@ extern "C" int gpi_struct_sizes(int64_t* out, int n) {
                          (int64_t)sizeof(gpi_vo_precision_desc), (int64_t)sizeof(gpi_gp_sample_desc),
                          (int64_t)sizeof(gpi_vo_galerkin_desc), (int64_t)sizeof(gpi_step_epilogue_desc),
                          (int64_t)sizeof(gpi_fom_desc), (int64_t)sizeof(gpi_random_field_desc),
-                         (int64_t)sizeof(gpi_vo_sparse), (int64_t)sizeof(gpi_draw_item)};
+                         (int64_t)sizeof(gpi_vo_sparse), (int64_t)sizeof(gpi_draw_item),
+                         (int64_t)sizeof(gpi_bn_exchange_desc)};
     const int k = (int)(sizeof(s) / sizeof(s[0]));
     if (!out || n < k) return GPI_ERR_ARG;
     for (int i = 0; i < k; ++i) out[i] = s[i];
@@ -610,7 +680,7 @@ extern "C" int gpi_random_subset(int32_t* out, int32_t n, int32_t k, uint64_t se
     return GPI_OK;
 }
 
-extern "C" int gpi_draws(const gpi_draw_item* items, int n_items, uint64_t seed, const uint64_t* offset, void* stream) {
+extern "C" int gpi_draws(const gpi_draw_item* items, int n_items, const uint64_t* offset, void* stream) {
     if (!items || n_items < 0 || n_items > GPI_MAX_DRAWS) return GPI_ERR_ARG;
     DrawArgs a;
     a.n = n_items;
@@ -638,7 +708,49 @@ extern "C" int gpi_draws(const gpi_draw_item* items, int n_items, uint64_t seed,
     }
     for (int k = n_items; k <= GPI_MAX_DRAWS; ++k) a.first_block[k] = nb;
     if (nb == 0) return GPI_OK;
-    hipLaunchKernelGGL(draws_kernel, dim3((unsigned)nb), dim3(256), lds, (hipStream_t)stream, a, seed, offset);
+    hipLaunchKernelGGL(draws_kernel, dim3((unsigned)nb), dim3(256), lds, (hipStream_t)stream, a, offset);
     GPI_CHECK_LAUNCH();
     return GPI_OK;
+}
+
+extern "C" int gpi_bn_exchange(const gpi_bn_exchange_desc* d, void* stream) {
+    if (!d || !d->stats || d->n < 1 || d->n > GPI_MAX_COUT || d->stat0 < 0 || d->stat0 + d->n > d->n_stats ||
+        (d->f0 != 0 && d->f0 != 2) || d->mode < GPI_BNX_FOLD || d->mode > GPI_BNX_PEER)
+        return GPI_ERR_ARG;
+    if (d->mode != GPI_BNX_PEER && !d->msg) return GPI_ERR_ARG;
+    if (d->mode != GPI_BNX_FOLD && !d->scale) return GPI_ERR_ARG;
+    if (d->mode == GPI_BNX_PEER) {
+        if (d->world < 1 || d->world > GPI_MAX_RANKS || d->rank < 0 || d->rank >= d->world || !d->seq) return GPI_ERR_ARG;
+        for (int p = 0; p < d->world; ++p)
+            if (!d->peer_buf[p] || !d->peer_flag[p]) return GPI_ERR_ARG;
+    }
+    hipLaunchKernelGGL(bn_exchange_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, *d);
+    GPI_CHECK_LAUNCH();
+    return GPI_OK;
+}
+
+extern "C" int gpi_peer_alloc(int64_t bytes, void** ptr, void* ipc_handle) {
+    if (bytes <= 0 || !ptr || !ipc_handle) return GPI_ERR_ARG;
+    static_assert(sizeof(hipIpcMemHandle_t) == 64, "IPC handle size");
+    if (hipMalloc(ptr, (size_t)bytes) != hipSuccess) return GPI_ERR_LAUNCH;
+    if (hipMemset(*ptr, 0, (size_t)bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
+        hipIpcGetMemHandle((hipIpcMemHandle_t*)ipc_handle, *ptr) != hipSuccess) {
+        (void)hipFree(*ptr);
+        *ptr = nullptr;
+        return GPI_ERR_LAUNCH;
+    }
+    return GPI_OK;
+}
+
+extern "C" int gpi_peer_open(const void* ipc_handle, void** ptr) {
+    if (!ipc_handle || !ptr) return GPI_ERR_ARG;
+    hipIpcMemHandle_t h;
+    memcpy(&h, ipc_handle, sizeof(h));
+    if (hipIpcOpenMemHandle(ptr, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) return GPI_ERR_LAUNCH;
+    return GPI_OK;
+}
+
+extern "C" int gpi_peer_close(void* ptr, int own) {
+    if (!ptr) return GPI_ERR_ARG;
+    return (own ? hipFree(ptr) : hipIpcCloseMemHandle(ptr)) == hipSuccess ? GPI_OK : GPI_ERR_LAUNCH;
 }

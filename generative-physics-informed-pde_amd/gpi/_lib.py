@@ -188,12 +188,23 @@ DRAW_RANDN, DRAW_DROPOUT, DRAW_SUBSET = 0, 1, 2
 
 
 class DrawItem(C.Structure):
-    _fields_ = [('kind', i32), ('p', f32), ('out', vp), ('n', i64), ('k', i64), ('sub', u64)]
+    _fields_ = [('kind', i32), ('p', f32), ('out', vp), ('n', i64), ('k', i64), ('sub', u64), ('seed', u64)]
+
+
+GPI_MAX_RANKS = 16
+GPI_BNX_MSG = 64
+BNX_FOLD, BNX_UNFOLD, BNX_PEER = 0, 1, 2
+
+
+class BnExchangeDesc(C.Structure):
+    _fields_ = [('stats', vp), ('n_stats', i64), ('stat0', i32), ('n', i32), ('f0', i32), ('mode', i32),
+                ('scale', vp), ('msg', vp), ('rank', i32), ('world', i32),
+                ('peer_buf', vp * GPI_MAX_RANKS), ('peer_flag', vp * GPI_MAX_RANKS), ('seq', vp), ('err', vp)]
 
 
 STRUCTS = [Stat, Groups, ConvDesc, CodecCtx, ReduceItem, HeadDesc, GemmItem, RomDesc, ResidualDesc, AdamDesc,
            VoQueryDesc, VoMomentsDesc, VoConditionDesc, VoPrecisionDesc, GpSampleDesc,
-           VoGalerkinDesc, StepEpilogueDesc, FomDesc, RandomFieldDesc, VoSparse, DrawItem]
+           VoGalerkinDesc, StepEpilogueDesc, FomDesc, RandomFieldDesc, VoSparse, DrawItem, BnExchangeDesc]
 
 # name -> (restype, argtypes)
 SIGNATURES = {
@@ -228,7 +239,11 @@ SIGNATURES = {
     'gpi_fom_solve': (C.c_int, [C.POINTER(FomDesc), vp]),
     'gpi_random_field': (C.c_int, [C.POINTER(RandomFieldDesc), vp]),
     'gpi_randn': (C.c_int, [vp, i64, u64, vp, u64, vp]),
-    'gpi_draws': (C.c_int, [vp, C.c_int, u64, vp, vp]),
+    'gpi_draws': (C.c_int, [vp, C.c_int, vp, vp]),
+    'gpi_bn_exchange': (C.c_int, [C.POINTER(BnExchangeDesc), vp]),
+    'gpi_peer_alloc': (C.c_int, [i64, C.POINTER(vp), vp]),
+    'gpi_peer_open': (C.c_int, [vp, C.POINTER(vp)]),
+    'gpi_peer_close': (C.c_int, [vp, C.c_int]),
     'gpi_dropout_masks': (C.c_int, [vp, i64, f32, u64, vp, u64, vp]),
     'gpi_rng_advance': (C.c_int, [vp, u64, vp]),
     'gpi_stream_signal': (C.c_int, [vp, vp, vp]),

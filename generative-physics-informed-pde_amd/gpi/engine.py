@@ -710,7 +710,7 @@ class ElboEngine(object):
         run_reduce(self.reduce_enc[self.n_reduce_in:], self.ws, self.flat, sst)
 
     # ------------------------------------------------------------------ SyncBN (optional)
-    def set_sync_bn(self, allreduce, world):
+    def set_sync_bn(self, allreduce, world, exchange=None):
         """SyncBN mode (the exact-parity alternative to replica-BN): every BN
         layer normalises over the union of the ranks' batches of its codec call, as the reference does
         over its one process's batch (codec.py:164-173 in train mode).  allreduce(t): in-place SUM
@@ -723,7 +723,8 @@ class ElboEngine(object):
         with samples on some ranks only is refused).  The codec launches then go one by one (host
         hook between them); running_var's Bessel factor keeps the per-rank count (N/(N-1) for
         N = per-rank samples x pixels, >= 16384 here: a <1e-4 relative difference in the running
-        buffer only)."""
+        buffer only).  exchange: a gpi.peer.PeerExchange -- every seam in ONE launch through the ranks'
+        IPC-mapped buffers (gpi_bn_exchange GPI_BNX_PEER) instead of fold / allreduce / unfold."""
         # per-group sample counts: the encoder call (group 0), then the decoder's groups in order, and
         # the term presence flags (B_u, N_s, N_vo > 0), all summed over the ranks in ONE collective
         enc_n = [self.B_u if self.ep is not None else 0]
@@ -745,6 +746,8 @@ class ElboEngine(object):
         self.bn_global_counts = {'enc': tot[0], 'dec': tot[1:1 + len(self.dec_sizes)]}
         self.bn_sync = allreduce
         self.bn_world = int(world)
+        self.bn_exchange = exchange
+        self._bnx_msg = torch.zeros(L.GPI_BNX_MSG, dtype=torch.float64, device=dev)
 
     def _stats_view(self):
         R, G = L.GPI_REPLICAS, L.GPI_MAX_GROUPS
@@ -753,13 +756,21 @@ class ElboEngine(object):
 
     def _sync_stats(self, stat0, n, f0, kind):
         """All-reduce the replica-folded sums of stat slots [stat0, stat0 + n), fields f0, f0 + 1, scaled
-        per BN group by n_rank / N_global (set_sync_bn), back into replica 0."""
-        v = self._stats_view()
-        sub = v[:, :, stat0:stat0 + n, f0:f0 + 2].sum(0)        # replicas folded: [groups, n, 2]
-        self.bn_sync(sub)
-        sub.mul_(self.bn_scale[kind])
-        v[:, :, stat0:stat0 + n, f0:f0 + 2] = 0.0
-        v[0, :, stat0:stat0 + n, f0:f0 + 2] = sub
+        per BN group by n_rank / N_global (set_sync_bn), back into replica 0: gpi_bn_exchange FOLD, the
+        collective on the [groups, n, 2] message, UNFOLD -- or the one-shot peer form (one launch)."""
+        lib = _lib()
+        d = L.BnExchangeDesc(stats=self.ws.stats_ptr.value, n_stats=self.ws.n_stats, stat0=stat0, n=n, f0=f0,
+                             scale=self.bn_scale[kind].data_ptr(), msg=self._bnx_msg.data_ptr())
+        st = L.stream_handle()
+        if self.bn_exchange is not None:
+            self.bn_exchange.fill(d)
+            _run(lib.gpi_bn_exchange, C.byref(d), st, what='SyncBN peer exchange')
+            return
+        d.mode = L.BNX_FOLD
+        _run(lib.gpi_bn_exchange, C.byref(d), st, what='SyncBN fold')
+        self.bn_sync(self._bnx_msg[:L.GPI_MAX_GROUPS * n * 2])
+        d.mode = L.BNX_UNFOLD
+        _run(lib.gpi_bn_exchange, C.byref(d), st, what='SyncBN unfold')
 
     def _codec_kind(self, descs):
         return 'enc' if self.ep is not None and descs is self.enc_descs else 'dec'

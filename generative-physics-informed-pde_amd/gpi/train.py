@@ -51,7 +51,7 @@ class FusedElboStep(object):
 
     def __init__(self, model, X_pool, B_u, X_s=None, Y=None, F=None, lr=1e-2, betas=(0.9, 0.999), eps=1e-8,
                  seed=0, normalize=False, process_group=None, distributed=False, rank=0, world=1, subset_seed=None,
-                 graph_allreduce=True, sync_bn=False):
+                 graph_allreduce=True, sync_bn=False, bn_exchange='collective'):
         self.model = model
         self.flat = model.native_flat()
         self.N_s = 0 if X_s is None else int(X_s.shape[0])
@@ -67,10 +67,22 @@ class FusedElboStep(object):
         # default replica-BN (per-rank batch statistics, no collective in the codec).  Any distributed world
         # size, 1 included: a one-rank NCCL job runs (and captures) the same per-conv collectives as the
         # 8-GPU one (tools/dist_capture_probe.py --sync-bn)
+        # bn_exchange: 'collective' (each seam's message all-reduced over the process group: RCCL in the graph)
+        # or 'peer' (the one-shot exchange through the ranks' IPC-mapped buffers, gpi.peer: one launch per
+        # seam, any backend, capturable)
         self.sync_bn = bool(sync_bn) and bool(distributed)
+        self.bn_exchange = bn_exchange if self.sync_bn else None
+        self.handoff_flags = torch.zeros(8, dtype=torch.int32, device=self.flat.P.device)   # [0..3] flags, [4] error
+        self._peer = None
         if self.sync_bn:
             pg = process_group
-            self.engine.set_sync_bn(lambda t: dist.all_reduce(t, op=dist.ReduceOp.SUM, group=pg), self.world)
+            if bn_exchange not in ('collective', 'peer'):
+                raise ValueError("bn_exchange: 'collective' or 'peer'")
+            if bn_exchange == 'peer':
+                from .peer import PeerExchange
+                self._peer = PeerExchange(pg, err=self.handoff_flags[4:5])
+            self.engine.set_sync_bn(lambda t: dist.all_reduce(t, op=dist.ReduceOp.SUM, group=pg), self.world,
+                                    exchange=self._peer)
         dev = self.flat.P.device
         self.X_pool = X_pool.contiguous().float() if X_pool is not None else None
         self.X_s, self.Y, self.F = X_s, Y, F
@@ -151,7 +163,6 @@ class FusedElboStep(object):
         self.done_ctr = torch.zeros(1, dtype=torch.int32, device=dev)
         # side-stream hand-offs by device flags (gpi_stream_signal / gpi_stream_wait) instead of graph
         # events between the streams; GPI_HANDOFF=events keeps the events (A/B)
-        self.handoff_flags = torch.zeros(8, dtype=torch.int32, device=dev)   # [0..3] flags, [4] wait timeout
         self.handoff = os.environ.get('GPI_HANDOFF', 'flags') if self.graph_mode in ('single', 'streams') \
             else 'events'
         if self.graph_mode == 'streams' and self.handoff != 'flags':
@@ -218,17 +229,18 @@ class FusedElboStep(object):
                 for k, (c, prog) in enumerate((('enc', e.ep), ('dec', e.dp))):
                     if c in codecs and prog is not None and prog.drop_numel:
                         items.append(L.DrawItem(kind=L.DRAW_DROPOUT, p=prog.drop_rate, out=e.ws.fptr(prog.drop_off).value,
-                                                n=prog.drop_numel, sub=sub0 + 4 + k))
-            if subset and self.B_u:
+                                                n=prog.drop_numel, sub=sub0 + 4 + k, seed=self.seed))
+            if subset and self.B_u:     # (the subset's key: the seed every rank shares)
                 items.append(L.DrawItem(kind=L.DRAW_SUBSET, out=idx.data_ptr(), n=self.n_pool, k=self.n_sub,
-                                        sub=sub0 + 1))
+                                        sub=sub0 + 1, seed=self.subset_seed))
             ez = e.eps_z()
-            items.append(L.DrawItem(kind=L.DRAW_RANDN, out=ez.data_ptr(), n=ez.numel(), sub=sub0 + 2))
+            items.append(L.DrawItem(kind=L.DRAW_RANDN, out=ez.data_ptr(), n=ez.numel(), sub=sub0 + 2, seed=self.seed))
             if e.N_ex:
                 ex = e.eps_x()
-                items.append(L.DrawItem(kind=L.DRAW_RANDN, out=ex.data_ptr(), n=ex.numel(), sub=sub0 + 3))
+                items.append(L.DrawItem(kind=L.DRAW_RANDN, out=ex.data_ptr(), n=ex.numel(), sub=sub0 + 3,
+                                        seed=self.seed))
             arr = (L.DrawItem * len(items))(*items)
-            L.check(lib.gpi_draws(arr, len(items), self.seed, L.ptr(self.rng_off), st), 'step draws')
+            L.check(lib.gpi_draws(arr, len(items), L.ptr(self.rng_off), st), 'step draws')
             return
         if self.engine.has_dropout and codecs:   # Dropout2d channel scales (sub ids sub0 + 4 enc, + 5 dec)
             self.engine.draw_dropout(st, self.seed, L.ptr(self.rng_off), sub0 + 4, codecs=codecs)
@@ -355,8 +367,9 @@ class FusedElboStep(object):
         a learning-rate change reaches the device at the next replay)."""
         self.unroll = 1
         self.g_fb_k = self.g_side_k = None
-        if self.sync_bn and dist.get_backend(self.pg) != dist.Backend.NCCL:
-            raise RuntimeError('FusedElboStep.capture: SyncBN with a host-side backend (gloo) runs eagerly only')
+        if self.sync_bn and self.bn_exchange != 'peer' and dist.get_backend(self.pg) != dist.Backend.NCCL:
+            raise RuntimeError('FusedElboStep.capture: SyncBN over a host-side backend (gloo) runs eagerly only '
+                               "(bn_exchange='peer' captures with any backend)")
         torch.cuda.synchronize()
         saved = [t.clone() for t in self._mutable_state()]
         s = torch.cuda.Stream()

@@ -477,6 +477,44 @@ typedef struct gpi_bn_running_item {
 int gpi_bn_running_update(const gpi_bn_running_item* items, int n_items, int max_channels, const gpi_stat* stats,
                           int64_t n_stats, float momentum, void* stream);
 
+/* SyncBN exchange of one BN seam (the fp64 BN sums of stat slots [stat0, stat0 + n), fields f0 and f0 + 1, of
+ * every BN group; ElboEngine.set_sync_bn, codec.py:164-173 at the union batch).  One 64-thread launch:
+ *   GPI_BNX_FOLD    msg[g][c][f] = the GPI_REPLICAS copies summed in replica order (the caller all-reduces msg,
+ *                   e.g. over RCCL, then runs UNFOLD);
+ *   GPI_BNX_UNFOLD  replica 0 = msg * scale[g], the other replicas 0;
+ *   GPI_BNX_PEER    the one-shot peer all-reduce: FOLD into this rank's exchange buffer (slot seq & 1 of its two
+ *                   message slots), publish seq in its flag word, wait for every rank's flag to reach seq, sum
+ *                   the ranks' messages in rank order from their buffers (IPC-mapped: gpi_peer_alloc /
+ *                   gpi_peer_open), then UNFOLD -- no collective library, no host, graph-capturable.  *seq is
+ *                   this rank's exchange counter (every rank runs the same sequence of exchanges); a wait of
+ *                   more than ~10 s sets *err and the launch returns (the sums are then garbage, nothing hangs).
+ * n <= 8 channels (GPI_MAX_COUT).  The sum over the ranks of FOLD messages in rank order equals the RCCL path's
+ * for 2 ranks bit for bit (a + b), to rounding for more. */
+#define GPI_MAX_RANKS 16
+#define GPI_BNX_MSG 64            /* doubles per message: GPI_MAX_GROUPS x GPI_MAX_COUT x 2 */
+#define GPI_BNX_FOLD   0
+#define GPI_BNX_UNFOLD 1
+#define GPI_BNX_PEER   2
+typedef struct gpi_bn_exchange_desc {
+    gpi_stat* stats;
+    int64_t n_stats;
+    int32_t stat0, n, f0, mode;
+    const double* scale;               /* [GPI_MAX_GROUPS] n_rank / N_global per BN group */
+    double* msg;                       /* FOLD / UNFOLD: [GPI_BNX_MSG] */
+    int32_t rank, world;
+    double* peer_buf[GPI_MAX_RANKS];   /* PEER: each rank's exchange buffer, [2][GPI_BNX_MSG] doubles */
+    uint32_t* peer_flag[GPI_MAX_RANKS];/* PEER: each rank's flag word */
+    uint32_t* seq;                     /* PEER: this rank's exchange counter (device) */
+    uint32_t* err;                     /* PEER: wait timeout (sticky, like gpi_adam_desc.wait_err) */
+} gpi_bn_exchange_desc;
+int gpi_bn_exchange(const gpi_bn_exchange_desc* d, void* stream);
+/* Exchange buffers shared between the ranks' processes: gpi_peer_alloc allocates `bytes` of device memory (zeroed)
+ * and writes its IPC handle (64 bytes) to ipc_handle; gpi_peer_open maps another process's buffer from its handle;
+ * gpi_peer_close frees (own != 0) or unmaps it. */
+int gpi_peer_alloc(int64_t bytes, void** ptr, void* ipc_handle);
+int gpi_peer_open(const void* ipc_handle, void** ptr);
+int gpi_peer_close(void* ptr, int own);
+
 /* Partial-slab rows a conv backward launch writes: 4 per workgroup (one per wave). */
 int gpi_conv_blocks(const gpi_conv_desc* op, const gpi_groups* groups, int32_t* blocks);
 /* Launch geometry of one conv pass (fwd != 0: forward) for tuning / profiling tools:
@@ -640,8 +678,9 @@ typedef struct gpi_draw_item {
     int64_t n;                 /* values (randn, dropout) or pool size (subset) */
     int64_t k;                 /* subset size */
     uint64_t sub;              /* Philox sub stream */
+    uint64_t seed;             /* Philox key (the subset's: the seed shared by every rank) */
 } gpi_draw_item;
-int gpi_draws(const gpi_draw_item* items, int n_items, uint64_t seed, const uint64_t* offset, void* stream);
+int gpi_draws(const gpi_draw_item* items, int n_items, const uint64_t* offset, void* stream);
 int gpi_randn(float* out, int64_t n, uint64_t seed, const uint64_t* offset, uint64_t sub, void* stream);
 int gpi_rng_advance(uint64_t* offset, uint64_t by, void* stream);
 /* Dropout2d channel scales (nn.Dropout2d train mode, codec.py:177-178): out[i] = 0 with

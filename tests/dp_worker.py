@@ -213,8 +213,49 @@ def run_timeout(out):
     dist.destroy_process_group()
 
 
+def run_peer(out):
+    """SyncBN through the one-shot peer exchange (gpi.peer, IPC-mapped buffers of the two ranks' processes on
+    the box's GPU): three eager steps with bn_exchange='collective' (fold / gloo all-reduce / unfold), three
+    eager steps with 'peer', and three captured-graph replays with 'peer' (the exchange kernels spinning on
+    the other process's flags inside the graph), each from the same initial state; records the parameters."""
+    from gpi.train import FusedElboStep
+    from elbo_ref import load
+    rank, world = int(os.environ['RANK']), int(os.environ['WORLD_SIZE'])
+    torch.cuda.set_device(0)
+    dist.init_process_group('gloo')
+    d = load('elbo_c32.npz')
+    rec = {}
+    for tag, exch, cap in (('coll', 'collective', False), ('peer', 'peer', False), ('peer_graph', 'peer', True)):
+        model, _ = shard_model(d, rank)
+        ds = model._datasets['supervised']
+        Xu = torch.tensor(d['Xu'], device='cuda')
+        st = FusedElboStep(model, Xu, B_U, ds.get('X'), ds.get('Y'), ds.get('F_ROM_BC'), lr=1e-3, seed=50 + rank,
+                           subset_seed=9, distributed=True, rank=rank, world=world, sync_bn=True, bn_exchange=exch)
+        assert st.sync_bn and (st._peer is not None) == (exch == 'peer')
+        if cap:
+            st.capture()
+        for _ in range(3):
+            if cap:
+                st.step()
+            else:
+                st.step_eager()
+        torch.cuda.synchronize()
+        st.check_handoff()
+        rec[tag] = st.flat.P.cpu().numpy()
+        rec[tag + '.elbo'] = np.float64(st.elbo().item())
+        rec['n_shared'] = np.int64(st.flat.n_shared)
+        if st._peer is not None:
+            rec[tag + '.seq'] = np.int64(st._peer.seq.item())
+        dist.barrier()
+    np.savez(os.path.join(out, 'rank%d.npz' % rank), **rec)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 if __name__ == '__main__':
-    if len(sys.argv) > 2 and sys.argv[2] == 'c64sync':
+    if len(sys.argv) > 2 and sys.argv[2] == 'peer':
+        run_peer(sys.argv[1])
+    elif len(sys.argv) > 2 and sys.argv[2] == 'c64sync':
         run_c64_sync(sys.argv[1])
     elif len(sys.argv) > 2 and sys.argv[2] == 'timeout':
         run_timeout(sys.argv[1])

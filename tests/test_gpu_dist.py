@@ -304,3 +304,27 @@ def test_dp_hand_off_timeout_on_one_rank_stops_every_rank(device, tmp_path):
         assert int(rk[i]['err_word']) == 1, i              # rank 1: its wait; rank 0: set by its Adam
         assert int(rk[i]['P_same']) == 1 and int(rk[i]['mv_same']) == 1, i
         assert int(rk[i]['raised']) == 1, i
+
+
+def test_sync_bn_peer_exchange_two_ranks(device, tmp_path):
+    """The throughput SyncBN exchange (gpi_bn_exchange GPI_BNX_PEER through the ranks' IPC-mapped buffers: one
+    launch per BN seam, no collective call) with two ranks' processes on the box's GPU: three eager SyncBN steps
+    equal the collective form's (fold / gloo all-reduce / unfold) bit for bit -- the two-rank sum a + b either
+    way -- and three replays of the captured step graph (the exchange kernels spinning on the other process's
+    flags inside the graph) equal the eager peer steps bit for bit; the ranks' replicated parameters stay
+    identical.  (codec.py:164-173 at the union batch.)"""
+    env = dict(os.environ)
+    env['PYTHONUNBUFFERED'] = '1'
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node=2',
+           '--master-addr=127.0.0.1', '--master-port=%d' % _free_port(), os.path.join(HERE, 'dp_worker.py'),
+           str(tmp_path), 'peer']
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    rk = [dict(np.load(str(tmp_path / ('rank%d.npz' % i)))) for i in range(2)]
+    for i in range(2):
+        assert np.array_equal(rk[i]['peer'], rk[i]['coll']), i
+        assert np.array_equal(rk[i]['peer_graph'], rk[i]['peer']), i
+        assert rk[i]['peer.elbo'] == rk[i]['coll.elbo']
+        assert int(rk[i]['peer.seq']) > 0 and int(rk[i]['peer_graph.seq']) > 0
+    ns = int(rk[0]['n_shared'])
+    assert ns > 0 and np.array_equal(rk[0]['peer'][:ns], rk[1]['peer'][:ns])

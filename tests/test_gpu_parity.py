@@ -417,20 +417,21 @@ def test_step_draws_one_launch_matches_separate_launches(device, n, k):
     a = dict(idx=torch.full((k,), -1, dtype=torch.int32, device='cuda'), z=torch.full((nz,), 7.0, device='cuda'),
              x=torch.full((nx,), 7.0, device='cuda'), d=torch.full((nd,), 7.0, device='cuda'))
     b = {kk: v.clone() for kk, v in a.items()}
-    items = [L.DrawItem(kind=L.DRAW_DROPOUT, p=0.2, out=a['d'].data_ptr(), n=nd, sub=5),
-             L.DrawItem(kind=L.DRAW_SUBSET, out=a['idx'].data_ptr(), n=n, k=k, sub=1),
-             L.DrawItem(kind=L.DRAW_RANDN, out=a['z'].data_ptr(), n=nz, sub=2),
-             L.DrawItem(kind=L.DRAW_RANDN, out=a['x'].data_ptr(), n=nx, sub=3)]
+    sseed = 24680                        # the subset's own key (FusedElboStep: the seed shared by the ranks)
+    items = [L.DrawItem(kind=L.DRAW_DROPOUT, p=0.2, out=a['d'].data_ptr(), n=nd, sub=5, seed=seed),
+             L.DrawItem(kind=L.DRAW_SUBSET, out=a['idx'].data_ptr(), n=n, k=k, sub=1, seed=sseed),
+             L.DrawItem(kind=L.DRAW_RANDN, out=a['z'].data_ptr(), n=nz, sub=2, seed=seed),
+             L.DrawItem(kind=L.DRAW_RANDN, out=a['x'].data_ptr(), n=nx, sub=3, seed=seed)]
     arr = (L.DrawItem * len(items))(*items)
-    L.check(lib.gpi_draws(arr, len(items), seed, L.ptr(o), st), 'draws')
+    L.check(lib.gpi_draws(arr, len(items), L.ptr(o), st), 'draws')
     L.check(lib.gpi_dropout_masks(L.ptr(b['d']), nd, 0.2, seed, L.ptr(o), 5, st), 'masks')
-    L.check(lib.gpi_random_subset(L.ptr(b['idx']), n, k, seed, L.ptr(o), 1, st), 'subset')
+    L.check(lib.gpi_random_subset(L.ptr(b['idx']), n, k, sseed, L.ptr(o), 1, st), 'subset')
     L.check(lib.gpi_randn(L.ptr(b['z']), nz, seed, L.ptr(o), 2, st), 'randn z')
     L.check(lib.gpi_randn(L.ptr(b['x']), nx, seed, L.ptr(o), 3, st), 'randn x')
     torch.cuda.synchronize()
     for kk in a:
         assert torch.equal(a[kk], b[kk]), kk
-    assert np.array_equal(a['idx'].cpu().numpy(), random_subset(n, k, seed, 1 << 33, 1))
+    assert np.array_equal(a['idx'].cpu().numpy(), random_subset(n, k, sseed, 1 << 33, 1))
     assert set(torch.unique(a['d']).tolist()) <= {0.0, 1.25}
 
 
