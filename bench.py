@@ -408,7 +408,11 @@ def main():
     ap.add_argument('--no-roofline', action='store_true')
     ap.add_argument('--kprof', default=None, help='write the per-operator HIP-event profile (JSON) here')
     ap.add_argument('--sync-bn', action='store_true',
-                    help='SyncBN: BN statistics over the union of the ranks\' batches (N > 1; default replica-BN)')
+                    help='SyncBN: BN statistics over the union of the ranks\' batches (default replica-BN; at N = 1 '
+                         'a one-rank process group, to time the exchange)')
+    ap.add_argument('--bn-exchange', default='collective', choices=['collective', 'peer'],
+                    help="SyncBN seams: 'collective' (fold / RCCL all-reduce / unfold) or 'peer' (one-shot exchange "
+                         'through IPC-mapped buffers, one launch per seam)')
     args = ap.parse_args()
     dbg = sorted(k for k in os.environ if k.startswith('GPI_DBG_') or k == 'GPI_PHASE_TIMING')
     if dbg:
@@ -428,7 +432,7 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
-    distributed = world > 1
+    distributed = world > 1 or args.sync_bn
     # GPI_BENCH_BACKEND=gloo: rehearsal of the N > 1 path with every rank on the visible GPU(s)
     # (ranks share a device; RCCL refuses that).  The driver's multi-GPU runs use RCCL ('nccl').
     backend = os.environ.get('GPI_BENCH_BACKEND', 'nccl')
@@ -436,10 +440,17 @@ def main():
         local = local % torch.cuda.device_count()
     if distributed:
         torch.cuda.set_device(local)
+        kw = {}
+        if 'MASTER_ADDR' not in os.environ:          # --sync-bn at N = 1 without torchrun: a one-rank group
+            import socket
+            sk = socket.socket()
+            sk.bind(('127.0.0.1', 0))
+            kw = dict(init_method='tcp://127.0.0.1:%d' % sk.getsockname()[1], rank=0, world_size=1)
+            sk.close()
         if backend == 'nccl':
-            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local), **kw)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, **kw)
     device = torch.device('cuda', local)
     torch.cuda.set_device(device)
 
@@ -453,8 +464,9 @@ def main():
     # between two graphs, as with gloo)
     step = FusedElboStep(model, Xu, B_u, Xs, Y, F, lr=1e-2, seed=4321 + rank, subset_seed=777,
                          distributed=distributed, rank=rank, world=world,
-                         graph_allreduce=os.environ.get('GPI_GRAPH_ALLREDUCE', '1') == '1', sync_bn=args.sync_bn)
-    if not args.no_graph and not (step.sync_bn and backend != 'nccl'):
+                         graph_allreduce=os.environ.get('GPI_GRAPH_ALLREDUCE', '1') == '1', sync_bn=args.sync_bn,
+                         bn_exchange=args.bn_exchange)
+    if not args.no_graph and not (step.sync_bn and backend != 'nccl' and args.bn_exchange != 'peer'):
         step.capture(unroll=args.unroll)
     log('captured (graph mode %s, %d step(s) per replay); warm-up' % (step.graph_mode, step.unroll))
     step.run(args.warmup)
@@ -555,7 +567,7 @@ def main():
                        'world': world, 'backend': backend if distributed else None,
                        'allreduce': None if not distributed else
                        ('host-side between graphs' if args.no_graph or getattr(step, 'split_graph', True) else 'in-graph'),
-                       'bn': 'replica' if not getattr(step, 'sync_bn', False) else 'sync'},
+                       'bn': 'replica' if not getattr(step, 'sync_bn', False) else 'sync (%s exchange)' % step.bn_exchange},
             'elbo_last': elbo,
             'host_enqueue_ms_per_step': round(1e3 * (t_enq - t0) / args.steps, 4),
             'roofline': roof,

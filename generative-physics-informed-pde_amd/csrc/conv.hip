@@ -54,8 +54,11 @@ __device__ __forceinline__ int dq(int e, Div v) { return v.one ? e : (int)__umul
 // shader clock at phase boundary i to g_phase[b % 4096][i], the 100 MHz real-time
 // clock at entry / exit to g_rt[b % 4096][0 / 1].  Compiled out of the product.
 #ifdef GPI_PHASE_TIMING
-__device__ unsigned long long g_phase[4096 * 16];
-__device__ unsigned long long g_rt[4096 * 2];
+// (hidden visibility: the stamps address the arrays PC-relative -- as default-visibility symbols of a -fPIC
+// library each stamp loaded the address from the GOT first, one scalar-load round trip per stamp that
+// inflated every measured phase by ~0.5-1 k cycles, r06)
+__device__ __attribute__((visibility("hidden"))) unsigned long long g_phase[4096 * 16];
+__device__ __attribute__((visibility("hidden"))) unsigned long long g_rt[4096 * 2];
 #define PHASE(i)                                                                                     \
     do {                                                                                             \
         if (threadIdx.x == 0) g_phase[(blockIdx.x & 4095) * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
