@@ -22,6 +22,14 @@ using namespace gpi;
 
 namespace {
 
+// the log effective property of sample row `row` (x rows at d.x_stride), element t: stored, or drawn here
+// from q_X (x_draw: the head's fmaf(expf(logsigma), eps, mu), so both hold the same value)
+__device__ __forceinline__ float rom_x(const gpi_rom_desc& d, int64_t row, int t) {
+    const int64_t o = row * d.x_stride + t;
+    if (d.x_draw) return fmaf(expf(d.x_ls[o]), d.x_eps[o], d.x_mu[o]);
+    return d.x[o];
+}
+
 // Phase stamps of the timing build (make timing; tools/rom_probe.py): thread 0 of workgroup b writes
 // the shader clock at phase boundary i to g_rom_phase[b % 256][i].  Compiled out of the product.
 #ifdef GPI_PHASE_TIMING
@@ -214,13 +222,13 @@ __global__ __launch_bounds__(ROM_NT) void rom_kernel(gpi_rom_desc d, RomDims D) 
     const int s = blockIdx.x;
     const int tid = threadIdx.x, NT = ROM_NT;
     const int nc = D.nc;
-    const float* x = d.x + (int64_t)s * d.x_stride;
     const float* F = d.F + (int64_t)s * D.nn;
     RPHASE(0);
 
     bool bad = false;
     for (int t = tid; t < D.nT; t += NT) {
-        const float kv = d.input_kappa ? x[t] : expf(x[t]) + 1e-8f;
+        const float xv = rom_x(d, s, t);
+        const float kv = d.input_kappa ? xv : expf(xv) + 1e-8f;
         bad |= !(kv > 1e-12f);
         kp[t] = kv;
     }
@@ -543,7 +551,6 @@ __global__ __launch_bounds__(NT) void rom_kernel_fast(gpi_rom_desc d, RomDims D)
     double* lred = du + NN;           // [NW]
     const int s = blockIdx.x;
     const int tid = threadIdx.x;
-    const float* x = d.x + (int64_t)s * d.x_stride;
     const float* F = d.F + (int64_t)s * NN;
     const int nf = D.n, r = D.r;
     RPHASE(0);
@@ -570,7 +577,8 @@ __global__ __launch_bounds__(NT) void rom_kernel_fast(gpi_rom_desc d, RomDims D)
     }
     bool bad = false;
     for (int t = tid; t < NT2; t += NT) {
-        const float kv = d.input_kappa ? x[t] : expf(x[t]) + 1e-8f;
+        const float xv = rom_x(d, s, t);
+        const float kv = d.input_kappa ? xv : expf(xv) + 1e-8f;
         bad |= !(kv > 1e-12f);
         kp[t] = kv;
     }
@@ -780,10 +788,9 @@ __global__ __launch_bounds__(64) void rom_lane_kernel(gpi_rom_desc d) {
     const int s = blockIdx.x * 64 + lane;
     const bool act = s < d.n;
     const int sc = act ? s : 0;
-    const float* __restrict__ x = d.x + (int64_t)sc * d.x_stride;
     const float* __restrict__ F = d.F + (int64_t)sc * NN;
     auto kap = [&](int I, int J, int ul) -> float {
-        const float v = x[2 * (I + NC * J) + ul];
+        const float v = rom_x(d, sc, 2 * (I + NC * J) + ul);
         return d.input_kappa ? v : expf(v) + 1e-8f;
     };
     auto ch = [&](int I, int J) -> float {        // horizontal edge (I,J)-(I+1,J)
@@ -801,7 +808,7 @@ __global__ __launch_bounds__(64) void rom_lane_kernel(gpi_rom_desc d) {
     bool bad = false;
 #pragma unroll
     for (int t = 0; t < 2 * NC * NC; ++t) {
-        const float v = x[t];
+        const float v = rom_x(d, sc, t);
         bad |= !((d.input_kappa ? v : expf(v) + 1e-8f) > 1e-12f);
     }
     if (act && bad && d.flag) atomicOr(d.flag, 1);

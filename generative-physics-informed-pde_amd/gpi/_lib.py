@@ -99,10 +99,11 @@ class GemmItem(C.Structure):
 
 
 class RomDesc(C.Structure):
-    _fields_ = [('nc', i32), ('refine', i32), ('n', i32), ('mode', i32), ('input_kappa', i32), ('_pad', i32),
+    _fields_ = [('nc', i32), ('refine', i32), ('n', i32), ('mode', i32), ('input_kappa', i32), ('x_draw', i32),
                 ('x', vp), ('x_stride', i64), ('F', vp), ('mu_y', vp), ('Y', vp), ('logsig_y', vp),
                 ('loss_scale', f32), ('gx_accumulate', i32), ('dmu', vp), ('duc', vp), ('gx', vp), ('gx_stride', i64),
-                ('gacc_logsig', vp), ('loss_acc', vp), ('flag', vp), ('uc', vp), ('gls_part', vp)]
+                ('gacc_logsig', vp), ('loss_acc', vp), ('flag', vp), ('uc', vp), ('gls_part', vp),
+                ('x_mu', vp), ('x_ls', vp), ('x_eps', vp)]
 
 
 CGR_AUTO, CGR_BAND, CGR_STREAM, CGR_GENERAL = 0, 1, 2, 3

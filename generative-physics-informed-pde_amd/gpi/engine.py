@@ -390,6 +390,13 @@ class ElboEngine(object):
             r.logsig_y = flat.P.data_ptr() + 4 * flat.offset(g.logsigmas_y)
             r.loss_scale = scale
             r.gx_accumulate = 0
+            if self.rom_draw:
+                # the ROM draws its X~ rows from q_X itself (no wait on the head forward's xs)
+                qx = model.q_X['supervised' if slot == T_LOGL_Y else 'vo']
+                r.x_draw = 1
+                r.x_mu = flat.P.data_ptr() + 4 * flat.offset(qx._mean)
+                r.x_ls = flat.P.data_ptr() + 4 * flat.offset(qx._logsigma)
+                r.x_eps = ws.fptr(hb['eps_x'] + row0 * d_x).value
             r.gx = ws.fptr(hb['gxs'] + row0 * d_x).value
             r.gx_stride = d_x
             r.gacc_logsig = flat.gacc.data_ptr() + 8 * flat.offset(g.logsigmas_y)
@@ -407,7 +414,9 @@ class ElboEngine(object):
             return r
 
         self.rom_reduce = []
-
+        # GPI_ROM_EARLY=1 (free q_X only): the fused step's ROM runs at the very start of the step on
+        # the side stream, its inputs drawn from q_X in the kernel, concurrently with the encoder
+        self.rom_draw = os.environ.get('GPI_ROM_EARLY', '0') == '1' and not self.lockx
         self.roms = []
         self.rom = self.rom_vo = None
         if self.N_s > 0:
@@ -442,6 +451,7 @@ class ElboEngine(object):
         # two others, r03: kept 'forward')
         self.rom_at = os.environ.get('GPI_ROM_AT', 'forward')
         self._rom_deferred = False
+        self.rom_early_launched = False
         self._pending_sig = None       # hand-off flag the next main-stream codec call signals
         # callable(side stream handle) launched on the side stream ahead of the ROM (fused step)
         self.side_pre = None
@@ -577,12 +587,21 @@ class ElboEngine(object):
             else:
                 self._ev_start.record(torch.cuda.current_stream())
                 self._side.wait_event(self._ev_start)
+        # early ROM: after the side gate (the previous step's update and epilogue -- q_X, eps_x, the
+        # cleared term scratch -- are complete); needs the gate and a scratch this forward does not clear
+        early = (self.rom_draw and bool(self.roms) and self.side_done is not None and not zero_scratch
+                 and not (self.rom_at == 'backward' and not compute_value))
+        self.rom_early_launched = early
+        if early:
+            self.rom_side(C.c_void_p(self._side.cuda_stream))
+            self._ev_join.record(self._side)
+            self._pending_join = True
         self.forward_a(st, zero_gacc, zero_scratch)
         # rom_at 'backward': the ROM follows the backward's fork on the side stream (ahead of the
         # variational samples' head backward that needs it) -- one cross-stream dependency less per
         # step; only when the value is not read right after the forward
         self._rom_deferred = bool(self.roms) and self.rom_at == 'backward' and not compute_value
-        if self.roms and not self._rom_deferred:
+        if self.roms and not self._rom_deferred and not early:
             # the ROM solve only feeds the head backward: run it on a side stream,
             # concurrently with the decoder (fork here, join in backward / value).  The decoder
             # is enqueued first so that, in a captured graph, the main chain is the fork's first
@@ -596,7 +615,7 @@ class ElboEngine(object):
             if self.rom_first:
                 self._launch_roms()
         self.forward_b(st)
-        if self.roms and not self.rom_first and not self._rom_deferred:
+        if self.roms and not self.rom_first and not self._rom_deferred and not early:
             self._launch_roms()
         if running == 'now':
             self.running.launch(st)

@@ -215,7 +215,8 @@ typedef struct gpi_gemm_item {
 typedef struct gpi_rom_desc {
     int32_t nc, refine, n, mode;
     int32_t input_kappa;       /* 1: x holds kappa itself (ROM.__call__), 0: log effective property */
-    int32_t _pad;
+    int32_t x_draw;            /* 1: x is drawn here, x = x_mu + exp(x_ls) x_eps element-wise (the q_X sample of
+                                  components.py:167-172, the same fmaf as the head's), rows at x_stride */
     const float* x;            /* [n, 2 nc^2] log effective property */
     int64_t x_stride;
     const float* F;            /* [n, (nc+1)^2] F_ROM_BC */
@@ -235,6 +236,9 @@ typedef struct gpi_rom_desc {
     float* gls_part;           /* optional [n, d_y] (LOGLIK): per-sample d/d logsigma_y contributions written with
                                   plain stores instead of the fp64 atomics into gacc_logsig (32 x 4095 same-address
                                   atomics per C64 step); the caller reduces the n rows (gpi_wgrad_reduce item) */
+    const float* x_mu;         /* x_draw: [n, 2 nc^2] q_X means, log-sigmas and noise */
+    const float* x_ls;
+    const float* x_eps;
 } gpi_rom_desc;
 
 /* Coarse-grained residual on the fine grid (VirtualObservables CGR query,

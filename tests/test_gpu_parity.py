@@ -642,6 +642,36 @@ def test_flag_handoff_matches_event_handoff(device, monkeypatch):
     assert int(fl.handoff_flags[0].item()) == 4        # the tag of the last step (counter 3, + 1)
 
 
+def test_early_rom_matches_rom_after_head_forward(device, monkeypatch):
+    """GPI_ROM_EARLY=1: the captured step's ROM draws X~ = mu + exp(logsigma) eps from q_X in the kernel
+    and runs at the start of the step on the side stream (before the encoder) instead of after the
+    head forward; the step leaves bit for bit what the default order leaves over four replays."""
+    import copy
+    from gpi.train import FusedElboStep
+    d = load('elbo_c32.npz')
+    model_a, bs = build_golden_model(d)
+    model_b = copy.deepcopy(model_a)
+    Xu, Xs, Y, F = cuda(d['Xu']), cuda(d['Xs']), cuda(d['Y']), cuda(d['F'])
+    monkeypatch.setenv('GPI_GRAPH_MODE', 'streams')
+    late = FusedElboStep(model_a, Xu, bs, Xs, Y, F, lr=1e-3, seed=3)
+    monkeypatch.setenv('GPI_ROM_EARLY', '1')
+    early = FusedElboStep(model_b, Xu, bs, Xs, Y, F, lr=1e-3, seed=3)
+    if early.graph_mode != 'streams':
+        pytest.skip('the stream pair shares a hardware queue here: no side step gate (graph mode single)')
+    assert early.engine.rom_draw and not late.engine.rom_draw
+    late.capture()
+    early.capture()
+    assert early.engine.rom_early_launched and not late.engine.rom_early_launched
+    for _ in range(4):
+        late.step()
+        early.step()
+    torch.cuda.synchronize()
+    early.check_handoff()
+    for a, b in ((late.flat.P, early.flat.P), (late.m, early.m), (late.v, early.v),
+                 (late.last_terms, early.last_terms), (late.step_ctr, early.step_ctr)):
+        assert torch.equal(a, b)
+
+
 def test_unrolled_graph_matches_single_steps(device):
     """capture(unroll=3) + run(7) (two replays of the 3-step graph pair, then one single step) leaves
     exactly what seven step() replays leave: parameters, Adam moments, counters, subsets, flags."""
