@@ -28,20 +28,36 @@ def main():
     e = step.engine
     lib = L.lib()
     st = L.stream_handle()
+    found = []
     for prog, descs, ctx in ((e.ep, e.enc_descs, e.ectx), (e.dp, e.dec_descs, e.dctx)):
         for i, op in enumerate(prog.ops):
-            if pat not in op.name:
-                continue
             fn = lib.gpi_conv_forward if which == 'fwd' else lib.gpi_conv_backward
             if prog is e.dp and i == e.n_dec_sep and e.n_dec_sep < len(e.dec_descs) and which != 'fwd':
                 fn = lib.gpi_conv_loss_fused          # the decoder output conv runs fused in the step
-            t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            t0.record()
-            for _ in range(reps):
-                L.check(fn(C.byref(descs[i]), C.byref(ctx), st), op.name)
-            t1.record()
-            torch.cuda.synchronize()
-            print('%s.%s  %.2f us/launch' % (op.name, which, 1e3 * t0.elapsed_time(t1) / reps))
+            found.append((op.name, fn, descs[i], ctx))
+
+    def timed(launches):
+        t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        for name, fn, d, ctx in launches:            # warm
+            L.check(fn(C.byref(d), C.byref(ctx), st), name)
+        t0.record()
+        for _ in range(reps):
+            for name, fn, d, ctx in launches:
+                L.check(fn(C.byref(d), C.byref(ctx), st), name)
+        t1.record()
+        torch.cuda.synchronize()
+        return 1e3 * t0.elapsed_time(t1) / reps
+
+    sel = [f for f in found if pat in f[0]]
+    for f in sel:
+        print('%s.%s  %.2f us/launch' % (f[0], which, timed([f])))
+    # KPROBE_OTHER=substring: the selected op alone, the other alone, and the two alternating (a per-launch cost
+    # that only the alternation shows -- cold instruction cache, evicted operands -- is the pair's excess)
+    other = os.environ.get('KPROBE_OTHER')
+    if other and sel:
+        o = [f for f in found if other in f[0]][0]
+        a, b, ab = timed([sel[0]]), timed([o]), timed([sel[0], o])
+        print('alone %s %.2f  %s %.2f  alternating pair %.2f  excess %.2f us' % (sel[0][0], a, o[0], b, ab, ab - a - b))
 
 
 if __name__ == '__main__':

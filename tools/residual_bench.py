@@ -10,8 +10,9 @@ Fields resident in HBM, HIP events on the launch stream, 20 launches averaged (a
 `traffic`: HBM bytes per launch from the PMC passes of tools/r05_residual_pmc.sh (FETCH_SIZE / WRITE_SIZE,
 (2 FETCH + WRITE) x 1 KiB on gfx950), taken from profiles/*residual_traffic*.json only when the sha1 of
 csrc/stencil.hip + csrc/common.h recorded there is the current one (else null).
-CPU baseline ("port", oracle.fem): the same residual per field with scipy.sparse (K assembled from kappa,
-K_f yhat restricted by W^T) on one host core, a bounded sample of fields -- the reference assembles Gamma
+CPU baseline ("port", oracle.fem): the reference path per field -- FE assembly of K from kappa plus the residual
+W^T (K yhat - f), scipy.sparse -- on 16 single-threaded host processes (the step baseline's 16 cores), a bounded
+sample of fields -- the reference assembles Gamma
 with FEniCS per VO sample (physics/LinearElliptic.py:137-159) and evaluates Gamma y - alpha
 (VirtualObservables.py:990), which is slower still.
 """
@@ -63,18 +64,41 @@ def launch(lk, y, bc, nc, r, rf):
     L.check(L.lib().gpi_cgr_residual(C.byref(d), L.stream_handle()), 'cgr residual')
 
 
-def cpu_port(lk, y, bc, nc, n_fields):
-    """scipy.sparse restatement of one CGR residual per field (oracle-style, 1 core); seconds per field."""
+_W = {}
+
+
+def _cpu_init(n, nc):
+    os.environ['OMP_NUM_THREADS'] = '1'
     from oracle import fem
-    n = lk.shape[-1]
     mf = fem.unit_square_mesh(n)
-    mc = fem.unit_square_mesh(nc)
-    W = fem.prolongation_free(mc, mf)
-    t0 = time.perf_counter()
-    for f in range(n_fields):
+    _W['mf'], _W['W'] = mf, fem.prolongation_free(fem.unit_square_mesh(nc), mf)
+
+
+def _cpu_fields(args):
+    """CGR residuals of a chunk of fields in one worker (oracle.fem, scipy.sparse, one thread)."""
+    from oracle import fem
+    lk, y, bc = args
+    mf, W = _W['mf'], _W['W']
+    for f in range(lk.shape[0]):
         K, fe = fem.assemble_system(mf, np.exp(fem.image_to_cells(lk[f])), bc[f])
         _ = W.T @ (K @ y[f] - fe)
-    return (time.perf_counter() - t0) / n_fields
+    return lk.shape[0]
+
+
+def cpu_port(lk, y, bc, nc, workers):
+    """The reference path per field -- FE assembly of K from kappa, then W^T (K yhat - f) (oracle.fem restates
+    LinearElliptic.py:137-159 + VirtualObservables.py:990 with scipy.sparse) -- over `workers` host processes
+    of one thread each, the fields split evenly; fields per second of wall time (pool warmed first)."""
+    import concurrent.futures as cf
+    import multiprocessing as mp
+    n = lk.shape[-1]
+    chunks = [(lk[i::workers], y[i::workers], bc[i::workers]) for i in range(workers)]
+    with cf.ProcessPoolExecutor(workers, mp_context=mp.get_context('spawn'), initializer=_cpu_init,
+                                initargs=(n, nc)) as ex:
+        list(ex.map(_cpu_fields, [(c[0][:1], c[1][:1], c[2][:1]) for c in chunks]))      # warm every worker
+        t0 = time.perf_counter()
+        done = sum(ex.map(_cpu_fields, chunks))
+        return done / (time.perf_counter() - t0)
 
 
 def main():
@@ -84,6 +108,7 @@ def main():
     dev = torch.device('cuda', 0)
     tr, tr_file = traffic_entries()
     res = []
+    samples = {}
     for n, nc, N in CONFIGS:
         g = torch.Generator(device='cpu').manual_seed(n)
         lk = (0.8 * torch.randn(N, n, n, generator=g)).to(dev)
@@ -91,14 +116,6 @@ def main():
         bc = (torch.rand(N, 4, generator=g) - 0.5).to(dev)
         r = torch.empty(N, (nc + 1) ** 2, device=dev)
         rf = torch.empty(N, 2 * nc * nc, device=dev)
-        cpu = None
-        if n <= 128 and '--no-cpu' not in sys.argv:
-            ncpu = (2 if quick else 24) if n == 64 else (1 if quick else 3)
-            s = cpu_port(lk[:ncpu].cpu().numpy().astype(np.float64), y[:ncpu].cpu().numpy().astype(np.float64),
-                         bc[:ncpu].cpu().numpy().astype(np.float64), nc, ncpu)
-            cpu = dict(value=round(1.0 / s, 3), unit='fields/s', cores=1, kind='port',
-                       sample='%d fields of the %d^2 batch: oracle.fem scipy.sparse assembly + K yhat - f, W^T, '
-                              '1 host core' % (ncpu, n))
         for flux in (False, True):
             launch(lk, y, bc, nc, r, rf if flux else None)
             torch.cuda.synchronize()
@@ -121,9 +138,27 @@ def main():
                                                         algorithmic_bytes=byt,
                                                         traffic=round(te['traffic_bytes']) if te else None,
                                                         traffic_file=tr_file if te else None),
-                        cpu_baseline=cpu)
+                        cpu_baseline=None)
             res.append(line)
-            print(json.dumps(line), flush=True)
+        if n <= 128:
+            samples[n] = (lk[:512].cpu().numpy().astype(np.float64), y[:512].cpu().numpy().astype(np.float64),
+                          bc[:512].cpu().numpy().astype(np.float64), nc)
+    # CPU baselines after every GPU measurement (the worker pool stays off the host while kernels are timed)
+    for n, (lk, y, bc, nc) in samples.items():
+        if '--no-cpu' in sys.argv:
+            continue
+        # the same 16 host cores as the step's CPU baseline (bench.py), one single-threaded process each
+        workers = 16
+        ncpu = workers * ((2 if quick else 24) if n == 64 else (1 if quick else 3))
+        fps = cpu_port(lk[:ncpu], y[:ncpu], bc[:ncpu], nc, workers)
+        cpu = dict(value=round(fps, 2), unit='fields/s', cores=workers, kind='port',
+                   sample='%d fields of the %d^2 batch, reference-path FE assembly + residual W^T (K yhat - f) '
+                          '(oracle.fem, scipy.sparse), %d single-threaded host processes' % (ncpu, n, workers))
+        for line in res:
+            if line['grid'] == n:
+                line['cpu_baseline'] = cpu
+    for line in res:
+        print(json.dumps(line), flush=True)
     if out:
         with open(out, 'w') as fh:
             json.dump(res, fh, indent=1)
