@@ -357,11 +357,11 @@ def step_bytes(model, B_u, N_s, physics):
 
 
 def conv_source_sha():
-    """sha1 of csrc/conv.hip + csrc/common.h (the conv kernels' sources): PMC traffic figures are only
-    used for the code they were measured on."""
+    """sha1 of csrc/conv.hip + csrc/common.h (+ csrc/conv_shapes.h, the compile-time shapes, from r06): the
+    conv kernels' sources.  PMC traffic figures are only used for the code they were measured on."""
     import hashlib
     h = hashlib.sha1()
-    for f in ('conv.hip', 'common.h'):
+    for f in ('conv.hip', 'common.h', 'conv_shapes.h'):
         with open(os.path.join(PKG, 'csrc', f), 'rb') as fh:
             h.update(fh.read())
     return h.hexdigest()

@@ -25,6 +25,10 @@
 #include <stdlib.h>
 #include <stdio.h>
 #include <algorithm>
+#include <string.h>
+#include <string>
+#include <utility>
+#include <vector>
 
 using namespace gpi;
 
@@ -381,6 +385,96 @@ bool conv_geom(const gpi_conv_desc& d, const gpi_groups& g, ConvGeom& G, bool fw
         }
     }
     return true;
+}
+
+// ---------------------------------------------------------------------------------- compile-time shapes
+// Every conv launch of the C64 step has a fixed shape: the kernel variant, the B-independent fields of the
+// descriptor and the whole tile geometry (ConvGeom less the batch-dependent block counts).  conv_shapes.h
+// (written by tools/gen_conv_shapes.py from the launches one step makes) lists them; a launch whose shape
+// equals an entry runs the instantiation with SHP = that entry, which overwrites its by-value descriptor
+// and geometry with the entry's constants at entry (fold_shape): the address arithmetic, the staging
+// loops' trip counts and carries, the magic divisions and the variant branches fold to constants, and the
+// argument block no longer needs SGPRs (40 v_writelane spills and ~1200 instructions
+// before the first barrier of conv_bwd_kernel<3,1,0>).  Any other launch -- another grid, batch, tile
+// override -- takes the generic instantiation (SHP = -1); GPI_CONV_SHAPES=0 forces it (A/B, tests).
+#define SHAPE_D(X) X(k) X(stride) X(pad) X(upsample) X(cin) X(cout) X(h_in) X(w_in) X(h_out) X(w_out) \
+    X(in_bn) X(gout_mode) X(epilogue) X(gin_accumulate)
+#define SHAPE_G(X) X(th) X(tiles) X(rh) X(P) X(gh) X(PG) X(ph) X(zreg) X(npx) X(cg) X(fuse) X(vsum) X(vshift) \
+    X(ucls) X(lsum) X(split) X(xcd) X(alt) X(in_sq) X(in_sr) X(in_sc) X(g_sq) X(g_sr) X(g_sc)
+#define SHAPE_GD(X) X(d_in4) X(d_P4) X(d_g4) X(d_PG4) X(d_cin) X(d_cout) X(d_win) X(d_tp) X(d_wout) X(d_w2)
+#define SHAPE_A(X) X(th) X(rh) X(gh) X(ph) X(zreg) X(in_sq) X(in_sr) X(in_sc) X(g_sq) X(g_sr) X(g_sc)
+#define SHAPE_AD(X) X(d_in4) X(d_g4) X(d_tp)
+
+struct ShapeC {
+    // kernel variant: template arguments of the instantiation, and the signs of the offsets that switch work
+    int fwd, fusek, half, exf, v3, cp, npxk, upk, has_gin, drop, wout, ext_in;
+#define F(n) int D_##n;
+    SHAPE_D(F)
+#undef F
+#define F(n) int G_##n;
+    SHAPE_G(F)
+#undef F
+#define F(n) int M_##n, O_##n;
+    SHAPE_GD(F)
+#undef F
+#define F(n) int A_##n;
+    SHAPE_A(F)
+#undef F
+#define F(n) int AM_##n, AO_##n;
+    SHAPE_AD(F)
+#undef F
+};
+
+#if __has_include("conv_shapes.h")
+#include "conv_shapes.h"
+#endif
+#ifndef GPI_CONV_SHAPE_LIST
+#define GPI_CONV_SHAPE_LIST
+#define GPI_CONV_SHAPE_COUNT 0
+#endif
+constexpr ShapeC kShapes[GPI_CONV_SHAPE_COUNT + 1] = {GPI_CONV_SHAPE_LIST ShapeC{}};   // (+ a zero sentinel)
+constexpr int kNumShapes = GPI_CONV_SHAPE_COUNT;
+
+// the fused output conv's shape instantiation: which field groups it folds (bit 0 descriptor, 1 geometry,
+// 2 magic divisors); 0: none, the launch keeps the generic kernel
+#ifndef GPI_FUSE_FOLD
+#define GPI_FUSE_FOLD 0
+#endif
+
+// the launch's descriptor and geometry with the entry's constants (SHP >= 0; the host matched every field)
+template <int SHP>
+__device__ __forceinline__ void fold_shape(gpi_conv_desc& d, ConvGeom& G) {
+    if constexpr (SHP >= 0) {
+        constexpr ShapeC s = kShapes[SHP];
+        constexpr int fm = s.fusek ? GPI_FUSE_FOLD : 7;
+        if constexpr (fm & 1) {
+#define F(n) d.n = s.D_##n;
+        SHAPE_D(F)
+#undef F
+        }
+        if constexpr (fm & 2) {
+#define F(n) G.n = s.G_##n;
+        SHAPE_G(F)
+#undef F
+#define F(n) G.ha.n = s.A_##n;
+        SHAPE_A(F)
+#undef F
+        }
+        if constexpr (fm & 4) {
+#define F(n) G.n = Div{(uint32_t)s.M_##n, (uint32_t)s.O_##n};
+        SHAPE_GD(F)
+#undef F
+#define F(n) G.ha.n = Div{(uint32_t)s.AM_##n, (uint32_t)s.AO_##n};
+        SHAPE_AD(F)
+#undef F
+        }
+        if constexpr (s.has_gin) __builtin_assume(d.gin_off >= 0); else d.gin_off = -1;
+        if constexpr (s.drop) __builtin_assume(d.drop_off >= 0); else d.drop_off = -1;
+        if constexpr (s.wout) __builtin_assume(d.wpart_off >= 0); else d.wpart_off = -1;
+        if constexpr (s.ext_in) d.in_off = -1; else __builtin_assume(d.in_off >= 0);
+        // without half tiles every tile is a full one (the grid holds nblocks tiles, or 2 nblocks split roles)
+        if constexpr (!s.half) G.nfull = 0x7fffffff;
+    }
 }
 
 __device__ __forceinline__ void glds4(const float* g, float* lds_wave_base) {
@@ -741,9 +835,10 @@ __device__ __forceinline__ void store_px(float* p, const float (&v)[NPX]) {
 // header floats: gst fp64 [4*MAX_CIN] | sc | sh [MAX_CIN] | scratch [64] | red [16] | dropout scales [8]
 constexpr int FWD_HDR = 8 * GPI_MAX_CIN + 2 * GPI_MAX_CIN + 64 + 16 + 8;
 
-template <int K, int S, int UP, int CP, int NPX, bool HALF = false>
+template <int K, int S, int UP, int CP, int NPX, bool HALF = false, int SHP = -1>
 // (the channel-group instantiation NPX == 0 runs one workgroup per CU: no occupancy target)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NPX == 0 ? 1 : 5))) void conv_fwd_kernel(gpi_conv_desc d, gpi_codec_ctx c, ConvGeom G) {
+    fold_shape<SHP>(d, G);
     touch_kernargs<CONV_KARG_BYTES>();
     entry_signal(G);
     if (SKIP(G, 16)) return;
@@ -1208,8 +1303,9 @@ __host__ __device__ constexpr bool fuse_wlds(int ky) {
     return GPI_FUSE_WLDS <= 0 ? false : (GPI_FUSE_WLDS >= 5 ? true : (ky & 1 ? (ky / 2) < GPI_FUSE_WLDS : (ky / 2) < GPI_FUSE_WLDS - 2));
 }
 
-template <int K, int S, int UP, bool FUSE = false, bool HALF = false, bool V3 = false, bool EXF = false>
+template <int K, int S, int UP, bool FUSE = false, bool HALF = false, bool V3 = false, bool EXF = false, int SHP = -1>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (FUSE ? GPI_FUSE_WAVES : 4) : (V3 ? GPI_BWD3_WAVES : GPI_BWD_WAVES)))) void conv_bwd_kernel(gpi_conv_desc d, gpi_codec_ctx c, ConvGeom G) {
+    fold_shape<SHP>(d, G);
     touch_kernargs<CONV_KARG_BYTES>();
     entry_signal(G);
     if (SKIP(G, 16)) return;
@@ -2634,8 +2730,84 @@ bool xcd_mode(bool fwd, bool fuse, bool split, bool half) {
     return !half && (mode & (fuse ? 8 : fwd ? 1 : split ? 4 : 2)) != 0;
 }
 
+// The shape of a planned launch (compile-time shapes above): the kernel variant select_kernel picks, the
+// B-independent descriptor fields and the geometry.  Unused bytes stay zero (value-initialised), so two
+// shapes compare by their bytes.
+ShapeC shape_of(const gpi_conv_desc& d, const ConvGeom& G, bool fwd, bool fuse, int cp, bool exf) {
+    ShapeC s{};
+    const bool half = G.nfull < G.nblocks;
+    s.fwd = fwd;
+    s.fusek = fuse;
+    s.has_gin = d.gin_off >= 0;
+    s.drop = d.drop_off >= 0;
+    s.wout = d.wpart_off >= 0;
+    s.ext_in = d.in_off < 0;
+    if (fuse) {
+        s.half = half;
+        s.exf = exf;
+        s.upk = 0;
+    } else if (!fwd) {
+        const bool u = G.ucls != 0 || v3_op(d, G);
+        s.half = half;
+        s.upk = (d.upsample && u) ? 2 : d.upsample;
+        s.v3 = d.k == 3 && d.stride == 1 && !d.upsample && u;
+    } else {
+        // pick(): NPX = 0 (channel groups) only for the stride-1 / stride-2 convs of k <= 3 without upsampling,
+        // and its instantiation has no half-tile form
+        const int npx = G.cg > 1 ? 0 : G.npx;
+        s.npxk = (npx == 0 && !(d.upsample == 0 && d.k <= 3)) ? 1 : npx;
+        s.half = s.npxk == 0 ? 0 : half;
+        s.cp = cp;
+    }
+#define F(n) s.D_##n = d.n;
+    SHAPE_D(F)
+#undef F
+#define F(n) s.G_##n = G.n;
+    SHAPE_G(F)
+#undef F
+#define F(n) s.M_##n = (int)G.n.m, s.O_##n = (int)G.n.one;
+    SHAPE_GD(F)
+#undef F
+#define F(n) s.A_##n = G.ha.n;
+    SHAPE_A(F)
+#undef F
+#define F(n) s.AM_##n = (int)G.ha.n.m, s.AO_##n = (int)G.ha.n.one;
+    SHAPE_AD(F)
+#undef F
+    return s;
+}
+
+template <int I>
+conv_kernel_t shape_kernel() {
+    constexpr ShapeC s = kShapes[I];
+    // (not the fused output conv: with its shape folded the loss phase unrolls past its 5-wave VGPR budget --
+    // 173 spilled registers; its launch keeps the generic instantiation)
+    if constexpr (s.fusek != 0 && GPI_FUSE_FOLD == 0) return nullptr;
+    else if constexpr (s.fwd != 0) return conv_fwd_kernel<s.D_k, s.D_stride, s.D_upsample, s.cp, s.npxk, s.half != 0, I>;
+    else return conv_bwd_kernel<s.D_k, s.D_stride, s.upk, s.fusek != 0, s.half != 0, s.v3 != 0, s.exf != 0, I>;
+}
+
+template <int... I>
+conv_kernel_t shape_kernel_at(int i, std::integer_sequence<int, I...>) {
+    static const conv_kernel_t t[] = {shape_kernel<I>()..., nullptr};
+    return t[i];
+}
+
+// launches planned / planned with a compile-time shape since load (gpi_conv_shape_info); the shapes seen
+// while GPI_CONV_SHAPES_RECORD=1 (gpi_conv_shapes_dump, tools/gen_conv_shapes.py)
+int64_t g_shape_planned = 0, g_shape_matched = 0;
+std::vector<ShapeC> g_shapes_seen;
+
+// index of s in kShapes, or -1
+int shape_index(const ShapeC& s) {
+    for (int i = 0; i < kNumShapes; ++i)
+        if (memcmp(&kShapes[i], &s, sizeof(ShapeC)) == 0) return i;
+    return -1;
+}
+
+// dry: plan only (no device call) -- the shape recording of gpi_conv_shape_plan
 int launch(const gpi_conv_desc& d, const gpi_codec_ctx& c, hipStream_t st, bool fwd, bool fuse = false,
-           uint32_t* sig = nullptr, const int64_t* sig_epoch = nullptr) {
+           uint32_t* sig = nullptr, const int64_t* sig_epoch = nullptr, bool dry = false) {
     ConvGeom G;
     if (!conv_geom(d, c.groups, G, fwd, fuse)) return GPI_ERR_UNSUPPORTED;
     if (sig && !sig_epoch) return GPI_ERR_ARG;
@@ -2658,7 +2830,7 @@ int launch(const gpi_conv_desc& d, const gpi_codec_ctx& c, hipStream_t st, bool 
                                            G.ucls != 0 || (!fwd && v3_op(d, G)));
     if (!k) return GPI_ERR_UNSUPPORTED;
     static const float* zero = nullptr;
-    if (!zero) {
+    if (!zero && !dry) {
         void* p = nullptr;
         if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_zero_page)) != hipSuccess) return GPI_ERR_LAUNCH;
         zero = (const float*)p;
@@ -2683,6 +2855,23 @@ int launch(const gpi_conv_desc& d, const gpi_codec_ctx& c, hipStream_t st, bool 
     // 3 -> 0.5776 / 0.5770 ms per step
     static const int fuse_alt = env_int("GPI_FUSE_ALT", 1);
     G.alt = fuse ? fuse_alt : 0;
+    {
+        static const int shapes_on = env_int("GPI_CONV_SHAPES", 1), record = env_int("GPI_CONV_SHAPES_RECORD", 0);
+        const ShapeC s = shape_of(d, G, fwd, fuse, cp, exf);
+        g_shape_planned += dry ? 0 : 1;
+        const int si = shapes_on ? shape_index(s) : -1;
+        const conv_kernel_t ks = si >= 0 ? shape_kernel_at(si, std::make_integer_sequence<int, kNumShapes>{}) : nullptr;
+        if (ks) {
+            k = ks;
+            g_shape_matched += dry ? 0 : 1;
+        }
+        if (record || dry) {
+            bool seen = false;
+            for (const ShapeC& q : g_shapes_seen) seen = seen || memcmp(&q, &s, sizeof(ShapeC)) == 0;
+            if (!seen) g_shapes_seen.push_back(s);
+        }
+        if (dry) return GPI_OK;
+    }
 #ifdef GPI_PHASE_TIMING
     static const int dbg_print = env_int("GPI_DBG_PRINT", 0);
     if (dbg_print)
@@ -2830,6 +3019,35 @@ extern "C" int gpi_conv_launch_info(const gpi_conv_desc* op, const gpi_groups* g
     info[4] = G.npx;
     info[5] = G.P;
     info[6] = G.PG;
+    return GPI_OK;
+}
+
+extern "C" int gpi_conv_shape_info(int64_t* info) {
+    if (!info) return GPI_ERR_ARG;
+    info[0] = kNumShapes;
+    info[1] = g_shape_planned;
+    info[2] = g_shape_matched;
+    info[3] = (int64_t)g_shapes_seen.size();
+    return GPI_OK;
+}
+
+extern "C" int gpi_conv_shape_plan(const gpi_conv_desc* op, const gpi_codec_ctx* ctx, int fwd, int fuse) {
+    if (!op || !ctx) return GPI_ERR_ARG;
+    return launch(*op, *ctx, nullptr, fwd != 0, fuse != 0, nullptr, nullptr, true);
+}
+
+extern "C" int gpi_conv_shapes_dump(char* buf, int64_t len) {
+    if (!buf || len <= 0) return GPI_ERR_ARG;
+    std::string out = "#define GPI_CONV_SHAPE_COUNT " + std::to_string(g_shapes_seen.size()) + "\n#define GPI_CONV_SHAPE_LIST";
+    for (const ShapeC& s : g_shapes_seen) {
+        const int* f = reinterpret_cast<const int*>(&s);
+        out += " \\\n    {";
+        for (size_t i = 0; i < sizeof(ShapeC) / sizeof(int); ++i) out += (i ? "," : "") + std::to_string(f[i]);
+        out += "},";
+    }
+    out += "\n";
+    if ((int64_t)out.size() + 1 > len) return GPI_ERR_ARG;
+    memcpy(buf, out.c_str(), out.size() + 1);
     return GPI_OK;
 }
 

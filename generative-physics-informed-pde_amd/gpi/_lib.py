@@ -212,6 +212,9 @@ SIGNATURES = {
     'gpi_version': (C.c_int, []),
     'gpi_replicas': (C.c_int, []),
     'gpi_source_sha': (C.c_char_p, []),
+    'gpi_conv_shape_info': (C.c_int, [C.c_void_p]),
+    'gpi_conv_shapes_dump': (C.c_int, [C.c_char_p, C.c_int64]),
+    'gpi_conv_shape_plan': (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int]),
     'gpi_struct_sizes': (C.c_int, [C.POINTER(i64), C.c_int]),
     'gpi_error_string': (C.c_char_p, [C.c_int]),
     'gpi_conv_blocks': (C.c_int, [C.POINTER(ConvDesc), C.POINTER(Groups), C.POINTER(i32)]),
@@ -278,7 +281,7 @@ def source_sha():
     import glob
     import hashlib
     files = sorted(glob.glob(os.path.join(SRC_DIR, '*.hip')), key=os.path.basename)
-    files += [os.path.join(SRC_DIR, 'common.h'), INCLUDE_H]
+    files += [os.path.join(SRC_DIR, 'common.h'), os.path.join(SRC_DIR, 'conv_shapes.h'), INCLUDE_H]
     if not all(os.path.exists(f) for f in files):
         return None
     h = hashlib.sha1()

@@ -527,6 +527,17 @@ int gpi_conv_blocks(const gpi_conv_desc* op, const gpi_groups* groups, int32_t* 
  * (1 for the backward), info[5] / info[6] LDS row pitch (floats) of the input / output-gradient
  * images.  info holds >= 7 entries.  No device work. */
 int gpi_conv_launch_info(const gpi_conv_desc* op, const gpi_groups* groups, int fwd, int32_t* info);
+/* Compile-time conv shapes (csrc/conv_shapes.h): a launch whose shape -- kernel variant, batch-independent
+ * descriptor fields, tile geometry -- equals a built-in entry runs an instantiation with those values as
+ * constants (GPI_CONV_SHAPES=0: never).  info[0] built-in entries, info[1] conv launches planned since
+ * load, info[2] of them on a built-in shape, info[3] distinct shapes recorded (GPI_CONV_SHAPES_RECORD=1).
+ * gpi_conv_shapes_dump writes the recorded shapes as the text of conv_shapes.h (tools/gen_conv_shapes.py);
+ * GPI_ERR_ARG when len is too small.  No device work. */
+int gpi_conv_shape_info(int64_t* info);
+/* Plan one conv launch (fwd / fuse as gpi_conv_forward / _backward / _loss_fused) and record its shape
+ * without any device call (host-side shape generation). */
+int gpi_conv_shape_plan(const gpi_conv_desc* op, const gpi_codec_ctx* ctx, int fwd, int fuse);
+int gpi_conv_shapes_dump(char* buf, int64_t len);
 int gpi_conv_forward(const gpi_conv_desc* op, const gpi_codec_ctx* ctx, void* stream);
 int gpi_conv_backward(const gpi_conv_desc* op, const gpi_codec_ctx* ctx, void* stream);
 /* Forward AND backward of the decoder's output conv (Decoder.py:288-305 last_decoding conv3, 5x5,
