@@ -32,6 +32,12 @@
 
 using namespace gpi;
 
+// Contraction per expression only (C's FP_CONTRACT on): hipcc's default lets the backend fuse a multiply and
+// an add across statements wherever the schedule puts them together, so the generic kernels and the
+// compile-time shape instantiations (fold_shape) rounded a few products differently (1-ulp differences in
+// the decoder's half tiles, r06); with contraction fixed by the source both compute the same bits.
+#pragma clang fp contract(on)
+
 namespace {
 
 constexpr int HALO = 4;   // zero halo columns on each side of an LDS row image
@@ -805,8 +811,11 @@ __device__ __forceinline__ void st2(float* p, f32x2 v) {
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ void st4(float* p, f32x4 v) {
-    // no 16-byte atomic store exists to lower it from; as two 8-byte halves it measured slower
-    asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(p), "v"(v));
+    // no 16-byte atomic store exists to lower it from; as two 8-byte halves it measured slower.
+    // The s_nop: a store of more than 8 data bytes reads its data VGPRs after issue, and a VALU write to them
+    // right behind it is a hazard the compiler's hazard recognizer does not see through inline asm -- the
+    // compile-time shape instantiations scheduled such a write there and stored clobbered values (r06)
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" : : "v"(p), "v"(v));
 }
 __device__ __forceinline__ void st1(float* p, float v) {
     __hip_atomic_store((__attribute__((address_space(1))) float*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2856,7 +2865,9 @@ int launch(const gpi_conv_desc& d, const gpi_codec_ctx& c, hipStream_t st, bool 
     static const int fuse_alt = env_int("GPI_FUSE_ALT", 1);
     G.alt = fuse ? fuse_alt : 0;
     {
-        static const int shapes_on = env_int("GPI_CONV_SHAPES", 1), record = env_int("GPI_CONV_SHAPES_RECORD", 0);
+        // (GPI_CONV_SHAPES read per launch: a debugging run can compare both forms of one op in one process)
+        const int shapes_on = env_int("GPI_CONV_SHAPES", 1);
+        static const int record = env_int("GPI_CONV_SHAPES_RECORD", 0);
         const ShapeC s = shape_of(d, G, fwd, fuse, cp, exf);
         g_shape_planned += dry ? 0 : 1;
         const int si = shapes_on ? shape_index(s) : -1;
