@@ -46,8 +46,8 @@ RIDGE_FLOP_PER_B = F32_PEAK_TFS * 1e12 / (HBM_PEAK_GBS * 1e9)   # 19.7 flop/B
 # tools/pmc_traffic.py.  Used for roofline.traffic when the dominant operator is listed.
 # One file per bench configuration (the entry for an operator is used only when it was measured on this
 # conv.hip / common.h and at this run's algorithmic bytes, i.e. the same shape).
-TRAFFIC_FILES = {'c64': ['r05_traffic.json', 'r04_traffic.json'], 'c128': ['r05_traffic_c128.json', 'r04_traffic_c128.json'],
-                 'c256': ['r05_traffic_c256.json', 'r04_traffic_c256.json'], 'c32': ['r05_traffic_c32.json']}
+TRAFFIC_FILES = {'c64': ['r06_traffic.json', 'r05_traffic.json'], 'c128': ['r06_traffic_c128.json', 'r05_traffic_c128.json'],
+                 'c256': ['r06_traffic_c256.json', 'r05_traffic_c256.json'], 'c32': ['r05_traffic_c32.json']}
 
 
 def traffic_json(config):

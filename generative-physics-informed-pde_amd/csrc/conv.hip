@@ -442,9 +442,12 @@ constexpr ShapeC kShapes[GPI_CONV_SHAPE_COUNT + 1] = {GPI_CONV_SHAPE_LIST ShapeC
 constexpr int kNumShapes = GPI_CONV_SHAPE_COUNT;
 
 // the fused output conv's shape instantiation: which field groups it folds (bit 0 descriptor, 1 geometry,
-// 2 magic divisors); 0: none, the launch keeps the generic kernel
+// 2 magic divisors); 0: none, the launch keeps the generic kernel.  Its 5-wave budget is at 95 VGPRs already:
+// with the descriptor folded as well the loss phase unrolls and spills (173 registers; 2-11 for the single
+// groups under hipcc's default contraction), geometry + divisors fit (92 VGPRs) and cut the prologue from
+// 1448 to 933 instructions (620 -> 371 VALU)
 #ifndef GPI_FUSE_FOLD
-#define GPI_FUSE_FOLD 0
+#define GPI_FUSE_FOLD 6
 #endif
 
 // the launch's descriptor and geometry with the entry's constants (SHP >= 0; the host matched every field)
@@ -2789,8 +2792,7 @@ ShapeC shape_of(const gpi_conv_desc& d, const ConvGeom& G, bool fwd, bool fuse, 
 template <int I>
 conv_kernel_t shape_kernel() {
     constexpr ShapeC s = kShapes[I];
-    // (not the fused output conv: with its shape folded the loss phase unrolls past its 5-wave VGPR budget --
-    // 173 spilled registers; its launch keeps the generic instantiation)
+    // (the fused output conv only with GPI_FUSE_FOLD != 0: see there)
     if constexpr (s.fusek != 0 && GPI_FUSE_FOLD == 0) return nullptr;
     else if constexpr (s.fwd != 0) return conv_fwd_kernel<s.D_k, s.D_stride, s.D_upsample, s.cp, s.npxk, s.half != 0, I>;
     else return conv_bwd_kernel<s.D_k, s.D_stride, s.upk, s.fusek != 0, s.half != 0, s.v3 != 0, s.exf != 0, I>;

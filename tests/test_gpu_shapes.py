@@ -49,8 +49,8 @@ def run_step(tmp_path, name, shapes_on):
 
 def test_bench_step_launches_run_on_their_shapes(device):
     """One eager step of the bench workload: 45 conv launches (23 encoder + decoder forwards, 22 backwards
-    incl. the fused output conv), 44 of them on a compile-time shape (the fused output conv keeps the
-    generic instantiation: folded, it spills)."""
+    incl. the fused output conv), every one on its compile-time shape (the fused output conv with its
+    geometry folded, GPI_FUSE_FOLD)."""
     import bench
     from gpi.train import FusedElboStep
     model, data, (B_u, N_s), physics = bench.build('c64', device, seed=1)
@@ -64,7 +64,7 @@ def test_bench_step_launches_run_on_their_shapes(device):
     n1 = shape_info()
     assert n1[0] > 0
     planned, matched = n1[1] - n0[1], n1[2] - n0[2]
-    assert planned == 45 and matched == planned - 1, (planned, matched)
+    assert planned == 45 and matched == planned, (planned, matched)
 
 
 def test_shape_kernels_bit_identical_to_generic(device, tmp_path):
