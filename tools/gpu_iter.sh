@@ -9,7 +9,8 @@
 #   IT_STEPS    bench steps per A/B arm (default 400)
 #   IT_PHASE    operator names for tools/phase_probe.py (timing build) or empty
 #   IT_BENCH    1: the default bench line (CPU baseline + roofline) -> gpurun_out/bench_TAG.json
-#   IT_PROF     1: rocprofv3 --kernel-trace --stats of a short bench run (kernel stats + step timeline)
+#   IT_PROF     1: rocprofv3 --kernel-trace --stats of a short bench run (kernel stats + step timeline);
+#               IT_PROF_UNROLL steps per graph replay there (default 1)
 set -u
 TAG=${1:-iter}
 shift || true
@@ -57,7 +58,7 @@ fi
 if [ "${IT_PROF:-0}" = "1" ]; then
     cd /tmp && export TMPDIR=/tmp
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o run -- \
-        python3 "$R/bench.py" --steps 20 --warmup 5 --unroll 1 --no-cpu-baseline --no-roofline > "$OUT/prof_$TAG.log" 2>&1
+        python3 "$R/bench.py" --steps 20 --warmup 5 --unroll ${IT_PROF_UNROLL:-1} --no-cpu-baseline --no-roofline > "$OUT/prof_$TAG.log" 2>&1
     rc=$?
     echo "rocprof rc=$rc"
     cd "$R"
