@@ -356,6 +356,17 @@ def step_bytes(model, B_u, N_s, physics):
     return B_u * per_u + N_s * per_s, dict(S_enc=s_enc, S_dec=s_dec, per_unlabeled=per_u, per_labeled=per_s)
 
 
+def conv_shape_info():
+    """Compile-time conv shapes (csrc/conv_shapes.h): table entries, conv launches planned since load and how many
+    of them ran a shape instantiation (the graph's launches are planned once, at capture)."""
+    import ctypes as C
+    from gpi import _lib as L
+    info = (C.c_int64 * 4)()
+    if L.lib().gpi_conv_shape_info(info) != 0:
+        return None
+    return {'table': int(info[0]), 'launches_planned': int(info[1]), 'on_shape': int(info[2])}
+
+
 def conv_source_sha():
     """sha1 of csrc/conv.hip + csrc/common.h (+ csrc/conv_shapes.h, the compile-time shapes, from r06): the
     conv kernels' sources.  PMC traffic figures are only used for the code they were measured on."""
@@ -570,6 +581,7 @@ def main():
                        'bn': 'replica' if not getattr(step, 'sync_bn', False) else 'sync (%s exchange)' % step.bn_exchange},
             'elbo_last': elbo,
             'host_enqueue_ms_per_step': round(1e3 * (t_enq - t0) / args.steps, 4),
+            'conv_shapes': conv_shape_info(),
             'roofline': roof,
             'cpu_baseline': cpu,
         }

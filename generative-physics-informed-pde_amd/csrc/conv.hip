@@ -431,7 +431,10 @@ struct ShapeC {
 #undef F
 };
 
-#if __has_include("conv_shapes.h")
+// (GPI_SHAPES_FILE: another table, for A/B builds of other tile rules -- tools/shape_variant.sh)
+#if defined(GPI_SHAPES_FILE)
+#include GPI_SHAPES_FILE
+#elif __has_include("conv_shapes.h")
 #include "conv_shapes.h"
 #endif
 #ifndef GPI_CONV_SHAPE_LIST
