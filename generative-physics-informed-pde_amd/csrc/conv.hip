@@ -2716,7 +2716,9 @@ int cp_of(const gpi_conv_desc& d) {
     const int cout = d.cout;
     if (cout <= 2) return 2;
     if (cout <= 4) return 4;
-    const bool wide8 = d.k == 7 || (d.k == 3 && d.stride == 1 && !d.upsample);
+    // GPI_FWD_CP6=1: the 3x3 stride-1 ones with 5-6 outputs on 6 as well (A/B of the rule on the shape kernels)
+    static const int cp6 = env_int("GPI_FWD_CP6", 0);
+    const bool wide8 = d.k == 7 || (d.k == 3 && d.stride == 1 && !d.upsample && !cp6);
     return (cout <= 6 && !wide8) ? 6 : 8;
 }
 
