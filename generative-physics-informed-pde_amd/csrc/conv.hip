@@ -443,6 +443,16 @@ struct ShapeC {
 #endif
 constexpr ShapeC kShapes[GPI_CONV_SHAPE_COUNT + 1] = {GPI_CONV_SHAPE_LIST ShapeC{}};   // (+ a zero sentinel)
 constexpr int kNumShapes = GPI_CONV_SHAPE_COUNT;
+// Translation units of the shape instantiations: entries [kBounds[p], kBounds[p + 1]) are instantiated by this file
+// compiled with GPI_CONV_SHAPE_PART = p (part 0: the bench workload's shapes, with the launch code; parts 1-3: the
+// other configurations' shapes, each part its own object so they compile in parallel)
+#ifndef GPI_CONV_SHAPE_BOUNDS
+#define GPI_CONV_SHAPE_BOUNDS {0, GPI_CONV_SHAPE_COUNT, GPI_CONV_SHAPE_COUNT, GPI_CONV_SHAPE_COUNT, GPI_CONV_SHAPE_COUNT}
+#endif
+constexpr int kBounds[5] = GPI_CONV_SHAPE_BOUNDS;
+#ifndef GPI_CONV_SHAPE_PART
+#define GPI_CONV_SHAPE_PART 0
+#endif
 
 // the fused output conv's shape instantiation: which field groups it folds (bit 0 descriptor, 1 geometry,
 // 2 magic divisors); 0: none, the launch keeps the generic kernel.  Its 5-wave budget is at 95 VGPRs already:
@@ -2653,6 +2663,55 @@ bool vsum_op(const gpi_conv_desc& d, const ConvGeom& G) {
 
 typedef void (*conv_kernel_t)(gpi_conv_desc, gpi_codec_ctx, ConvGeom);
 
+// entries whose instantiation spills at its occupancy target (the folded loops unroll further than the generic
+// kernel's): their launches keep the generic kernel (GPI_CONV_SHAPE_NOFOLD in conv_shapes.h, from
+// tools/kernel_resources.sh after a build; tools/gen_conv_shapes.py carries the list over)
+#ifndef GPI_CONV_SHAPE_NOFOLD
+#define GPI_CONV_SHAPE_NOFOLD {-1}
+#endif
+constexpr int kNoFold[] = GPI_CONV_SHAPE_NOFOLD;
+constexpr bool no_fold(int i) {
+    for (int v : kNoFold)
+        if (v == i) return true;
+    return false;
+}
+
+template <int I>
+conv_kernel_t shape_kernel() {
+    constexpr ShapeC s = kShapes[I];
+    // (the fused output conv only with GPI_FUSE_FOLD != 0: see there)
+    if constexpr ((s.fusek != 0 && GPI_FUSE_FOLD == 0) || no_fold(I)) return nullptr;
+    else if constexpr (s.fwd != 0) return conv_fwd_kernel<s.D_k, s.D_stride, s.D_upsample, s.cp, s.npxk, s.half != 0, I>;
+    else return conv_bwd_kernel<s.D_k, s.D_stride, s.upk, s.fusek != 0, s.half != 0, s.v3 != 0, s.exf != 0, I>;
+}
+
+// kernel of entry LO + i, entries [LO, LO + n) instantiated here
+template <int LO, int... I>
+conv_kernel_t shape_kernel_at(int i, std::integer_sequence<int, I...>) {
+    static const conv_kernel_t t[] = {shape_kernel<LO + I>()..., nullptr};
+    return t[i];
+}
+
+}  // namespace
+
+// the other parts' tables of kernels (hidden: not part of the library's interface)
+namespace gpi_conv_parts {
+__attribute__((visibility("hidden"))) void* shape_part1(int i);
+__attribute__((visibility("hidden"))) void* shape_part2(int i);
+__attribute__((visibility("hidden"))) void* shape_part3(int i);
+#if GPI_CONV_SHAPE_PART > 0
+#define GPI_PART_FN_(p) shape_part##p
+#define GPI_PART_FN(p) GPI_PART_FN_(p)
+void* GPI_PART_FN(GPI_CONV_SHAPE_PART)(int i) {
+    constexpr int lo = kBounds[GPI_CONV_SHAPE_PART], n = kBounds[GPI_CONV_SHAPE_PART + 1] - lo;
+    return (void*)shape_kernel_at<lo>(i, std::make_integer_sequence<int, n>{});
+}
+#endif
+}  // namespace gpi_conv_parts
+
+namespace {
+#if GPI_CONV_SHAPE_PART == 0
+
 template <int K, int S, int UP, int NPX, bool HALF>
 conv_kernel_t pick_cp_h(int cp) {
     if (cp == 2) return conv_fwd_kernel<K, S, UP, 2, NPX, HALF>;
@@ -2794,19 +2853,13 @@ ShapeC shape_of(const gpi_conv_desc& d, const ConvGeom& G, bool fwd, bool fuse, 
     return s;
 }
 
-template <int I>
-conv_kernel_t shape_kernel() {
-    constexpr ShapeC s = kShapes[I];
-    // (the fused output conv only with GPI_FUSE_FOLD != 0: see there)
-    if constexpr (s.fusek != 0 && GPI_FUSE_FOLD == 0) return nullptr;
-    else if constexpr (s.fwd != 0) return conv_fwd_kernel<s.D_k, s.D_stride, s.D_upsample, s.cp, s.npxk, s.half != 0, I>;
-    else return conv_bwd_kernel<s.D_k, s.D_stride, s.upk, s.fusek != 0, s.half != 0, s.v3 != 0, s.exf != 0, I>;
-}
-
-template <int... I>
-conv_kernel_t shape_kernel_at(int i, std::integer_sequence<int, I...>) {
-    static const conv_kernel_t t[] = {shape_kernel<I>()..., nullptr};
-    return t[i];
+// kernel of table entry i, from the part that instantiates it
+conv_kernel_t shape_kernel_any(int i) {
+    if (i < 0 || i >= kNumShapes) return nullptr;
+    if (i < kBounds[1]) return shape_kernel_at<0>(i, std::make_integer_sequence<int, kBounds[1]>{});
+    if (i < kBounds[2]) return (conv_kernel_t)gpi_conv_parts::shape_part1(i - kBounds[1]);
+    if (i < kBounds[3]) return (conv_kernel_t)gpi_conv_parts::shape_part2(i - kBounds[2]);
+    return (conv_kernel_t)gpi_conv_parts::shape_part3(i - kBounds[3]);
 }
 
 // launches planned / planned with a compile-time shape since load (gpi_conv_shape_info); the shapes seen
@@ -2878,7 +2931,7 @@ int launch(const gpi_conv_desc& d, const gpi_codec_ctx& c, hipStream_t st, bool 
         const ShapeC s = shape_of(d, G, fwd, fuse, cp, exf);
         g_shape_planned += dry ? 0 : 1;
         const int si = shapes_on ? shape_index(s) : -1;
-        const conv_kernel_t ks = si >= 0 ? shape_kernel_at(si, std::make_integer_sequence<int, kNumShapes>{}) : nullptr;
+        const conv_kernel_t ks = si >= 0 ? shape_kernel_any(si) : nullptr;
         if (ks) {
             k = ks;
             g_shape_matched += dry ? 0 : 1;
@@ -2989,8 +3042,10 @@ __global__ __launch_bounds__(256) void bn_running_kernel(const gpi_bn_running_it
     if (c == 0) *it.num_batches_tracked += it.n_calls;
 }
 
+#endif  // GPI_CONV_SHAPE_PART == 0
 }  // namespace
 
+#if GPI_CONV_SHAPE_PART == 0
 extern "C" int gpi_bn_running_update(const gpi_bn_running_item* items, int n_items, int max_channels,
                                      const gpi_stat* stats, int64_t n_stats, float momentum, void* stream) {
     if (n_items < 0 || max_channels < 1 || (n_items > 0 && (!items || !stats))) return GPI_ERR_ARG;
@@ -3153,3 +3208,4 @@ extern "C" int gpi_wgrad_reduce(const gpi_reduce_item* items, int n_items, const
     GPI_CHECK_LAUNCH();
     return GPI_OK;
 }
+#endif  // GPI_CONV_SHAPE_PART == 0
