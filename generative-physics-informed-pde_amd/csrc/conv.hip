@@ -2638,13 +2638,14 @@ size_t bwd_lds(const gpi_conv_desc& d, const ConvGeom& G) {
 
 // One slab row per tile for the MFMA backward (G.lsum): the weight-gradient accumulators fit the
 // kernel's 2 x 2 register blocks (cout K, cin K <= 32), not the single-channel stride-2 input conv's
-// own form, and the four partial rows fit the LDS after the header.  Off by default (GPI_LSUM=1 turns
-// it on): a quarter of the slab bytes, but the two extra barriers and the LDS pass cost more than the
-// stores and the smaller reductions save -- 0.6315 vs 0.6258 ms/step (r03, 3 x 600 replays per arm).
+// own form, and the four partial rows fit the LDS after the header.  On every launch it cost more than the
+// stores and the smaller reductions save with the generic kernels -- 0.6315 vs 0.6258 ms/step (r03, 3 x 600
+// replays per arm).  Default 2 since r06: only on output planes of <= 16 x 16 pixels (3: <= 8 x 8; 1: every
+// launch; 0: off), where the four slab rows per tile are as many bytes as the launch's own operands (PMC:
+// TransDown3.conv2.bwd 2.7-3.0x its algorithmic bytes) -- with the shape kernels 0.4384-0.4393 vs 0.4413-0.4419
+// ms/step (profiles/r06k_ab_lsum.txt)
 bool lsum_op(const gpi_conv_desc& d, const ConvGeom& G) {
-    // GPI_LSUM=2 / 3: only on output planes of <= 16 x 16 / <= 8 x 8 pixels, where the four slab rows per
-    // tile are as many bytes as the launch's own operands (PMC: TransDown3.conv2.bwd 3.0x its algorithmic bytes)
-    static const int on = env_int("GPI_LSUM", 0);
+    static const int on = env_int("GPI_LSUM", 2);
     if (!on || vop_op(d) || G.fuse) return false;
     if ((on == 2 && d.h_out * d.w_out > 256) || (on == 3 && d.h_out * d.w_out > 64)) return false;
     if (d.k == 7 && d.stride == 2 && !d.upsample && d.cin == 1 && d.gin_off < 0 && d.cout <= 16) return false;
