@@ -241,11 +241,14 @@ bool conv_geom(const gpi_conv_desc& d, const gpi_groups& g, ConvGeom& G, bool fw
     // LastTransUp.conv1 23.9 -> 32.5); 512-px tiles for the single-channel input conv (forward 11.0 -> 10.3 us;
     // the backward, with the column-shift weight gradient, 0.5535 vs 0.5554 ms/step: profiles/r04z_ab_s2c1.txt)
     static const int t_fwdup32 = env_int("GPI_TILE_FWDUP32", 16), t_bwdups = env_int("GPI_TILE_BWDUPS", 16),
-                     t_bwd32k3 = env_int("GPI_TILE_BWD32K3", 16), t_s2c1f = env_int("GPI_TILE_S2C1F", 512);
+                     t_bwd32k3 = env_int("GPI_TILE_BWD32K3", 16), t_s2c1f = env_int("GPI_TILE_S2C1F", 512),
+                     t_fwdwide = env_int("GPI_TILE_FWDWIDE", 8);   // the 3x3 forward of >= 10 channels, 32 wide
     const int target =
         d.stride == 2 ? (d.cin == 1 ? (fwd ? t_s2c1f : t_s2c1) : (fwd ? t_s2 : t_s2brows * d.w_out))
         : fwd ? (d.w_out >= 64 ? t_fwd64
-                               : (d.w_out >= 32 ? (d.upsample && d.w_out == 32 ? t_fwdup32 : t_fwdrows) * d.w_out : t_fwd))
+                               : (d.w_out >= 32 ? (d.upsample && d.w_out == 32 ? t_fwdup32
+                                                   : (d.k == 3 && d.cin >= 10 && d.w_out == 32 ? t_fwdwide : t_fwdrows)) * d.w_out
+                                                : t_fwd))
               : (d.upsample ? (d.w_out >= 32 ? t_bwdup / 64 * min(d.w_out, 64) : t_bwdups * d.w_out)
                             : (d.w_out >= 64 ? t_bwd
                                              : (d.w_out == 32 && d.k == 3 && d.cin <= 8 ? t_bwd32k3 : t_bwdrows) * d.w_out));
