@@ -33,14 +33,13 @@ def main():
         e.rom_first = True
     if variant == 'enc_reduce_main':
         e.enc_reduce = 'main'
-    step.capture()
-    for _ in range(30):
-        step.step()
+    unroll = int(os.environ.get('GPI_UNROLL', '4'))     # as bench.py: steps per graph replay
+    step.capture(unroll=unroll)
+    step.run(32)
     torch.cuda.synchronize()
     t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0.record()
-    for _ in range(steps):
-        step.step()
+    step.run(steps)
     t1.record()
     torch.cuda.synchronize()
     print('%-10s %.4f ms/step' % (variant, t0.elapsed_time(t1) / steps))
