@@ -29,6 +29,8 @@
 #include <string>
 #include <utility>
 #include <vector>
+#include <atomic>
+#include <mutex>
 
 using namespace gpi;
 
@@ -1316,6 +1318,11 @@ __host__ __device__ inline int vop_mid_floats(int gh, int w_out, int rowlen, boo
 #ifndef GPI_FUSE_WAVES
 #define GPI_FUSE_WAVES 5
 #endif
+// ... of its compile-time shape instantiation (geometry folded: 80 VGPRs fit 6 waves without spills, where the
+// generic kernel spills 14-15)
+#ifndef GPI_FUSE_SHP_WAVES
+#define GPI_FUSE_SHP_WAVES 5
+#endif
 // fused output conv forward: which of the K weight-pair taps come by broadcast LDS read (one ds_read_b64 of
 // the (co 0, co 1) pair) instead of two v_readlane (GPI_FUSE_WLDS = how many; the odd taps first).  The
 // launch: 30.29 / 30.52 us with every pair by readlane, 29.63 / 29.55 with 4 of 5 by LDS, 29.40 / 29.44 with
@@ -1332,7 +1339,7 @@ __host__ __device__ constexpr bool fuse_wlds(int ky) {
 }
 
 template <int K, int S, int UP, bool FUSE = false, bool HALF = false, bool V3 = false, bool EXF = false, int SHP = -1>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (FUSE ? GPI_FUSE_WAVES : 4) : (V3 ? GPI_BWD3_WAVES : GPI_BWD_WAVES)))) void conv_bwd_kernel(gpi_conv_desc d, gpi_codec_ctx c, ConvGeom G) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K == 5 ? (FUSE ? (SHP >= 0 ? GPI_FUSE_SHP_WAVES : GPI_FUSE_WAVES) : 4) : (V3 ? GPI_BWD3_WAVES : GPI_BWD_WAVES)))) void conv_bwd_kernel(gpi_conv_desc d, gpi_codec_ctx c, ConvGeom G) {
     fold_shape<SHP>(d, G);
     touch_kernargs<CONV_KARG_BYTES>();
     entry_signal(G);
@@ -2868,8 +2875,10 @@ conv_kernel_t shape_kernel_any(int i) {
 
 // launches planned / planned with a compile-time shape since load (gpi_conv_shape_info); the shapes seen
 // while GPI_CONV_SHAPES_RECORD=1 (gpi_conv_shapes_dump, tools/gen_conv_shapes.py)
-int64_t g_shape_planned = 0, g_shape_matched = 0;
+// (atomic counters and a lock around the recording: launches may come from more than one host thread)
+std::atomic<int64_t> g_shape_planned{0}, g_shape_matched{0};
 std::vector<ShapeC> g_shapes_seen;
+std::mutex g_shapes_mu;
 
 // index of s in kShapes, or -1
 int shape_index(const ShapeC& s) {
@@ -2941,6 +2950,7 @@ int launch(const gpi_conv_desc& d, const gpi_codec_ctx& c, hipStream_t st, bool 
             g_shape_matched += dry ? 0 : 1;
         }
         if (record || dry) {
+            std::lock_guard<std::mutex> lk(g_shapes_mu);
             bool seen = false;
             for (const ShapeC& q : g_shapes_seen) seen = seen || memcmp(&q, &s, sizeof(ShapeC)) == 0;
             if (!seen) g_shapes_seen.push_back(s);
@@ -3104,7 +3114,10 @@ extern "C" int gpi_conv_shape_info(int64_t* info) {
     info[0] = kNumShapes;
     info[1] = g_shape_planned;
     info[2] = g_shape_matched;
-    info[3] = (int64_t)g_shapes_seen.size();
+    {
+        std::lock_guard<std::mutex> lk(g_shapes_mu);
+        info[3] = (int64_t)g_shapes_seen.size();
+    }
     return GPI_OK;
 }
 
@@ -3115,6 +3128,7 @@ extern "C" int gpi_conv_shape_plan(const gpi_conv_desc* op, const gpi_codec_ctx*
 
 extern "C" int gpi_conv_shapes_dump(char* buf, int64_t len) {
     if (!buf || len <= 0) return GPI_ERR_ARG;
+    std::lock_guard<std::mutex> lk(g_shapes_mu);
     std::string out = "#define GPI_CONV_SHAPE_COUNT " + std::to_string(g_shapes_seen.size()) + "\n#define GPI_CONV_SHAPE_LIST";
     for (const ShapeC& s : g_shapes_seen) {
         const int* f = reinterpret_cast<const int*>(&s);

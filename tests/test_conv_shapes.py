@@ -33,3 +33,43 @@ def test_shape_info_counts_without_device():
     info = (C.c_int64 * 4)()
     assert L.lib().gpi_conv_shape_info(info) == 0
     assert info[0] == len([l for l in open(SHAPES_H) if l.strip().startswith('{')])
+
+
+def _define(name):
+    for line in open(SHAPES_H):
+        if line.startswith('#define ' + name + ' '):
+            return line.split(None, 2)[2].strip()
+    return None
+
+
+def test_shape_parts_and_nofold_list_are_consistent():
+    """The table's parts (one object of conv.hip each, GPI_CONV_SHAPE_PART) cover it in order, and the entries
+    left to the generic kernels (GPI_CONV_SHAPE_NOFOLD) are entries of it."""
+    n = int(_define('GPI_CONV_SHAPE_COUNT'))
+    bounds = [int(v) for v in _define('GPI_CONV_SHAPE_BOUNDS').strip('{}').split(',')]
+    assert len(bounds) == 5 and bounds[0] == 0 and bounds[-1] == n
+    assert all(a <= b for a, b in zip(bounds, bounds[1:]))
+    nofold = [int(v) for v in _define('GPI_CONV_SHAPE_NOFOLD').strip('{}').split(',')]
+    assert all(v == -1 or 0 <= v < n for v in nofold)
+
+
+def test_no_shape_instantiation_spills():
+    """Every compile-time shape instantiation in the built objects fits its occupancy target without spilling
+    (a regenerated table can move an entry that spills out of GPI_CONV_SHAPE_NOFOLD's list: this catches it).
+    Needs the built objects (csrc/build/conv*.o); skipped without them."""
+    import glob
+    import pytest
+    objs = sorted(glob.glob(os.path.join(PKG, 'csrc', 'build', 'conv*.o')))
+    if not objs:
+        pytest.skip('conv objects not built here')
+    tool = os.path.join(ROOT, 'tools', 'kernel_resources.sh')
+    bad = []
+    for o in objs:
+        r = subprocess.run(['bash', tool, o, 'conv_'], capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr[-1000:]
+        for line in r.stdout.splitlines():
+            name, f = line.split()[0], line.split()
+            # shape instantiations carry a non-negative last template argument (ELi<n>EE); -1 prints as Lin1
+            if 'Lin1EE' not in name and int(f[f.index('spill') + 1]) > 0:
+                bad.append(line)
+    assert not bad, bad
